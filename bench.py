@@ -1,0 +1,220 @@
+"""Training throughput of the N2N U-Net step on MI355X (BASELINE.json metric, config 1).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
+
+A step = noise synthesis + neighbour sub-sampling + no-grad UNet(256^2) + UNet(128^2) fwd/bwd
++ N2N loss + [RCCL all-reduce of the flat gradient] + Adam, on bs=64 patches per rank of
+synthetic 256x256x1 data (weak scaling: global batch = 64 * N).  Prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector, spec
+PEAK_HBM_GBS = 8000.0
+
+
+def conv_flops(h, w, cin, cout, k):
+    return 2.0 * h * w * cin * cout * k * k
+
+
+def unet_fwd_flops(H, W, C=1, nf=48):
+    """analytic forward FLOPs of arch_unet.UNet per image (== torch FlopCounter)"""
+    f = conv_flops(H, W, C, nf, 3) + conv_flops(H, W, nf, nf, 3)
+    for l in range(1, 6):
+        f += conv_flops(H >> l, W >> l, nf, nf, 3)
+    f += conv_flops(H >> 5, W >> 5, nf, nf, 1) * 4          # up5 deconv (per output pixel group)
+    f += 2 * conv_flops(H >> 4, W >> 4, 2 * nf, 2 * nf, 3)
+    for l in (3, 2, 1):
+        f += conv_flops(H >> (l + 1), W >> (l + 1), 2 * nf, 2 * nf, 1) * 4
+        f += conv_flops(H >> l, W >> l, 3 * nf, 2 * nf, 3) + conv_flops(H >> l, W >> l, 2 * nf, 2 * nf, 3)
+    f += conv_flops(H >> 1, W >> 1, 2 * nf, 2 * nf, 1) * 4
+    f += conv_flops(H, W, 2 * nf + C, 96, 3) + conv_flops(H, W, 96, 96, 3)
+    f += 2 * conv_flops(H, W, 96, 96, 1) + conv_flops(H, W, 96, C, 1)
+    return f
+
+
+def synthetic_clean(n, H, W, seed, device):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    lo = torch.rand(n, 1, H // 8, W // 8, generator=g)
+    return F.interpolate(lo, size=(H, W), mode="bilinear", align_corners=False).to(device)
+
+
+def time_dominant_kernel(bs, H, W, device, reps=5):
+    """dec_conv1b-shaped 3x3 conv (96->96 at 256^2, bs images) through the same k_fwd kernel the
+    step uses, timed with HIP events on the stream it is launched on."""
+    from image_denoising_amd import _lib
+
+    x = torch.randn(bs, H, W, 96, device=device)
+    w = torch.randn(96, 96, 3, 3, device=device) * 0.05
+    b = torch.zeros(96, device=device)
+    y = torch.empty_like(x)
+    s = torch.cuda.current_stream(device)
+    run = lambda: _lib.call("dn_conv2d_forward", x.data_ptr(), 96, bs, H, W, 96, w.data_ptr(),
+                            b.data_ptr(), 96, 3, 1, y.data_ptr(), 96, s.cuda_stream)
+    run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        run()
+    e1.record(s)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    flops = bs * conv_flops(H, W, 96, 96, 3)
+    del x, y
+    return ms, flops
+
+
+def cpu_baseline(seconds_budget=20.0):
+    """The oracle (torch-CPU restatement of the reference N2N step, validated against the
+    reference in tests/test_oracle_golden.py) on a bounded sample of config 1."""
+    import numpy as np
+
+    from image_denoising_amd.arch_unet import reference_init
+    from oracle import philox, unet_ref
+
+    threads = min(os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    bs, H = 4, 256
+    torch.manual_seed(0)
+    flat = reference_init(1, 1, 48)
+    clean = synthetic_clean(bs, H, H, 0, "cpu")
+    noisy = clean + (25.0 / 255.0) * torch.from_numpy(
+        philox.normal(0, 0, np.arange(clean.numel(), dtype=np.uint64)).reshape(clean.shape)).float()
+    rd = philox.rd_idx(1, 1, bs * (H // 2) * (H // 2))
+    unet_ref.n2n_step(flat, noisy, rd, 0.02)  # warm-up
+    times = []
+    t_end = time.perf_counter() + seconds_budget
+    while len(times) < 3 and (not times or time.perf_counter() + times[-1] < t_end):
+        t0 = time.perf_counter()
+        unet_ref.n2n_step(flat, noisy, rd, 0.02)
+        times.append(time.perf_counter() - t0)
+    med = sorted(times)[len(times) // 2]
+    return {"value": round(bs / med, 3), "unit": "patches/s", "cores": threads, "kind": "port",
+            "sample": f"oracle N2N step (torch-CPU restatement of train.py/arch_unet.py), bs={bs}, "
+                      f"{H}x{H}x1, nf=48, Adam; median of {len(times)} steps after 1 warm-up"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--bs", type=int, default=64, help="patches per GPU")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--channels", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--breakdown", action="store_true", help="per-phase HIP-event timing (stderr)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+
+    from image_denoising_amd import N2NTrainer, UNet
+
+    C, H, bs = args.channels, args.size, args.bs
+    torch.manual_seed(0)
+    net = UNet(in_nc=C, out_nc=C, n_feature=48).to(device)
+    tr = N2NTrainer(net, lr=3e-4, n_epoch=100, increase_ratio=2.0, seed=0)
+    clean = synthetic_clean(bs * C, H, H, 1000 + rank, device).view(bs, C, H, H).contiguous()
+
+    for _ in range(args.warmup):
+        tr.train_step(clean, epoch=1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = tr.train_step(clean, epoch=1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    loss_v = loss.cpu().tolist()
+
+    if args.breakdown and rank == 0:
+        breakdown(tr, clean, device)
+
+    if rank == 0:
+        ms_step = 1000.0 * elapsed / args.steps
+        value = world * bs * args.steps / elapsed
+        kms, kflops = time_dominant_kernel(bs, H, H, device)
+        achieved = kflops / (kms * 1e-3) / 1e12
+        step_flops = bs * (unet_fwd_flops(H, H, C) + 3 * unet_fwd_flops(H // 2, H // 2, C))
+        rec = {
+            "metric": "training patches/sec (256x256x1, bs=64 per GPU, N2N loss + Adam)",
+            "value": round(value, 2), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "BASELINE configs[1]: N2N step, UNet(n_feature=48), "
+                                   f"{bs}x{C}x{H}x{H} per GPU, Adam lr 3e-4",
+                       "global_batch": bs * world, "patch": [H, H, C], "parallelism": f"dp{world}"},
+            "step_tflops": round(step_flops / (ms_step * 1e-3) / 1e12, 2),
+            "step_frac_of_fp32_peak": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
+            "roofline": {"bound": "mfma", "kernel": "k_fwd<G_C3,NT=6,MT=4> (dec_conv1b 96->96 3x3 @256^2)",
+                         "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                         "avg_launch_ms": round(kms, 4), "flops_per_launch": kflops},
+            "loss": loss_v,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            rec["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def breakdown(tr, clean, device):
+    """per-phase HIP-event timing of one step (stderr)"""
+    from image_denoising_amd import _lib
+    from image_denoising_amd.n2n import n2n_loss, n2n_subsample
+
+    s = torch.cuda.current_stream(device)
+    N, C, H, W = clean.shape
+    b = tr._buffers(N, C, H, W, device)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(8)]
+    ev[0].record(s)
+    _lib.call("dn_add_gauss_noise", _lib.ptr(clean), N, C * H * W, 0.098, None, 0, 0, 0,
+              _lib.ptr(b["noisy"]), s.cuda_stream)
+    sub1, sub2, rd = n2n_subsample(b["noisy"], None, seed=1, offset=1)
+    ev[1].record(s)
+    tr.net._run_forward(b["noisy"], b["den"], b["ws_den"])
+    ev[2].record(s)
+    tr.net._run_forward(sub1, b["out"], b["ws_grad"])
+    ev[3].record(s)
+    loss3, dout = n2n_loss(b["out"], sub2, b["den"], rd, 0.02)
+    ev[4].record(s)
+    tr.net._run_backward(dout, tr.grad, b["ws_grad"], N, H // 2, W // 2)
+    ev[5].record(s)
+    ev[6].record(s)
+    ev[6].synchronize()
+    names = ["noise+subsample", "fwd 256 (no grad)", "fwd 128 (saved)", "loss", "bwd 128"]
+    for i, n in enumerate(names):
+        print(f"  {n:22s} {ev[i].elapsed_time(ev[i + 1]):8.3f} ms", file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,126 @@
+"""ctypes binding of libdenoise_hip.so (include/denoise_hip.h).
+
+The product path has no fallback: if the HIP library is missing or fails to load, importing
+anything that computes raises.  Tensors cross the boundary as raw device pointers; the HIP
+stream is torch's current stream on the tensor's device.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int64, c_size_t, c_uint8, c_uint64, c_void_p
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DN_LIB_PATH", os.path.join(_HERE, "libdenoise_hip.so"))
+
+
+class DnCfg(ctypes.Structure):
+    _fields_ = [("in_nc", c_int), ("out_nc", c_int), ("n_feature", c_int)]
+
+
+_F = c_void_p  # float*  (device)
+_U8 = c_void_p  # uint8_t* (device)
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "dn_version": (c_char_p, []),
+    "dn_last_error": (c_int, [c_char_p, c_size_t]),
+    "dn_unet_param_count": (c_int, [POINTER(DnCfg), POINTER(c_size_t)]),
+    "dn_unet_param_info": (c_int, [POINTER(DnCfg), c_int, POINTER(c_size_t), POINTER(c_size_t),
+                                   POINTER(c_size_t)]),
+    "dn_unet_workspace_size": (c_int, [POINTER(DnCfg), c_int, c_int, c_int, c_int,
+                                       POINTER(c_size_t)]),
+    "dn_unet_forward": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
+                                c_size_t, c_void_p]),
+    "dn_unet_backward": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
+                                 c_size_t, c_void_p]),
+    "dn_n2n_subsample": (c_int, [_F, c_int, c_int, c_int, c_int, _U8, c_uint64, c_uint64, c_uint64,
+                                 _F, _F, _U8, c_void_p]),
+    "dn_n2n_masks": (c_int, [_U8, c_int64, _U8, _U8, c_void_p]),
+    "dn_n2n_subimage_from_mask": (c_int, [_F, c_int, c_int, c_int, c_int, _U8, _F, c_void_p]),
+    "dn_add_gauss_noise": (c_int, [_F, c_int, c_int64, c_float, _F, c_uint64, c_uint64, c_uint64,
+                                   _F, c_void_p]),
+    "dn_loss_partials_size": (c_size_t, []),
+    "dn_n2n_loss": (c_int, [_F, _F, _F, _U8, c_int, c_int, c_int, c_int, c_float, _F, _F, c_void_p,
+                            c_void_p]),
+    "dn_structure_loss": (c_int, [_F, _F, _F, c_int, c_int, c_int, c_int, c_float, c_float,
+                                  c_float, _F, _F, _F, c_void_p, c_void_p]),
+    "dn_adam_step": (c_int, [_F, _F, _F, _F, c_int64, c_float, c_float, c_float, c_float, c_int64,
+                             c_float, c_void_p]),
+    "dn_conv2d_forward": (c_int, [_F, c_int, c_int, c_int, c_int, c_int, _F, _F, c_int, c_int,
+                                  c_int, _F, c_int, c_void_p]),
+    "dn_conv2d_backward_data": (c_int, [_F, c_int, c_int, c_int, c_int, _F, c_int, c_int, _F,
+                                        c_int, c_int, _F, c_int, c_void_p]),
+    "dn_conv2d_wgrad_slab_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "dn_conv2d_backward_weight": (c_int, [_F, _F, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                          _F, c_void_p, c_void_p]),
+    "dn_deconv2x2_forward": (c_int, [_F, c_int, c_int, c_int, c_int, _F, _F, c_int, _F, c_int,
+                                     c_int, c_void_p]),
+    "dn_deconv2x2_backward_data": (c_int, [_F, c_int, c_int, c_int, c_int, c_int, _F, c_int, _F,
+                                           _F, c_void_p]),
+    "dn_deconv2x2_wgrad_slab_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "dn_deconv2x2_backward_weight": (c_int, [_F, c_int, _F, c_int, c_int, c_int, c_int, c_int, _F,
+                                             c_void_p, c_void_p]),
+    "dn_maxpool2x2_forward": (c_int, [_F, c_int, c_int, c_int, c_int, _F, c_int, c_int, c_void_p]),
+    "dn_maxpool2x2_backward": (c_int, [_F, c_int, c_int, c_int, c_int, _F, c_int, c_int, c_int, _F,
+                                       c_void_p]),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded library (raises if it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libdenoise_hip.so not found at {LIB_PATH}; build it with "
+                "`python -m image_denoising_amd._build` (hipcc --offload-arch=gfx950)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    buf = ctypes.create_string_buffer(2048)
+    lib().dn_last_error(buf, 2048)
+    return buf.value.decode(errors="replace")
+
+
+class DenoiseHipError(RuntimeError):
+    pass
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        raise DenoiseHipError(f"{what} failed (status {status}): {last_error()}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)
+
+
+def ptr(t: torch.Tensor | None):
+    """device pointer of a contiguous tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise ValueError("tensor must be contiguous")
+    return t.data_ptr()
+
+
+def stream_of(t: torch.Tensor):
+    if t.device.type != "cuda":
+        raise ValueError(f"expected a GPU tensor, got device {t.device}")
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def cfg(in_nc: int, out_nc: int, n_feature: int) -> DnCfg:
+    return DnCfg(in_nc, out_nc, n_feature)

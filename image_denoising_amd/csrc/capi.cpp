@@ -1,0 +1,304 @@
+// extern "C" boundary of libdenoise_hip.so (declared in include/denoise_hip.h).
+// Validates arguments, maps failures to dn_status + a thread-local message, never throws.
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "unet.h"
+
+using namespace dn;
+
+namespace {
+
+dn_status fail(int code, const std::string& msg) {
+  set_error(msg);
+  return code;
+}
+
+dn_status hip_status(hipError_t e, const char* what) {
+  if (e == hipSuccess) return DN_OK;
+  return fail(DN_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define DN_GUARD_BEGIN try {
+#define DN_GUARD_END                                              \
+  }                                                               \
+  catch (const std::exception& ex) { return fail(DN_ERR_ARG, ex.what()); } \
+  catch (...) { return fail(DN_ERR_ARG, "unknown C++ exception"); }
+
+}  // namespace
+
+extern "C" {
+
+const char* dn_version(void) { return "denoise_hip 0.1.0 gfx950"; }
+
+int dn_last_error(char* buf, size_t len) {
+  const std::string& s = g_last_error;
+  if (buf && len) {
+    size_t n = s.size() < len - 1 ? s.size() : len - 1;
+    std::memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return (int)s.size();
+}
+
+dn_status dn_unet_param_count(const dn_unet_cfg* cfg, size_t* count) {
+  DN_GUARD_BEGIN
+  if (!cfg || !count) return fail(DN_ERR_ARG, "null argument");
+  ParamLayout P;
+  std::string err;
+  if (!build_params(*cfg, P, err)) return fail(DN_ERR_ARG, err);
+  *count = (size_t)P.total;
+  return DN_OK;
+  DN_GUARD_END
+}
+
+dn_status dn_unet_param_info(const dn_unet_cfg* cfg, int index, size_t* w_off, size_t* w_count,
+                             size_t* b_count) {
+  DN_GUARD_BEGIN
+  if (!cfg || !w_off || !w_count || !b_count) return fail(DN_ERR_ARG, "null argument");
+  ParamLayout P;
+  std::string err;
+  if (!build_params(*cfg, P, err)) return fail(DN_ERR_ARG, err);
+  if (index < 0 || index >= NL) return fail(DN_ERR_ARG, "layer index out of range");
+  *w_off = (size_t)P.L[index].woff;
+  *w_count = (size_t)P.L[index].wcount;
+  *b_count = (size_t)P.L[index].cout;
+  return DN_OK;
+  DN_GUARD_END
+}
+
+dn_status dn_unet_workspace_size(const dn_unet_cfg* cfg, int N, int H, int W, int with_backward,
+                                 size_t* bytes) {
+  DN_GUARD_BEGIN
+  if (!cfg || !bytes) return fail(DN_ERR_ARG, "null argument");
+  Plan p;
+  std::string err;
+  if (!build_plan(*cfg, N, H, W, with_backward != 0, p, err)) return fail(DN_ERR_ARG, err);
+  *bytes = (size_t)p.total_floats * sizeof(float);
+  return DN_OK;
+  DN_GUARD_END
+}
+
+dn_status dn_unet_forward(const dn_unet_cfg* cfg, const float* params, const float* x, float* y,
+                          int N, int H, int W, void* ws, size_t ws_bytes, void* stream) {
+  DN_GUARD_BEGIN
+  if (!cfg || !params || !x || !y || !ws) return fail(DN_ERR_ARG, "null argument");
+  Plan p;
+  std::string err;
+  // a workspace sized for the backward keeps the same forward offsets
+  if (!build_plan(*cfg, N, H, W, false, p, err)) return fail(DN_ERR_ARG, err);
+  if (ws_bytes < (size_t)p.total_floats * sizeof(float))
+    return fail(DN_ERR_WORKSPACE, "workspace smaller than dn_unet_workspace_size()");
+  return unet_forward(p, params, x, y, static_cast<float*>(ws), (hipStream_t)stream);
+  DN_GUARD_END
+}
+
+dn_status dn_unet_backward(const dn_unet_cfg* cfg, const float* params, const float* dy,
+                           float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
+                           void* stream) {
+  DN_GUARD_BEGIN
+  if (!cfg || !params || !dy || !dparams || !ws) return fail(DN_ERR_ARG, "null argument");
+  Plan p;
+  std::string err;
+  if (!build_plan(*cfg, N, H, W, true, p, err)) return fail(DN_ERR_ARG, err);
+  if (ws_bytes < (size_t)p.total_floats * sizeof(float))
+    return fail(DN_ERR_WORKSPACE,
+                "workspace smaller than dn_unet_workspace_size(with_backward=1)");
+  return unet_backward(p, params, dy, dparams, static_cast<float*>(ws), (hipStream_t)stream);
+  DN_GUARD_END
+}
+
+dn_status dn_n2n_subsample(const float* img, int N, int C, int H, int W, const uint8_t* rd_idx_in,
+                           uint64_t seed, uint64_t offset, uint64_t cell_base, float* sub1,
+                           float* sub2, uint8_t* rd_idx_out, void* stream) {
+  if (!img || !sub1 || !sub2) return fail(DN_ERR_ARG, "null argument");
+  if (N < 0 || C < 1 || H < 0 || W < 0 || (H & 1) || (W & 1))
+    return fail(DN_ERR_ARG, "H and W must be even");
+  if ((long)N * H * W == 0) return DN_OK;
+  return hip_status(launch_subsample(img, N, C, H, W, rd_idx_in, seed, offset, cell_base, sub1,
+                                     sub2, rd_idx_out, (hipStream_t)stream),
+                    "dn_n2n_subsample");
+}
+
+dn_status dn_n2n_masks(const uint8_t* rd_idx, int64_t ncells, uint8_t* mask1, uint8_t* mask2,
+                       void* stream) {
+  if (ncells < 0) return fail(DN_ERR_ARG, "ncells < 0");
+  if (ncells == 0) return DN_OK;
+  if (!rd_idx || !mask1 || !mask2) return fail(DN_ERR_ARG, "null argument");
+  return hip_status(launch_masks(rd_idx, ncells, mask1, mask2, (hipStream_t)stream),
+                    "dn_n2n_masks");
+}
+
+dn_status dn_n2n_subimage_from_mask(const float* img, int N, int C, int H, int W,
+                                    const uint8_t* mask, float* sub, void* stream) {
+  if (N < 0 || C < 1 || (H & 1) || (W & 1)) return fail(DN_ERR_ARG, "H and W must be even");
+  if ((long)N * H * W == 0) return DN_OK;
+  if (!img || !mask || !sub) return fail(DN_ERR_ARG, "null argument");
+  return hip_status(launch_subimage_from_mask(img, N, C, H, W, mask, sub, (hipStream_t)stream),
+                    "dn_n2n_subimage_from_mask");
+}
+
+dn_status dn_add_gauss_noise(const float* clean, int N, int64_t per_image, float std_,
+                             const float* std_per_image, uint64_t seed, uint64_t offset,
+                             uint64_t elem_base, float* noisy, void* stream) {
+  if (N < 0 || per_image < 0) return fail(DN_ERR_ARG, "negative size");
+  if ((long)N * per_image == 0) return DN_OK;
+  if (!clean || !noisy) return fail(DN_ERR_ARG, "null argument");
+  return hip_status(launch_noise(clean, N, per_image, std_, std_per_image, seed, offset, elem_base,
+                                 noisy, (hipStream_t)stream),
+                    "dn_add_gauss_noise");
+}
+
+size_t dn_loss_partials_size(void) { return loss_partials_bytes(); }
+
+dn_status dn_n2n_loss(const float* out, const float* sub2, const float* den, const uint8_t* rd_idx,
+                      int N, int C, int h, int w, float lambda, float* dout, float* loss3,
+                      void* partial_ws, void* stream) {
+  if (!out || !sub2 || !den || !rd_idx || !dout || !loss3 || !partial_ws)
+    return fail(DN_ERR_ARG, "null argument");
+  if (N < 1 || C < 1 || h < 1 || w < 1) return fail(DN_ERR_ARG, "empty loss input");
+  return hip_status(launch_n2n_loss(out, sub2, den, rd_idx, N, C, h, w, lambda, dout, loss3,
+                                    partial_ws, (hipStream_t)stream),
+                    "dn_n2n_loss");
+}
+
+dn_status dn_structure_loss(const float* pred, const float* pred2, const float* target, int N, int C,
+                            int H, int W, float alpha, float beta, float gamma, float* dpred,
+                            float* dpred2, float* loss5, void* partial_ws, void* stream) {
+  if (!pred || !pred2 || !target || !dpred || !dpred2 || !loss5 || !partial_ws)
+    return fail(DN_ERR_ARG, "null argument");
+  if (N < 1 || C < 1 || H < 2 || W < 2) return fail(DN_ERR_ARG, "Structure_loss needs H, W >= 2");
+  return hip_status(launch_structure_loss(pred, pred2, target, N, C, H, W, alpha, beta, gamma,
+                                          dpred, dpred2, loss5, partial_ws, (hipStream_t)stream),
+                    "dn_structure_loss");
+}
+
+dn_status dn_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                       float lr, float beta1, float beta2, float eps, int64_t step,
+                       float grad_scale, void* stream) {
+  if (n < 0 || step < 1) return fail(DN_ERR_ARG, "n >= 0 and step >= 1 required");
+  if (n == 0) return DN_OK;
+  if (!param || !grad || !exp_avg || !exp_avg_sq) return fail(DN_ERR_ARG, "null argument");
+  // scalars exactly as torch/optim/adam.py _single_tensor_adam computes them (python floats)
+  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  const double step_size = (double)lr / bc1;
+  const double bc2s = std::sqrt(bc2);
+  return hip_status(launch_adam(param, grad, exp_avg, exp_avg_sq, n, (float)(1.0 - (double)beta1),
+                                beta2, (float)(1.0 - (double)beta2), (float)step_size,
+                                (float)bc2s, eps, grad_scale, (hipStream_t)stream),
+                    "dn_adam_step");
+}
+
+// ---- op-level entry points ------------------------------------------------------------
+dn_status dn_conv2d_forward(const float* x, int x_stride, int N, int H, int W, int Cin,
+                            const float* w, const float* b, int Cout, int ksize, int act, float* y,
+                            int y_stride, void* stream) {
+  if (!x || !w || !b || !y) return fail(DN_ERR_ARG, "null argument");
+  if (ksize != 1 && ksize != 3) return fail(DN_ERR_ARG, "ksize must be 1 or 3");
+  if (N < 1 || H < 1 || W < 1 || Cin < 1 || x_stride < Cin || y_stride < Cout)
+    return fail(DN_ERR_ARG, "bad shape");
+  if (!fwd_supported(ksize == 3 ? G_C3 : G_C1, Cout))
+    return fail(DN_ERR_ARG, "unsupported Cout for this kernel build");
+  return hip_status(conv_forward(View{const_cast<float*>(x), x_stride, 0}, N, H, W, Cin, w, b, Cout,
+                                 ksize, act, View{y, y_stride, 0}, OUT_NHWC, (hipStream_t)stream),
+                    "dn_conv2d_forward");
+}
+
+dn_status dn_conv2d_backward_data(const float* dz, int N, int H, int W, int Cout, const float* w,
+                                  int Cin, int ksize, const float* mask, int mask_stride,
+                                  int accumulate, float* dx, int dx_stride, void* stream) {
+  if (!dz || !w || !dx) return fail(DN_ERR_ARG, "null argument");
+  if (ksize != 1 && ksize != 3) return fail(DN_ERR_ARG, "ksize must be 1 or 3");
+  if (N < 1 || H < 1 || W < 1 || Cout < 1 || dx_stride < Cin) return fail(DN_ERR_ARG, "bad shape");
+  if (mask && accumulate) return fail(DN_ERR_ARG, "mask and accumulate are exclusive");
+  if (!fwd_supported(ksize == 3 ? G_C3 : G_C1, Cin))
+    return fail(DN_ERR_ARG, "unsupported Cin for this kernel build");
+  const int epi = mask ? EPI_MASK : (accumulate ? EPI_ACCUM : EPI_PLAIN);
+  return hip_status(conv_dgrad(View{const_cast<float*>(dz), Cout, 0}, N, H, W, Cout, w, Cin, Cin,
+                               ksize, epi, View{const_cast<float*>(mask), mask_stride, 0},
+                               View{dx, dx_stride, 0}, (hipStream_t)stream),
+                    "dn_conv2d_backward_data");
+}
+
+size_t dn_conv2d_wgrad_slab_size(int N, int H, int W, int Cin, int Cout, int ksize) {
+  const int mode = ksize == 3 ? W_C3 : W_C1;
+  const int sp = wgrad_splits(mode, N, H, W, Cin, Cout);
+  return sizeof(float) * (size_t)sp * ((size_t)Cout * Cin * ksize * ksize + Cout);
+}
+
+dn_status dn_conv2d_backward_weight(const float* dz, const float* x, int x_stride, int N, int H,
+                                    int W, int Cin, int Cout, int ksize, float* dwb, void* slab,
+                                    void* stream) {
+  if (!dz || !x || !dwb || !slab) return fail(DN_ERR_ARG, "null argument");
+  if (ksize != 1 && ksize != 3) return fail(DN_ERR_ARG, "ksize must be 1 or 3");
+  const int mode = ksize == 3 ? W_C3 : W_C1;
+  if (!wgrad_supported(mode, Cout, Cin)) return fail(DN_ERR_ARG, "unsupported Cout");
+  if (mode == W_C1 && Cin > 96) return fail(DN_ERR_ARG, "1x1 wgrad supports Cin <= 96");
+  const int sp = wgrad_splits(mode, N, H, W, Cin, Cout);
+  return hip_status(wgrad(mode, View{const_cast<float*>(dz), Cout, 0},
+                          View{const_cast<float*>(x), x_stride, 0}, N, H, W, Cout, Cin, dwb,
+                          static_cast<float*>(slab), sp, (hipStream_t)stream),
+                    "dn_conv2d_backward_weight");
+}
+
+dn_status dn_deconv2x2_forward(const float* x, int N, int H, int W, int Cin, const float* w,
+                               const float* b, int Cout, float* y, int y_stride, int y_off,
+                               void* stream) {
+  if (!x || !w || !b || !y) return fail(DN_ERR_ARG, "null argument");
+  if (!fwd_supported(G_C1, Cout)) return fail(DN_ERR_ARG, "unsupported Cout");
+  return hip_status(deconv_forward(View{const_cast<float*>(x), Cin, 0}, N, H, W, Cin, w, b, Cout,
+                                   View{y, y_stride, y_off}, (hipStream_t)stream),
+                    "dn_deconv2x2_forward");
+}
+
+dn_status dn_deconv2x2_backward_data(const float* dy, int dy_stride, int N, int H, int W, int Cout,
+                                     const float* w, int Cin, const float* mask, float* dx,
+                                     void* stream) {
+  if (!dy || !w || !dx) return fail(DN_ERR_ARG, "null argument");
+  if (!fwd_supported(G_DN2, Cin)) return fail(DN_ERR_ARG, "unsupported Cin");
+  return hip_status(deconv_dgrad(View{const_cast<float*>(dy), dy_stride, 0}, N, H, W, Cout, w, Cin,
+                                 View{const_cast<float*>(mask), Cin, 0},
+                                 mask ? EPI_MASK : EPI_PLAIN, View{dx, Cin, 0},
+                                 (hipStream_t)stream),
+                    "dn_deconv2x2_backward_data");
+}
+
+size_t dn_deconv2x2_wgrad_slab_size(int N, int H, int W, int Cin, int Cout) {
+  const int sp = wgrad_splits(W_UP2, N, H, W, Cin, Cout);
+  return sizeof(float) * (size_t)sp * ((size_t)Cout * Cin * 4 + Cout);
+}
+
+dn_status dn_deconv2x2_backward_weight(const float* dy, int dy_stride, const float* x, int N, int H,
+                                       int W, int Cin, int Cout, float* dwb, void* slab,
+                                       void* stream) {
+  if (!dy || !x || !dwb || !slab) return fail(DN_ERR_ARG, "null argument");
+  if (!wgrad_supported(W_UP2, Cout, Cin)) return fail(DN_ERR_ARG, "unsupported Cout");
+  const int sp = wgrad_splits(W_UP2, N, H, W, Cin, Cout);
+  return hip_status(wgrad(W_UP2, View{const_cast<float*>(dy), dy_stride, 0},
+                          View{const_cast<float*>(x), Cin, 0}, N, H, W, Cout, Cin, dwb,
+                          static_cast<float*>(slab), sp, (hipStream_t)stream),
+                    "dn_deconv2x2_backward_weight");
+}
+
+dn_status dn_maxpool2x2_forward(const float* x, int N, int H, int W, int C, float* y, int y_stride,
+                                int y_off, void* stream) {
+  if (!x || !y) return fail(DN_ERR_ARG, "null argument");
+  if ((H & 1) || (W & 1) || (C & 3) || (y_stride & 3) || (y_off & 3))
+    return fail(DN_ERR_ARG, "H, W even and C, y_stride, y_off multiples of 4 required");
+  return hip_status(launch_pool_fwd(x, N, H, W, C, y, y_stride, y_off, (hipStream_t)stream),
+                    "dn_maxpool2x2_forward");
+}
+
+dn_status dn_maxpool2x2_backward(const float* x, int N, int H, int W, int C, const float* dy,
+                                 int dy_stride, int dy_off, int act, float* dx, void* stream) {
+  if (!x || !dy || !dx) return fail(DN_ERR_ARG, "null argument");
+  if ((H & 1) || (W & 1) || (C & 3) || (dy_stride & 3) || (dy_off & 3))
+    return fail(DN_ERR_ARG, "H, W even and C, dy_stride, dy_off multiples of 4 required");
+  return hip_status(launch_pool_bwd(x, N, H, W, C, dy, dy_stride, dy_off, act, dx,
+                                    (hipStream_t)stream),
+                    "dn_maxpool2x2_backward");
+}
+
+}  // extern "C"

@@ -1,0 +1,401 @@
+// Convolution kernels of the N2N U-Net for gfx950 (MI355X).
+//
+// Every arithmetic op of arch_unet.py's UNet that reduces over channels (3x3 conv
+// arch_unet.py:116-181, 1x1 "nin" convs :186-190, ConvTranspose2d(2,2) :57) and its
+// autograd backward is expressed as one of two implicit-GEMM kernels on the fp32 matrix
+// cores (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation, the same
+// 157.3 TFLOP/s peak as the fp32 vector ALUs):
+//
+//   k_fwd   output-stationary: out[p][n] = epi( sum_t sum_k in[gather(p,t)][k] * W[t][k][n] )
+//           -> conv forward, conv data-gradient (flipped/transposed weight view),
+//              deconv forward (1x1 GEMM + scatter epilogue), deconv data-gradient.
+//   k_wgrad weight-gradient: partial dW over a slice of pixels, one slab per split,
+//           then k_reduce sums the slabs in a fixed order (deterministic, no atomics).
+//
+// Data layout: activations NHWC fp32 (channels contiguous), weights in the reference's
+// PyTorch layout read through a strided view (no repacking pass).
+#include "dn_internal.h"
+
+namespace dn {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// smallest x >= v with x % mod == res  (LDS strides chosen for conflict-free ds_read_b32)
+constexpr int cround(int v, int mod, int res) { return v + (((res - v % mod) % mod) + mod) % mod; }
+
+// ------------------------------------------------------------------------------------
+// Forward-style implicit GEMM.
+//   Workgroup = 4 waves; tile = TH x 16 output pixels x NP output channels.
+//   Wave w owns tile rows [w*MT, w*MT+MT); fragment m = one row of 16 pixels (MFMA M),
+//   fragment n = 16 output channels (MFMA N).  K = taps x input channels, staged through
+//   LDS 8 channels at a time: input tile with halo as [channel][pixel], weights as
+//   [tap][channel][n].  MFMA k-lane group g (lane>>4) takes channel 4s+g of the stage.
+// ------------------------------------------------------------------------------------
+template <int GATHER, int NT, int MT>
+struct FwdCfg {
+  static constexpr int TW = 16, TH = 4 * MT, KC = 8;
+  static constexpr int TAPS = GATHER == G_C3 ? 9 : (GATHER == G_DN2 ? 4 : 1);
+  static constexpr int IH = GATHER == G_C3 ? TH + 2 : (GATHER == G_DN2 ? 2 * TH : TH);
+  static constexpr int IW = GATHER == G_C3 ? TW + 2 : (GATHER == G_DN2 ? 2 * TW : TW);
+  // channel stride of the input tile: lanes (i, g) of a 32-lane half hit distinct banks
+  static constexpr int XCS = cround(IH * IW, 32, GATHER == G_DN2 ? 1 : 16);
+  static constexpr int NP = NT * 16;
+  static constexpr int WNS = cround(NP, 32, 16);
+  static constexpr int LX = KC * XCS, LW = TAPS * KC * WNS;
+};
+
+template <int GATHER, int NT, int MT>
+__global__ __launch_bounds__(256) void k_fwd(FwdArgs a) {
+  using C = FwdCfg<GATHER, NT, MT>;
+  __shared__ float lds[C::LX + C::LW];
+  float* lx = lds;
+  float* lw = lds + C::LX;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int tiles_x = (a.OW + C::TW - 1) / C::TW;
+  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
+  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
+  const int n = blockIdx.y;
+  const int iy0 = GATHER == G_C3 ? ty0 - 1 : (GATHER == G_DN2 ? 2 * ty0 : ty0);
+  const int ix0 = GATHER == G_C3 ? tx0 - 1 : (GATHER == G_DN2 ? 2 * tx0 : tx0);
+  const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
+  const long wz = (long)blockIdx.z * a.wv.sZ + a.wv.off;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < NT; ++q) acc[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < a.K; k0 += C::KC) {
+    __syncthreads();
+    // stage the input tile (with halo), channel-major, zero outside the image / past K
+    for (int e = tid; e < C::KC * C::IH * C::IW; e += 256) {
+      const int kk = e % C::KC, pix = e / C::KC;
+      const int iy = pix / C::IW, ix = pix - iy * C::IW;
+      const int gy = iy0 + iy, gx = ix0 + ix;
+      float v = 0.f;
+      if (k0 + kk < a.K && gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt)
+        v = inb[((long)gy * a.IWt + gx) * a.in_stride + k0 + kk];
+      lx[kk * C::XCS + pix] = v;
+    }
+    // stage the weight slab [tap][k][n]
+    for (int e = tid; e < C::TAPS * C::KC * C::NP; e += 256) {
+      const int nn = e % C::NP, r = e / C::NP;
+      const int kk = r % C::KC, t = r / C::KC;
+      const int k = k0 + kk;
+      float v = 0.f;
+      if (k < a.K && nn < a.NOUT) {
+        const int tm = a.wv.flip ? (a.wv.taps - 1 - t) : t;
+        v = a.wv.w[wz + (long)k * a.wv.sK + (long)nn * a.wv.sN + (long)tm * a.wv.sT];
+      }
+      lw[(t * C::KC + kk) * C::WNS + nn] = v;
+    }
+    __syncthreads();
+
+#pragma unroll
+    for (int t = 0; t < C::TAPS; ++t) {
+#pragma unroll
+      for (int s = 0; s < C::KC / 4; ++s) {
+        const int kk = 4 * s + lg;
+        float av[MT], bv[NT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int r = wave * MT + m;
+          int off;
+          if (GATHER == G_C3) off = (r + t / 3) * C::IW + li + t % 3;
+          else if (GATHER == G_DN2) off = (2 * r + t / 2) * C::IW + 2 * li + (t & 1);
+          else off = r * C::IW + li;
+          av[m] = lx[kk * C::XCS + off];
+        }
+#pragma unroll
+        for (int q = 0; q < NT; ++q) bv[q] = lw[(t * C::KC + kk) * C::WNS + q * 16 + li];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int q = 0; q < NT; ++q) acc[m][q] = mfma4(av[m], bv[q], acc[m][q]);
+      }
+    }
+  }
+
+  // epilogue: C/D map of 16x16 MFMA: col (n) = lane&15, row (pixel x) = 4*(lane>>4) + reg
+  const int ab = blockIdx.z;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int gy = ty0 + wave * MT + m;
+    if (gy >= a.OH) continue;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      const int c = q * 16 + li;
+      if (c >= a.NOUT) continue;
+      const float bias = (a.epi == EPI_BIAS || a.epi == EPI_BIAS_ACT) ? a.bias[c] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gx = tx0 + 4 * lg + r;
+        if (gx >= a.OW) continue;
+        float v = acc[m][q][r];
+        long pix = ((long)n * a.OH + gy) * a.OW + gx;
+        if (a.epi == EPI_BIAS) {
+          v = v + bias;
+        } else if (a.epi == EPI_BIAS_ACT) {
+          v = v + bias;
+          v = v > 0.f ? v : v * 0.2f;
+        } else if (a.epi == EPI_MASK) {
+          const float mk = a.mask[pix * a.mask_stride + a.mask_off + c];
+          v = mk > 0.f ? v : v * 0.2f;
+        }
+        long oi;
+        if (a.out_layout == OUT_NHWC) {
+          oi = pix * a.out_stride + a.out_off + c;
+        } else if (a.out_layout == OUT_NCHW) {
+          oi = (((long)n * a.NOUT + c) * a.OH + gy) * a.OW + gx;
+        } else {
+          oi = (((long)n * 2 * a.OH + 2 * gy + (ab >> 1)) * 2 * a.OW + 2 * gx + (ab & 1)) *
+                   a.out_stride + a.out_off + c;
+        }
+        if (a.epi == EPI_ACCUM) v += a.out[oi];
+        a.out[oi] = v;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Weight gradient.  MFMA M = output channels (gradient operand G), N = input channels x
+// taps (input operand X), K = pixels.  One workgroup = all output channels x 16*CIF input
+// channels x all taps, accumulated over a contiguous range of pixel chunks (a "split");
+// it writes its partial dW/db into slab[split].  The slabs are summed by k_reduce.
+// ------------------------------------------------------------------------------------
+template <int MODE, int MF, int NW, int CIF>
+struct WgCfg {
+  static constexpr int TAPS = MODE == W_C3 ? 9 : (MODE == W_UP2 ? 4 : 1);
+  static constexpr int PR = MODE == W_UP2 ? 2 : 4;
+  static constexpr int PC = MODE == W_C3 ? 32 : 16;
+  static constexpr int NPIX = PR * PC;
+  static constexpr int COP = MF * NW * 16;
+  static constexpr int AH = MODE == W_UP2 ? 2 * PR : PR, AW = MODE == W_UP2 ? 2 * PC : PC;
+  static constexpr int ACS = cround(AH * AW, 32, 2);
+  static constexpr int BH = MODE == W_C3 ? PR + 2 : PR, BW = MODE == W_C3 ? PC + 2 : PC;
+  static constexpr int BCS = cround(BH * BW, 32, 2);
+  static constexpr int CIN_T = 16 * CIF;
+  static constexpr int NF = TAPS * CIF;
+  static constexpr int LA = COP * ACS, LB = CIN_T * BCS;
+  static constexpr int NTHR = NW * 64;
+};
+
+template <int MODE, int MF, int NW, int CIF>
+__global__ __launch_bounds__(NW * 64) void k_wgrad(WgradArgs a) {
+  using C = WgCfg<MODE, MF, NW, CIF>;
+  __shared__ float lds[C::LA + C::LB];
+  float* la = lds;
+  float* lb = lds + C::LA;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int ci0 = blockIdx.y * C::CIN_T;
+  const int ux = (a.KW + C::PC - 1) / C::PC, uy = (a.KH + C::PR - 1) / C::PR;
+  const long U = (long)a.N * uy * ux;
+  const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
+  const int GH = MODE == W_UP2 ? 2 * a.KH : a.KH, GW = MODE == W_UP2 ? 2 * a.KW : a.KW;
+  const bool do_bias = blockIdx.y == 0;
+
+  f32x4 acc[MF][C::NF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int f = 0; f < C::NF; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+
+  for (long u = u_beg; u < u_end; ++u) {
+    const int n = (int)(u / ((long)uy * ux));
+    const int rem = (int)(u - (long)n * uy * ux);
+    const int py0 = (rem / ux) * C::PR, px0 = (rem % ux) * C::PC;
+    __syncthreads();
+    {  // stage G: [co][AH*AW]
+      const int ay0 = MODE == W_UP2 ? 2 * py0 : py0, ax0 = MODE == W_UP2 ? 2 * px0 : px0;
+      const float* gb = a.g + (long)n * GH * GW * a.g_stride + a.g_off;
+      for (int e = tid; e < C::COP * C::AH * C::AW; e += C::NTHR) {
+        const int co = e % C::COP, pix = e / C::COP;
+        const int ay = pix / C::AW, ax = pix - ay * C::AW;
+        const int gy = ay0 + ay, gx = ax0 + ax;
+        float v = 0.f;
+        if (co < a.Cout && gy < GH && gx < GW) v = gb[((long)gy * GW + gx) * a.g_stride + co];
+        la[co * C::ACS + pix] = v;
+      }
+    }
+    {  // stage X: [ci][BH*BW] (halo for 3x3)
+      const int by0 = MODE == W_C3 ? py0 - 1 : py0, bx0 = MODE == W_C3 ? px0 - 1 : px0;
+      const float* xb = a.x + (long)n * a.KH * a.KW * a.x_stride + a.x_off;
+      for (int e = tid; e < C::CIN_T * C::BH * C::BW; e += C::NTHR) {
+        const int ci = e % C::CIN_T, pix = e / C::CIN_T;
+        const int by = pix / C::BW, bx = pix - by * C::BW;
+        const int gy = by0 + by, gx = bx0 + bx;
+        float v = 0.f;
+        if (ci0 + ci < a.Cin && gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW)
+          v = xb[((long)gy * a.KW + gx) * a.x_stride + ci0 + ci];
+        lb[ci * C::BCS + pix] = v;
+      }
+    }
+    __syncthreads();
+    if (do_bias && tid < C::COP) {
+      for (int p = 0; p < C::AH * C::AW; ++p) bsum += la[tid * C::ACS + p];
+    }
+#pragma unroll 2
+    for (int ks = 0; ks < C::NPIX / 4; ++ks) {
+      const int pr = (4 * ks) / C::PC;
+      const int pc = (4 * ks) % C::PC + lg;  // this lane's pixel (k = lg)
+      float av[MF];
+      if (MODE != W_UP2) {
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+          av[i] = la[((wave * MF + i) * 16 + li) * C::ACS + pr * C::PC + pc];
+      }
+#pragma unroll
+      for (int f = 0; f < C::NF; ++f) {
+        const int tap = f / CIF, cf = f % CIF;
+        float bv;
+        if (MODE == W_C3)
+          bv = lb[(cf * 16 + li) * C::BCS + (pr + tap / 3) * C::BW + pc + tap % 3];
+        else
+          bv = lb[(cf * 16 + li) * C::BCS + pr * C::BW + pc];
+        if (MODE == W_UP2) {
+#pragma unroll
+          for (int i = 0; i < MF; ++i) {
+            const float at = la[((wave * MF + i) * 16 + li) * C::ACS +
+                                (2 * pr + (tap >> 1)) * C::AW + 2 * pc + (tap & 1)];
+            acc[i][f] = mfma4(at, bv, acc[i][f]);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < MF; ++i) acc[i][f] = mfma4(av[i], bv, acc[i][f]);
+        }
+      }
+    }
+  }
+
+  float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int f = 0; f < C::NF; ++f) {
+      const int tap = f / CIF, cf = f % CIF;
+      const int ci = ci0 + cf * 16 + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = (wave * MF + i) * 16 + 4 * lg + r;
+        if (co < a.Cout && ci < a.Cin) {
+          const long widx = a.wlayout == 0 ? ((long)co * a.Cin + ci) * C::TAPS + tap
+                                           : ((long)ci * a.Cout + co) * C::TAPS + tap;
+          slab[widx] = acc[i][f][r];
+        }
+      }
+    }
+  if (do_bias && tid < a.Cout) slab[(long)a.Cout * a.Cin * C::TAPS + tid] = bsum;
+}
+
+// out[e] = sum_s slab[s][e], fixed order in s (bit-reproducible)
+__global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ slab, long stride,
+                                                int splits, long n, float* __restrict__ out) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  float s = 0.f;
+  for (int i = 0; i < splits; ++i) s += slab[(long)i * stride + e];
+  out[e] = s;
+}
+
+// ------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------
+template <int GATHER, int NT, int MT>
+static hipError_t run_fwd(const FwdArgs& a, hipStream_t s) {
+  using C = FwdCfg<GATHER, NT, MT>;
+  const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
+  dim3 grid(tx * ty, a.N, a.out_layout == OUT_UP2 ? 4 : 1);
+  hipLaunchKernelGGL((k_fwd<GATHER, NT, MT>), grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+bool fwd_supported(int gather, int nout) {
+  const int nt = (nout + 15) / 16;
+  if (gather == G_C3) return nt == 3 || nt == 6 || nt == 9;
+  if (gather == G_C1) return nt == 1 || nt == 3 || nt == 6;
+  if (gather == G_DN2) return nt == 3 || nt == 6;
+  return false;
+}
+
+hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s) {
+  const int nt = (a.NOUT + 15) / 16;
+  if (gather == G_C3) {
+    if (nt == 3) return run_fwd<G_C3, 3, 4>(a, s);
+    if (nt == 6) return run_fwd<G_C3, 6, 4>(a, s);
+    if (nt == 9) return run_fwd<G_C3, 9, 2>(a, s);
+  } else if (gather == G_C1) {
+    if (nt == 1) return run_fwd<G_C1, 1, 4>(a, s);
+    if (nt == 3) return run_fwd<G_C1, 3, 4>(a, s);
+    if (nt == 6) return run_fwd<G_C1, 6, 4>(a, s);
+  } else if (gather == G_DN2) {
+    if (nt == 3) return run_fwd<G_DN2, 3, 4>(a, s);
+    if (nt == 6) return run_fwd<G_DN2, 6, 4>(a, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int MODE, int MF, int NW, int CIF>
+static hipError_t run_wgrad(const WgradArgs& a, int splits, hipStream_t s) {
+  using C = WgCfg<MODE, MF, NW, CIF>;
+  dim3 grid(splits, (a.Cin + C::CIN_T - 1) / C::CIN_T, 1);
+  hipLaunchKernelGGL((k_wgrad<MODE, MF, NW, CIF>), grid, dim3(C::NTHR), 0, s, a);
+  return hipGetLastError();
+}
+
+bool wgrad_supported(int mode, int cout, int cin) {
+  (void)cin;
+  const int cf = (cout + 15) / 16;
+  if (mode == W_C3 || mode == W_UP2) return cf == 3 || cf == 6;
+  if (mode == W_C1) return cf == 1 || cf == 6;
+  return false;
+}
+
+int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
+  (void)Cout;
+  int pr = mode == W_UP2 ? 2 : 4, pc = mode == W_C3 ? 32 : 16;
+  int cin_t = mode == W_C1 ? 96 : 16;
+  long units = (long)N * ((KH + pr - 1) / pr) * ((KW + pc - 1) / pc);
+  long cib = (Cin + cin_t - 1) / cin_t;
+  long want = (2048 + cib - 1) / cib;  // ~2048 workgroups in flight
+  if (want > 256) want = 256;
+  long per = units / want;
+  if (per < 2) want = (units + 1) / 2;  // at least ~2 chunks per split
+  if (want < 1) want = 1;
+  return (int)want;
+}
+
+hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s) {
+  const int cf = (a.Cout + 15) / 16;
+  if (mode == W_C3) {
+    if (cf == 3) return run_wgrad<W_C3, 1, 3, 1>(a, splits, s);
+    if (cf == 6) return run_wgrad<W_C3, 2, 3, 1>(a, splits, s);
+  } else if (mode == W_C1) {
+    if (cf == 1) return run_wgrad<W_C1, 1, 1, 6>(a, splits, s);
+    if (cf == 6) return run_wgrad<W_C1, 2, 3, 6>(a, splits, s);
+  } else if (mode == W_UP2) {
+    if (cf == 3) return run_wgrad<W_UP2, 1, 3, 1>(a, splits, s);
+    if (cf == 6) return run_wgrad<W_UP2, 2, 3, 1>(a, splits, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_reduce(const float* slab, long slab_stride, int splits, long n, float* out,
+                         hipStream_t s) {
+  const long blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(k_reduce, dim3((unsigned)blocks), dim3(256), 0, s, slab, slab_stride, splits,
+                     n, out);
+  return hipGetLastError();
+}
+
+}  // namespace dn

@@ -1,0 +1,102 @@
+// Internal declarations shared by the HIP kernels and the host orchestration.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace dn {
+
+// How an output pixel of the implicit-GEMM kernel gathers its input pixels.
+enum Gather {
+  G_C3 = 0,   // 3x3, stride 1, pad 1: in(y+ky-1, x+kx-1), 9 taps     (conv fwd / conv dgrad)
+  G_C1 = 1,   // 1x1: in(y, x), 1 tap                                  (1x1 conv, deconv fwd)
+  G_DN2 = 2,  // in(2y+a, 2x+b), 4 taps                                (deconv data-grad)
+};
+
+// How the weight-gradient kernel pairs its two operands over the pixel (K) dimension.
+enum WMode {
+  W_C3 = 0,   // dW[co][ci][t] = sum_p G[p][co] * X[p + off(t)][ci]
+  W_C1 = 1,   // dW[co][ci]    = sum_p G[p][co] * X[p][ci]
+  W_UP2 = 2,  // dW[ci][co][t] = sum_p X[p][ci] * G[2p + ab(t)][co]   (deconv)
+};
+
+enum Epi {
+  EPI_BIAS = 0,      // acc + bias
+  EPI_BIAS_ACT = 1,  // leaky_relu(acc + bias, 0.2)
+  EPI_PLAIN = 2,     // acc
+  EPI_MASK = 3,      // acc * (mask > 0 ? 1 : 0.2)   (LeakyReLU backward through the saved output)
+  EPI_ACCUM = 4,     // out += acc
+};
+
+enum OutLayout {
+  OUT_NHWC = 0,  // out[((n*OH+y)*OW+x)*stride + off + c]
+  OUT_NCHW = 1,  // out[((n*NOUT+c)*OH+y)*OW+x]
+  OUT_UP2 = 2,   // deconv scatter: out[((n*2OH+2y+a)*2OW+2x+b)*stride + off + c], ab = blockIdx.z
+};
+
+// Strided view of the weight tensor as B[t][k][n] (t = tap, k = reduction channel, n = output).
+struct WView {
+  const float* w;
+  long off, sK, sN, sT, sZ;  // idx = off + k*sK + n*sN + tap(t)*sT + blockIdx.z*sZ
+  int taps;
+  int flip;                  // tap(t) = flip ? taps-1-t : t
+};
+
+struct FwdArgs {
+  const float* in; int in_stride, in_off; int IHt, IWt;  // NHWC input, spatial dims
+  int N, OH, OW;                                         // output domain (deconv: input res)
+  int K, NOUT;                                           // reduction channels, output channels
+  WView wv;
+  const float* bias;
+  int epi;
+  float* out; int out_stride, out_off; int out_layout;
+  const float* mask; int mask_stride, mask_off;
+};
+
+struct WgradArgs {
+  const float* g; int g_stride, g_off;  // gradient operand (rows = co), NHWC
+  const float* x; int x_stride, x_off;  // input operand (cols = ci), NHWC
+  int N, KH, KW;                        // pixel (K) domain; for W_UP2 g is at 2KH x 2KW
+  int Cout, Cin;
+  float* slab; long slab_stride;        // one [W ; b] image per split
+  int wlayout;                          // 0: [co][ci][t]  1: [ci][co][t]
+};
+
+// ---- launchers (conv.hip) ----
+hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s);
+int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
+hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s);
+hipError_t launch_reduce(const float* slab, long slab_stride, int splits, long n, float* out,
+                         hipStream_t s);
+bool fwd_supported(int gather, int nout);
+bool wgrad_supported(int mode, int cout, int cin);
+
+// ---- elementwise launchers (elementwise.hip) ----
+hipError_t launch_pool_fwd(const float* a, int N, int H, int W, int C, float* out, int os, int oo,
+                           hipStream_t s);
+hipError_t launch_pool_bwd(const float* a, int N, int H, int W, int C, const float* dp, int ds,
+                           int doff, int act, float* da, hipStream_t s);
+hipError_t launch_nchw_to_slice(const float* x, int N, int C, int H, int W, float* dst, int ds,
+                                int doff, hipStream_t s);
+hipError_t launch_subsample(const float* img, int N, int C, int H, int W, const uint8_t* rd_in,
+                            uint64_t seed, uint64_t offset, uint64_t cell_base, float* sub1,
+                            float* sub2, uint8_t* rd_out, hipStream_t s);
+hipError_t launch_masks(const uint8_t* rd, int64_t ncells, uint8_t* m1, uint8_t* m2, hipStream_t s);
+hipError_t launch_subimage_from_mask(const float* img, int N, int C, int H, int W,
+                                     const uint8_t* mask, float* sub, hipStream_t s);
+hipError_t launch_noise(const float* clean, int N, int64_t per_image, float std_,
+                        const float* std_per_image, uint64_t seed, uint64_t offset,
+                        uint64_t elem_base, float* noisy, hipStream_t s);
+size_t loss_partials_bytes();
+hipError_t launch_n2n_loss(const float* out, const float* sub2, const float* den,
+                           const uint8_t* rd, int N, int C, int h, int w, float lambda,
+                           float* dout, float* loss3, void* partials, hipStream_t s);
+hipError_t launch_structure_loss(const float* pred, const float* pred2, const float* tgt, int N,
+                                 int C, int H, int W, float alpha, float beta, float gamma,
+                                 float* dpred, float* dpred2, float* loss5, void* partials,
+                                 hipStream_t s);
+hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float w1,
+                       float b2, float w2, float step_size, float bc2s, float eps, float gscale,
+                       hipStream_t s);
+
+}  // namespace dn

@@ -1,0 +1,422 @@
+// U-Net orchestration for the N2N training path: parameter layout (reference state_dict
+// order), workspace plan (NHWC activation arena, gradient buffers, weight-gradient slabs),
+// and the forward / backward launch sequences.  Mirrors arch_unet.py:100-260 (UNet) and
+// the autograd graph that `loss.backward()` replays for it.
+#include "unet.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+
+namespace dn {
+
+thread_local std::string g_last_error;
+
+void set_error(const std::string& s) { g_last_error = s; }
+
+// ------------------------------------------------------------------------------------
+// parameters: arch_unet.py:115-192 registration order (== state_dict order)
+// ------------------------------------------------------------------------------------
+static const char* kNames[NL] = {
+    "enc_conv0", "enc_conv1", "enc_conv2", "enc_conv3", "enc_conv4", "enc_conv5", "enc_conv6",
+    "up5.deconv", "dec_conv5a", "dec_conv5b", "up4.deconv", "dec_conv4a", "dec_conv4b",
+    "up3.deconv", "dec_conv3a", "dec_conv3b", "up2.deconv", "dec_conv2a", "dec_conv2b",
+    "up1.deconv", "dec_conv1a", "dec_conv1b", "nin_a", "nin_b", "nin_c"};
+
+const char* layer_name(int i) { return (i >= 0 && i < NL) ? kNames[i] : ""; }
+
+bool build_params(const dn_unet_cfg& c, ParamLayout& P, std::string& err) {
+  const int C = c.in_nc, OC = c.out_nc, nf = c.n_feature;
+  if (C < 1 || C > 4 || OC < 1 || OC > 16) {
+    err = "in_nc must be in [1,4] and out_nc in [1,16]";
+    return false;
+  }
+  if (nf != 48) {
+    err = "n_feature must be 48 (kernel tiles are instantiated for the reference width)";
+    return false;
+  }
+  auto conv = [&](int i, int cout, int cin, int k) { P.L[i] = {cout, cin, k, false, 0, 0}; };
+  auto dec = [&](int i, int cin, int cout) { P.L[i] = {cout, cin, 2, true, 0, 0}; };
+  conv(ENC0, nf, C, 3);
+  for (int i = ENC1; i <= ENC6; ++i) conv(i, nf, nf, 3);
+  dec(UP5, nf, nf);
+  conv(D5A, 2 * nf, 2 * nf, 3);
+  conv(D5B, 2 * nf, 2 * nf, 3);
+  dec(UP4, 2 * nf, 2 * nf);
+  conv(D4A, 2 * nf, 3 * nf, 3);
+  conv(D4B, 2 * nf, 2 * nf, 3);
+  dec(UP3, 2 * nf, 2 * nf);
+  conv(D3A, 2 * nf, 3 * nf, 3);
+  conv(D3B, 2 * nf, 2 * nf, 3);
+  dec(UP2, 2 * nf, 2 * nf);
+  conv(D2A, 2 * nf, 3 * nf, 3);
+  conv(D2B, 2 * nf, 2 * nf, 3);
+  dec(UP1, 2 * nf, 2 * nf);
+  conv(D1A, 96, 2 * nf + C, 3);  // arch_unet.py:177 (hard-wired 96)
+  conv(D1B, 96, 96, 3);
+  conv(NINA, 96, 96, 1);
+  conv(NINB, 96, 96, 1);
+  conv(NINC, OC, 96, 1);
+  long off = 0;
+  for (int i = 0; i < NL; ++i) {
+    Layer& L = P.L[i];
+    L.wcount = (long)L.cout * L.cin * L.k * L.k;
+    L.woff = off;
+    off += L.wcount + L.cout;
+  }
+  P.total = off;
+  return true;
+}
+
+// ------------------------------------------------------------------------------------
+// workspace plan (offsets in floats, 256-byte aligned)
+// ------------------------------------------------------------------------------------
+bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, std::string& err) {
+  if (N < 1 || H < 32 || W < 32 || (H % 32) || (W % 32)) {
+    err = "N >= 1 and H, W must be positive multiples of 32 (5 pooling levels)";
+    return false;
+  }
+  if (!build_params(c, p.P, err)) return false;
+  p.N = N; p.H = H; p.W = W;
+  p.C = c.in_nc; p.OC = c.out_nc; p.nf = c.n_feature;
+  const int nf = p.nf;
+  long off = 0;
+  auto px = [&](int lvl) { return (long)N * (H >> lvl) * (W >> lvl); };
+  auto alloc = [&](int lvl, int ch) {
+    long o = off;
+    off += (px(lvl) * ch + 63) / 64 * 64;
+    return o;
+  };
+  p.c1s = 2 * nf + p.C;
+  p.c1 = alloc(0, p.c1s);
+  p.a0 = alloc(0, nf);
+  p.a1 = alloc(0, nf);
+  for (int l = 1; l <= 4; ++l) {  // c2..c5 concat buffers (c5 is [u5 | p4] = 2nf)
+    p.cs[l] = (l == 4) ? 2 * nf : 3 * nf;
+    p.c[l] = alloc(l, p.cs[l]);
+  }
+  for (int l = 1; l <= 4; ++l) p.a[l] = alloc(l, nf);  // a2..a5 live at levels 1..4
+  p.p5 = alloc(5, nf);
+  p.a6 = alloc(5, nf);
+  for (int l = 1; l <= 4; ++l) {
+    p.da[l] = alloc(l, 2 * nf);
+    p.db[l] = alloc(l, 2 * nf);
+  }
+  p.d1a = alloc(0, 96);
+  p.d1b = alloc(0, 96);
+  p.na = alloc(0, 96);
+  p.nb = alloc(0, 96);
+  p.fwd_floats = off;
+  if (bwd) {
+    p.g_nb = alloc(0, 96);
+    p.g_na = alloc(0, 96);
+    p.g_d1b = alloc(0, 96);
+    p.g_d1a = alloc(0, 96);
+    p.g_c1 = alloc(0, 2 * nf);
+    for (int l = 1; l <= 4; ++l) {
+      p.g_c[l] = alloc(l, p.cs[l]);
+      p.g_da[l] = alloc(l, 2 * nf);
+      p.g_db[l] = alloc(l, 2 * nf);
+      p.g_a[l] = alloc(l, nf);
+    }
+    p.g_a6 = alloc(5, nf);
+    p.g_p5 = alloc(5, nf);
+    p.g_a0 = alloc(0, nf);
+    p.g_a1 = alloc(0, nf);
+    // slab: max over layers of splits * (W + b)
+    long slab = 0;
+    for (int i = 0; i < NL; ++i) {
+      const Layer& L = p.P.L[i];
+      int lvl = layer_level(i);
+      int KH = H >> lvl, KW = W >> lvl;
+      int mode = L.deconv ? W_UP2 : (L.k == 3 ? W_C3 : W_C1);
+      if (L.deconv) { KH = H >> (lvl + 1); KW = W >> (lvl + 1); }
+      int sp = wgrad_splits(mode, N, KH, KW, L.cin, L.cout);
+      p.splits[i] = sp;
+      slab = std::max(slab, (long)sp * (L.wcount + L.cout));
+    }
+    p.slab = alloc(0, 0);
+    off = p.slab + (slab + 63) / 64 * 64;
+    p.slab_floats = slab;
+  }
+  p.total_floats = off;
+  p.with_bwd = bwd;
+  return true;
+}
+
+// output level of every layer (deconvs: level of their OUTPUT)
+int layer_level(int i) {
+  switch (i) {
+    case ENC0: case ENC1: return 0;
+    case ENC2: return 1;
+    case ENC3: return 2;
+    case ENC4: return 3;
+    case ENC5: return 4;
+    case ENC6: return 5;
+    case UP5: case D5A: case D5B: return 4;
+    case UP4: case D4A: case D4B: return 3;
+    case UP3: case D3A: case D3B: return 2;
+    case UP2: case D2A: case D2B: return 1;
+    default: return 0;  // UP1, D1A, D1B, NIN*
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// op helpers
+// ------------------------------------------------------------------------------------
+#define DN_TRY(x)                                                         \
+  do {                                                                    \
+    hipError_t e_ = (x);                                                  \
+    if (e_ != hipSuccess) {                                               \
+      set_error(std::string("HIP error in ") + #x + ": " + hipGetErrorString(e_)); \
+      return DN_ERR_HIP;                                                  \
+    }                                                                     \
+  } while (0)
+
+hipError_t conv_forward(const View& in, int N, int H, int W, int K, const float* w,
+                        const float* b, int cout, int ksize, int act, const View& out,
+                        int out_layout, hipStream_t s) {
+  FwdArgs a{};
+  a.in = in.p; a.in_stride = in.stride; a.in_off = in.off; a.IHt = H; a.IWt = W;
+  a.N = N; a.OH = H; a.OW = W; a.K = K; a.NOUT = cout;
+  if (ksize == 3) a.wv = WView{w, 0, 9, (long)K * 9, 1, 0, 9, 0};
+  else a.wv = WView{w, 0, 1, (long)K, 0, 0, 1, 0};
+  a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
+  a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = out_layout;
+  return launch_fwd(ksize == 3 ? G_C3 : G_C1, a, s);
+}
+
+// dx (channels [0, nout)) from dz [N,H,W,cout]; weight [cout][cin_total][k][k]
+hipError_t conv_dgrad(const View& dz, int N, int H, int W, int cout, const float* w, int cin_total,
+                      int nout, int ksize, int epi, const View& mask, const View& dx,
+                      hipStream_t s) {
+  FwdArgs a{};
+  a.in = dz.p; a.in_stride = dz.stride; a.in_off = dz.off; a.IHt = H; a.IWt = W;
+  a.N = N; a.OH = H; a.OW = W; a.K = cout; a.NOUT = nout;
+  if (ksize == 3) a.wv = WView{w, 0, (long)cin_total * 9, 9, 1, 0, 9, 1};
+  else a.wv = WView{w, 0, (long)cin_total, 1, 0, 0, 1, 0};
+  a.bias = nullptr; a.epi = epi;
+  a.out = dx.p; a.out_stride = dx.stride; a.out_off = dx.off; a.out_layout = OUT_NHWC;
+  a.mask = mask.p; a.mask_stride = mask.stride; a.mask_off = mask.off;
+  return launch_fwd(ksize == 3 ? G_C3 : G_C1, a, s);
+}
+
+// ConvTranspose2d(cin, cout, 2, 2): x [N,h,w,cin] -> out at (2y+a, 2x+b)
+hipError_t deconv_forward(const View& x, int N, int h, int w, int cin, const float* wt,
+                          const float* b, int cout, const View& out, hipStream_t s) {
+  FwdArgs a{};
+  a.in = x.p; a.in_stride = x.stride; a.in_off = x.off; a.IHt = h; a.IWt = w;
+  a.N = N; a.OH = h; a.OW = w; a.K = cin; a.NOUT = cout;
+  a.wv = WView{wt, 0, (long)cout * 4, 4, 0, 1, 1, 0};
+  a.bias = b; a.epi = EPI_BIAS;
+  a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = OUT_UP2;
+  return launch_fwd(G_C1, a, s);
+}
+
+// dx [N,h,w,cin] = sum_{ab,co} dy[2y+a][2x+b][co] * W[ci][co][ab]  (* leaky'(mask))
+hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const float* wt, int cin,
+                        const View& mask, int epi, const View& dx, hipStream_t s) {
+  FwdArgs a{};
+  a.in = dy.p; a.in_stride = dy.stride; a.in_off = dy.off; a.IHt = 2 * h; a.IWt = 2 * w;
+  a.N = N; a.OH = h; a.OW = w; a.K = cout; a.NOUT = cin;
+  a.wv = WView{wt, 0, 4, (long)cout * 4, 1, 0, 4, 0};
+  a.bias = nullptr; a.epi = epi;
+  a.out = dx.p; a.out_stride = dx.stride; a.out_off = dx.off; a.out_layout = OUT_NHWC;
+  a.mask = mask.p; a.mask_stride = mask.stride; a.mask_off = mask.off;
+  return launch_fwd(G_DN2, a, s);
+}
+
+hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, int cout, int cin,
+                 float* dwb, float* slab, int splits, hipStream_t s) {
+  WgradArgs a{};
+  a.g = g.p; a.g_stride = g.stride; a.g_off = g.off;
+  a.x = x.p; a.x_stride = x.stride; a.x_off = x.off;
+  a.N = N; a.KH = KH; a.KW = KW; a.Cout = cout; a.Cin = cin;
+  const int taps = mode == W_C3 ? 9 : (mode == W_UP2 ? 4 : 1);
+  const long n = (long)cout * cin * taps + cout;
+  a.slab = slab; a.slab_stride = n;
+  a.wlayout = mode == W_UP2 ? 1 : 0;
+  hipError_t e = launch_wgrad(mode, a, splits, s);
+  if (e != hipSuccess) return e;
+  return launch_reduce(slab, n, splits, n, dwb, s);
+}
+
+// ------------------------------------------------------------------------------------
+// forward: arch_unet.py:194-260 (non-blind-spot branch)
+// ------------------------------------------------------------------------------------
+dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
+                       hipStream_t s) {
+  const int N = p.N, nf = p.nf, C = p.C;
+  auto H = [&](int l) { return p.H >> l; };
+  auto Wd = [&](int l) { return p.W >> l; };
+  auto Wt = [&](int i) { return prm + p.P.L[i].woff; };
+  auto Bs = [&](int i) { return prm + p.P.L[i].woff + p.P.L[i].wcount; };
+  auto V = [&](long off, int stride, int coff = 0) { return View{ws + off, stride, coff}; };
+
+  // pool0 = x: stored as channels [2nf, 2nf+C) of the up1 concat buffer
+  DN_TRY(launch_nchw_to_slice(x, N, C, p.H, p.W, ws + p.c1, p.c1s, 2 * nf, s));
+  DN_TRY(conv_forward(V(p.c1, p.c1s, 2 * nf), N, H(0), Wd(0), C, Wt(ENC0), Bs(ENC0), nf, 3, 1,
+                      V(p.a0, nf), OUT_NHWC, s));
+  DN_TRY(conv_forward(V(p.a0, nf), N, H(0), Wd(0), nf, Wt(ENC1), Bs(ENC1), nf, 3, 1, V(p.a1, nf),
+                      OUT_NHWC, s));
+  // pool1 -> skip slice of c2
+  DN_TRY(launch_pool_fwd(ws + p.a1, N, H(0), Wd(0), nf, ws + p.c[1], p.cs[1], 2 * nf, s));
+  // enc_conv2..5 + pool2..5 (pool_k -> skip slice of c_{k+1}; pool5 -> p5)
+  for (int l = 1; l <= 4; ++l) {
+    const int li = ENC2 + (l - 1);
+    const int skip_off = (l == 4) ? nf : 2 * nf;  // where p_l lives inside c_l
+    (void)skip_off;
+    const View in = (l == 4) ? V(p.c[4], p.cs[4], nf) : V(p.c[l], p.cs[l], 2 * nf);
+    DN_TRY(conv_forward(in, N, H(l), Wd(l), nf, Wt(li), Bs(li), nf, 3, 1, V(p.a[l], nf), OUT_NHWC,
+                        s));
+    if (l < 4) {
+      const int tgt_off = (l + 1 == 4) ? nf : 2 * nf;
+      DN_TRY(launch_pool_fwd(ws + p.a[l], N, H(l), Wd(l), nf, ws + p.c[l + 1], p.cs[l + 1],
+                             tgt_off, s));
+    } else {
+      DN_TRY(launch_pool_fwd(ws + p.a[4], N, H(4), Wd(4), nf, ws + p.p5, nf, 0, s));
+    }
+  }
+  DN_TRY(conv_forward(V(p.p5, nf), N, H(5), Wd(5), nf, Wt(ENC6), Bs(ENC6), nf, 3, 1, V(p.a6, nf),
+                      OUT_NHWC, s));
+  // decoder: up5 (a6 -> c5[0:nf]); dec5a/b at level 4
+  DN_TRY(deconv_forward(V(p.a6, nf), N, H(5), Wd(5), nf, Wt(UP5), Bs(UP5), nf, V(p.c[4], p.cs[4], 0),
+                        s));
+  const int up_idx[5] = {0, UP2, UP3, UP4, UP5};
+  const int da_idx[5] = {0, D2A, D3A, D4A, D5A};
+  for (int l = 4; l >= 1; --l) {
+    if (l < 4) {  // up_{l+1}: d_{l+1}b -> c_l[0:2nf]
+      DN_TRY(deconv_forward(V(p.db[l + 1], 2 * nf), N, H(l + 1), Wd(l + 1), 2 * nf,
+                            Wt(up_idx[l + 1]), Bs(up_idx[l + 1]), 2 * nf, V(p.c[l], p.cs[l], 0),
+                            s));
+    }
+    const int ia = da_idx[l], ib = da_idx[l] + 1;
+    DN_TRY(conv_forward(V(p.c[l], p.cs[l]), N, H(l), Wd(l), p.cs[l], Wt(ia), Bs(ia), 2 * nf, 3, 1,
+                        V(p.da[l], 2 * nf), OUT_NHWC, s));
+    DN_TRY(conv_forward(V(p.da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ib), Bs(ib), 2 * nf, 3, 1,
+                        V(p.db[l], 2 * nf), OUT_NHWC, s));
+  }
+  // up1: d2b -> c1[0:2nf]
+  DN_TRY(deconv_forward(V(p.db[1], 2 * nf), N, H(1), Wd(1), 2 * nf, Wt(UP1), Bs(UP1), 2 * nf,
+                        V(p.c1, p.c1s, 0), s));
+  DN_TRY(conv_forward(V(p.c1, p.c1s), N, H(0), Wd(0), p.c1s, Wt(D1A), Bs(D1A), 96, 3, 1,
+                      V(p.d1a, 96), OUT_NHWC, s));
+  DN_TRY(conv_forward(V(p.d1a, 96), N, H(0), Wd(0), 96, Wt(D1B), Bs(D1B), 96, 3, 1, V(p.d1b, 96),
+                      OUT_NHWC, s));
+  DN_TRY(conv_forward(V(p.d1b, 96), N, H(0), Wd(0), 96, Wt(NINA), Bs(NINA), 96, 1, 1, V(p.na, 96),
+                      OUT_NHWC, s));
+  DN_TRY(conv_forward(V(p.na, 96), N, H(0), Wd(0), 96, Wt(NINB), Bs(NINB), 96, 1, 1, V(p.nb, 96),
+                      OUT_NHWC, s));
+  DN_TRY(conv_forward(V(p.nb, 96), N, H(0), Wd(0), 96, Wt(NINC), Bs(NINC), p.OC, 1, 0,
+                      View{y, 0, 0}, OUT_NCHW, s));
+  return DN_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// backward: the autograd graph of the forward above, in reverse.  Data gradients fuse
+// LeakyReLU' into their epilogue (mask = the layer input, which is the previous layer's
+// post-activation output); skip gradients are accumulated into the concat-gradient buffers.
+// ------------------------------------------------------------------------------------
+dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* ws,
+                        hipStream_t s) {
+  const int N = p.N, nf = p.nf, C = p.C;
+  auto H = [&](int l) { return p.H >> l; };
+  auto Wd = [&](int l) { return p.W >> l; };
+  auto Wt = [&](int i) { return prm + p.P.L[i].woff; };
+  auto G = [&](int i) { return dprm + p.P.L[i].woff; };
+  auto V = [&](long off, int stride, int coff = 0) { return View{ws + off, stride, coff}; };
+  float* slab = ws + p.slab;
+  const View none{nullptr, 0, 0};
+  const int OC = p.OC;
+
+  // dy arrives NCHW [N, OC, H, W]; for OC == 1 that equals NHWC.  For OC > 1 transpose
+  // into g_c1's storage first (free at this point).
+  View dyv{const_cast<float*>(dy), OC, 0};
+  if (OC > 1) {
+    DN_TRY(launch_nchw_to_slice(dy, N, OC, p.H, p.W, ws + p.g_c1, OC, 0, s));
+    dyv = V(p.g_c1, OC);
+  }
+  // nin_c (1x1, no act): wgrad + dgrad (-> g_nb, masked by nb)
+  DN_TRY(wgrad(W_C1, dyv, V(p.nb, 96), N, H(0), Wd(0), OC, 96, G(NINC), slab, p.splits[NINC], s));
+  DN_TRY(conv_dgrad(dyv, N, H(0), Wd(0), OC, Wt(NINC), 96, 96, 1, EPI_MASK, V(p.nb, 96),
+                    V(p.g_nb, 96), s));
+  DN_TRY(wgrad(W_C1, V(p.g_nb, 96), V(p.na, 96), N, H(0), Wd(0), 96, 96, G(NINB), slab,
+               p.splits[NINB], s));
+  DN_TRY(conv_dgrad(V(p.g_nb, 96), N, H(0), Wd(0), 96, Wt(NINB), 96, 96, 1, EPI_MASK, V(p.na, 96),
+                    V(p.g_na, 96), s));
+  DN_TRY(wgrad(W_C1, V(p.g_na, 96), V(p.d1b, 96), N, H(0), Wd(0), 96, 96, G(NINA), slab,
+               p.splits[NINA], s));
+  DN_TRY(conv_dgrad(V(p.g_na, 96), N, H(0), Wd(0), 96, Wt(NINA), 96, 96, 1, EPI_MASK,
+                    V(p.d1b, 96), V(p.g_d1b, 96), s));
+  DN_TRY(wgrad(W_C3, V(p.g_d1b, 96), V(p.d1a, 96), N, H(0), Wd(0), 96, 96, G(D1B), slab,
+               p.splits[D1B], s));
+  DN_TRY(conv_dgrad(V(p.g_d1b, 96), N, H(0), Wd(0), 96, Wt(D1B), 96, 96, 3, EPI_MASK,
+                    V(p.d1a, 96), V(p.g_d1a, 96), s));
+  DN_TRY(wgrad(W_C3, V(p.g_d1a, 96), V(p.c1, p.c1s), N, H(0), Wd(0), 96, p.c1s, G(D1A), slab,
+               p.splits[D1A], s));
+  // only the up1 part of the concat needs a gradient (pool0 is the network input)
+  DN_TRY(conv_dgrad(V(p.g_d1a, 96), N, H(0), Wd(0), 96, Wt(D1A), p.c1s, 2 * nf, 3, EPI_PLAIN, none,
+                    V(p.g_c1, 2 * nf), s));
+
+  // decoder levels 1..4: up_{l}(d_{l+1}b ...) ; here "dU" for level l-1's deconv
+  const int up_idx[6] = {UP1, UP2, UP3, UP4, UP5, 0};
+  const int da_idx[5] = {0, D2A, D3A, D4A, D5A};
+  View dU = V(p.g_c1, 2 * nf);  // gradient of up1's output
+  for (int l = 1; l <= 4; ++l) {
+    const int iu = up_idx[l - 1];  // deconv producing level l-1 from level l
+    // deconv wgrad: x = d_l b (level l), dU at level l-1
+    DN_TRY(wgrad(W_UP2, dU, V(p.db[l], 2 * nf), N, H(l), Wd(l), 2 * nf, 2 * nf, G(iu), slab,
+                 p.splits[iu], s));
+    DN_TRY(deconv_dgrad(dU, N, H(l), Wd(l), 2 * nf, Wt(iu), 2 * nf, V(p.db[l], 2 * nf), EPI_MASK,
+                        V(p.g_db[l], 2 * nf), s));
+    const int ia = da_idx[l], ib = ia + 1;
+    DN_TRY(wgrad(W_C3, V(p.g_db[l], 2 * nf), V(p.da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, 2 * nf,
+                 G(ib), slab, p.splits[ib], s));
+    DN_TRY(conv_dgrad(V(p.g_db[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ib), 2 * nf, 2 * nf, 3,
+                      EPI_MASK, V(p.da[l], 2 * nf), V(p.g_da[l], 2 * nf), s));
+    DN_TRY(wgrad(W_C3, V(p.g_da[l], 2 * nf), V(p.c[l], p.cs[l]), N, H(l), Wd(l), 2 * nf, p.cs[l],
+                 G(ia), slab, p.splits[ia], s));
+    DN_TRY(conv_dgrad(V(p.g_da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ia), p.cs[l], p.cs[l], 3,
+                      EPI_PLAIN, none, V(p.g_c[l], p.cs[l]), s));
+    dU = V(p.g_c[l], p.cs[l], 0);  // [u_{l+1} grad | skip grad]
+  }
+  // up5: x = a6 (level 5), dU = g_c5[0:nf]
+  DN_TRY(wgrad(W_UP2, V(p.g_c[4], p.cs[4], 0), V(p.a6, nf), N, H(5), Wd(5), nf, nf, G(UP5), slab,
+               p.splits[UP5], s));
+  DN_TRY(deconv_dgrad(V(p.g_c[4], p.cs[4], 0), N, H(5), Wd(5), nf, Wt(UP5), nf, V(p.a6, nf),
+                      EPI_MASK, V(p.g_a6, nf), s));
+  // enc_conv6 (input p5, level 5)
+  DN_TRY(wgrad(W_C3, V(p.g_a6, nf), V(p.p5, nf), N, H(5), Wd(5), nf, nf, G(ENC6), slab,
+               p.splits[ENC6], s));
+  DN_TRY(conv_dgrad(V(p.g_a6, nf), N, H(5), Wd(5), nf, Wt(ENC6), nf, nf, 3, EPI_PLAIN, none,
+                    V(p.g_p5, nf), s));
+  // pool5 backward -> g_a5 (level 4)
+  DN_TRY(launch_pool_bwd(ws + p.a[4], N, H(4), Wd(4), nf, ws + p.g_p5, nf, 0, 1, ws + p.g_a[4], s));
+  // enc_conv5..2: input p_{l} = skip slice of c_l; gradient accumulates into g_c_l's skip slice
+  for (int l = 4; l >= 1; --l) {
+    const int li = ENC2 + (l - 1);
+    const int skip = (l == 4) ? nf : 2 * nf;
+    DN_TRY(wgrad(W_C3, V(p.g_a[l], nf), V(p.c[l], p.cs[l], skip), N, H(l), Wd(l), nf, nf, G(li),
+                 slab, p.splits[li], s));
+    DN_TRY(conv_dgrad(V(p.g_a[l], nf), N, H(l), Wd(l), nf, Wt(li), nf, nf, 3, EPI_ACCUM, none,
+                      V(p.g_c[l], p.cs[l], skip), s));
+    // pool_l backward: d p_l (skip slice) -> gradient of the level l-1 activation
+    if (l > 1) {
+      DN_TRY(launch_pool_bwd(ws + p.a[l - 1], N, H(l - 1), Wd(l - 1), nf, ws + p.g_c[l], p.cs[l],
+                             skip, 1, ws + p.g_a[l - 1], s));
+    } else {
+      DN_TRY(launch_pool_bwd(ws + p.a1, N, H(0), Wd(0), nf, ws + p.g_c[1], p.cs[1], skip, 1,
+                             ws + p.g_a1, s));
+    }
+  }
+  // enc_conv1 (input a0), enc_conv0 (input x = c1 slice; no data gradient needed)
+  DN_TRY(wgrad(W_C3, V(p.g_a1, nf), V(p.a0, nf), N, H(0), Wd(0), nf, nf, G(ENC1), slab,
+               p.splits[ENC1], s));
+  DN_TRY(conv_dgrad(V(p.g_a1, nf), N, H(0), Wd(0), nf, Wt(ENC1), nf, nf, 3, EPI_MASK, V(p.a0, nf),
+                    V(p.g_a0, nf), s));
+  DN_TRY(wgrad(W_C3, V(p.g_a0, nf), V(p.c1, p.c1s, 2 * nf), N, H(0), Wd(0), nf, C, G(ENC0), slab,
+               p.splits[ENC0], s));
+  return DN_OK;
+}
+
+}  // namespace dn

@@ -1,0 +1,80 @@
+// Host-side U-Net plan and orchestration (internal).
+#pragma once
+#include <string>
+
+#include "../../include/denoise_hip.h"
+#include "dn_internal.h"
+
+namespace dn {
+
+enum LayerIdx {
+  ENC0, ENC1, ENC2, ENC3, ENC4, ENC5, ENC6,
+  UP5, D5A, D5B, UP4, D4A, D4B, UP3, D3A, D3B, UP2, D2A, D2B, UP1, D1A, D1B,
+  NINA, NINB, NINC, NL
+};
+
+struct Layer {
+  int cout, cin, k;
+  bool deconv;   // ConvTranspose2d: weight [cin][cout][2][2]
+  long woff;     // float offset of the weight in the flat buffer (bias follows)
+  long wcount;
+};
+
+struct ParamLayout {
+  Layer L[NL];
+  long total;
+};
+
+struct View {
+  float* p;
+  int stride;
+  int off;
+};
+
+struct Plan {
+  ParamLayout P;
+  int N, H, W, C, OC, nf;
+  bool with_bwd;
+  // forward activations (NHWC, offsets in floats)
+  int c1s;
+  long c1, a0, a1;
+  long c[5]; int cs[5];         // concat buffers at levels 1..4
+  long a[5];                    // a2..a5 at levels 1..4
+  long p5, a6;
+  long da[5], db[5];            // decoder conv outputs at levels 1..4
+  long d1a, d1b, na, nb;
+  long fwd_floats;
+  // gradients
+  long g_nb, g_na, g_d1b, g_d1a, g_c1;
+  long g_c[5], g_da[5], g_db[5], g_a[5];
+  long g_a6, g_p5, g_a0, g_a1;
+  long slab, slab_floats;
+  int splits[NL];
+  long total_floats;
+};
+
+void set_error(const std::string& s);
+extern thread_local std::string g_last_error;
+const char* layer_name(int i);
+int layer_level(int i);
+bool build_params(const dn_unet_cfg& c, ParamLayout& P, std::string& err);
+bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, std::string& err);
+dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
+                       hipStream_t s);
+dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* ws,
+                        hipStream_t s);
+
+hipError_t conv_forward(const View& in, int N, int H, int W, int K, const float* w,
+                        const float* b, int cout, int ksize, int act, const View& out,
+                        int out_layout, hipStream_t s);
+hipError_t conv_dgrad(const View& dz, int N, int H, int W, int cout, const float* w, int cin_total,
+                      int nout, int ksize, int epi, const View& mask, const View& dx,
+                      hipStream_t s);
+hipError_t deconv_forward(const View& x, int N, int h, int w, int cin, const float* wt,
+                          const float* b, int cout, const View& out, hipStream_t s);
+hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const float* wt, int cin,
+                        const View& mask, int epi, const View& dx, hipStream_t s);
+hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, int cout, int cin,
+                 float* dwb, float* slab, int splits, hipStream_t s);
+
+}  // namespace dn

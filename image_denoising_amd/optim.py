@@ -1,0 +1,61 @@
+"""Adam over the flat parameter buffer + the reference's MultiStepLR schedule.
+
+train.py:332-340: optim.Adam(network.parameters(), lr=opt.lr) and
+MultiStepLR(milestones=[int(20r)-1, int(40r)-1, int(60r)-1, int(80r)-1], gamma=opt.gamma),
+r = n_epoch/100, stepped once per epoch (train.py:375).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+class FlatAdam:
+    """torch.optim.Adam (amsgrad=False, weight_decay=0) as ONE fused HIP kernel over a flat
+    fp32 buffer; state tensors are flat too.  `grad_scale` folds the 1/world_size of a
+    data-parallel all-reduce(sum) into the same pass."""
+
+    def __init__(self, params: torch.Tensor, lr: float = 3e-4, betas=(0.9, 0.999),
+                 eps: float = 1e-8):
+        if params.dtype != torch.float32 or not params.is_contiguous():
+            raise ValueError("FlatAdam needs a contiguous fp32 buffer")
+        self.params = params
+        self.lr = lr
+        self.betas = betas
+        self.eps = eps
+        self.exp_avg = torch.zeros_like(params)
+        self.exp_avg_sq = torch.zeros_like(params)
+        self.step_count = 0
+
+    def step(self, grad: torch.Tensor, grad_scale: float = 1.0) -> None:
+        if grad.shape != self.params.shape:
+            raise ValueError("grad and params differ in shape")
+        self.step_count += 1
+        b1, b2 = self.betas
+        _lib.call("dn_adam_step", _lib.ptr(self.params), _lib.ptr(grad.contiguous()),
+                  _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq), self.params.numel(),
+                  float(self.lr), float(b1), float(b2), float(self.eps), self.step_count,
+                  float(grad_scale), _lib.stream_of(self.params))
+
+    def state_dict(self):
+        return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
+                "lr": self.lr, "betas": self.betas, "eps": self.eps}
+
+    def load_state_dict(self, sd):
+        self.step_count = int(sd["step"])
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        self.lr, self.betas, self.eps = sd["lr"], tuple(sd["betas"]), sd["eps"]
+
+
+def reference_milestones(n_epoch: int):
+    ratio = n_epoch / 100
+    return [int(20 * ratio) - 1, int(40 * ratio) - 1, int(60 * ratio) - 1, int(80 * ratio) - 1]
+
+
+def lr_at_epoch(epoch: int, base_lr: float, n_epoch: int, gamma: float = 0.5) -> float:
+    """lr in effect during 1-based `epoch` (MultiStepLR.last_epoch == epoch-1)."""
+    last = epoch - 1
+    k = sum(1 for m in reference_milestones(n_epoch) if m <= last)
+    return base_lr * gamma ** k

@@ -1,0 +1,104 @@
+"""The N2N training step (training_script.md:128-155 with train.py's sub-sampler), fused on
+the HIP path with no host synchronisation:
+
+    noisy  = clean + sigma*N(0,1)                     dn_add_gauss_noise   (train.py:84-94)
+    sub1, sub2, rd = neighbour sub-sample(noisy)      dn_n2n_subsample     (train.py:141-190)
+    den    = UNet(noisy)            [no grad]         dn_unet_forward      (arch_unet.py:194)
+    out    = UNet(sub1)             [saved]           dn_unet_forward
+    loss, dout = N2N loss(out, sub2, den[rd])         dn_n2n_loss          (training_script.md:148-153)
+    dW     = backward(dout)                           dn_unet_backward
+    [data parallel: one RCCL all-reduce(sum) of the flat dW]
+    Adam(W, dW / world)                               dn_adam_step         (train.py:332, :368)
+
+Data parallelism: one process per GPU; rank r owns patches [r*B, (r+1)*B) of the global batch.
+The Philox streams are keyed on GLOBAL element/cell indices and the step number, so the
+noise and the mask pair of a patch do not depend on the world size.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .arch_unet import UNet
+from .n2n import n2n_loss, n2n_subsample
+from .optim import FlatAdam, lr_at_epoch
+
+
+class N2NTrainer:
+    def __init__(self, net: UNet, lr: float = 3e-4, n_epoch: int = 100,
+                 increase_ratio: float = 2.0, gamma: float = 0.5, noise_std: float = 25.0 / 255.0,
+                 seed: int = 0, distributed: bool | None = None):
+        self.net = net
+        self.base_lr = lr
+        self.n_epoch = n_epoch
+        self.increase_ratio = increase_ratio
+        self.gamma = gamma
+        self.noise_std = noise_std
+        self.seed = seed
+        self.distributed = dist.is_available() and dist.is_initialized() if distributed is None \
+            else distributed
+        self.world = dist.get_world_size() if self.distributed else 1
+        self.rank = dist.get_rank() if self.distributed else 0
+        if self.distributed:  # identical replicas: broadcast rank 0's initial weights
+            dist.broadcast(net.flat_params, src=0)
+        self.opt = FlatAdam(net.flat_params, lr=lr)
+        self.grad = torch.zeros_like(net.flat_params)
+        self.global_step = 0
+        self._bufs = {}
+
+    def lambda_for(self, epoch: int) -> float:
+        # training_script.md:148 Lambda = epoch / n_epoch * ratio
+        return epoch / self.n_epoch * self.increase_ratio
+
+    def _buffers(self, N, C, H, W, device):
+        key = (N, C, H, W, device)
+        b = self._bufs.get(key)
+        if b is None:
+            h, w = H // 2, W // 2
+            f = dict(dtype=torch.float32, device=device)
+            b = dict(
+                noisy=torch.empty((N, C, H, W), **f),
+                den=torch.empty((N, self.net.out_nc, H, W), **f),
+                out=torch.empty((N, self.net.out_nc, h, w), **f),
+                ws_den=self.net._workspace(N, H, W, with_backward=False, fresh=True),
+                ws_grad=self.net._workspace(N, h, w, with_backward=True, fresh=True),
+            )
+            self._bufs = {key: b}
+        return b
+
+    def train_step(self, clean: torch.Tensor, epoch: int = 1, rd_idx: torch.Tensor | None = None,
+                   noisy: torch.Tensor | None = None) -> torch.Tensor:
+        """One N2N step on this rank's local batch. Returns loss3 = [loss1, loss2, loss_all]
+        (device tensor; read it only when needed — reading syncs the host)."""
+        clean = clean.contiguous()
+        N, C, H, W = clean.shape
+        if C != self.net.in_nc or self.net.in_nc != self.net.out_nc:
+            raise ValueError("N2N needs in_nc == out_nc == input channels")
+        b = self._buffers(N, C, H, W, clean.device)
+        stream = _lib.stream_of(clean)
+        step = self.global_step
+        if noisy is None:
+            noisy = b["noisy"]
+            per = C * H * W
+            _lib.call("dn_add_gauss_noise", _lib.ptr(clean), N, per, float(self.noise_std), None,
+                      self.seed, 2 * step, self.rank * N * per, _lib.ptr(noisy), stream)
+        else:
+            noisy = noisy.contiguous()
+        cells = N * (H // 2) * (W // 2)
+        sub1, sub2, rd = n2n_subsample(noisy, rd_idx, seed=self.seed + 1, offset=2 * step + 1,
+                                       cell_base=self.rank * cells)
+        # no-grad full-resolution pass (training_script.md:141-142)
+        self.net._run_forward(noisy, b["den"], b["ws_den"])
+        # gradient pass at half resolution (training_script.md:146)
+        self.net._run_forward(sub1, b["out"], b["ws_grad"])
+        loss3, dout = n2n_loss(b["out"], sub2, b["den"], rd, self.lambda_for(epoch))
+        self.net._run_backward(dout, self.grad, b["ws_grad"], N, H // 2, W // 2)
+        scale = 1.0
+        if self.distributed and self.world > 1:
+            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)  # RCCL over xGMI, one per step
+            scale = 1.0 / self.world
+        self.opt.lr = lr_at_epoch(epoch, self.base_lr, self.n_epoch, self.gamma)
+        self.opt.step(self.grad, grad_scale=scale)
+        self.global_step += 1
+        return loss3

@@ -1,0 +1,168 @@
+/*
+ * denoise_hip.h — C-ABI of libdenoise_hip.so, the MI355X (gfx950) Neighbor2Neighbor
+ * U-Net training path.
+ *
+ * The reference (lmh9507/image_denoising) is pure Python/PyTorch and has no FFI; its
+ * "interface" is a set of Python callables.  Every entry point below names the
+ * reference callable it replaces (file:line in the reference tree).  The Python
+ * package `image_denoising_amd` binds these with ctypes.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a caller-owned DEVICE buffer (PyTorch tensors are used only as
+ *     containers); the library never allocates device memory — sizes come from the
+ *     *_size queries;
+ *   - all work is enqueued asynchronously on `stream` (a hipStream_t passed as void*;
+ *     NULL = the legacy default stream); nothing synchronises the host;
+ *   - the return value is a dn_status: 0 = ok, < 0 = error.  The message of the last
+ *     error on the calling thread is available from dn_last_error();
+ *   - network tensors at the boundary are NCHW fp32 contiguous, exactly like the
+ *     reference's torch tensors; activations inside the workspace are NHWC fp32;
+ *   - parameters live in ONE flat fp32 buffer in the reference's state_dict order
+ *     (arch_unet.py:100-192, e.g. enc_conv0.weight, enc_conv0.bias, ..., nin_c.bias)
+ *     with PyTorch layouts (Conv2d OIHW, ConvTranspose2d (in,out,kh,kw)), so
+ *     checkpoints round-trip without repacking.  Gradients use the same layout.
+ */
+#ifndef DENOISE_HIP_H
+#define DENOISE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int dn_status;
+#define DN_OK 0
+#define DN_ERR_ARG (-1)         /* bad shape / unsupported configuration */
+#define DN_ERR_WORKSPACE (-2)   /* workspace too small */
+#define DN_ERR_HIP (-3)         /* a HIP runtime call failed */
+
+/* U-Net configuration: arch_unet.py:101-106 UNet(in_nc, out_nc, n_feature, blindspot=False). */
+typedef struct dn_unet_cfg {
+  int in_nc;      /* input channels  (1 or 3)  */
+  int out_nc;     /* output channels (1 or 3)  */
+  int n_feature;  /* 48 (the only width the reference trains, train.py:30) */
+} dn_unet_cfg;
+
+/* ---- library / errors ---------------------------------------------------------- */
+const char* dn_version(void);
+/* copies the last error message of this thread into buf (NUL-terminated); returns its length */
+int dn_last_error(char* buf, size_t len);
+
+/* ---- parameters ---------------------------------------------------------------- */
+/* number of floats of the flat parameter buffer (1,256,689 for in=out=1, nf=48) */
+dn_status dn_unet_param_count(const dn_unet_cfg* cfg, size_t* count);
+/* offset (floats) and size of the weight of layer `index` (0..24, state_dict order);
+   the bias follows the weight directly.  Used by the host mirror for state_dict views. */
+dn_status dn_unet_param_info(const dn_unet_cfg* cfg, int index, size_t* w_off, size_t* w_count,
+                             size_t* b_count);
+
+/* ---- U-Net forward / backward: arch_unet.py:194-260 (UNet.forward) + autograd ---- */
+/* bytes of workspace for a batch N x H x W (H, W multiples of 32).  with_backward=1 sizes the
+   saved activations, gradient buffers and weight-gradient slabs needed by dn_unet_backward. */
+dn_status dn_unet_workspace_size(const dn_unet_cfg* cfg, int N, int H, int W, int with_backward,
+                                 size_t* bytes);
+/* y[N,out_nc,H,W] = UNet(x[N,in_nc,H,W]).  Activations are kept in ws for a later backward
+   when ws was sized with with_backward=1. */
+dn_status dn_unet_forward(const dn_unet_cfg* cfg, const float* params, const float* x, float* y,
+                          int N, int H, int W, void* ws, size_t ws_bytes, void* stream);
+/* dparams = dL/dparams given dy = dL/dy, for the activations saved by the last
+   dn_unet_forward on the same ws (same N,H,W).  dparams is overwritten (not accumulated). */
+dn_status dn_unet_backward(const dn_unet_cfg* cfg, const float* params, const float* dy,
+                           float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
+                           void* stream);
+
+/* ---- Neighbor2Neighbor sub-sampler: train.py:134-190 ------------------------------ */
+/* One call replaces generate_mask_pair + 2x generate_subimages (train.py:141-190,
+   training_script.md:137-139).  img is NCHW [N,C,H,W]; sub1/sub2 are NCHW [N,C,H/2,W/2].
+   rd_idx (one byte per 2x2 cell, values 0..7 indexing the pair table of train.py:151-154):
+     - rd_idx_in != NULL: parity mode, the caller's per-cell choices are used;
+     - rd_idx_in == NULL: counter-based Philox4x32-10 keyed on (seed, offset) and the GLOBAL
+       cell index cell_base + (n*H/2 + i)*W/2 + j, so the mask stream does not depend on how
+       a batch is sharded over ranks.
+   rd_idx_out (nullable) receives the choices actually used. */
+dn_status dn_n2n_subsample(const float* img, int N, int C, int H, int W, const uint8_t* rd_idx_in,
+                           uint64_t seed, uint64_t offset, uint64_t cell_base, float* sub1,
+                           float* sub2, uint8_t* rd_idx_out, void* stream);
+/* generate_mask_pair output format (train.py:141-172): two bool[N*H/2*W/2*4] masks from rd_idx */
+dn_status dn_n2n_masks(const uint8_t* rd_idx, int64_t ncells, uint8_t* mask1, uint8_t* mask2,
+                       void* stream);
+/* generate_subimages(img, mask) (train.py:175-190) for a single bool mask */
+dn_status dn_n2n_subimage_from_mask(const float* img, int N, int C, int H, int W,
+                                    const uint8_t* mask, float* sub, void* stream);
+
+/* ---- noise synthesis: train.py:84-101 AugmentNoise.add_train_noise (gauss) -------- */
+/* noisy = clean + std_n * N(0,1); std_per_image (nullable, [N]) overrides std (gauss_range).
+   Normals come from Philox4x32-10 + Box-Muller keyed on (seed, offset, elem_base + e). */
+dn_status dn_add_gauss_noise(const float* clean, int N, int64_t per_image, float std_,
+                             const float* std_per_image, uint64_t seed, uint64_t offset,
+                             uint64_t elem_base, float* noisy, void* stream);
+
+/* ---- losses ------------------------------------------------------------------------ */
+/* N2N regularised loss, training_script.md:141-153.  out, sub2: [N,C,h,w]; den: [N,C,2h,2w]
+   (the no-grad full-resolution denoised image, sub-sampled in-kernel with rd_idx).
+     loss1 = mean((out-sub2)^2); loss2 = lambda * mean(((out-sub2) - (den1-den2))^2)
+   Writes dout = d(loss1+loss2)/d out and loss3 = {loss1, loss2, loss1+loss2} (device floats).
+   partial_ws must hold dn_loss_partials_size() bytes. */
+size_t dn_loss_partials_size(void);
+dn_status dn_n2n_loss(const float* out, const float* sub2, const float* den, const uint8_t* rd_idx,
+                      int N, int C, int h, int w, float lambda, float* dout, float* loss3,
+                      void* partial_ws, void* stream);
+/* Structure_loss, util.py:41-70 (alpha=1, beta=.5, gamma=.5, reduction='mean'):
+   L = alpha*L1(pred,tgt) + beta*(L1 TV of pred2 over H + over W)/2 + gamma*L1(pred2,tgt).
+   Writes dpred, dpred2 and loss5 = {pixel, tv1, tv2, cst, total}. */
+dn_status dn_structure_loss(const float* pred, const float* pred2, const float* target, int N, int C,
+                            int H, int W, float alpha, float beta, float gamma, float* dpred,
+                            float* dpred2, float* loss5, void* partial_ws, void* stream);
+
+/* ---- optimiser: torch.optim.Adam as used at train.py:332, :368 --------------------- */
+/* One fused Adam step over n floats (torch _single_tensor_adam math, amsgrad=False,
+   weight_decay=0).  step is the 1-based step count after increment.  grad_scale multiplies
+   the gradient first (1/world_size after an all-reduce sum). */
+dn_status dn_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                       float lr, float beta1, float beta2, float eps, int64_t step,
+                       float grad_scale, void* stream);
+
+/* ---- op-level entry points (NHWC), used by the tests and the tiled-inference path ---- */
+/* 3x3/pad1 (ksize=3) or 1x1 (ksize=1) convolution + bias (+ LeakyReLU(0.2) if act).
+   x: [N,H,W,*] with channel stride x_stride; y: [N,H,W,*] stride y_stride.
+   w: [Cout,Cin,k,k] (PyTorch OIHW), b: [Cout].  arch_unet.py:65-78 conv_func, :113 act. */
+dn_status dn_conv2d_forward(const float* x, int x_stride, int N, int H, int W, int Cin,
+                            const float* w, const float* b, int Cout, int ksize, int act, float* y,
+                            int y_stride, void* stream);
+/* dx = conv^T(dz) [* leaky'(mask)] : data gradient (mask nullable; mask_stride). If accumulate,
+   dx += result.  dx stride dx_stride. */
+dn_status dn_conv2d_backward_data(const float* dz, int N, int H, int W, int Cout, const float* w,
+                                  int Cin, int ksize, const float* mask, int mask_stride,
+                                  int accumulate, float* dx, int dx_stride, void* stream);
+/* dw [Cout,Cin,k,k] and db [Cout] (contiguous after dw) from dz [N,H,W,Cout] and x.
+   slab must hold dn_conv2d_wgrad_slab_size() bytes. */
+size_t dn_conv2d_wgrad_slab_size(int N, int H, int W, int Cin, int Cout, int ksize);
+dn_status dn_conv2d_backward_weight(const float* dz, const float* x, int x_stride, int N, int H,
+                                    int W, int Cin, int Cout, int ksize, float* dwb, void* slab,
+                                    void* stream);
+/* ConvTranspose2d(Cin, Cout, 2, 2) (arch_unet.py:57): x [N,H,W,Cin] -> y [N,2H,2W,*]
+   (written at channel offset y_off of stride y_stride, i.e. directly into a concat buffer). */
+dn_status dn_deconv2x2_forward(const float* x, int N, int H, int W, int Cin, const float* w,
+                               const float* b, int Cout, float* y, int y_stride, int y_off,
+                               void* stream);
+dn_status dn_deconv2x2_backward_data(const float* dy, int dy_stride, int N, int H, int W, int Cout,
+                                     const float* w, int Cin, const float* mask, float* dx,
+                                     void* stream);
+size_t dn_deconv2x2_wgrad_slab_size(int N, int H, int W, int Cin, int Cout);
+dn_status dn_deconv2x2_backward_weight(const float* dy, int dy_stride, const float* x, int N, int H,
+                                       int W, int Cin, int Cout, float* dwb, void* slab,
+                                       void* stream);
+/* MaxPool2d(2) (arch_unet.py:120-135) on NHWC x [N,H,W,C] -> y (channel stride y_stride, offset y_off) */
+dn_status dn_maxpool2x2_forward(const float* x, int N, int H, int W, int C, float* y, int y_stride,
+                                int y_off, void* stream);
+/* dx = route(dy -> argmax, first max in row-major wins) * leaky'(x) if act else route only */
+dn_status dn_maxpool2x2_backward(const float* x, int N, int H, int W, int C, const float* dy,
+                                 int dy_stride, int dy_off, int act, float* dx, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DENOISE_HIP_H */

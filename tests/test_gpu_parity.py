@@ -1,0 +1,426 @@
+"""HIP path vs the CPU oracle / reference fixtures, through the C-ABI.  Needs an MI355X."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+FP32_TOL = 1e-4  # north_star: 1e-4 relative fp32
+
+
+def rel_err(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from image_denoising_amd import _lib
+
+    _lib.lib()
+    torch.manual_seed(1234)
+
+
+def L():
+    from image_denoising_amd import _lib
+
+    return _lib
+
+
+def S():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def nhwc(t):  # NCHW -> NHWC contiguous
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+# ---------------------------------------------------------------------------------------
+# neighbour sub-sampler (bit-exact)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("case", ["a", "b", "c"])
+def test_subsample_matches_reference_fixture(golden, case):
+    from image_denoising_amd import n2n
+
+    g = golden("subsampler.npz")
+    img = torch.from_numpy(g[f"{case}_img"]).to(DEV)
+    rd = torch.from_numpy(g[f"{case}_rd"]).to(DEV)
+    s1, s2, rd_used = n2n.n2n_subsample(img, rd)
+    assert np.array_equal(s1.cpu().numpy(), g[f"{case}_sub1"])
+    assert np.array_equal(s2.cpu().numpy(), g[f"{case}_sub2"])
+    m1, m2 = n2n.rd_to_masks(rd)
+    from oracle import n2n_ref
+
+    o1, o2 = n2n_ref.masks_from_rd(g[f"{case}_rd"])
+    assert np.array_equal(m1.cpu().numpy(), o1) and np.array_equal(m2.cpu().numpy(), o2)
+    if case == "a":
+        assert np.array_equal(m1.cpu().numpy(), g["a_mask1"])
+    # drop-in generate_subimages(img, mask)
+    assert torch.equal(n2n.generate_subimages(img, m1), s1)
+    assert torch.equal(n2n.generate_subimages(img, m2), s2)
+
+
+def test_subsample_philox_stream_bitexact():
+    from image_denoising_amd import n2n
+    from oracle import n2n_ref, philox
+
+    img = torch.rand(3, 2, 64, 96, device=DEV)
+    cells = 3 * 32 * 48
+    s1, s2, rd = n2n.n2n_subsample(img, None, seed=11, offset=5, cell_base=777)
+    ref_rd = philox.rd_idx(11, 5, cells, cell_base=777)
+    assert np.array_equal(rd.cpu().numpy(), ref_rd)
+    c1, c2 = n2n_ref.subimages_closed_form(img.cpu().numpy(), ref_rd)
+    assert np.array_equal(s1.cpu().numpy(), c1) and np.array_equal(s2.cpu().numpy(), c2)
+    # mask pair never coincides, one True per cell
+    m1, m2 = n2n.rd_to_masks(rd)
+    m1, m2 = m1.view(-1, 4), m2.view(-1, 4)
+    assert (m1.sum(1) == 1).all() and (m2.sum(1) == 1).all() and not (m1 & m2).any()
+
+
+def test_subsample_empty_batch():
+    from image_denoising_amd import n2n
+
+    img = torch.empty(0, 1, 8, 8, device=DEV)
+    s1, s2, rd = n2n.n2n_subsample(img)
+    assert s1.shape == (0, 1, 4, 4) and rd.numel() == 0
+
+
+def test_gauss_noise_matches_philox_oracle():
+    from image_denoising_amd.n2n import AugmentNoise
+    from oracle import philox
+
+    clean = torch.rand(2, 1, 32, 48, device=DEV)
+    aug = AugmentNoise("gauss25", seed=9)
+    noisy = aug.add_train_noise(clean, offset=4)
+    z = philox.normal(9, 4, np.arange(clean.numel(), dtype=np.uint64)).reshape(clean.shape)
+    ref = clean.cpu().numpy().astype(np.float64) + (25.0 / 255.0) * z
+    assert np.abs(noisy.cpu().numpy() - ref).max() < 2e-6
+
+
+# ---------------------------------------------------------------------------------------
+# op-level convolution kernels vs torch fp32 on the CPU
+# ---------------------------------------------------------------------------------------
+def _conv_ref(x, w, b, k, act):
+    y = F.conv2d(x, w, b, padding=k // 2)
+    return F.leaky_relu(y, 0.2) if act else y
+
+
+@pytest.mark.parametrize("cin,cout,k,H,W", [
+    (1, 48, 3, 32, 32), (3, 48, 3, 32, 48), (48, 48, 3, 32, 32), (48, 48, 3, 8, 8),
+    (48, 48, 3, 4, 4), (96, 96, 3, 16, 16), (144, 96, 3, 16, 32), (97, 96, 3, 32, 32),
+    (99, 96, 3, 32, 32), (96, 96, 1, 32, 32), (96, 1, 1, 32, 32), (96, 3, 1, 16, 16),
+])
+def test_conv_forward(cin, cout, k, H, W):
+    _lib = L()
+    N = 2
+    x = torch.randn(N, cin, H, W)
+    w = torch.randn(cout, cin, k, k) * 0.1
+    b = torch.randn(cout) * 0.1
+    act = 1 if cout > 3 else 0
+    xg, wg, bg = nhwc(x).to(DEV), w.to(DEV), b.to(DEV)
+    y = torch.empty(N, H, W, cout, device=DEV)
+    _lib.call("dn_conv2d_forward", xg.data_ptr(), cin, N, H, W, cin, wg.data_ptr(), bg.data_ptr(),
+              cout, k, act, y.data_ptr(), cout, S())
+    ref = _conv_ref(x, w, b, k, act)
+    assert rel_err(nchw(y.cpu()).numpy(), ref.numpy()) < FP32_TOL
+
+
+@pytest.mark.parametrize("cin,cout,k,H", [
+    (48, 48, 3, 32), (96, 96, 3, 16), (144, 96, 3, 16), (48, 96, 3, 8), (96, 96, 1, 32),
+    (96, 1, 1, 16), (96, 3, 1, 16),
+])
+@pytest.mark.parametrize("mode", ["plain", "mask", "accum"])
+def test_conv_backward_data(cin, cout, k, H, mode):
+    _lib = L()
+    N, W = 2, H
+    x = torch.randn(N, cin, H, W, requires_grad=True)
+    w = torch.randn(cout, cin, k, k) * 0.1
+    dz = torch.randn(N, cout, H, W)
+    F.conv2d(x, w, None, padding=k // 2).backward(dz)
+    ref = x.grad
+    mask = torch.randn(N, cin, H, W)
+    base = torch.randn(N, cin, H, W)
+    if mode == "mask":
+        ref = torch.where(mask > 0, ref, ref * 0.2)
+    if mode == "accum":
+        ref = ref + base
+    dx = nhwc(base).to(DEV) if mode == "accum" else torch.zeros(N, H, W, cin, device=DEV)
+    mg = nhwc(mask).to(DEV)
+    _lib.call("dn_conv2d_backward_data", nhwc(dz).to(DEV).data_ptr(), N, H, W, cout,
+              w.to(DEV).data_ptr(), cin, k, mg.data_ptr() if mode == "mask" else None, cin,
+              1 if mode == "accum" else 0, dx.data_ptr(), cin, S())
+    assert rel_err(nchw(dx.cpu()).numpy(), ref.numpy()) < FP32_TOL
+
+
+@pytest.mark.parametrize("cin,cout,k,N,H,W", [
+    (48, 48, 3, 2, 32, 32), (96, 96, 3, 2, 16, 16), (144, 96, 3, 2, 16, 16),
+    (97, 96, 3, 2, 32, 32), (1, 48, 3, 2, 32, 32), (3, 48, 3, 1, 32, 32), (48, 48, 3, 3, 8, 8),
+    (48, 48, 3, 4, 4, 4), (96, 96, 1, 2, 32, 32), (96, 1, 1, 2, 32, 32), (96, 3, 1, 2, 16, 16),
+    (96, 96, 3, 8, 64, 64),
+])
+def test_conv_backward_weight(cin, cout, k, N, H, W):
+    _lib = L()
+    x = torch.randn(N, cin, H, W)
+    w = (torch.randn(cout, cin, k, k) * 0.1).requires_grad_(True)
+    b = torch.zeros(cout, requires_grad=True)
+    dz = torch.randn(N, cout, H, W)
+    F.conv2d(x, w, b, padding=k // 2).backward(dz)
+    nbytes = _lib.lib().dn_conv2d_wgrad_slab_size(N, H, W, cin, cout, k)
+    slab = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    dwb = torch.full((cout * cin * k * k + cout,), float("nan"), device=DEV)
+    _lib.call("dn_conv2d_backward_weight", nhwc(dz).to(DEV).data_ptr(), nhwc(x).to(DEV).data_ptr(),
+              cin, N, H, W, cin, cout, k, dwb.data_ptr(), slab.data_ptr(), S())
+    out = dwb.cpu().numpy()
+    nw = cout * cin * k * k
+    assert rel_err(out[:nw], w.grad.numpy().reshape(-1)) < FP32_TOL
+    assert rel_err(out[nw:], b.grad.numpy()) < FP32_TOL
+
+
+@pytest.mark.parametrize("cin,cout,H", [(48, 48, 4), (96, 96, 8), (96, 96, 16)])
+def test_deconv_forward_backward(cin, cout, H):
+    _lib = L()
+    N, W = 2, H
+    x = torch.randn(N, cin, H, W)
+    xr = x.clone().requires_grad_(True)
+    w = (torch.randn(cin, cout, 2, 2) * 0.1).requires_grad_(True)
+    b = (torch.randn(cout) * 0.1).requires_grad_(True)
+    y = F.conv_transpose2d(xr, w, b, stride=2)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    # forward into a strided concat buffer at channel offset 0 (skip after it)
+    stride = cout + 8
+    yg = torch.zeros(N, 2 * H, 2 * W, stride, device=DEV)
+    xg = nhwc(x).to(DEV)
+    wg, bg = w.detach().to(DEV), b.detach().to(DEV)
+    _lib.call("dn_deconv2x2_forward", xg.data_ptr(), N, H, W, cin, wg.data_ptr(), bg.data_ptr(),
+              cout, yg.data_ptr(), stride, 0, S())
+    assert rel_err(nchw(yg[..., :cout].cpu()).numpy(), y.detach().numpy()) < FP32_TOL
+    assert float(yg[..., cout:].abs().max()) == 0.0
+    # data gradient (with and without the LeakyReLU mask)
+    dyg = torch.zeros(N, 2 * H, 2 * W, stride, device=DEV)
+    dyg[..., :cout] = nhwc(dy).to(DEV)
+    dx = torch.empty(N, H, W, cin, device=DEV)
+    _lib.call("dn_deconv2x2_backward_data", dyg.data_ptr(), stride, N, H, W, cout, wg.data_ptr(),
+              cin, None, dx.data_ptr(), S())
+    assert rel_err(nchw(dx.cpu()).numpy(), xr.grad.numpy()) < FP32_TOL
+    mask = torch.randn(N, cin, H, W)
+    _lib.call("dn_deconv2x2_backward_data", dyg.data_ptr(), stride, N, H, W, cout, wg.data_ptr(),
+              cin, nhwc(mask).to(DEV).data_ptr(), dx.data_ptr(), S())
+    refm = torch.where(mask > 0, xr.grad, xr.grad * 0.2)
+    assert rel_err(nchw(dx.cpu()).numpy(), refm.numpy()) < FP32_TOL
+    # weight gradient
+    nbytes = _lib.lib().dn_deconv2x2_wgrad_slab_size(N, H, W, cin, cout)
+    slab = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    dwb = torch.empty(cin * cout * 4 + cout, device=DEV)
+    _lib.call("dn_deconv2x2_backward_weight", dyg.data_ptr(), stride, xg.data_ptr(), N, H, W, cin,
+              cout, dwb.data_ptr(), slab.data_ptr(), S())
+    out = dwb.cpu().numpy()
+    assert rel_err(out[:cin * cout * 4], w.grad.numpy().reshape(-1)) < FP32_TOL
+    assert rel_err(out[cin * cout * 4:], b.grad.numpy()) < FP32_TOL
+
+
+@pytest.mark.parametrize("ties", [False, True])
+def test_maxpool_forward_backward(ties):
+    _lib = L()
+    N, C, H, W = 2, 48, 16, 24
+    x = torch.randint(-2, 3, (N, C, H, W)).float() if ties else torch.randn(N, C, H, W)
+    xr = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xr, 2)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xg = nhwc(x).to(DEV)
+    yg = torch.zeros(N, H // 2, W // 2, 2 * C, device=DEV)  # into the second half of a concat
+    _lib.call("dn_maxpool2x2_forward", xg.data_ptr(), N, H, W, C, yg.data_ptr(), 2 * C, C, S())
+    assert torch.equal(nchw(yg[..., C:].cpu()), y.detach())
+    dyg = torch.zeros(N, H // 2, W // 2, 2 * C, device=DEV)
+    dyg[..., C:] = nhwc(dy).to(DEV)
+    for act in (0, 1):
+        dx = torch.empty(N, H, W, C, device=DEV)
+        _lib.call("dn_maxpool2x2_backward", xg.data_ptr(), N, H, W, C, dyg.data_ptr(), 2 * C, C,
+                  act, dx.data_ptr(), S())
+        ref = xr.grad if not act else torch.where(x > 0, xr.grad, xr.grad * 0.2)
+        assert torch.equal(nchw(dx.cpu()), ref), f"act={act}"
+
+
+# ---------------------------------------------------------------------------------------
+# whole U-Net vs reference fixtures
+# ---------------------------------------------------------------------------------------
+def _net(C):
+    from image_denoising_amd import UNet
+
+    torch.manual_seed(0)
+    return UNet(in_nc=C, out_nc=C, n_feature=48).to(DEV)
+
+
+@pytest.mark.parametrize("C,name", [(1, "unet_c1.npz"), (3, "unet_c3.npz")])
+def test_unet_forward_backward_vs_reference(golden, C, name):
+    g = golden(name)
+    net = _net(C)
+    x = torch.from_numpy(g["x"]).to(DEV)
+    with torch.no_grad():
+        y0 = net(x)
+    assert rel_err(y0.cpu().numpy(), g["y"]) < FP32_TOL
+    y = net(x)
+    assert torch.equal(y.detach(), y0)  # grad path == no-grad path
+    loss = (y ** 2).mean()
+    loss.backward()
+    grad = torch.cat([p.grad.reshape(-1) for p in net.parameters()]).cpu().numpy()
+    if "grad" in g:
+        ref = g["grad"]
+        off = 0
+        from oracle.unet_ref import layer_table
+
+        for name_, ws, bl, _ in layer_table(C, C):
+            n = int(np.prod(ws)) + bl
+            assert rel_err(grad[off:off + n], ref[off:off + n]) < FP32_TOL, name_
+            off += n
+    else:
+        assert rel_err(grad[g["grad_idx"]], g["grad_sample"]) < FP32_TOL
+    norms = [float(p.grad.norm()) for p in net.parameters()]
+    assert rel_err(norms, g["grad_norms"]) < FP32_TOL
+
+
+def test_unet_rectangular_and_deep_levels_vs_oracle():
+    from oracle import unet_ref
+
+    net = _net(1)
+    x = torch.rand(3, 1, 32, 96)
+    with torch.no_grad():
+        y = net(x.to(DEV)).cpu()
+    ref = unet_ref.forward(net.flat_params.cpu(), x, 1, 1)
+    assert rel_err(y.numpy(), ref.numpy()) < FP32_TOL
+
+
+def test_unet_rejects_bad_shapes():
+    net = _net(1)
+    with pytest.raises(ValueError):
+        net(torch.rand(1, 1, 48, 64, device=DEV))
+    with pytest.raises(ValueError):
+        net(torch.rand(1, 3, 64, 64, device=DEV))
+
+
+# ---------------------------------------------------------------------------------------
+# losses, Adam, the full N2N step
+# ---------------------------------------------------------------------------------------
+def test_n2n_loss_vs_oracle(golden):
+    from image_denoising_amd import n2n
+    from oracle import n2n_ref
+
+    g = golden("n2n_step.npz")
+    out = torch.from_numpy(g["out"]).to(DEV)
+    noisy = torch.from_numpy(g["noisy"]).to(DEV)
+    rd = torch.from_numpy(g["rd"]).to(DEV)
+    _, sub2, _ = n2n.n2n_subsample(noisy, rd)
+    den = torch.from_numpy(g["den"]).to(DEV)
+    loss3, dout = n2n.n2n_loss(out, sub2, den, rd, float(g["lam"]))
+    l = loss3.cpu().numpy()
+    assert abs(l[0] - float(g["loss1"])) <= 1e-5 * float(g["loss1"])
+    assert abs(l[1] - float(g["loss2"])) <= 1e-4 * float(g["loss2"]) + 1e-12
+    assert abs(l[2] - float(g["loss"])) <= 1e-5 * float(g["loss"])
+    assert rel_err(dout.cpu().numpy(), g["dout"]) < 1e-5
+    # oracle restatement agrees too
+    r = n2n_ref.n2n_loss(g["out"], sub2.cpu().numpy(), g["den"], g["rd"], float(g["lam"]))
+    assert abs(r[2] - float(l[2])) <= 1e-5 * r[2]
+
+
+def test_structure_loss_vs_reference(golden):
+    from image_denoising_amd.util import Structure_loss
+
+    g = golden("structure_loss.npz")
+    pred = torch.from_numpy(g["pred"]).to(DEV).requires_grad_(True)
+    pred2 = torch.from_numpy(g["pred2"]).to(DEV).requires_grad_(True)
+    tgt = torch.from_numpy(g["target"]).to(DEV)
+    L_ = Structure_loss()(pred, pred2, tgt)
+    L_.backward()
+    assert abs(float(L_) - float(g["loss"])) < 1e-6
+    assert rel_err(pred.grad.cpu().numpy(), g["dpred"]) < 1e-5
+    assert rel_err(pred2.grad.cpu().numpy(), g["dpred2"]) < 1e-5
+
+
+def test_adam_matches_torch_adam():
+    from image_denoising_amd.optim import FlatAdam
+
+    n = 100_003
+    p0 = torch.randn(n) * 0.05
+    pt = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.Adam([pt], lr=3e-4)
+    pg = p0.clone().to(DEV)
+    fa = FlatAdam(pg, lr=3e-4)
+    for _ in range(3):
+        g = torch.randn(n) * torch.logspace(-9, 0, n)
+        pt.grad = g.clone()
+        opt.step()
+        fa.step(g.to(DEV))
+    assert torch.allclose(pg.cpu(), pt.detach(), rtol=0, atol=1e-7)
+    assert float((pg.cpu() != pt.detach()).float().mean()) < 1e-3
+
+
+def test_n2n_step_vs_reference(golden):
+    from image_denoising_amd import N2NTrainer
+    from image_denoising_amd.arch_unet import reference_init
+
+    g = golden("n2n_step.npz")
+    net = _net(1)
+    torch.manual_seed(0)
+    pre = reference_init(1, 1, 48).numpy()
+    tr = N2NTrainer(net, lr=3e-4, n_epoch=100, increase_ratio=2.0)
+    noisy = torch.from_numpy(g["noisy"]).to(DEV)
+    rd = torch.from_numpy(g["rd"]).to(DEV)
+    loss3 = tr.train_step(noisy, epoch=1, rd_idx=rd, noisy=noisy).cpu().numpy()
+    assert abs(loss3[0] - float(g["loss1"])) <= 1e-4 * float(g["loss1"])
+    assert abs(loss3[2] - float(g["loss"])) <= 1e-4 * float(g["loss"])
+    grad = tr.grad.cpu().numpy()
+    assert rel_err(grad[g["grad_idx"]], g["grad_sample"]) < FP32_TOL
+    post = net.flat_params.cpu().numpy()
+    upd, ref_upd = post[g["post_idx"]] - pre[g["post_idx"]], g["post_sample"] - pre[g["post_idx"]]
+    bad = np.abs(upd - ref_upd) > 1e-6
+    assert bad.mean() < 2e-3, bad.mean()
+    assert np.abs(upd - ref_upd).max() <= 6.1e-4  # never more than 2*lr apart
+
+
+def test_n2n_step_deterministic():
+    from image_denoising_amd import N2NTrainer
+
+    clean = torch.rand(4, 1, 64, 64, device=DEV)
+    res = []
+    for _ in range(2):
+        net = _net(1)
+        tr = N2NTrainer(net, seed=3)
+        for e in range(2):
+            tr.train_step(clean, epoch=1)
+        res.append((net.flat_params.clone(), tr.grad.clone()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+def test_config1_full_size_step_properties():
+    """BASELINE config 1 (bs=64, 256x256x1): one full N2N step; per-image independence lets a
+    single image be checked against the oracle at full resolution."""
+    from image_denoising_amd import N2NTrainer
+    from oracle import unet_ref
+
+    net = _net(1)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    clean = F.interpolate(torch.rand(64, 1, 32, 32, generator=g), size=(256, 256),
+                          mode="bilinear", align_corners=False).to(DEV)
+    tr = N2NTrainer(net, seed=0)
+    flat0 = net.flat_params.detach().cpu().clone()
+    loss3 = tr.train_step(clean, epoch=1)
+    torch.cuda.synchronize()
+    l = loss3.cpu().numpy()
+    assert np.isfinite(l).all() and l[0] > 0
+    den0 = tr._bufs[next(iter(tr._bufs))]["den"][:2].cpu()
+    noisy0 = tr._bufs[next(iter(tr._bufs))]["noisy"][:2].cpu()
+    ref = unet_ref.forward(flat0, noisy0, 1, 1)
+    assert rel_err(den0.numpy(), ref.numpy()) < FP32_TOL
+    assert torch.isfinite(tr.grad).all()
