@@ -62,8 +62,10 @@ def time_dominant_kernel(bs, H, W, device, reps=5):
     b = torch.zeros(96, device=device)
     y = torch.empty_like(x)
     s = torch.cuda.current_stream(device)
+    pk = _lib.scratch(_lib.lib().dn_conv2d_pack_size(96, 96, 3, 0), device)
     run = lambda: _lib.call("dn_conv2d_forward", x.data_ptr(), 96, bs, H, W, 96, w.data_ptr(),
-                            b.data_ptr(), 96, 3, 1, y.data_ptr(), 96, s.cuda_stream)
+                            b.data_ptr(), 96, 3, 1, y.data_ptr(), 96, pk.data_ptr(), pk.numel(),
+                            s.cuda_stream)
     run()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)

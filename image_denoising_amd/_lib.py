@@ -36,6 +36,8 @@ SIGNATURES = {
                                 c_size_t, c_void_p]),
     "dn_unet_backward": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
                                  c_size_t, c_void_p]),
+    "dn_unet_debug_buffers": (c_int, [POINTER(DnCfg), c_int, c_int, c_int, c_int,
+                                      POINTER(c_int64), c_int, POINTER(c_int)]),
     "dn_n2n_subsample": (c_int, [_F, c_int, c_int, c_int, c_int, _U8, c_uint64, c_uint64, c_uint64,
                                  _F, _F, _U8, c_void_p]),
     "dn_n2n_masks": (c_int, [_U8, c_int64, _U8, _U8, c_void_p]),
@@ -49,17 +51,19 @@ SIGNATURES = {
                                   c_float, _F, _F, _F, c_void_p, c_void_p]),
     "dn_adam_step": (c_int, [_F, _F, _F, _F, c_int64, c_float, c_float, c_float, c_float, c_int64,
                              c_float, c_void_p]),
+    "dn_conv2d_pack_size": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "dn_deconv2x2_pack_size": (c_size_t, [c_int, c_int, c_int]),
     "dn_conv2d_forward": (c_int, [_F, c_int, c_int, c_int, c_int, c_int, _F, _F, c_int, c_int,
-                                  c_int, _F, c_int, c_void_p]),
+                                  c_int, _F, c_int, c_void_p, c_size_t, c_void_p]),
     "dn_conv2d_backward_data": (c_int, [_F, c_int, c_int, c_int, c_int, _F, c_int, c_int, _F,
-                                        c_int, c_int, _F, c_int, c_void_p]),
+                                        c_int, c_int, _F, c_int, c_void_p, c_size_t, c_void_p]),
     "dn_conv2d_wgrad_slab_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "dn_conv2d_backward_weight": (c_int, [_F, _F, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                           _F, c_void_p, c_void_p]),
     "dn_deconv2x2_forward": (c_int, [_F, c_int, c_int, c_int, c_int, _F, _F, c_int, _F, c_int,
-                                     c_int, c_void_p]),
+                                     c_int, c_void_p, c_size_t, c_void_p]),
     "dn_deconv2x2_backward_data": (c_int, [_F, c_int, c_int, c_int, c_int, c_int, _F, c_int, _F,
-                                           _F, c_void_p]),
+                                           _F, c_void_p, c_size_t, c_void_p]),
     "dn_deconv2x2_wgrad_slab_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "dn_deconv2x2_backward_weight": (c_int, [_F, c_int, _F, c_int, c_int, c_int, c_int, c_int, _F,
                                              c_void_p, c_void_p]),
@@ -120,6 +124,11 @@ def stream_of(t: torch.Tensor):
     if t.device.type != "cuda":
         raise ValueError(f"expected a GPU tensor, got device {t.device}")
     return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def scratch(nbytes: int, device) -> torch.Tensor:
+    """caller-owned device scratch (the library never allocates)"""
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
 
 def cfg(in_nc: int, out_nc: int, n_feature: int) -> DnCfg:

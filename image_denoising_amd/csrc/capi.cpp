@@ -109,13 +109,51 @@ dn_status dn_unet_backward(const dn_unet_cfg* cfg, const float* params, const fl
   DN_GUARD_END
 }
 
+dn_status dn_unet_debug_buffers(const dn_unet_cfg* cfg, int N, int H, int W, int with_backward,
+                                int64_t* desc, int max_entries, int* n_entries) {
+  DN_GUARD_BEGIN
+  if (!cfg || !desc || !n_entries) return fail(DN_ERR_ARG, "null argument");
+  Plan p;
+  std::string err;
+  if (!build_plan(*cfg, N, H, W, with_backward != 0, p, err)) return fail(DN_ERR_ARG, err);
+  int n = 0;
+  auto add = [&](long off, int stride, int level) {
+    if (n < max_entries) {
+      desc[3 * n] = off;
+      desc[3 * n + 1] = stride;
+      desc[3 * n + 2] = level;
+    }
+    ++n;
+  };
+  const int nf = p.nf;
+  add(p.c1, p.c1s, 0); add(p.a0, nf, 0); add(p.a1, nf, 0);
+  for (int l = 1; l <= 4; ++l) add(p.c[l], p.cs[l], l);
+  for (int l = 1; l <= 4; ++l) add(p.a[l], nf, l);
+  add(p.p5, nf, 5); add(p.a6, nf, 5);
+  for (int l = 1; l <= 4; ++l) add(p.da[l], 2 * nf, l);
+  for (int l = 1; l <= 4; ++l) add(p.db[l], 2 * nf, l);
+  add(p.d1a, 96, 0); add(p.d1b, 96, 0); add(p.na, 96, 0); add(p.nb, 96, 0);
+  if (with_backward) {
+    add(p.g_nb, 96, 0); add(p.g_na, 96, 0); add(p.g_d1b, 96, 0); add(p.g_d1a, 96, 0);
+    add(p.g_c1, 2 * nf, 0);
+    for (int l = 1; l <= 4; ++l) add(p.g_c[l], p.cs[l], l);
+    for (int l = 1; l <= 4; ++l) add(p.g_da[l], 2 * nf, l);
+    for (int l = 1; l <= 4; ++l) add(p.g_db[l], 2 * nf, l);
+    for (int l = 1; l <= 4; ++l) add(p.g_a[l], nf, l);
+    add(p.g_a6, nf, 5); add(p.g_p5, nf, 5); add(p.g_a0, nf, 0); add(p.g_a1, nf, 0);
+  }
+  *n_entries = n;
+  return DN_OK;
+  DN_GUARD_END
+}
+
 dn_status dn_n2n_subsample(const float* img, int N, int C, int H, int W, const uint8_t* rd_idx_in,
                            uint64_t seed, uint64_t offset, uint64_t cell_base, float* sub1,
                            float* sub2, uint8_t* rd_idx_out, void* stream) {
-  if (!img || !sub1 || !sub2) return fail(DN_ERR_ARG, "null argument");
   if (N < 0 || C < 1 || H < 0 || W < 0 || (H & 1) || (W & 1))
     return fail(DN_ERR_ARG, "H and W must be even");
   if ((long)N * H * W == 0) return DN_OK;
+  if (!img || !sub1 || !sub2) return fail(DN_ERR_ARG, "null argument");
   return hip_status(launch_subsample(img, N, C, H, W, rd_idx_in, seed, offset, cell_base, sub1,
                                      sub2, rd_idx_out, (hipStream_t)stream),
                     "dn_n2n_subsample");
@@ -192,34 +230,59 @@ dn_status dn_adam_step(float* param, const float* grad, float* exp_avg, float* e
 }
 
 // ---- op-level entry points ------------------------------------------------------------
+size_t dn_conv2d_pack_size(int Cin, int Cout, int ksize, int backward_data) {
+  if ((ksize != 1 && ksize != 3) || Cin < 1 || Cout < 1) return 0;
+  const long n = backward_data ? conv_dgrad_pack_size(Cout, Cin, ksize)
+                               : conv_fwd_pack_size(Cin, Cout, ksize);
+  return n < 0 ? 0 : sizeof(float) * (size_t)n;
+}
+
+size_t dn_deconv2x2_pack_size(int Cin, int Cout, int backward_data) {
+  if (Cin < 1 || Cout < 1) return 0;
+  const long n = backward_data ? deconv_dgrad_pack_size(Cout, Cin) : deconv_fwd_pack_size(Cin, Cout);
+  return n < 0 ? 0 : sizeof(float) * (size_t)n;
+}
+
+static dn_status need_pack(void* ws, size_t have, size_t need) {
+  if (need == 0) return fail(DN_ERR_ARG, "unsupported channel count for this kernel build");
+  if (!ws || have < need) return fail(DN_ERR_WORKSPACE, "pack scratch smaller than *_pack_size()");
+  return DN_OK;
+}
+
 dn_status dn_conv2d_forward(const float* x, int x_stride, int N, int H, int W, int Cin,
                             const float* w, const float* b, int Cout, int ksize, int act, float* y,
-                            int y_stride, void* stream) {
+                            int y_stride, void* pack_ws, size_t pack_bytes, void* stream) {
   if (!x || !w || !b || !y) return fail(DN_ERR_ARG, "null argument");
   if (ksize != 1 && ksize != 3) return fail(DN_ERR_ARG, "ksize must be 1 or 3");
   if (N < 1 || H < 1 || W < 1 || Cin < 1 || x_stride < Cin || y_stride < Cout)
     return fail(DN_ERR_ARG, "bad shape");
-  if (!fwd_supported(ksize == 3 ? G_C3 : G_C1, Cout))
-    return fail(DN_ERR_ARG, "unsupported Cout for this kernel build");
-  return hip_status(conv_forward(View{const_cast<float*>(x), x_stride, 0}, N, H, W, Cin, w, b, Cout,
-                                 ksize, act, View{y, y_stride, 0}, OUT_NHWC, (hipStream_t)stream),
-                    "dn_conv2d_forward");
+  if (dn_status st = need_pack(pack_ws, pack_bytes, dn_conv2d_pack_size(Cin, Cout, ksize, 0))) return st;
+  hipStream_t s = (hipStream_t)stream;
+  float* wp = static_cast<float*>(pack_ws);
+  hipError_t e = pack_conv_fwd(w, Cin, Cout, ksize, wp, s);
+  if (e == hipSuccess)
+    e = conv_forward(View{const_cast<float*>(x), x_stride, 0}, N, H, W, Cin, wp, b, Cout, ksize,
+                     act, View{y, y_stride, 0}, OUT_NHWC, s);
+  return hip_status(e, "dn_conv2d_forward");
 }
 
 dn_status dn_conv2d_backward_data(const float* dz, int N, int H, int W, int Cout, const float* w,
                                   int Cin, int ksize, const float* mask, int mask_stride,
-                                  int accumulate, float* dx, int dx_stride, void* stream) {
+                                  int accumulate, float* dx, int dx_stride, void* pack_ws,
+                                  size_t pack_bytes, void* stream) {
   if (!dz || !w || !dx) return fail(DN_ERR_ARG, "null argument");
   if (ksize != 1 && ksize != 3) return fail(DN_ERR_ARG, "ksize must be 1 or 3");
   if (N < 1 || H < 1 || W < 1 || Cout < 1 || dx_stride < Cin) return fail(DN_ERR_ARG, "bad shape");
   if (mask && accumulate) return fail(DN_ERR_ARG, "mask and accumulate are exclusive");
-  if (!fwd_supported(ksize == 3 ? G_C3 : G_C1, Cin))
-    return fail(DN_ERR_ARG, "unsupported Cin for this kernel build");
+  if (dn_status st = need_pack(pack_ws, pack_bytes, dn_conv2d_pack_size(Cin, Cout, ksize, 1))) return st;
   const int epi = mask ? EPI_MASK : (accumulate ? EPI_ACCUM : EPI_PLAIN);
-  return hip_status(conv_dgrad(View{const_cast<float*>(dz), Cout, 0}, N, H, W, Cout, w, Cin, Cin,
-                               ksize, epi, View{const_cast<float*>(mask), mask_stride, 0},
-                               View{dx, dx_stride, 0}, (hipStream_t)stream),
-                    "dn_conv2d_backward_data");
+  hipStream_t s = (hipStream_t)stream;
+  float* wp = static_cast<float*>(pack_ws);
+  hipError_t e = pack_conv_dgrad(w, Cin, Cin, Cout, ksize, wp, s);
+  if (e == hipSuccess)
+    e = conv_dgrad(View{const_cast<float*>(dz), Cout, 0}, N, H, W, Cout, wp, Cin, ksize, epi,
+                   View{const_cast<float*>(mask), mask_stride, 0}, View{dx, dx_stride, 0}, s);
+  return hip_status(e, "dn_conv2d_backward_data");
 }
 
 size_t dn_conv2d_wgrad_slab_size(int N, int H, int W, int Cin, int Cout, int ksize) {
@@ -245,24 +308,34 @@ dn_status dn_conv2d_backward_weight(const float* dz, const float* x, int x_strid
 
 dn_status dn_deconv2x2_forward(const float* x, int N, int H, int W, int Cin, const float* w,
                                const float* b, int Cout, float* y, int y_stride, int y_off,
-                               void* stream) {
+                               void* pack_ws, size_t pack_bytes, void* stream) {
   if (!x || !w || !b || !y) return fail(DN_ERR_ARG, "null argument");
-  if (!fwd_supported(G_C1, Cout)) return fail(DN_ERR_ARG, "unsupported Cout");
-  return hip_status(deconv_forward(View{const_cast<float*>(x), Cin, 0}, N, H, W, Cin, w, b, Cout,
-                                   View{y, y_stride, y_off}, (hipStream_t)stream),
-                    "dn_deconv2x2_forward");
+  if (N < 1 || H < 1 || W < 1 || Cin < 1 || y_stride < y_off + Cout)
+    return fail(DN_ERR_ARG, "bad shape");
+  if (dn_status st = need_pack(pack_ws, pack_bytes, dn_deconv2x2_pack_size(Cin, Cout, 0))) return st;
+  hipStream_t s = (hipStream_t)stream;
+  float* wp = static_cast<float*>(pack_ws);
+  hipError_t e = pack_deconv_fwd(w, Cin, Cout, wp, s);
+  if (e == hipSuccess)
+    e = deconv_forward(View{const_cast<float*>(x), Cin, 0}, N, H, W, Cin, wp, b, Cout,
+                       View{y, y_stride, y_off}, s);
+  return hip_status(e, "dn_deconv2x2_forward");
 }
 
 dn_status dn_deconv2x2_backward_data(const float* dy, int dy_stride, int N, int H, int W, int Cout,
                                      const float* w, int Cin, const float* mask, float* dx,
-                                     void* stream) {
+                                     void* pack_ws, size_t pack_bytes, void* stream) {
   if (!dy || !w || !dx) return fail(DN_ERR_ARG, "null argument");
-  if (!fwd_supported(G_DN2, Cin)) return fail(DN_ERR_ARG, "unsupported Cin");
-  return hip_status(deconv_dgrad(View{const_cast<float*>(dy), dy_stride, 0}, N, H, W, Cout, w, Cin,
-                                 View{const_cast<float*>(mask), Cin, 0},
-                                 mask ? EPI_MASK : EPI_PLAIN, View{dx, Cin, 0},
-                                 (hipStream_t)stream),
-                    "dn_deconv2x2_backward_data");
+  if (N < 1 || H < 1 || W < 1 || Cout < 1 || dy_stride < Cout) return fail(DN_ERR_ARG, "bad shape");
+  if (dn_status st = need_pack(pack_ws, pack_bytes, dn_deconv2x2_pack_size(Cin, Cout, 1))) return st;
+  hipStream_t s = (hipStream_t)stream;
+  float* wp = static_cast<float*>(pack_ws);
+  hipError_t e = pack_deconv_dgrad(w, Cout, Cin, wp, s);
+  if (e == hipSuccess)
+    e = deconv_dgrad(View{const_cast<float*>(dy), dy_stride, 0}, N, H, W, Cout, wp, Cin,
+                     View{const_cast<float*>(mask), Cin, 0}, mask ? EPI_MASK : EPI_PLAIN,
+                     View{dx, Cin, 0}, s);
+  return hip_status(e, "dn_deconv2x2_backward_data");
 }
 
 size_t dn_deconv2x2_wgrad_slab_size(int N, int H, int W, int Cin, int Cout) {

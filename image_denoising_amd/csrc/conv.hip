@@ -32,12 +32,17 @@ constexpr int cround(int v, int mod, int res) { return v + (((res - v % mod) % m
 //   Workgroup = 4 waves; tile = TH x 16 output pixels x NP output channels.
 //   Wave w owns tile rows [w*MT, w*MT+MT); fragment m = one row of 16 pixels (MFMA M),
 //   fragment n = 16 output channels (MFMA N).  K = taps x input channels, staged through
-//   LDS 8 channels at a time: input tile with halo as [channel][pixel], weights as
-//   [tap][channel][n].  MFMA k-lane group g (lane>>4) takes channel 4s+g of the stage.
+//   LDS KC channels at a time:
+//     - weights come pre-packed (k_pack) as one LDS image per chunk, [tap][k][n] padded to
+//       WNS, and are copied by global_load_lds_dwordx4 into a double-buffered slab;
+//     - the input tile (with halo) is prefetched into registers (float4 along channels)
+//       while the previous chunk computes, then written channel-major [k][pixel].
+//   MFMA k-lane group g (lane>>4) takes channel 4s+g of the stage.
 // ------------------------------------------------------------------------------------
 template <int GATHER, int NT, int MT>
 struct FwdCfg {
-  static constexpr int TW = 16, TH = 4 * MT, KC = 8;
+  static constexpr int TW = 16, TH = 4 * MT;
+  static constexpr int KC = GATHER == G_C1 ? 32 : (NT >= 9 ? 4 : 8);
   static constexpr int TAPS = GATHER == G_C3 ? 9 : (GATHER == G_DN2 ? 4 : 1);
   static constexpr int IH = GATHER == G_C3 ? TH + 2 : (GATHER == G_DN2 ? 2 * TH : TH);
   static constexpr int IW = GATHER == G_C3 ? TW + 2 : (GATHER == G_DN2 ? 2 * TW : TW);
@@ -45,15 +50,25 @@ struct FwdCfg {
   static constexpr int XCS = cround(IH * IW, 32, GATHER == G_DN2 ? 1 : 16);
   static constexpr int NP = NT * 16;
   static constexpr int WNS = cround(NP, 32, 16);
-  static constexpr int LX = KC * XCS, LW = TAPS * KC * WNS;
+  static constexpr int LW = (TAPS * KC * WNS + 255) / 256 * 256;  // one chunk's weight image
+  static constexpr int LX = KC * XCS;
+  static constexpr int QPP = KC / 4;                              // float4 quads per pixel
+  static constexpr int XQ = IH * IW * QPP;
+  static constexpr int XITEMS = (XQ + 255) / 256;
 };
 
+__device__ __forceinline__ void glds16(const float* g, float* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
 template <int GATHER, int NT, int MT>
-__global__ __launch_bounds__(256) void k_fwd(FwdArgs a) {
+__global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a) {
   using C = FwdCfg<GATHER, NT, MT>;
-  __shared__ float lds[C::LX + C::LW];
+  __shared__ __attribute__((aligned(16))) float lds[C::LX + 2 * C::LW];
   float* lx = lds;
-  float* lw = lds + C::LX;
+  float* lw0 = lds + C::LX;
+  float* lw1 = lw0 + C::LW;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
@@ -64,7 +79,9 @@ __global__ __launch_bounds__(256) void k_fwd(FwdArgs a) {
   const int iy0 = GATHER == G_C3 ? ty0 - 1 : (GATHER == G_DN2 ? 2 * ty0 : ty0);
   const int ix0 = GATHER == G_C3 ? tx0 - 1 : (GATHER == G_DN2 ? 2 * tx0 : tx0);
   const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
-  const long wz = (long)blockIdx.z * a.wv.sZ + a.wv.off;
+  const float* wp = a.wp + (long)blockIdx.z * a.wp_z;
+  const bool vec = ((a.in_stride | a.in_off) & 3) == 0;
+  const int nch = (a.K + C::KC - 1) / C::KC;
 
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -72,32 +89,62 @@ __global__ __launch_bounds__(256) void k_fwd(FwdArgs a) {
 #pragma unroll
     for (int q = 0; q < NT; ++q) acc[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int k0 = 0; k0 < a.K; k0 += C::KC) {
-    __syncthreads();
-    // stage the input tile (with halo), channel-major, zero outside the image / past K
-    for (int e = tid; e < C::KC * C::IH * C::IW; e += 256) {
-      const int kk = e % C::KC, pix = e / C::KC;
-      const int iy = pix / C::IW, ix = pix - iy * C::IW;
-      const int gy = iy0 + iy, gx = ix0 + ix;
-      float v = 0.f;
-      if (k0 + kk < a.K && gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt)
-        v = inb[((long)gy * a.IWt + gx) * a.in_stride + k0 + kk];
-      lx[kk * C::XCS + pix] = v;
-    }
-    // stage the weight slab [tap][k][n]
-    for (int e = tid; e < C::TAPS * C::KC * C::NP; e += 256) {
-      const int nn = e % C::NP, r = e / C::NP;
-      const int kk = r % C::KC, t = r / C::KC;
-      const int k = k0 + kk;
-      float v = 0.f;
-      if (k < a.K && nn < a.NOUT) {
-        const int tm = a.wv.flip ? (a.wv.taps - 1 - t) : t;
-        v = a.wv.w[wz + (long)k * a.wv.sK + (long)nn * a.wv.sN + (long)tm * a.wv.sT];
+  float4 xr[C::XITEMS];
+  auto load_x = [&](int k0) {
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * 256;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < C::XQ) {
+        const int q = e % C::QPP, pix = e / C::QPP;
+        const int iy = pix / C::IW, ix = pix - iy * C::IW;
+        const int gy = iy0 + iy, gx = ix0 + ix, k = k0 + 4 * q;
+        if (gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt && k < a.K) {
+          const float* p = inb + ((long)gy * a.IWt + gx) * a.in_stride + k;
+          if (vec && k + 4 <= a.K) {
+            v = *reinterpret_cast<const float4*>(p);
+          } else {
+            v.x = p[0];
+            if (k + 1 < a.K) v.y = p[1];
+            if (k + 2 < a.K) v.z = p[2];
+            if (k + 3 < a.K) v.w = p[3];
+          }
+        }
       }
-      lw[(t * C::KC + kk) * C::WNS + nn] = v;
+      xr[it] = v;
     }
-    __syncthreads();
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * 256;
+      if (e < C::XQ) {
+        const int q = e % C::QPP, pix = e / C::QPP;
+        float* d = lx + 4 * q * C::XCS + pix;
+        d[0] = xr[it].x;
+        d[C::XCS] = xr[it].y;
+        d[2 * C::XCS] = xr[it].z;
+        d[3 * C::XCS] = xr[it].w;
+      }
+    }
+  };
+  auto load_w = [&](int c, float* dst) {
+    const float* src = wp + (long)c * C::LW;
+#pragma unroll
+    for (int p = wave; p < C::LW / 256; p += 4) glds16(src + p * 256 + lane * 4, dst + p * 256);
+  };
 
+  load_w(0, lw0);
+  load_x(0);
+  store_x();
+  __syncthreads();
+
+  for (int c = 0; c < nch; ++c) {
+    const float* lw = (c & 1) ? lw1 : lw0;
+    if (c + 1 < nch) {  // prefetch the next chunk while this one computes
+      load_w(c + 1, (c & 1) ? lw0 : lw1);
+      load_x((c + 1) * C::KC);
+    }
 #pragma unroll
     for (int t = 0; t < C::TAPS; ++t) {
 #pragma unroll
@@ -121,6 +168,9 @@ __global__ __launch_bounds__(256) void k_fwd(FwdArgs a) {
           for (int q = 0; q < NT; ++q) acc[m][q] = mfma4(av[m], bv[q], acc[m][q]);
       }
     }
+    __syncthreads();  // all waves done with lx and this weight buffer
+    if (c + 1 < nch) store_x();
+    __syncthreads();  // next chunk's input tile written, its weight DMA landed (vmcnt(0))
   }
 
   // epilogue: C/D map of 16x16 MFMA: col (n) = lane&15, row (pixel x) = 4*(lane>>4) + reg
@@ -162,6 +212,27 @@ __global__ __launch_bounds__(256) void k_fwd(FwdArgs a) {
         a.out[oi] = v;
       }
     }
+  }
+}
+
+// Weight packing: the per-chunk LDS image [chunk][tap][k][n] (zero padded) of a strided
+// weight view, one image set per blockIdx.z value (deconv forward: one per (a,b)).
+__global__ __launch_bounds__(256) void k_pack(WView wv, int K, int NOUT, int KC, int TAPS, int WNS,
+                                              int LW, int nch, int nz, float* __restrict__ out) {
+  const long per_z = (long)nch * LW, total = per_z * nz;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int z = (int)(e / per_z);
+    const long r = e - (long)z * per_z;
+    const int c = (int)(r / LW), q = (int)(r % LW);
+    float v = 0.f;
+    if (q < TAPS * KC * WNS) {
+      const int t = q / (KC * WNS), kk = (q / WNS) % KC, nn = q % WNS, k = c * KC + kk;
+      if (k < K && nn < NOUT) {
+        const int tm = wv.flip ? (wv.taps - 1 - t) : t;
+        v = wv.w[wv.off + (long)z * wv.sZ + (long)k * wv.sK + (long)nn * wv.sN + (long)tm * wv.sT];
+      }
+    }
+    out[e] = v;
   }
 }
 
@@ -320,12 +391,55 @@ static hipError_t run_fwd(const FwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int GATHER, int NT, int MT>
+static void geom(FwdGeom& g) {
+  using C = FwdCfg<GATHER, NT, MT>;
+  g.KC = C::KC; g.TAPS = C::TAPS; g.WNS = C::WNS; g.LW = C::LW;
+}
+
 bool fwd_supported(int gather, int nout) {
   const int nt = (nout + 15) / 16;
   if (gather == G_C3) return nt == 3 || nt == 6 || nt == 9;
   if (gather == G_C1) return nt == 1 || nt == 3 || nt == 6;
   if (gather == G_DN2) return nt == 3 || nt == 6;
   return false;
+}
+
+bool fwd_geometry(int gather, int nout, FwdGeom& g) {
+  const int nt = (nout + 15) / 16;
+  if (gather == G_C3) {
+    if (nt == 3) { geom<G_C3, 3, 4>(g); return true; }
+    if (nt == 6) { geom<G_C3, 6, 4>(g); return true; }
+    if (nt == 9) { geom<G_C3, 9, 2>(g); return true; }
+  } else if (gather == G_C1) {
+    if (nt == 1) { geom<G_C1, 1, 4>(g); return true; }
+    if (nt == 3) { geom<G_C1, 3, 4>(g); return true; }
+    if (nt == 6) { geom<G_C1, 6, 4>(g); return true; }
+  } else if (gather == G_DN2) {
+    if (nt == 3) { geom<G_DN2, 3, 4>(g); return true; }
+    if (nt == 6) { geom<G_DN2, 6, 4>(g); return true; }
+  }
+  return false;
+}
+
+long pack_floats(int gather, int nout, int K, int nz) {
+  FwdGeom g;
+  if (!fwd_geometry(gather, nout, g)) return -1;
+  const long nch = (K + g.KC - 1) / g.KC;
+  return nch * g.LW * nz;
+}
+
+hipError_t launch_pack(int gather, const WView& wv, int K, int nout, int nz, float* out,
+                       hipStream_t s) {
+  FwdGeom g;
+  if (!fwd_geometry(gather, nout, g)) return hipErrorInvalidValue;
+  const int nch = (K + g.KC - 1) / g.KC;
+  const long total = (long)nch * g.LW * nz;
+  long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_pack, dim3((unsigned)blocks), dim3(256), 0, s, wv, K, nout, g.KC, g.TAPS,
+                     g.WNS, g.LW, nch, nz, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s) {

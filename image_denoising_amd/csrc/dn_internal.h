@@ -46,7 +46,7 @@ struct FwdArgs {
   const float* in; int in_stride, in_off; int IHt, IWt;  // NHWC input, spatial dims
   int N, OH, OW;                                         // output domain (deconv: input res)
   int K, NOUT;                                           // reduction channels, output channels
-  WView wv;
+  const float* wp; long wp_z;                            // packed weights (k_pack), z stride
   const float* bias;
   int epi;
   float* out; int out_stride, out_off; int out_layout;
@@ -62,7 +62,14 @@ struct WgradArgs {
   int wlayout;                          // 0: [co][ci][t]  1: [ci][co][t]
 };
 
+// geometry of the packed per-chunk weight image of the forward-family kernel
+struct FwdGeom { int KC, TAPS, WNS, LW; };
+
 // ---- launchers (conv.hip) ----
+bool fwd_geometry(int gather, int nout, FwdGeom& g);
+long pack_floats(int gather, int nout, int K, int nz);  // floats of a packed weight set
+hipError_t launch_pack(int gather, const WView& wv, int K, int nout, int nz, float* out,
+                       hipStream_t s);
 hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s);
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
 hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s);

@@ -328,7 +328,7 @@ __global__ void k_structure_finalize(const double* __restrict__ partials, int nb
 
 // ------------------------------------------------------------------------------------
 // Adam (torch/optim/adam.py _single_tensor_adam, amsgrad=False, weight_decay=0):
-//   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, value=1-b2)
+//   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, value=1-b2)   (lerp as ATen's vectorised fmadd)
 //   denom = v.sqrt() / sqrt(bc2) + eps; p.addcdiv_(m, denom, value=-lr/bc1)
 // Contraction is disabled so every op rounds like the eager CPU kernels.
 // ------------------------------------------------------------------------------------
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     const float gg = gscale == 1.f ? g[i] : g[i] * gscale;
     const float mo = m[i];
-    const float mm = mo + w1 * (gg - mo);       // lerp, weight < 0.5 branch
+    const float mm = fmaf(w1, gg - mo, mo);     // ATen lerp_vec: fmadd(weight, end-start, start)
     const float vv = v[i] * b2 + (w2 * gg) * gg;  // addcmul: self + (value*t1)*t2
     const float denom = sqrtf(vv) / bc2s + eps;
     p[i] = p[i] + (-step_size * mm) / denom;      // addcdiv: self + (value*t1)/t2

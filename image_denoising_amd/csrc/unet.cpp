@@ -71,6 +71,8 @@ bool build_params(const dn_unet_cfg& c, ParamLayout& P, std::string& err) {
 // ------------------------------------------------------------------------------------
 // workspace plan (offsets in floats, 256-byte aligned)
 // ------------------------------------------------------------------------------------
+int dgrad_nout(const Plan& p, int i);
+
 bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, std::string& err) {
   if (N < 1 || H < 32 || W < 32 || (H % 32) || (W % 32)) {
     err = "N >= 1 and H, W must be positive multiples of 32 (5 pooling levels)";
@@ -106,6 +108,22 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
   p.d1b = alloc(0, 96);
   p.na = alloc(0, 96);
   p.nb = alloc(0, 96);
+  // packed forward weights (rebuilt by every dn_unet_forward from the flat parameters)
+  auto alloc_f = [&](long n) {
+    long o = off;
+    off += (n + 63) / 64 * 64;
+    return o;
+  };
+  for (int i = 0; i < NL; ++i) {
+    const Layer& L = p.P.L[i];
+    const long n = L.deconv ? deconv_fwd_pack_size(L.cin, L.cout)
+                            : conv_fwd_pack_size(L.cin, L.cout, L.k);
+    if (n < 0) {
+      err = std::string("no forward kernel tile for layer ") + kNames[i];
+      return false;
+    }
+    p.packF[i] = alloc_f(n);
+  }
   p.fwd_floats = off;
   if (bwd) {
     p.g_nb = alloc(0, 96);
@@ -123,6 +141,18 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
     p.g_p5 = alloc(5, nf);
     p.g_a0 = alloc(0, nf);
     p.g_a1 = alloc(0, nf);
+    for (int i = 0; i < NL; ++i) {  // packed data-gradient weights
+      const Layer& L = p.P.L[i];
+      long n = 0;
+      if (i == ENC0) n = 0;  // the network input needs no gradient
+      else if (L.deconv) n = deconv_dgrad_pack_size(L.cout, L.cin);
+      else n = conv_dgrad_pack_size(L.cout, dgrad_nout(p, i), L.k);
+      if (n < 0) {
+        err = std::string("no data-gradient kernel tile for layer ") + kNames[i];
+        return false;
+      }
+      p.packB[i] = alloc_f(n);
+    }
     // slab: max over layers of splits * (W + b)
     long slab = 0;
     for (int i = 0; i < NL; ++i) {
@@ -142,6 +172,12 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
   p.total_floats = off;
   p.with_bwd = bwd;
   return true;
+}
+
+// channels of the data gradient a layer's backward must produce
+int dgrad_nout(const Plan& p, int i) {
+  if (i == D1A) return 2 * p.nf;  // only the up1 part of [up1 | x]
+  return p.P.L[i].cin;
 }
 
 // output level of every layer (deconvs: level of their OUTPUT)
@@ -173,53 +209,85 @@ int layer_level(int i) {
     }                                                                     \
   } while (0)
 
-hipError_t conv_forward(const View& in, int N, int H, int W, int K, const float* w,
+WView conv_fwd_view(const float* w, int K, int ksize) {
+  return ksize == 3 ? WView{w, 0, 9, (long)K * 9, 1, 0, 9, 0} : WView{w, 0, 1, (long)K, 0, 0, 1, 0};
+}
+WView conv_dgrad_view(const float* w, int cin_total, int ksize) {  // flipped + transposed
+  return ksize == 3 ? WView{w, 0, (long)cin_total * 9, 9, 1, 0, 9, 1}
+                    : WView{w, 0, (long)cin_total, 1, 0, 0, 1, 0};
+}
+WView deconv_fwd_view(const float* w, int cout) { return WView{w, 0, (long)cout * 4, 4, 0, 1, 1, 0}; }
+WView deconv_dgrad_view(const float* w, int cout) { return WView{w, 0, 4, (long)cout * 4, 1, 0, 4, 0}; }
+
+long conv_fwd_pack_size(int K, int cout, int ksize) {
+  return pack_floats(ksize == 3 ? G_C3 : G_C1, cout, K, 1);
+}
+long conv_dgrad_pack_size(int cout, int nout, int ksize) {
+  return pack_floats(ksize == 3 ? G_C3 : G_C1, nout, cout, 1);
+}
+long deconv_fwd_pack_size(int cin, int cout) { return pack_floats(G_C1, cout, cin, 4); }
+long deconv_dgrad_pack_size(int cout, int cin) { return pack_floats(G_DN2, cin, cout, 1); }
+
+hipError_t pack_conv_fwd(const float* w, int K, int cout, int ksize, float* out, hipStream_t s) {
+  return launch_pack(ksize == 3 ? G_C3 : G_C1, conv_fwd_view(w, K, ksize), K, cout, 1, out, s);
+}
+hipError_t pack_conv_dgrad(const float* w, int cin_total, int nout, int cout, int ksize, float* out,
+                           hipStream_t s) {
+  return launch_pack(ksize == 3 ? G_C3 : G_C1, conv_dgrad_view(w, cin_total, ksize), cout, nout, 1,
+                     out, s);
+}
+hipError_t pack_deconv_fwd(const float* w, int cin, int cout, float* out, hipStream_t s) {
+  return launch_pack(G_C1, deconv_fwd_view(w, cout), cin, cout, 4, out, s);
+}
+hipError_t pack_deconv_dgrad(const float* w, int cout, int cin, float* out, hipStream_t s) {
+  return launch_pack(G_DN2, deconv_dgrad_view(w, cout), cout, cin, 1, out, s);
+}
+
+hipError_t conv_forward(const View& in, int N, int H, int W, int K, const float* wp,
                         const float* b, int cout, int ksize, int act, const View& out,
                         int out_layout, hipStream_t s) {
   FwdArgs a{};
   a.in = in.p; a.in_stride = in.stride; a.in_off = in.off; a.IHt = H; a.IWt = W;
   a.N = N; a.OH = H; a.OW = W; a.K = K; a.NOUT = cout;
-  if (ksize == 3) a.wv = WView{w, 0, 9, (long)K * 9, 1, 0, 9, 0};
-  else a.wv = WView{w, 0, 1, (long)K, 0, 0, 1, 0};
+  a.wp = wp; a.wp_z = 0;
   a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
   a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = out_layout;
   return launch_fwd(ksize == 3 ? G_C3 : G_C1, a, s);
 }
 
-// dx (channels [0, nout)) from dz [N,H,W,cout]; weight [cout][cin_total][k][k]
-hipError_t conv_dgrad(const View& dz, int N, int H, int W, int cout, const float* w, int cin_total,
-                      int nout, int ksize, int epi, const View& mask, const View& dx,
-                      hipStream_t s) {
+// dx (channels [0, nout)) from dz [N,H,W,cout]; wp = pack_conv_dgrad(...)
+hipError_t conv_dgrad(const View& dz, int N, int H, int W, int cout, const float* wp, int nout,
+                      int ksize, int epi, const View& mask, const View& dx, hipStream_t s) {
   FwdArgs a{};
   a.in = dz.p; a.in_stride = dz.stride; a.in_off = dz.off; a.IHt = H; a.IWt = W;
   a.N = N; a.OH = H; a.OW = W; a.K = cout; a.NOUT = nout;
-  if (ksize == 3) a.wv = WView{w, 0, (long)cin_total * 9, 9, 1, 0, 9, 1};
-  else a.wv = WView{w, 0, (long)cin_total, 1, 0, 0, 1, 0};
+  a.wp = wp; a.wp_z = 0;
   a.bias = nullptr; a.epi = epi;
   a.out = dx.p; a.out_stride = dx.stride; a.out_off = dx.off; a.out_layout = OUT_NHWC;
   a.mask = mask.p; a.mask_stride = mask.stride; a.mask_off = mask.off;
   return launch_fwd(ksize == 3 ? G_C3 : G_C1, a, s);
 }
 
-// ConvTranspose2d(cin, cout, 2, 2): x [N,h,w,cin] -> out at (2y+a, 2x+b)
-hipError_t deconv_forward(const View& x, int N, int h, int w, int cin, const float* wt,
+// ConvTranspose2d(cin, cout, 2, 2): x [N,h,w,cin] -> out at (2y+a, 2x+b); wp = pack_deconv_fwd
+hipError_t deconv_forward(const View& x, int N, int h, int w, int cin, const float* wp,
                           const float* b, int cout, const View& out, hipStream_t s) {
   FwdArgs a{};
   a.in = x.p; a.in_stride = x.stride; a.in_off = x.off; a.IHt = h; a.IWt = w;
   a.N = N; a.OH = h; a.OW = w; a.K = cin; a.NOUT = cout;
-  a.wv = WView{wt, 0, (long)cout * 4, 4, 0, 1, 1, 0};
+  a.wp = wp; a.wp_z = pack_floats(G_C1, cout, cin, 1);
   a.bias = b; a.epi = EPI_BIAS;
   a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = OUT_UP2;
   return launch_fwd(G_C1, a, s);
 }
 
-// dx [N,h,w,cin] = sum_{ab,co} dy[2y+a][2x+b][co] * W[ci][co][ab]  (* leaky'(mask))
-hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const float* wt, int cin,
+// dx [N,h,w,cin] = sum_{ab,co} dy[2y+a][2x+b][co] * W[ci][co][ab]  (* leaky'(mask));
+// wp = pack_deconv_dgrad
+hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const float* wp, int cin,
                         const View& mask, int epi, const View& dx, hipStream_t s) {
   FwdArgs a{};
   a.in = dy.p; a.in_stride = dy.stride; a.in_off = dy.off; a.IHt = 2 * h; a.IWt = 2 * w;
   a.N = N; a.OH = h; a.OW = w; a.K = cout; a.NOUT = cin;
-  a.wv = WView{wt, 0, 4, (long)cout * 4, 1, 0, 4, 0};
+  a.wp = wp; a.wp_z = 0;
   a.bias = nullptr; a.epi = epi;
   a.out = dx.p; a.out_stride = dx.stride; a.out_off = dx.off; a.out_layout = OUT_NHWC;
   a.mask = mask.p; a.mask_stride = mask.stride; a.mask_off = mask.off;
@@ -249,10 +317,16 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   const int N = p.N, nf = p.nf, C = p.C;
   auto H = [&](int l) { return p.H >> l; };
   auto Wd = [&](int l) { return p.W >> l; };
-  auto Wt = [&](int i) { return prm + p.P.L[i].woff; };
+  auto Wt = [&](int i) { return ws + p.packF[i]; };  // packed forward weights
   auto Bs = [&](int i) { return prm + p.P.L[i].woff + p.P.L[i].wcount; };
   auto V = [&](long off, int stride, int coff = 0) { return View{ws + off, stride, coff}; };
 
+  for (int i = 0; i < NL; ++i) {  // pack the weights into the kernels' per-chunk LDS images
+    const Layer& L = p.P.L[i];
+    const float* w = prm + L.woff;
+    if (L.deconv) DN_TRY(pack_deconv_fwd(w, L.cin, L.cout, ws + p.packF[i], s));
+    else DN_TRY(pack_conv_fwd(w, L.cin, L.cout, L.k, ws + p.packF[i], s));
+  }
   // pool0 = x: stored as channels [2nf, 2nf+C) of the up1 concat buffer
   DN_TRY(launch_nchw_to_slice(x, N, C, p.H, p.W, ws + p.c1, p.c1s, 2 * nf, s));
   DN_TRY(conv_forward(V(p.c1, p.c1s, 2 * nf), N, H(0), Wd(0), C, Wt(ENC0), Bs(ENC0), nf, 3, 1,
@@ -264,8 +338,6 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // enc_conv2..5 + pool2..5 (pool_k -> skip slice of c_{k+1}; pool5 -> p5)
   for (int l = 1; l <= 4; ++l) {
     const int li = ENC2 + (l - 1);
-    const int skip_off = (l == 4) ? nf : 2 * nf;  // where p_l lives inside c_l
-    (void)skip_off;
     const View in = (l == 4) ? V(p.c[4], p.cs[4], nf) : V(p.c[l], p.cs[l], 2 * nf);
     DN_TRY(conv_forward(in, N, H(l), Wd(l), nf, Wt(li), Bs(li), nf, 3, 1, V(p.a[l], nf), OUT_NHWC,
                         s));
@@ -282,7 +354,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // decoder: up5 (a6 -> c5[0:nf]); dec5a/b at level 4
   DN_TRY(deconv_forward(V(p.a6, nf), N, H(5), Wd(5), nf, Wt(UP5), Bs(UP5), nf, V(p.c[4], p.cs[4], 0),
                         s));
-  const int up_idx[5] = {0, UP2, UP3, UP4, UP5};
+  const int up_idx[6] = {0, UP1, UP2, UP3, UP4, UP5};  // up_idx[k]: level k -> level k-1
   const int da_idx[5] = {0, D2A, D3A, D4A, D5A};
   for (int l = 4; l >= 1; --l) {
     if (l < 4) {  // up_{l+1}: d_{l+1}b -> c_l[0:2nf]
@@ -322,10 +394,16 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   const int N = p.N, nf = p.nf, C = p.C;
   auto H = [&](int l) { return p.H >> l; };
   auto Wd = [&](int l) { return p.W >> l; };
-  auto Wt = [&](int i) { return prm + p.P.L[i].woff; };
+  auto Wt = [&](int i) { return ws + p.packB[i]; };  // packed data-gradient weights
   auto G = [&](int i) { return dprm + p.P.L[i].woff; };
   auto V = [&](long off, int stride, int coff = 0) { return View{ws + off, stride, coff}; };
   float* slab = ws + p.slab;
+  for (int i = ENC1; i < NL; ++i) {  // flipped/transposed weight images for the data gradients
+    const Layer& L = p.P.L[i];
+    const float* w = prm + L.woff;
+    if (L.deconv) DN_TRY(pack_deconv_dgrad(w, L.cout, L.cin, ws + p.packB[i], s));
+    else DN_TRY(pack_conv_dgrad(w, L.cin, dgrad_nout(p, i), L.cout, L.k, ws + p.packB[i], s));
+  }
   const View none{nullptr, 0, 0};
   const int OC = p.OC;
 
@@ -338,24 +416,24 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   }
   // nin_c (1x1, no act): wgrad + dgrad (-> g_nb, masked by nb)
   DN_TRY(wgrad(W_C1, dyv, V(p.nb, 96), N, H(0), Wd(0), OC, 96, G(NINC), slab, p.splits[NINC], s));
-  DN_TRY(conv_dgrad(dyv, N, H(0), Wd(0), OC, Wt(NINC), 96, 96, 1, EPI_MASK, V(p.nb, 96),
+  DN_TRY(conv_dgrad(dyv, N, H(0), Wd(0), OC, Wt(NINC), 96, 1, EPI_MASK, V(p.nb, 96),
                     V(p.g_nb, 96), s));
   DN_TRY(wgrad(W_C1, V(p.g_nb, 96), V(p.na, 96), N, H(0), Wd(0), 96, 96, G(NINB), slab,
                p.splits[NINB], s));
-  DN_TRY(conv_dgrad(V(p.g_nb, 96), N, H(0), Wd(0), 96, Wt(NINB), 96, 96, 1, EPI_MASK, V(p.na, 96),
+  DN_TRY(conv_dgrad(V(p.g_nb, 96), N, H(0), Wd(0), 96, Wt(NINB), 96, 1, EPI_MASK, V(p.na, 96),
                     V(p.g_na, 96), s));
   DN_TRY(wgrad(W_C1, V(p.g_na, 96), V(p.d1b, 96), N, H(0), Wd(0), 96, 96, G(NINA), slab,
                p.splits[NINA], s));
-  DN_TRY(conv_dgrad(V(p.g_na, 96), N, H(0), Wd(0), 96, Wt(NINA), 96, 96, 1, EPI_MASK,
+  DN_TRY(conv_dgrad(V(p.g_na, 96), N, H(0), Wd(0), 96, Wt(NINA), 96, 1, EPI_MASK,
                     V(p.d1b, 96), V(p.g_d1b, 96), s));
   DN_TRY(wgrad(W_C3, V(p.g_d1b, 96), V(p.d1a, 96), N, H(0), Wd(0), 96, 96, G(D1B), slab,
                p.splits[D1B], s));
-  DN_TRY(conv_dgrad(V(p.g_d1b, 96), N, H(0), Wd(0), 96, Wt(D1B), 96, 96, 3, EPI_MASK,
+  DN_TRY(conv_dgrad(V(p.g_d1b, 96), N, H(0), Wd(0), 96, Wt(D1B), 96, 3, EPI_MASK,
                     V(p.d1a, 96), V(p.g_d1a, 96), s));
   DN_TRY(wgrad(W_C3, V(p.g_d1a, 96), V(p.c1, p.c1s), N, H(0), Wd(0), 96, p.c1s, G(D1A), slab,
                p.splits[D1A], s));
   // only the up1 part of the concat needs a gradient (pool0 is the network input)
-  DN_TRY(conv_dgrad(V(p.g_d1a, 96), N, H(0), Wd(0), 96, Wt(D1A), p.c1s, 2 * nf, 3, EPI_PLAIN, none,
+  DN_TRY(conv_dgrad(V(p.g_d1a, 96), N, H(0), Wd(0), 96, Wt(D1A), 2 * nf, 3, EPI_PLAIN, none,
                     V(p.g_c1, 2 * nf), s));
 
   // decoder levels 1..4: up_{l}(d_{l+1}b ...) ; here "dU" for level l-1's deconv
@@ -372,11 +450,11 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     const int ia = da_idx[l], ib = ia + 1;
     DN_TRY(wgrad(W_C3, V(p.g_db[l], 2 * nf), V(p.da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, 2 * nf,
                  G(ib), slab, p.splits[ib], s));
-    DN_TRY(conv_dgrad(V(p.g_db[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ib), 2 * nf, 2 * nf, 3,
+    DN_TRY(conv_dgrad(V(p.g_db[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ib), 2 * nf, 3,
                       EPI_MASK, V(p.da[l], 2 * nf), V(p.g_da[l], 2 * nf), s));
     DN_TRY(wgrad(W_C3, V(p.g_da[l], 2 * nf), V(p.c[l], p.cs[l]), N, H(l), Wd(l), 2 * nf, p.cs[l],
                  G(ia), slab, p.splits[ia], s));
-    DN_TRY(conv_dgrad(V(p.g_da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ia), p.cs[l], p.cs[l], 3,
+    DN_TRY(conv_dgrad(V(p.g_da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ia), p.cs[l], 3,
                       EPI_PLAIN, none, V(p.g_c[l], p.cs[l]), s));
     dU = V(p.g_c[l], p.cs[l], 0);  // [u_{l+1} grad | skip grad]
   }
@@ -388,7 +466,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   // enc_conv6 (input p5, level 5)
   DN_TRY(wgrad(W_C3, V(p.g_a6, nf), V(p.p5, nf), N, H(5), Wd(5), nf, nf, G(ENC6), slab,
                p.splits[ENC6], s));
-  DN_TRY(conv_dgrad(V(p.g_a6, nf), N, H(5), Wd(5), nf, Wt(ENC6), nf, nf, 3, EPI_PLAIN, none,
+  DN_TRY(conv_dgrad(V(p.g_a6, nf), N, H(5), Wd(5), nf, Wt(ENC6), nf, 3, EPI_PLAIN, none,
                     V(p.g_p5, nf), s));
   // pool5 backward -> g_a5 (level 4)
   DN_TRY(launch_pool_bwd(ws + p.a[4], N, H(4), Wd(4), nf, ws + p.g_p5, nf, 0, 1, ws + p.g_a[4], s));
@@ -398,7 +476,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     const int skip = (l == 4) ? nf : 2 * nf;
     DN_TRY(wgrad(W_C3, V(p.g_a[l], nf), V(p.c[l], p.cs[l], skip), N, H(l), Wd(l), nf, nf, G(li),
                  slab, p.splits[li], s));
-    DN_TRY(conv_dgrad(V(p.g_a[l], nf), N, H(l), Wd(l), nf, Wt(li), nf, nf, 3, EPI_ACCUM, none,
+    DN_TRY(conv_dgrad(V(p.g_a[l], nf), N, H(l), Wd(l), nf, Wt(li), nf, 3, EPI_ACCUM, none,
                       V(p.g_c[l], p.cs[l], skip), s));
     // pool_l backward: d p_l (skip slice) -> gradient of the level l-1 activation
     if (l > 1) {
@@ -412,7 +490,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   // enc_conv1 (input a0), enc_conv0 (input x = c1 slice; no data gradient needed)
   DN_TRY(wgrad(W_C3, V(p.g_a1, nf), V(p.a0, nf), N, H(0), Wd(0), nf, nf, G(ENC1), slab,
                p.splits[ENC1], s));
-  DN_TRY(conv_dgrad(V(p.g_a1, nf), N, H(0), Wd(0), nf, Wt(ENC1), nf, nf, 3, EPI_MASK, V(p.a0, nf),
+  DN_TRY(conv_dgrad(V(p.g_a1, nf), N, H(0), Wd(0), nf, Wt(ENC1), nf, 3, EPI_MASK, V(p.a0, nf),
                     V(p.g_a0, nf), s));
   DN_TRY(wgrad(W_C3, V(p.g_a0, nf), V(p.c1, p.c1s, 2 * nf), N, H(0), Wd(0), nf, C, G(ENC0), slab,
                p.splits[ENC0], s));

@@ -43,11 +43,13 @@ struct Plan {
   long p5, a6;
   long da[5], db[5];            // decoder conv outputs at levels 1..4
   long d1a, d1b, na, nb;
+  long packF[NL];               // packed forward weight images
   long fwd_floats;
   // gradients
   long g_nb, g_na, g_d1b, g_d1a, g_c1;
   long g_c[5], g_da[5], g_db[5], g_a[5];
   long g_a6, g_p5, g_a0, g_a1;
+  long packB[NL];               // packed data-gradient weight images
   long slab, slab_floats;
   int splits[NL];
   long total_floats;
@@ -57,6 +59,7 @@ void set_error(const std::string& s);
 extern thread_local std::string g_last_error;
 const char* layer_name(int i);
 int layer_level(int i);
+int dgrad_nout(const Plan& p, int i);
 bool build_params(const dn_unet_cfg& c, ParamLayout& P, std::string& err);
 bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, std::string& err);
 dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
@@ -64,15 +67,27 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
 dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* ws,
                         hipStream_t s);
 
-hipError_t conv_forward(const View& in, int N, int H, int W, int K, const float* w,
+WView conv_fwd_view(const float* w, int K, int ksize);
+WView conv_dgrad_view(const float* w, int cin_total, int ksize);
+WView deconv_fwd_view(const float* w, int cout);
+WView deconv_dgrad_view(const float* w, int cout);
+long conv_fwd_pack_size(int K, int cout, int ksize);
+long conv_dgrad_pack_size(int cout, int nout, int ksize);
+long deconv_fwd_pack_size(int cin, int cout);
+long deconv_dgrad_pack_size(int cout, int cin);
+hipError_t pack_conv_fwd(const float* w, int K, int cout, int ksize, float* out, hipStream_t s);
+hipError_t pack_conv_dgrad(const float* w, int cin_total, int nout, int cout, int ksize, float* out,
+                           hipStream_t s);
+hipError_t pack_deconv_fwd(const float* w, int cin, int cout, float* out, hipStream_t s);
+hipError_t pack_deconv_dgrad(const float* w, int cout, int cin, float* out, hipStream_t s);
+hipError_t conv_forward(const View& in, int N, int H, int W, int K, const float* wp,
                         const float* b, int cout, int ksize, int act, const View& out,
                         int out_layout, hipStream_t s);
-hipError_t conv_dgrad(const View& dz, int N, int H, int W, int cout, const float* w, int cin_total,
-                      int nout, int ksize, int epi, const View& mask, const View& dx,
-                      hipStream_t s);
-hipError_t deconv_forward(const View& x, int N, int h, int w, int cin, const float* wt,
+hipError_t conv_dgrad(const View& dz, int N, int H, int W, int cout, const float* wp, int nout,
+                      int ksize, int epi, const View& mask, const View& dx, hipStream_t s);
+hipError_t deconv_forward(const View& x, int N, int h, int w, int cin, const float* wp,
                           const float* b, int cout, const View& out, hipStream_t s);
-hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const float* wt, int cin,
+hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const float* wp, int cin,
                         const View& mask, int epi, const View& dx, hipStream_t s);
 hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, int cout, int cin,
                  float* dwb, float* slab, int splits, hipStream_t s);

@@ -73,6 +73,12 @@ dn_status dn_unet_backward(const dn_unet_cfg* cfg, const float* params, const fl
                            float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
                            void* stream);
 
+/* Debug/introspection: (offset_floats, channel_stride, level) of every NHWC buffer of the
+   workspace plan, in the order c1 a0 a1 c2..c5 a2..a5 p5 a6 d{2..5}a d{2..5}b d1a d1b nin_a nin_b
+   [g_nb g_na g_d1b g_d1a g_c1 g_c2..g_c5 g_d{2..5}a g_d{2..5}b g_a2..g_a5 g_a6 g_p5 g_a0 g_a1]. */
+dn_status dn_unet_debug_buffers(const dn_unet_cfg* cfg, int N, int H, int W, int with_backward,
+                                int64_t* desc, int max_entries, int* n_entries);
+
 /* ---- Neighbor2Neighbor sub-sampler: train.py:134-190 ------------------------------ */
 /* One call replaces generate_mask_pair + 2x generate_subimages (train.py:141-190,
    training_script.md:137-139).  img is NCHW [N,C,H,W]; sub1/sub2 are NCHW [N,C,H/2,W/2].
@@ -125,17 +131,23 @@ dn_status dn_adam_step(float* param, const float* grad, float* exp_avg, float* e
                        float grad_scale, void* stream);
 
 /* ---- op-level entry points (NHWC), used by the tests and the tiled-inference path ---- */
+/* The forward-family kernels read weights pre-packed into per-chunk LDS images; the caller
+   provides that scratch (pack_ws, pack_bytes >= the *_pack_size query).  backward_data=1
+   sizes the flipped/transposed image used by the data gradient. */
+size_t dn_conv2d_pack_size(int Cin, int Cout, int ksize, int backward_data);
+size_t dn_deconv2x2_pack_size(int Cin, int Cout, int backward_data);
 /* 3x3/pad1 (ksize=3) or 1x1 (ksize=1) convolution + bias (+ LeakyReLU(0.2) if act).
    x: [N,H,W,*] with channel stride x_stride; y: [N,H,W,*] stride y_stride.
    w: [Cout,Cin,k,k] (PyTorch OIHW), b: [Cout].  arch_unet.py:65-78 conv_func, :113 act. */
 dn_status dn_conv2d_forward(const float* x, int x_stride, int N, int H, int W, int Cin,
                             const float* w, const float* b, int Cout, int ksize, int act, float* y,
-                            int y_stride, void* stream);
+                            int y_stride, void* pack_ws, size_t pack_bytes, void* stream);
 /* dx = conv^T(dz) [* leaky'(mask)] : data gradient (mask nullable; mask_stride). If accumulate,
    dx += result.  dx stride dx_stride. */
 dn_status dn_conv2d_backward_data(const float* dz, int N, int H, int W, int Cout, const float* w,
                                   int Cin, int ksize, const float* mask, int mask_stride,
-                                  int accumulate, float* dx, int dx_stride, void* stream);
+                                  int accumulate, float* dx, int dx_stride, void* pack_ws,
+                                  size_t pack_bytes, void* stream);
 /* dw [Cout,Cin,k,k] and db [Cout] (contiguous after dw) from dz [N,H,W,Cout] and x.
    slab must hold dn_conv2d_wgrad_slab_size() bytes. */
 size_t dn_conv2d_wgrad_slab_size(int N, int H, int W, int Cin, int Cout, int ksize);
@@ -146,10 +158,10 @@ dn_status dn_conv2d_backward_weight(const float* dz, const float* x, int x_strid
    (written at channel offset y_off of stride y_stride, i.e. directly into a concat buffer). */
 dn_status dn_deconv2x2_forward(const float* x, int N, int H, int W, int Cin, const float* w,
                                const float* b, int Cout, float* y, int y_stride, int y_off,
-                               void* stream);
+                               void* pack_ws, size_t pack_bytes, void* stream);
 dn_status dn_deconv2x2_backward_data(const float* dy, int dy_stride, int N, int H, int W, int Cout,
                                      const float* w, int Cin, const float* mask, float* dx,
-                                     void* stream);
+                                     void* pack_ws, size_t pack_bytes, void* stream);
 size_t dn_deconv2x2_wgrad_slab_size(int N, int H, int W, int Cin, int Cout);
 dn_status dn_deconv2x2_backward_weight(const float* dy, int dy_stride, const float* x, int N, int H,
                                        int W, int Cin, int Cout, float* dwb, void* slab,

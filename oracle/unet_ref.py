@@ -42,42 +42,95 @@ def unflatten(flat: torch.Tensor, in_nc: int, out_nc: int, nf: int = 48):
     return out
 
 
-def forward(flat: torch.Tensor, x: torch.Tensor, in_nc: int, out_nc: int, nf: int = 48):
-    """arch_unet.py:194-260 with the same op order (conv -> LeakyReLU(0.2) -> pool ...)."""
+class _LeakyWithMask(torch.autograd.Function):
+    """LeakyReLU(0.2) whose backward slope is taken from a given (e.g. fp32 device) activation"""
+
+    @staticmethod
+    def forward(ctx, z, ref):
+        ctx.save_for_backward(ref)
+        return F.leaky_relu(z, 0.2)
+
+    @staticmethod
+    def backward(ctx, g):
+        (ref,) = ctx.saved_tensors
+        return torch.where(ref > 0, g, g * 0.2), None
+
+
+class _PoolWithArgmax(torch.autograd.Function):
+    """MaxPool2d(2) whose backward routes to the argmax (first max, row-major) of `ref`"""
+
+    @staticmethod
+    def forward(ctx, a, ref):
+        _, idx = F.max_pool2d(ref, 2, return_indices=True)
+        ctx.save_for_backward(idx)
+        ctx.shape = a.shape
+        return F.max_pool2d(a, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        return F.max_unpool2d(g, idx, 2, output_size=ctx.shape[-2:]), None
+
+
+def forward(flat: torch.Tensor, x: torch.Tensor, in_nc: int, out_nc: int, nf: int = 48,
+            record: dict | None = None, masks: dict | None = None):
+    """arch_unet.py:194-260 with the same op order (conv -> LeakyReLU(0.2) -> pool ...).
+    `record` (optional) receives the intermediate tensors under the workspace names
+    (c1 a0 a1 c2..c5 a2..a5 p5 a6 d2a..d5b d1a d1b na nb) with retain_grad() set.
+    `masks` (optional) maps the post-activation names to tensors (e.g. the device's fp32
+    activations) that decide LeakyReLU slopes and max-pool routing in the backward, so a
+    high-precision backward can be compared with a low-precision one without the slope flips
+    that tiny forward rounding differences cause at pre-activations near zero."""
     P = unflatten(flat, in_nc, out_nc, nf)
-    act = lambda t: F.leaky_relu(t, 0.2)
     conv = lambda t, n, pad=1: F.conv2d(t, P[n][0], P[n][1], 1, pad)
     up = lambda t, skip, n: torch.cat([F.conv_transpose2d(t, P[n][0], P[n][1], 2), skip], 1)
+
+    def act(t, name):
+        if masks is not None:
+            return _LeakyWithMask.apply(t, masks[name].to(t.dtype))
+        return F.leaky_relu(t, 0.2)
+
+    def pool(t, name):
+        if masks is not None:
+            return _PoolWithArgmax.apply(t, masks[name].to(t.dtype))
+        return F.max_pool2d(t, 2)
+
+    def rec(name, t):
+        if record is not None and t.requires_grad:
+            t.retain_grad()
+            record[name] = t
+        return t
+
     pool0 = x
-    h = act(conv(x, "enc_conv0"))
-    h = act(conv(h, "enc_conv1"))
-    h = F.max_pool2d(h, 2)
+    h = rec("a0", act(conv(x, "enc_conv0"), "a0"))
+    h = rec("a1", act(conv(h, "enc_conv1"), "a1"))
+    h = pool(h, "a1")
     pool1 = h
-    h = F.max_pool2d(act(conv(h, "enc_conv2")), 2)
+    h = pool(rec("a2", act(conv(h, "enc_conv2"), "a2")), "a2")
     pool2 = h
-    h = F.max_pool2d(act(conv(h, "enc_conv3")), 2)
+    h = pool(rec("a3", act(conv(h, "enc_conv3"), "a3")), "a3")
     pool3 = h
-    h = F.max_pool2d(act(conv(h, "enc_conv4")), 2)
+    h = pool(rec("a4", act(conv(h, "enc_conv4"), "a4")), "a4")
     pool4 = h
-    h = F.max_pool2d(act(conv(h, "enc_conv5")), 2)
-    h = act(conv(h, "enc_conv6"))
-    h = up(h, pool4, "up5.deconv")
-    h = act(conv(h, "dec_conv5a"))
-    h = act(conv(h, "dec_conv5b"))
-    h = up(h, pool3, "up4.deconv")
-    h = act(conv(h, "dec_conv4a"))
-    h = act(conv(h, "dec_conv4b"))
-    h = up(h, pool2, "up3.deconv")
-    h = act(conv(h, "dec_conv3a"))
-    h = act(conv(h, "dec_conv3b"))
-    h = up(h, pool1, "up2.deconv")
-    h = act(conv(h, "dec_conv2a"))
-    h = act(conv(h, "dec_conv2b"))
-    h = up(h, pool0, "up1.deconv")
-    h = act(conv(h, "dec_conv1a"))
-    h = act(conv(h, "dec_conv1b"))
-    h = act(conv(h, "nin_a", 0))
-    h = act(conv(h, "nin_b", 0))
+    h = rec("p5", pool(rec("a5", act(conv(h, "enc_conv5"), "a5")), "a5"))
+    h = rec("a6", act(conv(h, "enc_conv6"), "a6"))
+    h = rec("c5", up(h, pool4, "up5.deconv"))
+    h = rec("d5a", act(conv(h, "dec_conv5a"), "d5a"))
+    h = rec("d5b", act(conv(h, "dec_conv5b"), "d5b"))
+    h = rec("c4", up(h, pool3, "up4.deconv"))
+    h = rec("d4a", act(conv(h, "dec_conv4a"), "d4a"))
+    h = rec("d4b", act(conv(h, "dec_conv4b"), "d4b"))
+    h = rec("c3", up(h, pool2, "up3.deconv"))
+    h = rec("d3a", act(conv(h, "dec_conv3a"), "d3a"))
+    h = rec("d3b", act(conv(h, "dec_conv3b"), "d3b"))
+    h = rec("c2", up(h, pool1, "up2.deconv"))
+    h = rec("d2a", act(conv(h, "dec_conv2a"), "d2a"))
+    h = rec("d2b", act(conv(h, "dec_conv2b"), "d2b"))
+    h = rec("c1", up(h, pool0, "up1.deconv"))
+    h = rec("d1a", act(conv(h, "dec_conv1a"), "d1a"))
+    h = rec("d1b", act(conv(h, "dec_conv1b"), "d1b"))
+    h = rec("na", act(conv(h, "nin_a", 0), "na"))
+    h = rec("nb", act(conv(h, "nin_b", 0), "nb"))
     return conv(h, "nin_c", 0)
 
 
