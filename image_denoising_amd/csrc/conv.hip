@@ -240,113 +240,177 @@ __global__ __launch_bounds__(256) void k_pack(WView wv, int K, int NOUT, int KC,
 // Weight gradient.  MFMA M = output channels (gradient operand G), N = input channels x
 // taps (input operand X), K = pixels.  One workgroup = all output channels x 16*CIF input
 // channels x all taps, accumulated over a contiguous range of pixel chunks (a "split");
-// it writes its partial dW/db into slab[split].  The slabs are summed by k_reduce.
+// it writes its partial dW/db into slab[split]; k_reduce sums the slabs in a fixed order.
+//   LDS keeps both operands in their natural NHWC order: G chunk [pixel][GS] and the input
+//   chunk (with halo for 3x3) [pixel][XS]; the strides make the 16x16x4 fragment reads
+//   conflict-free.  The next chunk is prefetched into registers (float4 along channels)
+//   while the current one computes.  The bias gradient rides along as one extra MFMA per
+//   k-step against a ones vector (only in the workgroups of input-channel block 0).
 // ------------------------------------------------------------------------------------
 template <int MODE, int MF, int NW, int CIF>
 struct WgCfg {
   static constexpr int TAPS = MODE == W_C3 ? 9 : (MODE == W_UP2 ? 4 : 1);
-  static constexpr int PR = MODE == W_UP2 ? 2 : 4;
-  static constexpr int PC = MODE == W_C3 ? 32 : 16;
-  static constexpr int NPIX = PR * PC;
-  static constexpr int COP = MF * NW * 16;
-  static constexpr int AH = MODE == W_UP2 ? 2 * PR : PR, AW = MODE == W_UP2 ? 2 * PC : PC;
-  static constexpr int ACS = cround(AH * AW, 32, 2);
-  static constexpr int BH = MODE == W_C3 ? PR + 2 : PR, BW = MODE == W_C3 ? PC + 2 : PC;
-  static constexpr int BCS = cround(BH * BW, 32, 2);
+  static constexpr int PR = (MODE == W_UP2 || MF >= 2) ? 1 : 2;
+  static constexpr int PC = MODE == W_UP2 ? 16 : 32;
+  static constexpr int NPIX = PR * PC;                 // K-pixels per chunk
+  static constexpr int COP = MF * NW * 16;             // output channels (padded)
+  static constexpr int GH = MODE == W_UP2 ? 2 * PR : PR, GW = MODE == W_UP2 ? 2 * PC : PC;
+  static constexpr int GS = cround(COP, 32, MODE == W_UP2 ? 8 : 16);
+  static constexpr int XH = MODE == W_C3 ? PR + 2 : PR, XW = MODE == W_C3 ? PC + 2 : PC;
   static constexpr int CIN_T = 16 * CIF;
+  static constexpr int XS = cround(CIN_T, 32, 16);
   static constexpr int NF = TAPS * CIF;
-  static constexpr int LA = COP * ACS, LB = CIN_T * BCS;
+  static constexpr int LG = GH * GW * GS, LX = XH * XW * XS;
   static constexpr int NTHR = NW * 64;
+  static constexpr int GQ = GH * GW * (COP / 4), XQ = XH * XW * (CIN_T / 4);  // float4 items
+  static constexpr int GITEMS = (GQ + NTHR - 1) / NTHR, XITEMS = (XQ + NTHR - 1) / NTHR;
 };
 
 template <int MODE, int MF, int NW, int CIF>
-__global__ __launch_bounds__(NW * 64) void k_wgrad(WgradArgs a) {
+__global__ __launch_bounds__(NW * 64, MF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a) {
   using C = WgCfg<MODE, MF, NW, CIF>;
-  __shared__ float lds[C::LA + C::LB];
-  float* la = lds;
-  float* lb = lds + C::LA;
+  __shared__ __attribute__((aligned(16))) float lds[C::LG + C::LX];
+  float* lg_ = lds;
+  float* lx = lds + C::LG;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int li = lane & 15, lg = lane >> 4;
+  const int li = lane & 15, lgp = lane >> 4;
   const int ci0 = blockIdx.y * C::CIN_T;
   const int ux = (a.KW + C::PC - 1) / C::PC, uy = (a.KH + C::PR - 1) / C::PR;
   const long U = (long)a.N * uy * ux;
   const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
-  const int GH = MODE == W_UP2 ? 2 * a.KH : a.KH, GW = MODE == W_UP2 ? 2 * a.KW : a.KW;
+  const int GHt = MODE == W_UP2 ? 2 * a.KH : a.KH, GWt = MODE == W_UP2 ? 2 * a.KW : a.KW;
   const bool do_bias = blockIdx.y == 0;
+  const bool gvec = ((a.g_stride | a.g_off | a.Cout) & 3) == 0;
+  const bool xvec = ((a.x_stride | a.x_off | a.Cin) & 3) == 0;
 
   f32x4 acc[MF][C::NF];
+  f32x4 accb[MF];
 #pragma unroll
-  for (int i = 0; i < MF; ++i)
+  for (int i = 0; i < MF; ++i) {
+    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int f = 0; f < C::NF; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;
+  }
 
-  for (long u = u_beg; u < u_end; ++u) {
+  float4 gr[C::GITEMS], xr[C::XITEMS];
+  auto load = [&](long u) {
     const int n = (int)(u / ((long)uy * ux));
     const int rem = (int)(u - (long)n * uy * ux);
     const int py0 = (rem / ux) * C::PR, px0 = (rem % ux) * C::PC;
-    __syncthreads();
-    {  // stage G: [co][AH*AW]
-      const int ay0 = MODE == W_UP2 ? 2 * py0 : py0, ax0 = MODE == W_UP2 ? 2 * px0 : px0;
-      const float* gb = a.g + (long)n * GH * GW * a.g_stride + a.g_off;
-      for (int e = tid; e < C::COP * C::AH * C::AW; e += C::NTHR) {
-        const int co = e % C::COP, pix = e / C::COP;
-        const int ay = pix / C::AW, ax = pix - ay * C::AW;
-        const int gy = ay0 + ay, gx = ax0 + ax;
-        float v = 0.f;
-        if (co < a.Cout && gy < GH && gx < GW) v = gb[((long)gy * GW + gx) * a.g_stride + co];
-        la[co * C::ACS + pix] = v;
+    const int gy0 = MODE == W_UP2 ? 2 * py0 : py0, gx0 = MODE == W_UP2 ? 2 * px0 : px0;
+    const float* gb = a.g + (long)n * GHt * GWt * a.g_stride + a.g_off;
+#pragma unroll
+    for (int it = 0; it < C::GITEMS; ++it) {
+      const int e = tid + it * C::NTHR;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < C::GQ) {
+        const int q = e % (C::COP / 4), pix = e / (C::COP / 4);
+        const int y = pix / C::GW, x = pix - y * C::GW;
+        const int gy = gy0 + y, gx = gx0 + x, co = 4 * q;
+        if (gy < GHt && gx < GWt && co < a.Cout) {
+          const float* p = gb + ((long)gy * GWt + gx) * a.g_stride + co;
+          if (gvec) {
+            v = *reinterpret_cast<const float4*>(p);
+          } else {
+            v.x = p[0];
+            if (co + 1 < a.Cout) v.y = p[1];
+            if (co + 2 < a.Cout) v.z = p[2];
+            if (co + 3 < a.Cout) v.w = p[3];
+          }
+        }
+      }
+      gr[it] = v;
+    }
+    const int xy0 = MODE == W_C3 ? py0 - 1 : py0, xx0 = MODE == W_C3 ? px0 - 1 : px0;
+    const float* xb = a.x + (long)n * a.KH * a.KW * a.x_stride + a.x_off;
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * C::NTHR;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < C::XQ) {
+        const int q = e % (C::CIN_T / 4), pix = e / (C::CIN_T / 4);
+        const int y = pix / C::XW, x = pix - y * C::XW;
+        const int gy = xy0 + y, gx = xx0 + x, ci = ci0 + 4 * q;
+        if (gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW && ci < a.Cin) {
+          const float* p = xb + ((long)gy * a.KW + gx) * a.x_stride + ci;
+          if (xvec) {
+            v = *reinterpret_cast<const float4*>(p);
+          } else {
+            v.x = p[0];
+            if (ci + 1 < a.Cin) v.y = p[1];
+            if (ci + 2 < a.Cin) v.z = p[2];
+            if (ci + 3 < a.Cin) v.w = p[3];
+          }
+        }
+      }
+      xr[it] = v;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int it = 0; it < C::GITEMS; ++it) {
+      const int e = tid + it * C::NTHR;
+      if (e < C::GQ) {
+        const int q = e % (C::COP / 4), pix = e / (C::COP / 4);
+        *reinterpret_cast<float4*>(lg_ + pix * C::GS + 4 * q) = gr[it];
       }
     }
-    {  // stage X: [ci][BH*BW] (halo for 3x3)
-      const int by0 = MODE == W_C3 ? py0 - 1 : py0, bx0 = MODE == W_C3 ? px0 - 1 : px0;
-      const float* xb = a.x + (long)n * a.KH * a.KW * a.x_stride + a.x_off;
-      for (int e = tid; e < C::CIN_T * C::BH * C::BW; e += C::NTHR) {
-        const int ci = e % C::CIN_T, pix = e / C::CIN_T;
-        const int by = pix / C::BW, bx = pix - by * C::BW;
-        const int gy = by0 + by, gx = bx0 + bx;
-        float v = 0.f;
-        if (ci0 + ci < a.Cin && gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW)
-          v = xb[((long)gy * a.KW + gx) * a.x_stride + ci0 + ci];
-        lb[ci * C::BCS + pix] = v;
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * C::NTHR;
+      if (e < C::XQ) {
+        const int q = e % (C::CIN_T / 4), pix = e / (C::CIN_T / 4);
+        *reinterpret_cast<float4*>(lx + pix * C::XS + 4 * q) = xr[it];
       }
     }
-    __syncthreads();
-    if (do_bias && tid < C::COP) {
-      for (int p = 0; p < C::AH * C::AW; ++p) bsum += la[tid * C::ACS + p];
-    }
-#pragma unroll 2
+  };
+
+  if (u_beg < u_end) {
+    load(u_beg);
+    store();
+  }
+  __syncthreads();
+  for (long u = u_beg; u < u_end; ++u) {
+    if (u + 1 < u_end) load(u + 1);
+#pragma unroll 1
     for (int ks = 0; ks < C::NPIX / 4; ++ks) {
       const int pr = (4 * ks) / C::PC;
-      const int pc = (4 * ks) % C::PC + lg;  // this lane's pixel (k = lg)
-      float av[MF];
-      if (MODE != W_UP2) {
+      const int pc = (4 * ks) % C::PC + lgp;  // this lane's pixel (k = lane>>4)
+      float av[MF][MODE == W_UP2 ? 4 : 1];
 #pragma unroll
-        for (int i = 0; i < MF; ++i)
-          av[i] = la[((wave * MF + i) * 16 + li) * C::ACS + pr * C::PC + pc];
+      for (int i = 0; i < MF; ++i) {
+        const int co = (wave * MF + i) * 16 + li;
+        if (MODE == W_UP2) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            av[i][t] = lg_[((2 * pr + (t >> 1)) * C::GW + 2 * pc + (t & 1)) * C::GS + co];
+        } else {
+          av[i][0] = lg_[(pr * C::PC + pc) * C::GS + co];
+        }
       }
 #pragma unroll
       for (int f = 0; f < C::NF; ++f) {
         const int tap = f / CIF, cf = f % CIF;
         float bv;
         if (MODE == W_C3)
-          bv = lb[(cf * 16 + li) * C::BCS + (pr + tap / 3) * C::BW + pc + tap % 3];
+          bv = lx[((pr + tap / 3) * C::XW + pc + tap % 3) * C::XS + cf * 16 + li];
         else
-          bv = lb[(cf * 16 + li) * C::BCS + pr * C::BW + pc];
-        if (MODE == W_UP2) {
+          bv = lx[(pr * C::XW + pc) * C::XS + cf * 16 + li];
 #pragma unroll
-          for (int i = 0; i < MF; ++i) {
-            const float at = la[((wave * MF + i) * 16 + li) * C::ACS +
-                                (2 * pr + (tap >> 1)) * C::AW + 2 * pc + (tap & 1)];
-            acc[i][f] = mfma4(at, bv, acc[i][f]);
-          }
-        } else {
+        for (int i = 0; i < MF; ++i)
+          acc[i][f] = mfma4(av[i][MODE == W_UP2 ? tap : 0], bv, acc[i][f]);
+      }
+      if (do_bias) {
 #pragma unroll
-          for (int i = 0; i < MF; ++i) acc[i][f] = mfma4(av[i], bv, acc[i][f]);
-        }
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+          for (int t = 0; t < (MODE == W_UP2 ? 4 : 1); ++t) accb[i] = mfma4(av[i][t], 1.0f, accb[i]);
       }
     }
+    __syncthreads();
+    if (u + 1 < u_end) store();
+    __syncthreads();
   }
 
   float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
@@ -358,7 +422,7 @@ __global__ __launch_bounds__(NW * 64) void k_wgrad(WgradArgs a) {
       const int ci = ci0 + cf * 16 + li;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = (wave * MF + i) * 16 + 4 * lg + r;
+        const int co = (wave * MF + i) * 16 + 4 * lgp + r;
         if (co < a.Cout && ci < a.Cin) {
           const long widx = a.wlayout == 0 ? ((long)co * a.Cin + ci) * C::TAPS + tap
                                            : ((long)ci * a.Cout + co) * C::TAPS + tap;
@@ -366,17 +430,45 @@ __global__ __launch_bounds__(NW * 64) void k_wgrad(WgradArgs a) {
         }
       }
     }
-  if (do_bias && tid < a.Cout) slab[(long)a.Cout * a.Cin * C::TAPS + tid] = bsum;
+  if (do_bias && li == 0) {
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = (wave * MF + i) * 16 + 4 * lgp + r;
+        if (co < a.Cout) slab[(long)a.Cout * a.Cin * C::TAPS + co] = accb[i][r];
+      }
+  }
 }
 
-// out[e] = sum_s slab[s][e], fixed order in s (bit-reproducible)
+// out[e] = sum_s slab[s][e], fixed order in s (bit-reproducible).  Four consecutive
+// elements per thread; loads are batched 8 splits ahead of the (sequential) adds.
 __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ slab, long stride,
                                                 int splits, long n, float* __restrict__ out) {
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= n) return;
-  float s = 0.f;
-  for (int i = 0; i < splits; ++i) s += slab[(long)i * stride + e];
-  out[e] = s;
+  const long e0 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (e0 >= n) return;
+  const int cnt = (int)((n - e0) < 4 ? (n - e0) : 4);
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  int i = 0;
+  for (; i + 8 <= splits; i += 8) {
+    float v[8][4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        v[j][c] = c < cnt ? slab[(long)(i + j) * stride + e0 + c] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s[c] += v[j][c];
+  }
+  for (; i < splits; ++i)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < cnt) s[c] += slab[(long)i * stride + e0 + c];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    if (c < cnt) out[e0 + c] = s[c];
 }
 
 // ------------------------------------------------------------------------------------
@@ -467,6 +559,15 @@ static hipError_t run_wgrad(const WgradArgs& a, int splits, hipStream_t s) {
   return hipGetLastError();
 }
 
+// (CIN_T, PR, PC) of the template that launch_wgrad picks for (mode, cout)
+static void wgrad_tile(int mode, int cout, int& cin_t, int& pr, int& pc) {
+  const int cf = (cout + 15) / 16;
+  pc = 32;
+  if (mode == W_C3) { cin_t = 16; pr = cf >= 6 ? 1 : 2; }
+  else if (mode == W_UP2) { cin_t = 16; pr = 1; pc = 16; }
+  else { cin_t = cf == 1 ? 32 : 96; pr = cf >= 6 ? 1 : 2; }
+}
+
 bool wgrad_supported(int mode, int cout, int cin) {
   (void)cin;
   const int cf = (cout + 15) / 16;
@@ -475,16 +576,18 @@ bool wgrad_supported(int mode, int cout, int cin) {
   return false;
 }
 
+// Splits: enough workgroups for ~one full wave of resident workgroups (about 4 per CU on
+// 256 CUs), at least two pixel chunks each, and a bounded slab.
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
-  (void)Cout;
-  int pr = mode == W_UP2 ? 2 : 4, pc = mode == W_C3 ? 32 : 16;
-  int cin_t = mode == W_C1 ? 96 : 16;
-  long units = (long)N * ((KH + pr - 1) / pr) * ((KW + pc - 1) / pc);
-  long cib = (Cin + cin_t - 1) / cin_t;
-  long want = (2048 + cib - 1) / cib;  // ~2048 workgroups in flight
-  if (want > 256) want = 256;
-  long per = units / want;
-  if (per < 2) want = (units + 1) / 2;  // at least ~2 chunks per split
+  int cin_t, pr, pc;
+  wgrad_tile(mode, Cout, cin_t, pr, pc);
+  const int taps = mode == W_C3 ? 9 : (mode == W_UP2 ? 4 : 1);
+  const long units = (long)N * ((KH + pr - 1) / pr) * ((KW + pc - 1) / pc);
+  const long cib = (Cin + cin_t - 1) / cin_t;
+  long want = (1024 + cib - 1) / cib;
+  const long slab_cap = (16L << 20) / ((long)Cout * Cin * taps + Cout);  // <= 64 MB of slab
+  if (want > slab_cap) want = slab_cap;
+  if (want > units / 2) want = units / 2;
   if (want < 1) want = 1;
   return (int)want;
 }
@@ -495,7 +598,7 @@ hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s)
     if (cf == 3) return run_wgrad<W_C3, 1, 3, 1>(a, splits, s);
     if (cf == 6) return run_wgrad<W_C3, 2, 3, 1>(a, splits, s);
   } else if (mode == W_C1) {
-    if (cf == 1) return run_wgrad<W_C1, 1, 1, 6>(a, splits, s);
+    if (cf == 1) return run_wgrad<W_C1, 1, 1, 2>(a, splits, s);
     if (cf == 6) return run_wgrad<W_C1, 2, 3, 6>(a, splits, s);
   } else if (mode == W_UP2) {
     if (cf == 3) return run_wgrad<W_UP2, 1, 3, 1>(a, splits, s);
@@ -506,7 +609,7 @@ hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s)
 
 hipError_t launch_reduce(const float* slab, long slab_stride, int splits, long n, float* out,
                          hipStream_t s) {
-  const long blocks = (n + 255) / 256;
+  const long blocks = ((n + 3) / 4 + 255) / 256;
   hipLaunchKernelGGL(k_reduce, dim3((unsigned)blocks), dim3(256), 0, s, slab, slab_stride, splits,
                      n, out);
   return hipGetLastError();
