@@ -79,6 +79,18 @@ def time_dominant_kernel(bs, H, W, device, reps=5):
     return ms, flops
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
+    (tools/pmc.sh + tools/pmc_summary.py; FETCH_SIZE x2 gfx950 correction), or None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_dominant.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d.get("traffic_bytes"), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(seconds_budget=20.0):
     """The oracle (torch-CPU restatement of the reference N2N step, validated against the
     reference in tests/test_oracle_golden.py) on a bounded sample of config 1."""
@@ -166,6 +178,7 @@ def main():
         kms, kflops = time_dominant_kernel(bs, H, H, device)
         achieved = kflops / (kms * 1e-3) / 1e12
         step_flops = bs * (unet_fwd_flops(H, H, C) + 3 * unet_fwd_flops(H // 2, H // 2, C))
+        traffic, traffic_src = pmc_traffic() if (bs, H, C) == (64, 256, 1) else (None, None)
         rec = {
             "metric": "training patches/sec (256x256x1, bs=64 per GPU, N2N loss + Adam)",
             "value": round(value, 2), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
@@ -178,7 +191,8 @@ def main():
             "step_frac_of_fp32_peak": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
             "roofline": {"bound": "mfma", "kernel": "k_fwd<G_C3,NT=6,MT=4> (dec_conv1b 96->96 3x3 @256^2)",
                          "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+                         "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                          "avg_launch_ms": round(kms, 4), "flops_per_launch": kflops},
             "loss": loss_v,
         }

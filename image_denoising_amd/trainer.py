@@ -17,9 +17,9 @@ noise and the mask pair of a patch do not depend on the world size.
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
 
 from . import _lib
+from . import dist as dp
 from .arch_unet import UNet
 from .n2n import n2n_loss, n2n_subsample
 from .optim import FlatAdam, lr_at_epoch
@@ -36,12 +36,10 @@ class N2NTrainer:
         self.gamma = gamma
         self.noise_std = noise_std
         self.seed = seed
-        self.distributed = dist.is_available() and dist.is_initialized() if distributed is None \
-            else distributed
-        self.world = dist.get_world_size() if self.distributed else 1
-        self.rank = dist.get_rank() if self.distributed else 0
+        self.distributed = dp.is_distributed() if distributed is None else distributed
+        self.world, self.rank = dp.world_and_rank() if self.distributed else (1, 0)
         if self.distributed:  # identical replicas: broadcast rank 0's initial weights
-            dist.broadcast(net.flat_params, src=0)
+            dp.broadcast_params(net.flat_params)
         self.opt = FlatAdam(net.flat_params, lr=lr)
         self.grad = torch.zeros_like(net.flat_params)
         self.global_step = 0
@@ -78,26 +76,23 @@ class N2NTrainer:
         b = self._buffers(N, C, H, W, clean.device)
         stream = _lib.stream_of(clean)
         step = self.global_step
+        elem_base, cell_base = dp.shard_bases(self.rank, N, C, H, W)
         if noisy is None:
             noisy = b["noisy"]
-            per = C * H * W
-            _lib.call("dn_add_gauss_noise", _lib.ptr(clean), N, per, float(self.noise_std), None,
-                      self.seed, 2 * step, self.rank * N * per, _lib.ptr(noisy), stream)
+            _lib.call("dn_add_gauss_noise", _lib.ptr(clean), N, C * H * W, float(self.noise_std),
+                      None, self.seed, 2 * step, elem_base, _lib.ptr(noisy), stream)
         else:
             noisy = noisy.contiguous()
-        cells = N * (H // 2) * (W // 2)
         sub1, sub2, rd = n2n_subsample(noisy, rd_idx, seed=self.seed + 1, offset=2 * step + 1,
-                                       cell_base=self.rank * cells)
+                                       cell_base=cell_base)
         # no-grad full-resolution pass (training_script.md:141-142)
         self.net._run_forward(noisy, b["den"], b["ws_den"])
         # gradient pass at half resolution (training_script.md:146)
         self.net._run_forward(sub1, b["out"], b["ws_grad"])
         loss3, dout = n2n_loss(b["out"], sub2, b["den"], rd, self.lambda_for(epoch))
         self.net._run_backward(dout, self.grad, b["ws_grad"], N, H // 2, W // 2)
-        scale = 1.0
-        if self.distributed and self.world > 1:
-            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)  # RCCL over xGMI, one per step
-            scale = 1.0 / self.world
+        # RCCL all-reduce(sum) over xGMI, one per step; 1/world folded into Adam
+        scale = dp.allreduce_grads(self.grad) if self.distributed else 1.0
         self.opt.lr = lr_at_epoch(epoch, self.base_lr, self.n_epoch, self.gamma)
         self.opt.step(self.grad, grad_scale=scale)
         self.global_step += 1

@@ -1,0 +1,23 @@
+"""Runs the bench's dominant kernel (dec_conv1b-shaped 3x3 conv 96->96, 64 x 256^2) a few times:
+the workload profiled with rocprofv3 --pmc for the roofline 'traffic' field."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from image_denoising_amd import _lib  # noqa: E402
+
+bs, H, W = 64, 256, 256
+dev = torch.device("cuda", 0)
+x = torch.randn(bs, H, W, 96, device=dev)
+w = torch.randn(96, 96, 3, 3, device=dev) * 0.05
+b = torch.zeros(96, device=dev)
+y = torch.empty_like(x)
+pk = _lib.scratch(_lib.lib().dn_conv2d_pack_size(96, 96, 3, 0), dev)
+s = torch.cuda.current_stream(dev).cuda_stream
+for _ in range(int(os.environ.get("REPS", "4"))):
+    _lib.call("dn_conv2d_forward", x.data_ptr(), 96, bs, H, W, 96, w.data_ptr(), b.data_ptr(), 96,
+              3, 1, y.data_ptr(), 96, pk.data_ptr(), pk.numel(), s)
+torch.cuda.synchronize()
+print("done")
