@@ -55,6 +55,9 @@ struct FwdCfg {
   static constexpr int QPP = KC / 4;                              // float4 quads per pixel
   static constexpr int XQ = IH * IW * QPP;
   static constexpr int XITEMS = (XQ + 255) / 256;
+  static constexpr int PS = NP + 4;             // epilogue staging: pixel stride (floats)
+  static constexpr int LST = 4 * 16 * PS;       // 4 waves x 16 pixels x PS
+  static constexpr int LTOT = (LX + 2 * LW) > LST ? (LX + 2 * LW) : LST;
 };
 
 __device__ __forceinline__ void glds16(const float* g, float* l) {
@@ -65,7 +68,7 @@ __device__ __forceinline__ void glds16(const float* g, float* l) {
 template <int GATHER, int NT, int MT>
 __global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a) {
   using C = FwdCfg<GATHER, NT, MT>;
-  __shared__ __attribute__((aligned(16))) float lds[C::LX + 2 * C::LW];
+  __shared__ __attribute__((aligned(16))) float lds[C::LTOT];
   float* lx = lds;
   float* lw0 = lds + C::LX;
   float* lw1 = lw0 + C::LW;
@@ -173,8 +176,62 @@ __global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a) {
     __syncthreads();  // next chunk's input tile written, its weight DMA landed (vmcnt(0))
   }
 
-  // epilogue: C/D map of 16x16 MFMA: col (n) = lane&15, row (pixel x) = 4*(lane>>4) + reg
+  // epilogue.  C/D map of 16x16 MFMA: col (n) = lane&15, row (pixel x) = 4*(lane>>4) + reg.
   const int ab = blockIdx.z;
+  const bool vec_out = a.out_layout != OUT_NCHW && ((a.out_stride | a.out_off | a.NOUT) & 3) == 0 &&
+                       (a.epi != EPI_MASK || ((a.mask_stride | a.mask_off) & 3) == 0);
+  if (vec_out) {
+    // Stage each 16-pixel row of the wave's tile through LDS and write whole pixels
+    // (NOUT contiguous channels) as float4: 1 KiB contiguous per wave store instead of
+    // 64-byte pieces.  All LDS is free here (the main loop ended on a barrier).
+    float* st = lds + wave * 16 * C::PS;
+    const int NQ = a.NOUT >> 2;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+#pragma unroll
+      for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[(4 * lg + r) * C::PS + q * 16 + li] = acc[m][q][r];
+      __syncthreads();
+      const int gy = ty0 + wave * MT + m;
+      if (gy < a.OH) {
+        for (int e = lane; e < 16 * NQ; e += 64) {
+          const int p = e / NQ, c = 4 * (e - p * NQ);
+          const int gx = tx0 + p;
+          if (gx >= a.OW) continue;
+          float4 v = *reinterpret_cast<const float4*>(st + p * C::PS + c);
+          const long pix = ((long)n * a.OH + gy) * a.OW + gx;
+          if (a.epi == EPI_BIAS || a.epi == EPI_BIAS_ACT) {
+            const float4 b = *reinterpret_cast<const float4*>(a.bias + c);
+            v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+            if (a.epi == EPI_BIAS_ACT) {
+              v.x = v.x > 0.f ? v.x : v.x * 0.2f; v.y = v.y > 0.f ? v.y : v.y * 0.2f;
+              v.z = v.z > 0.f ? v.z : v.z * 0.2f; v.w = v.w > 0.f ? v.w : v.w * 0.2f;
+            }
+          } else if (a.epi == EPI_MASK) {
+            const float4 mk =
+                *reinterpret_cast<const float4*>(a.mask + pix * a.mask_stride + a.mask_off + c);
+            v.x = mk.x > 0.f ? v.x : v.x * 0.2f; v.y = mk.y > 0.f ? v.y : v.y * 0.2f;
+            v.z = mk.z > 0.f ? v.z : v.z * 0.2f; v.w = mk.w > 0.f ? v.w : v.w * 0.2f;
+          }
+          long oi;
+          if (a.out_layout == OUT_NHWC)
+            oi = pix * a.out_stride + a.out_off + c;
+          else
+            oi = (((long)n * 2 * a.OH + 2 * gy + (ab >> 1)) * 2 * a.OW + 2 * gx + (ab & 1)) *
+                     a.out_stride + a.out_off + c;
+          float4* o = reinterpret_cast<float4*>(a.out + oi);
+          if (a.epi == EPI_ACCUM) {
+            const float4 old = *o;
+            v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
+          }
+          *o = v;
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     const int gy = ty0 + wave * MT + m;
@@ -280,9 +337,9 @@ __global__ __launch_bounds__(NW * 64, MF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a)
   const long U = (long)a.N * uy * ux;
   const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
   const int GHt = MODE == W_UP2 ? 2 * a.KH : a.KH, GWt = MODE == W_UP2 ? 2 * a.KW : a.KW;
-  const bool do_bias = blockIdx.y == 0;
-  const bool gvec = ((a.g_stride | a.g_off | a.Cout) & 3) == 0;
-  const bool xvec = ((a.x_stride | a.x_off | a.Cin) & 3) == 0;
+  const bool do_bias = a.bias && blockIdx.y == 0;
+  const bool gvec = ((a.g_stride | a.g_off) & 3) == 0;
+  const bool xvec = ((a.x_stride | a.x_off) & 3) == 0;
 
   f32x4 acc[MF][C::NF];
   f32x4 accb[MF];
@@ -310,7 +367,7 @@ __global__ __launch_bounds__(NW * 64, MF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a)
         const int gy = gy0 + y, gx = gx0 + x, co = 4 * q;
         if (gy < GHt && gx < GWt && co < a.Cout) {
           const float* p = gb + ((long)gy * GWt + gx) * a.g_stride + co;
-          if (gvec) {
+          if (gvec && co + 4 <= a.Cout) {
             v = *reinterpret_cast<const float4*>(p);
           } else {
             v.x = p[0];
@@ -334,7 +391,7 @@ __global__ __launch_bounds__(NW * 64, MF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a)
         const int gy = xy0 + y, gx = xx0 + x, ci = ci0 + 4 * q;
         if (gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW && ci < a.Cin) {
           const float* p = xb + ((long)gy * a.KW + gx) * a.x_stride + ci;
-          if (xvec) {
+          if (xvec && ci + 4 <= a.Cin) {
             v = *reinterpret_cast<const float4*>(p);
           } else {
             v.x = p[0];
@@ -424,8 +481,9 @@ __global__ __launch_bounds__(NW * 64, MF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a)
       for (int r = 0; r < 4; ++r) {
         const int co = (wave * MF + i) * 16 + 4 * lgp + r;
         if (co < a.Cout && ci < a.Cin) {
-          const long widx = a.wlayout == 0 ? ((long)co * a.Cin + ci) * C::TAPS + tap
-                                           : ((long)ci * a.Cout + co) * C::TAPS + tap;
+          const long widx =
+              a.wlayout == 0 ? ((long)co * a.cin_total + a.ci_base + ci) * C::TAPS + tap
+                             : ((long)(a.ci_base + ci) * a.Cout + co) * C::TAPS + tap;
           slab[widx] = acc[i][f][r];
         }
       }
@@ -436,39 +494,151 @@ __global__ __launch_bounds__(NW * 64, MF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = (wave * MF + i) * 16 + 4 * lgp + r;
-        if (co < a.Cout) slab[(long)a.Cout * a.Cin * C::TAPS + co] = accb[i][r];
+        if (co < a.Cout) slab[(long)a.Cout * a.cin_total * C::TAPS + co] = accb[i][r];
       }
   }
 }
 
-// out[e] = sum_s slab[s][e], fixed order in s (bit-reproducible).  Four consecutive
-// elements per thread; loads are batched 8 splits ahead of the (sequential) adds.
+// ------------------------------------------------------------------------------------
+// 3x3 weight gradient, asynchronous staging.  Workgroup = all Cout (16*CO_FR) x CIB = 16*WN
+// input channels x 9 taps; wave (wm, wn) owns CO_FR/WM output-channel fragments x the 16
+// input channels wn x 9 taps = 27 MFMA tiles.  Each K stage is one image row segment of 32
+// pixels: both operands are copied by per-lane-addressed global_load_lds_dwordx4 (padding
+// and out-of-image halo read a zero buffer) into one of two LDS buffers while the other is
+// consumed -- one barrier per stage, no staging registers.
+// ------------------------------------------------------------------------------------
+template <int CO_FR, int WM, int WN>
+struct Wg3Cfg {
+  static constexpr int COUT = 16 * CO_FR, MFW = CO_FR / WM, CIB = 16 * WN;
+  static constexpr int NW = WM * WN, NTHR = 64 * NW;
+  static constexpr int PC = 32, XW = PC + 2, XH = 3;
+  static constexpr int LGF = PC * COUT;                               // G floats per stage
+  static constexpr int LXF = (XH * XW * CIB + 255) / 256 * 256;       // X floats per stage
+  static constexpr int LGP = LGF / 256, LXP = LXF / 256;              // 1 KiB DMA pieces
+  static constexpr int LBUF = LGF + LXF;
+  static_assert(LGF % 256 == 0, "G stage must be whole 1 KiB pieces");
+};
+
+template <int CO_FR, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad3(WgradArgs a) {
+  using C = Wg3Cfg<CO_FR, WM, WN>;
+  __shared__ __attribute__((aligned(16))) float lds[2 * C::LBUF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 15, lgp = lane >> 4;
+  const int ci0 = blockIdx.y * C::CIB;
+  const int ux = (a.KW + C::PC - 1) / C::PC;
+  const long U = (long)a.N * a.KH * ux;
+  const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
+  const bool do_bias = a.bias && blockIdx.y == 0 && wn == 0;
+
+  f32x4 acc[C::MFW][9];
+  f32x4 accb[C::MFW];
+#pragma unroll
+  for (int i = 0; i < C::MFW; ++i) {
+    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  auto issue = [&](long u, float* buf) {
+    const int n = (int)(u / ((long)a.KH * ux));
+    const int rem = (int)(u - (long)n * a.KH * ux);
+    const int py = rem / ux, px0 = (rem % ux) * C::PC;
+    const float* gb = a.g + (long)n * a.KH * a.KW * a.g_stride + a.g_off;
+    for (int p = wave; p < C::LGP; p += C::NW) {
+      const int idx = p * 256 + lane * 4;
+      const int px = idx / C::COUT, co = idx - px * C::COUT;
+      const int gx = px0 + px;
+      const float* src = (gx < a.KW && co < a.Cout)
+                             ? gb + ((long)py * a.KW + gx) * a.g_stride + co : a.zeros;
+      glds16(src, buf + p * 256);
+    }
+    const float* xb = a.x + (long)n * a.KH * a.KW * a.x_stride + a.x_off;
+    for (int p = wave; p < C::LXP; p += C::NW) {
+      const int idx = p * 256 + lane * 4;
+      const int px = idx / C::CIB, q = idx - px * C::CIB;
+      const int yy = px / C::XW, xx = px - yy * C::XW;
+      const int gy = py - 1 + yy, gx = px0 - 1 + xx, ci = ci0 + q;
+      const bool ok = px < C::XH * C::XW && gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW &&
+                      ci < a.Cin;
+      const float* src = ok ? xb + ((long)gy * a.KW + gx) * a.x_stride + ci : a.zeros;
+      glds16(src, buf + C::LGF + p * 256);
+    }
+  };
+
+  if (u_beg < u_end) issue(u_beg, lds);
+  __syncthreads();
+  for (long u = u_beg; u < u_end; ++u) {
+    const int cb = (int)((u - u_beg) & 1);
+    const float* lg_ = lds + cb * C::LBUF;
+    const float* lx = lg_ + C::LGF;
+    if (u + 1 < u_end) issue(u + 1, lds + (cb ^ 1) * C::LBUF);
+#pragma unroll 2
+    for (int ks = 0; ks < C::PC / 4; ++ks) {
+      const int pc = 4 * ks + lgp;  // this lane's pixel (k = lane>>4)
+      float av[C::MFW];
+#pragma unroll
+      for (int i = 0; i < C::MFW; ++i)
+        av[i] = lg_[pc * C::COUT + (wm * C::MFW + i) * 16 + li];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const float bv = lx[((t / 3) * C::XW + pc + t % 3) * C::CIB + wn * 16 + li];
+#pragma unroll
+        for (int i = 0; i < C::MFW; ++i) acc[i][t] = mfma4(av[i], bv, acc[i][t]);
+      }
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < C::MFW; ++i) accb[i] = mfma4(av[i], 1.0f, accb[i]);
+      }
+    }
+    __syncthreads();  // next stage landed (vmcnt(0)); everyone done with this buffer
+  }
+
+  float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
+  const int ci = ci0 + wn * 16 + li;
+#pragma unroll
+  for (int i = 0; i < C::MFW; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = (wm * C::MFW + i) * 16 + 4 * lgp + r;
+        if (co < a.Cout && ci < a.Cin)
+          slab[((long)co * a.cin_total + a.ci_base + ci) * 9 + t] = acc[i][t][r];
+      }
+  if (do_bias && li == 0) {
+#pragma unroll
+    for (int i = 0; i < C::MFW; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = (wm * C::MFW + i) * 16 + 4 * lgp + r;
+        if (co < a.Cout) slab[(long)a.Cout * a.cin_total * 9 + co] = accb[i][r];
+      }
+  }
+}
+
+// out[e] = sum_s slab[s][e] in a fixed order (bit-reproducible): a workgroup owns 64
+// consecutive elements; wave w sums splits w, w+4, w+8, ... in order, then the four wave
+// partials are added in wave order.
 __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ slab, long stride,
                                                 int splits, long n, float* __restrict__ out) {
-  const long e0 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (e0 >= n) return;
-  const int cnt = (int)((n - e0) < 4 ? (n - e0) : 4);
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  int i = 0;
-  for (; i + 8 <= splits; i += 8) {
-    float v[8][4];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        v[j][c] = c < cnt ? slab[(long)(i + j) * stride + e0 + c] : 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) s[c] += v[j][c];
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long e = (long)blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (e < n) {
+    int i = wave;
+    for (; i + 12 < splits; i += 16) {  // four loads in flight per lane
+      const float v0 = slab[(long)i * stride + e], v1 = slab[(long)(i + 4) * stride + e];
+      const float v2 = slab[(long)(i + 8) * stride + e], v3 = slab[(long)(i + 12) * stride + e];
+      s += v0; s += v1; s += v2; s += v3;
+    }
+    for (; i < splits; i += 4) s += slab[(long)i * stride + e];
   }
-  for (; i < splits; ++i)
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      if (c < cnt) s[c] += slab[(long)i * stride + e0 + c];
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-    if (c < cnt) out[e0 + c] = s[c];
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && e < n) out[e] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
 }
 
 // ------------------------------------------------------------------------------------
@@ -536,17 +706,21 @@ hipError_t launch_pack(int gather, const WView& wv, int K, int nout, int nz, flo
 
 hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s) {
   const int nt = (a.NOUT + 15) / 16;
+  // small images: 4-row tiles so that the grid still fills the chip
+  const long big_tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16) *
+                         (a.out_layout == OUT_UP2 ? 4 : 1);
+  const bool small = big_tiles < 1024;
   if (gather == G_C3) {
-    if (nt == 3) return run_fwd<G_C3, 3, 4>(a, s);
-    if (nt == 6) return run_fwd<G_C3, 6, 4>(a, s);
-    if (nt == 9) return run_fwd<G_C3, 9, 2>(a, s);
+    if (nt == 3) return small ? run_fwd<G_C3, 3, 1>(a, s) : run_fwd<G_C3, 3, 4>(a, s);
+    if (nt == 6) return small ? run_fwd<G_C3, 6, 1>(a, s) : run_fwd<G_C3, 6, 4>(a, s);
+    if (nt == 9) return small ? run_fwd<G_C3, 9, 1>(a, s) : run_fwd<G_C3, 9, 2>(a, s);
   } else if (gather == G_C1) {
     if (nt == 1) return run_fwd<G_C1, 1, 4>(a, s);
-    if (nt == 3) return run_fwd<G_C1, 3, 4>(a, s);
-    if (nt == 6) return run_fwd<G_C1, 6, 4>(a, s);
+    if (nt == 3) return small ? run_fwd<G_C1, 3, 1>(a, s) : run_fwd<G_C1, 3, 4>(a, s);
+    if (nt == 6) return small ? run_fwd<G_C1, 6, 1>(a, s) : run_fwd<G_C1, 6, 4>(a, s);
   } else if (gather == G_DN2) {
-    if (nt == 3) return run_fwd<G_DN2, 3, 4>(a, s);
-    if (nt == 6) return run_fwd<G_DN2, 6, 4>(a, s);
+    if (nt == 3) return small ? run_fwd<G_DN2, 3, 1>(a, s) : run_fwd<G_DN2, 3, 4>(a, s);
+    if (nt == 6) return small ? run_fwd<G_DN2, 6, 1>(a, s) : run_fwd<G_DN2, 6, 4>(a, s);
   }
   return hipErrorInvalidValue;
 }
@@ -559,11 +733,29 @@ static hipError_t run_wgrad(const WgradArgs& a, int splits, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int CO_FR, int WM, int WN>
+static hipError_t run_wgrad3(const WgradArgs& a, int splits, hipStream_t s) {
+  using C = Wg3Cfg<CO_FR, WM, WN>;
+  dim3 grid(splits, (a.Cin + C::CIB - 1) / C::CIB, 1);
+  hipLaunchKernelGGL((k_wgrad3<CO_FR, WM, WN>), grid, dim3(C::NTHR), 0, s, a);
+  return hipGetLastError();
+}
+
+// the asynchronous 3x3 kernel needs 16-byte aligned pixels and channel quads that stay
+// inside each pixel's row (reads past Cin land on padding or a neighbouring slice)
+static bool wgrad3_ok(const WgradArgs& a) {
+  if (a.Cout != 48 && a.Cout != 96) return false;
+  if (a.Cin < 32) return false;  // a 32/48-channel block would be mostly padding
+  if ((a.g_stride | a.g_off | a.x_stride | a.x_off) & 3) return false;
+  if (a.x_off + ((a.Cin + 3) & ~3) > a.x_stride) return false;
+  return a.zeros != nullptr;
+}
+
 // (CIN_T, PR, PC) of the template that launch_wgrad picks for (mode, cout)
 static void wgrad_tile(int mode, int cout, int& cin_t, int& pr, int& pc) {
   const int cf = (cout + 15) / 16;
   pc = 32;
-  if (mode == W_C3) { cin_t = 16; pr = cf >= 6 ? 1 : 2; }
+  if (mode == W_C3) { cin_t = cf >= 6 ? 32 : 48; pr = 1; }
   else if (mode == W_UP2) { cin_t = 16; pr = 1; pc = 16; }
   else { cin_t = cf == 1 ? 32 : 96; pr = cf >= 6 ? 1 : 2; }
 }
@@ -584,7 +776,7 @@ int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
   const int taps = mode == W_C3 ? 9 : (mode == W_UP2 ? 4 : 1);
   const long units = (long)N * ((KH + pr - 1) / pr) * ((KW + pc - 1) / pc);
   const long cib = (Cin + cin_t - 1) / cin_t;
-  long want = (1024 + cib - 1) / cib;
+  long want = (768 + cib - 1) / cib;
   const long slab_cap = (16L << 20) / ((long)Cout * Cin * taps + Cout);  // <= 64 MB of slab
   if (want > slab_cap) want = slab_cap;
   if (want > units / 2) want = units / 2;
@@ -594,6 +786,10 @@ int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
 
 hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s) {
   const int cf = (a.Cout + 15) / 16;
+  if (mode == W_C3 && wgrad3_ok(a)) {
+    if (cf == 6) return run_wgrad3<6, 2, 2>(a, splits, s);
+    if (cf == 3) return run_wgrad3<3, 1, 3>(a, splits, s);
+  }
   if (mode == W_C3) {
     if (cf == 3) return run_wgrad<W_C3, 1, 3, 1>(a, splits, s);
     if (cf == 6) return run_wgrad<W_C3, 2, 3, 1>(a, splits, s);
@@ -609,7 +805,7 @@ hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s)
 
 hipError_t launch_reduce(const float* slab, long slab_stride, int splits, long n, float* out,
                          hipStream_t s) {
-  const long blocks = ((n + 3) / 4 + 255) / 256;
+  const long blocks = (n + 63) / 64;
   hipLaunchKernelGGL(k_reduce, dim3((unsigned)blocks), dim3(256), 0, s, slab, slab_stride, splits,
                      n, out);
   return hipGetLastError();

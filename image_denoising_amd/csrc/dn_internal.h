@@ -60,6 +60,9 @@ struct WgradArgs {
   int Cout, Cin;
   float* slab; long slab_stride;        // one [W ; b] image per split
   int wlayout;                          // 0: [co][ci][t]  1: [ci][co][t]
+  int cin_total, ci_base;               // weight tensor's Cin and this launch's first ci
+  int bias;                             // also produce the bias gradient
+  const float* zeros;                   // >= 16 zero bytes (LDS-DMA source for padding)
 };
 
 // geometry of the packed per-chunk weight image of the forward-family kernel
@@ -84,7 +87,7 @@ hipError_t launch_pool_fwd(const float* a, int N, int H, int W, int C, float* ou
 hipError_t launch_pool_bwd(const float* a, int N, int H, int W, int C, const float* dp, int ds,
                            int doff, int act, float* da, hipStream_t s);
 hipError_t launch_nchw_to_slice(const float* x, int N, int C, int H, int W, float* dst, int ds,
-                                int doff, hipStream_t s);
+                                int doff, int zero_to, hipStream_t s);
 hipError_t launch_subsample(const float* img, int N, int C, int H, int W, const uint8_t* rd_in,
                             uint64_t seed, uint64_t offset, uint64_t cell_base, float* sub1,
                             float* sub2, uint8_t* rd_out, hipStream_t s);

@@ -94,15 +94,17 @@ __global__ __launch_bounds__(256) void k_pool_bwd(const float* __restrict__ a, i
 }
 
 // NCHW network input -> channels [doff, doff+C) of an NHWC buffer (the up1 concat buffer,
-// arch_unet.py:240 `self.up1(x, pool0)` where pool0 is the raw input).
+// arch_unet.py:240 `self.up1(x, pool0)` where pool0 is the raw input); channels
+// [doff+C, zero_to) are the float4 padding of that buffer and are written as zeros.
 __global__ __launch_bounds__(256) void k_nchw_to_slice(const float* __restrict__ x, int N, int C,
                                                        int H, int W, float* __restrict__ dst,
-                                                       int ds, int doff) {
+                                                       int ds, int doff, int zero_to) {
   const long total = (long)N * H * W;
   const long hw = (long)H * W;
   for (long p = (long)blockIdx.x * 256 + threadIdx.x; p < total; p += (long)gridDim.x * 256) {
     const long n = p / hw, r = p - n * hw;
     for (int c = 0; c < C; ++c) dst[p * ds + doff + c] = x[(n * C + c) * hw + r];
+    for (int c = doff + C; c < zero_to; ++c) dst[p * ds + c] = 0.f;
   }
 }
 
@@ -370,10 +372,10 @@ hipError_t launch_pool_bwd(const float* a, int N, int H, int W, int C, const flo
 }
 
 hipError_t launch_nchw_to_slice(const float* x, int N, int C, int H, int W, float* dst, int ds,
-                                int doff, hipStream_t s) {
+                                int doff, int zero_to, hipStream_t s) {
   const long total = (long)N * H * W;
   hipLaunchKernelGGL(k_nchw_to_slice, dim3(grid_for(total, 256, 65536)), dim3(256), 0, s, x, N, C,
-                     H, W, dst, ds, doff);
+                     H, W, dst, ds, doff, zero_to);
   return hipGetLastError();
 }
 

@@ -89,7 +89,8 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
     off += (px(lvl) * ch + 63) / 64 * 64;
     return o;
   };
-  p.c1s = 2 * nf + p.C;
+  p.c1k = 2 * nf + p.C;             // [up1 | x] channels
+  p.c1s = (p.c1k + 3) / 4 * 4;      // stride padded to float4 (pad channels kept at zero)
   p.c1 = alloc(0, p.c1s);
   p.a0 = alloc(0, nf);
   p.a1 = alloc(0, nf);
@@ -166,7 +167,7 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
       slab = std::max(slab, (long)sp * (L.wcount + L.cout));
     }
     p.slab = alloc(0, 0);
-    off = p.slab + (slab + 63) / 64 * 64;
+    off = p.slab + 64 + (slab + 63) / 64 * 64;  // 64 zero floats in front (wgrad DMA padding)
     p.slab_floats = slab;
   }
   p.total_floats = off;
@@ -302,11 +303,16 @@ hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, 
   a.N = N; a.KH = KH; a.KW = KW; a.Cout = cout; a.Cin = cin;
   const int taps = mode == W_C3 ? 9 : (mode == W_UP2 ? 4 : 1);
   const long n = (long)cout * cin * taps + cout;
-  a.slab = slab; a.slab_stride = n;
+  // slab scratch layout: [64 zero floats | splits x (W + b)]
+  a.zeros = slab;
+  a.slab = slab + 64; a.slab_stride = n;
   a.wlayout = mode == W_UP2 ? 1 : 0;
-  hipError_t e = launch_wgrad(mode, a, splits, s);
+  a.cin_total = cin; a.ci_base = 0; a.bias = 1;
+  hipError_t e = hipMemsetAsync(slab, 0, 64 * sizeof(float), s);
   if (e != hipSuccess) return e;
-  return launch_reduce(slab, n, splits, n, dwb, s);
+  e = launch_wgrad(mode, a, splits, s);
+  if (e != hipSuccess) return e;
+  return launch_reduce(slab + 64, n, splits, n, dwb, s);
 }
 
 // ------------------------------------------------------------------------------------
@@ -328,7 +334,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     else DN_TRY(pack_conv_fwd(w, L.cin, L.cout, L.k, ws + p.packF[i], s));
   }
   // pool0 = x: stored as channels [2nf, 2nf+C) of the up1 concat buffer
-  DN_TRY(launch_nchw_to_slice(x, N, C, p.H, p.W, ws + p.c1, p.c1s, 2 * nf, s));
+  DN_TRY(launch_nchw_to_slice(x, N, C, p.H, p.W, ws + p.c1, p.c1s, 2 * nf, p.c1s, s));
   DN_TRY(conv_forward(V(p.c1, p.c1s, 2 * nf), N, H(0), Wd(0), C, Wt(ENC0), Bs(ENC0), nf, 3, 1,
                       V(p.a0, nf), OUT_NHWC, s));
   DN_TRY(conv_forward(V(p.a0, nf), N, H(0), Wd(0), nf, Wt(ENC1), Bs(ENC1), nf, 3, 1, V(p.a1, nf),
@@ -371,7 +377,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // up1: d2b -> c1[0:2nf]
   DN_TRY(deconv_forward(V(p.db[1], 2 * nf), N, H(1), Wd(1), 2 * nf, Wt(UP1), Bs(UP1), 2 * nf,
                         V(p.c1, p.c1s, 0), s));
-  DN_TRY(conv_forward(V(p.c1, p.c1s), N, H(0), Wd(0), p.c1s, Wt(D1A), Bs(D1A), 96, 3, 1,
+  DN_TRY(conv_forward(V(p.c1, p.c1s), N, H(0), Wd(0), p.c1k, Wt(D1A), Bs(D1A), 96, 3, 1,
                       V(p.d1a, 96), OUT_NHWC, s));
   DN_TRY(conv_forward(V(p.d1a, 96), N, H(0), Wd(0), 96, Wt(D1B), Bs(D1B), 96, 3, 1, V(p.d1b, 96),
                       OUT_NHWC, s));
@@ -411,7 +417,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   // into g_c1's storage first (free at this point).
   View dyv{const_cast<float*>(dy), OC, 0};
   if (OC > 1) {
-    DN_TRY(launch_nchw_to_slice(dy, N, OC, p.H, p.W, ws + p.g_c1, OC, 0, s));
+    DN_TRY(launch_nchw_to_slice(dy, N, OC, p.H, p.W, ws + p.g_c1, OC, 0, OC, s));
     dyv = V(p.g_c1, OC);
   }
   // nin_c (1x1, no act): wgrad + dgrad (-> g_nb, masked by nb)
@@ -430,7 +436,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                p.splits[D1B], s));
   DN_TRY(conv_dgrad(V(p.g_d1b, 96), N, H(0), Wd(0), 96, Wt(D1B), 96, 3, EPI_MASK,
                     V(p.d1a, 96), V(p.g_d1a, 96), s));
-  DN_TRY(wgrad(W_C3, V(p.g_d1a, 96), V(p.c1, p.c1s), N, H(0), Wd(0), 96, p.c1s, G(D1A), slab,
+  DN_TRY(wgrad(W_C3, V(p.g_d1a, 96), V(p.c1, p.c1s), N, H(0), Wd(0), 96, p.c1k, G(D1A), slab,
                p.splits[D1A], s));
   // only the up1 part of the concat needs a gradient (pool0 is the network input)
   DN_TRY(conv_dgrad(V(p.g_d1a, 96), N, H(0), Wd(0), 96, Wt(D1A), 2 * nf, 3, EPI_PLAIN, none,
