@@ -70,6 +70,15 @@ SIGNATURES = {
     "dn_maxpool2x2_forward": (c_int, [_F, c_int, c_int, c_int, c_int, _F, c_int, c_int, c_void_p]),
     "dn_maxpool2x2_backward": (c_int, [_F, c_int, c_int, c_int, c_int, _F, c_int, c_int, c_int, _F,
                                        c_void_p]),
+    "dn_eval_partials_size": (c_size_t, []),
+    "dn_u8_to_unit": (c_int, [_U8, c_int64, _F, c_void_p]),
+    "dn_tile_count": (c_int, [c_int, c_int, c_int]),
+    "dn_tile_extract": (c_int, [_U8, c_int, c_int, c_int, c_int, c_int, _F, c_void_p]),
+    "dn_tile_blend": (c_int, [_F, c_int, c_int, c_int, c_int, c_int, _F, _F, _U8, c_void_p]),
+    "dn_quantize_u8": (c_int, [_F, c_int64, c_int, _U8, c_void_p]),
+    "dn_psnr_u8": (c_int, [_U8, _U8, c_int64, c_void_p, c_void_p, c_void_p]),
+    "dn_ssim_u8": (c_int, [_U8, _U8, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "dn_l1_mean": (c_int, [_F, _F, c_int64, c_void_p, c_void_p, c_void_p]),
 }
 
 _lib = None

@@ -86,8 +86,12 @@ dn_status dn_unet_forward(const dn_unet_cfg* cfg, const float* params, const flo
   if (!cfg || !params || !x || !y || !ws) return fail(DN_ERR_ARG, "null argument");
   Plan p;
   std::string err;
-  // a workspace sized for the backward keeps the same forward offsets
-  if (!build_plan(*cfg, N, H, W, false, p, err)) return fail(DN_ERR_ARG, err);
+  // A workspace sized for the backward has the same forward offsets; only then does the
+  // forward save the activations the backward reads (the fused head writes d1b/na/nb).
+  if (!build_plan(*cfg, N, H, W, true, p, err)) return fail(DN_ERR_ARG, err);
+  if (ws_bytes < (size_t)p.total_floats * sizeof(float) &&
+      !build_plan(*cfg, N, H, W, false, p, err))
+    return fail(DN_ERR_ARG, err);
   if (ws_bytes < (size_t)p.total_floats * sizeof(float))
     return fail(DN_ERR_WORKSPACE, "workspace smaller than dn_unet_workspace_size()");
   return unet_forward(p, params, x, y, static_cast<float*>(ws), (hipStream_t)stream);
@@ -227,6 +231,78 @@ dn_status dn_adam_step(float* param, const float* grad, float* exp_avg, float* e
                                 beta2, (float)(1.0 - (double)beta2), (float)step_size,
                                 (float)bc2s, eps, grad_scale, (hipStream_t)stream),
                     "dn_adam_step");
+}
+
+// ---- evaluation path ----------------------------------------------------------------------
+size_t dn_eval_partials_size(void) { return EVAL_PARTS * sizeof(double); }
+
+dn_status dn_u8_to_unit(const uint8_t* x, int64_t n, float* y, void* stream) {
+  if (n < 0) return fail(DN_ERR_ARG, "n < 0");
+  if (n == 0) return DN_OK;
+  if (!x || !y) return fail(DN_ERR_ARG, "null argument");
+  return hip_status(launch_u8_to_unit(x, n, y, (hipStream_t)stream), "dn_u8_to_unit");
+}
+
+int dn_tile_count(int extent, int patch, int stride) {
+  if (extent < 1 || patch < 1 || stride < 1) return 0;
+  return (extent + stride - 1) / stride;  // range(0, extent, stride)
+}
+
+static bool tile_args_ok(int C, int H, int W, int patch, int stride) {
+  return C >= 1 && H >= 1 && W >= 1 && patch >= 1 && stride >= 1 && stride <= patch;
+}
+
+dn_status dn_tile_extract(const uint8_t* img, int C, int H, int W, int patch, int stride,
+                          float* tiles, void* stream) {
+  if (!img || !tiles) return fail(DN_ERR_ARG, "null argument");
+  if (!tile_args_ok(C, H, W, patch, stride))
+    return fail(DN_ERR_ARG, "need C,H,W,patch >= 1 and 1 <= stride <= patch");
+  return hip_status(launch_tile_extract(img, C, H, W, patch, stride, dn_tile_count(H, patch, stride),
+                                        dn_tile_count(W, patch, stride), tiles, (hipStream_t)stream),
+                    "dn_tile_extract");
+}
+
+dn_status dn_tile_blend(const float* pred, int C, int H, int W, int patch, int stride,
+                        const float* wmask, float* out, uint8_t* out_u8, void* stream) {
+  if (!pred || !wmask || (!out && !out_u8)) return fail(DN_ERR_ARG, "null argument");
+  if (!tile_args_ok(C, H, W, patch, stride))
+    return fail(DN_ERR_ARG, "need C,H,W,patch >= 1 and 1 <= stride <= patch");
+  return hip_status(launch_tile_blend(pred, C, H, W, patch, stride, dn_tile_count(H, patch, stride),
+                                      dn_tile_count(W, patch, stride), wmask, out, out_u8,
+                                      (hipStream_t)stream),
+                    "dn_tile_blend");
+}
+
+dn_status dn_quantize_u8(const float* x, int64_t n, int plus_half, uint8_t* y, void* stream) {
+  if (n < 0) return fail(DN_ERR_ARG, "n < 0");
+  if (n == 0) return DN_OK;
+  if (!x || !y) return fail(DN_ERR_ARG, "null argument");
+  return hip_status(launch_quantize_u8(x, n, plus_half, y, (hipStream_t)stream), "dn_quantize_u8");
+}
+
+dn_status dn_psnr_u8(const uint8_t* a, const uint8_t* b, int64_t n, void* part, double* psnr,
+                     void* stream) {
+  if (n < 1) return fail(DN_ERR_ARG, "n >= 1 required");
+  if (!a || !b || !part || !psnr) return fail(DN_ERR_ARG, "null argument");
+  return hip_status(launch_psnr(a, b, n, static_cast<double*>(part), psnr, (hipStream_t)stream),
+                    "dn_psnr_u8");
+}
+
+dn_status dn_ssim_u8(const uint8_t* a, const uint8_t* b, int C, int H, int W, int hwc, void* part,
+                     double* ssim, void* stream) {
+  if (C < 1 || H <= 10 || W <= 10) return fail(DN_ERR_ARG, "need C >= 1 and H, W > 10");
+  if (!a || !b || !part || !ssim) return fail(DN_ERR_ARG, "null argument");
+  return hip_status(launch_ssim(a, b, C, H, W, hwc, static_cast<double*>(part), ssim,
+                                (hipStream_t)stream),
+                    "dn_ssim_u8");
+}
+
+dn_status dn_l1_mean(const float* a, const float* b, int64_t n, void* part, double* l1,
+                     void* stream) {
+  if (n < 1) return fail(DN_ERR_ARG, "n >= 1 required");
+  if (!a || !b || !part || !l1) return fail(DN_ERR_ARG, "null argument");
+  return hip_status(launch_l1(a, b, n, static_cast<double*>(part), l1, (hipStream_t)stream),
+                    "dn_l1_mean");
 }
 
 // ---- op-level entry points ------------------------------------------------------------

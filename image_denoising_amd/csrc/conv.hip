@@ -57,7 +57,8 @@ struct FwdCfg {
   static constexpr int XITEMS = (XQ + 255) / 256;
   static constexpr int PS = NP + 4;             // epilogue staging: pixel stride (floats)
   static constexpr int LST = 4 * 16 * PS;       // 4 waves x 16 pixels x PS
-  static constexpr int LTOT = (LX + 2 * LW) > LST ? (LX + 2 * LW) : LST;
+  static constexpr int LT0 = (LX + 2 * LW) > LST ? (LX + 2 * LW) : LST;
+  static constexpr int LTOT = LT0 > 2 * HEAD_LW ? LT0 : 2 * HEAD_LW;  // HEAD: both 1x1 images
 };
 
 __device__ __forceinline__ void glds16(const float* g, float* l) {
@@ -65,10 +66,10 @@ __device__ __forceinline__ void glds16(const float* g, float* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
-template <int GATHER, int NT, int MT>
-__global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a) {
+template <int GATHER, int NT, int MT, bool HEAD = false>
+__global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a, HeadArgs hd) {
   using C = FwdCfg<GATHER, NT, MT>;
-  __shared__ __attribute__((aligned(16))) float lds[C::LTOT];
+  __shared__ __attribute__((aligned(16))) float lds[HEAD ? C::LTOT : C::LT0];
   float* lx = lds;
   float* lw0 = lds + C::LX;
   float* lw1 = lw0 + C::LW;
@@ -168,13 +169,102 @@ __global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a) {
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
-          for (int q = 0; q < NT; ++q) acc[m][q] = mfma4(av[m], bv[q], acc[m][q]);
+          for (int q = 0; q < NT; ++q)  // HEAD keeps the transposed tile (rows = channels)
+            acc[m][q] = HEAD ? mfma4(bv[q], av[m], acc[m][q]) : mfma4(av[m], bv[q], acc[m][q]);
       }
     }
     __syncthreads();  // all waves done with lx and this weight buffer
     if (c + 1 < nch) store_x();
     __syncthreads();  // next chunk's input tile written, its weight DMA landed (vmcnt(0))
   }
+
+  if constexpr (HEAD) {
+    // acc[m][q][r] = dec_conv1b pre-activation at pixel (row m, x = li), channel
+    // q*16 + 4*lg + r.  As the B operand of the next 16x16x4 MFMA, register r of fragment q
+    // supplies k = channel q*16 + 4g + r for lane group g: nin_a/nin_b consume the tile
+    // where it is, with the k order permuted the same way in their weight reads.
+    static_assert(GATHER == G_C3 && NT == 6, "head fusion is for the 96-channel dec_conv1b");
+    for (int p = wave; p < 2 * HEAD_LW / 256; p += 4) glds16(hd.wp + p * 256 + lane * 4, lds + p * 256);
+    auto bias_act = [](f32x4& v, float4 b) {
+      v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * 0.2f;
+    };
+    auto save = [&](float* dst, long pix, int q, const f32x4& v) {
+      *reinterpret_cast<float4*>(dst + pix * 96 + q * 16 + 4 * lg) = make_float4(v[0], v[1], v[2], v[3]);
+    };
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      const float4 b = *reinterpret_cast<const float4*>(a.bias + q * 16 + 4 * lg);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) bias_act(acc[m][q], b);
+    }
+    const int gx = tx0 + li;
+    if (hd.d1b) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int gy = ty0 + wave * MT + m;
+        if (gy < a.OH && gx < a.OW)
+#pragma unroll
+          for (int q = 0; q < NT; ++q) save(hd.d1b, ((long)n * a.OH + gy) * a.OW + gx, q, acc[m][q]);
+      }
+    }
+    __syncthreads();  // nin_a / nin_b images landed
+    const float* wa = lds;
+    const float* wb = lds + HEAD_LW;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int gy = ty0 + wave * MT + m;
+      const bool ok = gy < a.OH && gx < a.OW;
+      const long pix = ((long)n * a.OH + gy) * a.OW + gx;
+      f32x4 u[NT];
+#pragma unroll
+      for (int f = 0; f < NT; ++f) u[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float* wr = wa + (q * 16 + 4 * lg + r) * HEAD_WS + li;
+#pragma unroll
+          for (int f = 0; f < NT; ++f) u[f] = mfma4(wr[f * 16], acc[m][q][r], u[f]);
+        }
+#pragma unroll
+      for (int f = 0; f < NT; ++f) {
+        bias_act(u[f], *reinterpret_cast<const float4*>(hd.ba + f * 16 + 4 * lg));
+        if (hd.na && ok) save(hd.na, pix, f, u[f]);
+      }
+      f32x4 v[NT];
+#pragma unroll
+      for (int f = 0; f < NT; ++f) v[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float* wr = wb + (q * 16 + 4 * lg + r) * HEAD_WS + li;
+#pragma unroll
+          for (int f = 0; f < NT; ++f) v[f] = mfma4(wr[f * 16], u[q][r], v[f]);
+        }
+#pragma unroll
+      for (int f = 0; f < NT; ++f) {
+        bias_act(v[f], *reinterpret_cast<const float4*>(hd.bb + f * 16 + 4 * lg));
+        if (hd.nb && ok) save(hd.nb, pix, f, v[f]);
+      }
+      // nin_c: per-lane partial over its 24 channels, then across the 4 lane groups
+      for (int o = 0; o < hd.oc; ++o) {
+        float t = 0.f;
+#pragma unroll
+        for (int f = 0; f < NT; ++f) {
+          const float4 w = *reinterpret_cast<const float4*>(hd.wc + o * 96 + f * 16 + 4 * lg);
+          t = fmaf(w.x, v[f][0], t); t = fmaf(w.y, v[f][1], t);
+          t = fmaf(w.z, v[f][2], t); t = fmaf(w.w, v[f][3], t);
+        }
+        t += __shfl_xor(t, 16);
+        t += __shfl_xor(t, 32);
+        if (lg == 0 && ok) hd.y[(((long)n * hd.oc + o) * a.OH + gy) * a.OW + gx] = t + hd.bc[o];
+      }
+    }
+    return;
+  } else {
 
   // epilogue.  C/D map of 16x16 MFMA: col (n) = lane&15, row (pixel x) = 4*(lane>>4) + reg.
   const int ab = blockIdx.z;
@@ -269,6 +359,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a) {
         a.out[oi] = v;
       }
     }
+  }
   }
 }
 
@@ -649,7 +740,31 @@ static hipError_t run_fwd(const FwdArgs& a, hipStream_t s) {
   using C = FwdCfg<GATHER, NT, MT>;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
   dim3 grid(tx * ty, a.N, a.out_layout == OUT_UP2 ? 4 : 1);
-  hipLaunchKernelGGL((k_fwd<GATHER, NT, MT>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((k_fwd<GATHER, NT, MT>), grid, dim3(256), 0, s, a, HeadArgs{});
+  return hipGetLastError();
+}
+
+template <int MT>
+static hipError_t run_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s) {
+  using C = FwdCfg<G_C3, 6, MT>;
+  const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
+  dim3 grid(tx * ty, a.N, 1);
+  hipLaunchKernelGGL((k_fwd<G_C3, 6, MT, true>), grid, dim3(256), 0, s, a, h);
+  return hipGetLastError();
+}
+
+hipError_t launch_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s) {
+  if (a.NOUT != 96 || h.oc < 1) return hipErrorInvalidValue;
+  const long tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16);
+  return tiles < 1024 ? run_head<1>(a, h, s) : run_head<4>(a, h, s);
+}
+
+// nin_a / nin_b as two single-chunk images [k][n] with row stride HEAD_WS
+hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_pack, dim3((HEAD_LW + 255) / 256), dim3(256), 0, s, wa, 96, 96, 96, 1,
+                     HEAD_WS, HEAD_LW, 1, 1, out);
+  hipLaunchKernelGGL(k_pack, dim3((HEAD_LW + 255) / 256), dim3(256), 0, s, wb, 96, 96, 96, 1,
+                     HEAD_WS, HEAD_LW, 1, 1, out + HEAD_LW);
   return hipGetLastError();
 }
 

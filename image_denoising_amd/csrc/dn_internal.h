@@ -53,6 +53,19 @@ struct FwdArgs {
   const float* mask; int mask_stride, mask_off;
 };
 
+// Fused output head (arch_unet.py:186-190, 253-257): the dec_conv1b kernel keeps its
+// 96-channel tile in registers and runs nin_a -> nin_b -> nin_c on it.
+struct HeadArgs {
+  const float* wp;                    // packed [nin_a | nin_b] images, HEAD_LW floats each
+  const float* ba; const float* bb;   // nin_a / nin_b biases
+  const float* wc; const float* bc;   // nin_c weight [oc][96], bias [oc]
+  int oc;
+  float* y;                           // [N, oc, H, W]
+  float* d1b; float* na; float* nb;   // optional NHWC (stride 96) saves for the backward
+};
+constexpr int HEAD_WS = 100;   // k-row stride of a head weight image (conflict-free A reads)
+constexpr int HEAD_LW = 9728;  // 96 * HEAD_WS rounded up to 256 floats
+
 struct WgradArgs {
   const float* g; int g_stride, g_off;  // gradient operand (rows = co), NHWC
   const float* x; int x_stride, x_off;  // input operand (cols = ci), NHWC
@@ -74,6 +87,29 @@ long pack_floats(int gather, int nout, int K, int nz);  // floats of a packed we
 hipError_t launch_pack(int gather, const WView& wv, int K, int nout, int nz, float* out,
                        hipStream_t s);
 hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s);
+hipError_t launch_enc0_fwd(const float* x, int N, int C, int H, int W, const float* w,
+                           const float* b, float* out, float* cat, int cat_stride, int cat_off,
+                           int cat_zero_to, hipStream_t s);
+int enc0_wgrad_splits(int N, int H, int W);
+hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int x_stride,
+                             int x_off, int N, int C, int H, int W, float* slab, int splits,
+                             float* dwb, hipStream_t s);
+constexpr int EVAL_PARTS = 1024;
+hipError_t launch_u8_to_unit(const uint8_t* x, long n, float* y, hipStream_t s);
+hipError_t launch_tile_extract(const uint8_t* img, int C, int H, int W, int ps, int stride,
+                               int nti, int ntj, float* tiles, hipStream_t s);
+hipError_t launch_tile_blend(const float* pred, int C, int H, int W, int ps, int stride, int nti,
+                             int ntj, const float* wmask, float* out_unit, uint8_t* out_u8,
+                             hipStream_t s);
+hipError_t launch_quantize_u8(const float* x, long n, int plus_half, uint8_t* y, hipStream_t s);
+hipError_t launch_psnr(const uint8_t* a, const uint8_t* b, long n, double* part, double* out,
+                       hipStream_t s);
+hipError_t launch_ssim(const uint8_t* a, const uint8_t* b, int C, int H, int W, int hwc,
+                       double* part, double* out, hipStream_t s);
+hipError_t launch_l1(const float* a, const float* b, long n, double* part, double* out,
+                     hipStream_t s);
+hipError_t launch_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);
+hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s);
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
 hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s);
 hipError_t launch_reduce(const float* slab, long slab_stride, int splits, long n, float* out,

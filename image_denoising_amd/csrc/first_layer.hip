@@ -1,0 +1,175 @@
+// enc_conv0 (arch_unet.py:116-117, 196: Conv2d(in_nc, 48, 3, padding=1) + LeakyReLU(0.2)) for
+// gfx950.  With in_nc in {1, 3} the layer has 9 or 27 MACs per output channel: as an MFMA
+// implicit GEMM its K would be padded to 8 (fwd) / 16 (wgrad) channels, so it is written as a
+// direct VALU kernel that is HBM-bound on its 48-channel output instead.
+//
+//   k_enc0_fwd    one pixel per thread, all 48 output channels; weights (transposed, 4-channel
+//                 vectors) in LDS, broadcast reads; the 256 pixels x 48 channels of a block are
+//                 staged in LDS and written as one contiguous 48 KiB run of the NHWC output.
+//                 The same pass copies the network input into its slice of the up1 concat
+//                 buffer (the "pool0" skip of arch_unet.py:197, 247-248), zero-padding it to a
+//                 float4 boundary.
+//   k_enc0_wgrad  dW[co][ci][t] and db[co] as partial sums over a pixel range per block
+//                 (fixed order), one slab row per block; k_reduce adds the rows in order.
+#include "dn_internal.h"
+
+namespace dn {
+
+constexpr int E0_CO = 48;
+
+template <int C>
+__global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, int N, int H,
+                                                  int W, const float* __restrict__ w,
+                                                  const float* __restrict__ b,
+                                                  float* __restrict__ out, float* __restrict__ cat,
+                                                  int cat_stride, int cat_off, int cat_zero_to) {
+  constexpr int KT = 9 * C;
+  __shared__ __attribute__((aligned(16))) float wl[(KT + 1) * E0_CO];  // [tap*C+ci | bias][co]
+  __shared__ __attribute__((aligned(16))) float st[256 * E0_CO];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < KT * E0_CO; e += 256) {
+    const int co = e % E0_CO, j = e / E0_CO, t = j / C, ci = j - t * C;
+    wl[e] = w[(co * C + ci) * 9 + t];
+  }
+  if (tid < E0_CO) wl[KT * E0_CO + tid] = b[tid];
+  __syncthreads();
+
+  const long total = (long)N * H * W, hw = (long)H * W;
+  const long p0 = (long)blockIdx.x * 256;
+  const long p = p0 + tid;
+  if (p < total) {
+    const long n = p / hw;
+    const int r = (int)(p - n * hw), y = r / W, xx = r - y * W;
+    const float* xn = x + n * C * hw;
+    float xin[KT];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int yy = y + t / 3 - 1, xc = xx + t % 3 - 1;
+      const bool in = yy >= 0 && yy < H && xc >= 0 && xc < W;
+#pragma unroll
+      for (int ci = 0; ci < C; ++ci) xin[t * C + ci] = in ? xn[ci * hw + (long)yy * W + xc] : 0.f;
+    }
+    const float4* w4 = reinterpret_cast<const float4*>(wl);
+#pragma unroll
+    for (int cq = 0; cq < E0_CO / 4; ++cq) {
+      float4 v = w4[KT * (E0_CO / 4) + cq];
+#pragma unroll
+      for (int j = 0; j < KT; ++j) {
+        const float4 ww = w4[j * (E0_CO / 4) + cq];
+        v.x = fmaf(ww.x, xin[j], v.x); v.y = fmaf(ww.y, xin[j], v.y);
+        v.z = fmaf(ww.z, xin[j], v.z); v.w = fmaf(ww.w, xin[j], v.w);
+      }
+      v.x = v.x > 0.f ? v.x : v.x * 0.2f; v.y = v.y > 0.f ? v.y : v.y * 0.2f;
+      v.z = v.z > 0.f ? v.z : v.z * 0.2f; v.w = v.w > 0.f ? v.w : v.w * 0.2f;
+      *reinterpret_cast<float4*>(st + tid * E0_CO + 4 * cq) = v;
+    }
+    // the input's slice of the up1 concat buffer (centre tap = the pixel itself)
+    float* d = cat + p * cat_stride + cat_off;
+    if (C == 1 && cat_zero_to - cat_off == 4 && ((cat_stride | cat_off) & 3) == 0) {
+      *reinterpret_cast<float4*>(d) = make_float4(xin[4], 0.f, 0.f, 0.f);
+    } else {
+#pragma unroll
+      for (int ci = 0; ci < C; ++ci) d[ci] = xin[4 * C + ci];
+      for (int c = cat_off + C; c < cat_zero_to; ++c) cat[p * cat_stride + c] = 0.f;
+    }
+  }
+  __syncthreads();
+  const long npx = total - p0 < 256 ? total - p0 : 256;
+  const float4* s4 = reinterpret_cast<const float4*>(st);
+  float4* o4 = reinterpret_cast<float4*>(out + p0 * E0_CO);
+  for (int e = tid; e < npx * (E0_CO / 4); e += 256) o4[e] = s4[e];
+}
+
+// dW/db partials.  192 threads = 4 pixel groups x 48 output channels; a block owns pixels
+// [blk*per, (blk+1)*per) of the flattened N*H*W range, group g takes every 4th of them.
+// Slab row layout = the PyTorch parameter layout: W[co][ci][3][3] then b[co].
+template <int C>
+__global__ __launch_bounds__(192) void k_enc0_wgrad(const float* __restrict__ g, int g_stride,
+                                                    const float* __restrict__ x, int x_stride,
+                                                    int x_off, int N, int H, int W,
+                                                    long per, float* __restrict__ slab) {
+  constexpr int KT = 9 * C;
+  __shared__ float red[3][E0_CO][KT + 1];
+  const int tid = threadIdx.x, co = tid % E0_CO, grp = tid / E0_CO;
+  const long total = (long)N * H * W, hw = (long)H * W;
+  const long pb = (long)blockIdx.x * per;
+  const long pe = pb + per < total ? pb + per : total;
+  float acc[KT + 1];
+#pragma unroll
+  for (int j = 0; j <= KT; ++j) acc[j] = 0.f;
+  for (long p = pb + grp; p < pe; p += 4) {
+    const float gv = g[p * g_stride + co];
+    const long n = p / hw;
+    const int r = (int)(p - n * hw), y = r / W, xx = r - y * W;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int yy = y + t / 3 - 1, xc = xx + t % 3 - 1;
+      if (yy >= 0 && yy < H && xc >= 0 && xc < W) {
+        const float* xp = x + ((n * H + yy) * W + xc) * x_stride + x_off;
+#pragma unroll
+        for (int ci = 0; ci < C; ++ci) acc[ci * 9 + t] = fmaf(gv, xp[ci], acc[ci * 9 + t]);
+      }
+    }
+    acc[KT] += gv;
+  }
+  if (grp > 0)
+#pragma unroll
+    for (int j = 0; j <= KT; ++j) red[grp - 1][co][j] = acc[j];
+  __syncthreads();
+  if (grp == 0) {
+    const long n_el = (long)E0_CO * KT + E0_CO;
+    float* row = slab + (long)blockIdx.x * n_el;
+#pragma unroll
+    for (int j = 0; j < KT; ++j)
+      row[co * KT + j] = ((acc[j] + red[0][co][j]) + red[1][co][j]) + red[2][co][j];
+    row[E0_CO * KT + co] = ((acc[KT] + red[0][co][KT]) + red[1][co][KT]) + red[2][co][KT];
+  }
+}
+
+hipError_t launch_enc0_fwd(const float* x, int N, int C, int H, int W, const float* w,
+                           const float* b, float* out, float* cat, int cat_stride, int cat_off,
+                           int cat_zero_to, hipStream_t s) {
+  if (C < 1 || C > 3) return hipErrorInvalidValue;
+  const long total = (long)N * H * W;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (C == 1)
+    hipLaunchKernelGGL(k_enc0_fwd<1>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
+                       cat_off, cat_zero_to);
+  else if (C == 2)
+    hipLaunchKernelGGL(k_enc0_fwd<2>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
+                       cat_off, cat_zero_to);
+  else
+    hipLaunchKernelGGL(k_enc0_fwd<3>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
+                       cat_off, cat_zero_to);
+  return hipGetLastError();
+}
+
+int enc0_wgrad_splits(int N, int H, int W) {
+  const long total = (long)N * H * W;
+  long sp = (total + 511) / 512;  // >= 512 pixels per block
+  if (sp > 1024) sp = 1024;
+  return (int)(sp < 1 ? 1 : sp);
+}
+
+hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int x_stride,
+                             int x_off, int N, int C, int H, int W, float* slab, int splits,
+                             float* dwb, hipStream_t s) {
+  if (C < 1 || C > 3) return hipErrorInvalidValue;
+  const long total = (long)N * H * W;
+  const long per = (total + splits - 1) / splits;
+  if (C == 1)
+    hipLaunchKernelGGL(k_enc0_wgrad<1>, dim3(splits), dim3(192), 0, s, g, g_stride, x, x_stride,
+                       x_off, N, H, W, per, slab);
+  else if (C == 2)
+    hipLaunchKernelGGL(k_enc0_wgrad<2>, dim3(splits), dim3(192), 0, s, g, g_stride, x, x_stride,
+                       x_off, N, H, W, per, slab);
+  else
+    hipLaunchKernelGGL(k_enc0_wgrad<3>, dim3(splits), dim3(192), 0, s, g, g_stride, x, x_stride,
+                       x_off, N, H, W, per, slab);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const long n_el = (long)E0_CO * 9 * C + E0_CO;
+  return launch_reduce(slab, n_el, splits, n_el, dwb, s);
+}
+
+}  // namespace dn

@@ -125,6 +125,7 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
     }
     p.packF[i] = alloc_f(n);
   }
+  p.packH = alloc_f(2 * HEAD_LW);
   p.fwd_floats = off;
   if (bwd) {
     p.g_nb = alloc(0, 96);
@@ -162,7 +163,7 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
       int KH = H >> lvl, KW = W >> lvl;
       int mode = L.deconv ? W_UP2 : (L.k == 3 ? W_C3 : W_C1);
       if (L.deconv) { KH = H >> (lvl + 1); KW = W >> (lvl + 1); }
-      int sp = wgrad_splits(mode, N, KH, KW, L.cin, L.cout);
+      int sp = i == ENC0 ? enc0_wgrad_splits(N, KH, KW) : wgrad_splits(mode, N, KH, KW, L.cin, L.cout);
       p.splits[i] = sp;
       slab = std::max(slab, (long)sp * (L.wcount + L.cout));
     }
@@ -327,16 +328,15 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   auto Bs = [&](int i) { return prm + p.P.L[i].woff + p.P.L[i].wcount; };
   auto V = [&](long off, int stride, int coff = 0) { return View{ws + off, stride, coff}; };
 
-  for (int i = 0; i < NL; ++i) {  // pack the weights into the kernels' per-chunk LDS images
+  for (int i = ENC1; i < NINA; ++i) {  // pack the weights into the kernels' per-chunk LDS images
     const Layer& L = p.P.L[i];
     const float* w = prm + L.woff;
     if (L.deconv) DN_TRY(pack_deconv_fwd(w, L.cin, L.cout, ws + p.packF[i], s));
     else DN_TRY(pack_conv_fwd(w, L.cin, L.cout, L.k, ws + p.packF[i], s));
   }
-  // pool0 = x: stored as channels [2nf, 2nf+C) of the up1 concat buffer
-  DN_TRY(launch_nchw_to_slice(x, N, C, p.H, p.W, ws + p.c1, p.c1s, 2 * nf, p.c1s, s));
-  DN_TRY(conv_forward(V(p.c1, p.c1s, 2 * nf), N, H(0), Wd(0), C, Wt(ENC0), Bs(ENC0), nf, 3, 1,
-                      V(p.a0, nf), OUT_NHWC, s));
+  // enc_conv0, fused with pool0 = x -> channels [2nf, 2nf+C) of the up1 concat buffer
+  DN_TRY(launch_enc0_fwd(x, N, C, p.H, p.W, prm + p.P.L[ENC0].woff, Bs(ENC0), ws + p.a0,
+                         ws + p.c1, p.c1s, 2 * nf, p.c1s, s));
   DN_TRY(conv_forward(V(p.a0, nf), N, H(0), Wd(0), nf, Wt(ENC1), Bs(ENC1), nf, 3, 1, V(p.a1, nf),
                       OUT_NHWC, s));
   // pool1 -> skip slice of c2
@@ -379,14 +379,24 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
                         V(p.c1, p.c1s, 0), s));
   DN_TRY(conv_forward(V(p.c1, p.c1s), N, H(0), Wd(0), p.c1k, Wt(D1A), Bs(D1A), 96, 3, 1,
                       V(p.d1a, 96), OUT_NHWC, s));
-  DN_TRY(conv_forward(V(p.d1a, 96), N, H(0), Wd(0), 96, Wt(D1B), Bs(D1B), 96, 3, 1, V(p.d1b, 96),
-                      OUT_NHWC, s));
-  DN_TRY(conv_forward(V(p.d1b, 96), N, H(0), Wd(0), 96, Wt(NINA), Bs(NINA), 96, 1, 1, V(p.na, 96),
-                      OUT_NHWC, s));
-  DN_TRY(conv_forward(V(p.na, 96), N, H(0), Wd(0), 96, Wt(NINB), Bs(NINB), 96, 1, 1, V(p.nb, 96),
-                      OUT_NHWC, s));
-  DN_TRY(conv_forward(V(p.nb, 96), N, H(0), Wd(0), 96, Wt(NINC), Bs(NINC), p.OC, 1, 0,
-                      View{y, 0, 0}, OUT_NCHW, s));
+  // dec_conv1b + nin_a + nin_b + nin_c in one kernel (arch_unet.py:251-257); the
+  // intermediate activations are written only when a backward will read them
+  DN_TRY(launch_pack_head(conv_fwd_view(prm + p.P.L[NINA].woff, 96, 1),
+                          conv_fwd_view(prm + p.P.L[NINB].woff, 96, 1), ws + p.packH, s));
+  {
+    FwdArgs a{};
+    a.in = ws + p.d1a; a.in_stride = 96; a.in_off = 0; a.IHt = H(0); a.IWt = Wd(0);
+    a.N = N; a.OH = H(0); a.OW = Wd(0); a.K = 96; a.NOUT = 96;
+    a.wp = Wt(D1B); a.wp_z = 0; a.bias = Bs(D1B); a.epi = EPI_BIAS_ACT;
+    a.out = ws + p.d1b; a.out_stride = 96; a.out_off = 0; a.out_layout = OUT_NHWC;
+    HeadArgs h{};
+    h.wp = ws + p.packH;
+    h.ba = Bs(NINA); h.bb = Bs(NINB);
+    h.wc = prm + p.P.L[NINC].woff; h.bc = Bs(NINC); h.oc = p.OC;
+    h.y = y;
+    if (p.with_bwd) { h.d1b = ws + p.d1b; h.na = ws + p.na; h.nb = ws + p.nb; }
+    DN_TRY(launch_head(a, h, s));
+  }
   return DN_OK;
 }
 
@@ -498,8 +508,8 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                p.splits[ENC1], s));
   DN_TRY(conv_dgrad(V(p.g_a1, nf), N, H(0), Wd(0), nf, Wt(ENC1), nf, 3, EPI_MASK, V(p.a0, nf),
                     V(p.g_a0, nf), s));
-  DN_TRY(wgrad(W_C3, V(p.g_a0, nf), V(p.c1, p.c1s, 2 * nf), N, H(0), Wd(0), nf, C, G(ENC0), slab,
-               p.splits[ENC0], s));
+  DN_TRY(launch_enc0_wgrad(ws + p.g_a0, nf, ws + p.c1, p.c1s, 2 * nf, N, C, H(0), Wd(0), slab,
+                           p.splits[ENC0], G(ENC0), s));
   return DN_OK;
 }
 

@@ -44,6 +44,7 @@ struct Plan {
   long da[5], db[5];            // decoder conv outputs at levels 1..4
   long d1a, d1b, na, nb;
   long packF[NL];               // packed forward weight images
+  long packH;                   // fused head: nin_a | nin_b images (2 x HEAD_LW)
   long fwd_floats;
   // gradients
   long g_nb, g_na, g_d1b, g_d1a, g_c1;

@@ -173,6 +173,36 @@ dn_status dn_maxpool2x2_forward(const float* x, int N, int H, int W, int C, floa
 dn_status dn_maxpool2x2_backward(const float* x, int N, int H, int W, int C, const float* dy,
                                  int dy_stride, int dy_off, int act, float* dx, void* stream);
 
+/* ---- evaluation path: evaluation.py:23-114, evaluation_704.py:57-115, utils_eval.py:19-53 ----
+   Images are uint8 [C,H,W] (CHW) unless stated.  Metrics are written to a device double and
+   computed from fixed-order block partials (deterministic); part must hold
+   dn_eval_partials_size() bytes. */
+size_t dn_eval_partials_size(void);
+/* y = x / 255 (fp32)  -- evaluation.py:69 `noisy / 255.0` */
+dn_status dn_u8_to_unit(const uint8_t* x, int64_t n, float* y, void* stream);
+/* number of tiles per axis of the overlapping-tile loop (evaluation_704.py:80-81) */
+int dn_tile_count(int extent, int patch, int stride);
+/* tiles [nti*ntj, C, patch, patch] = img[:, r0:r0+patch, c0:c0+patch] / 255 with numpy 'reflect'
+   padding of edge tiles, r0 = ti*stride, c0 = tj*stride (evaluation_704.py:84-93) */
+dn_status dn_tile_extract(const uint8_t* img, int C, int H, int W, int patch, int stride,
+                          float* tiles, void* stream);
+/* out = sum_tiles clamp(pred,0,1)*wmask / sum wmask (0 -> 1), tiles in loop order; out_u8 =
+   clip(out*255, 0, 255) truncated (evaluation_704.py:100-115).  Either output may be NULL. */
+dn_status dn_tile_blend(const float* pred, int C, int H, int W, int patch, int stride,
+                        const float* wmask, float* out, uint8_t* out_u8, void* stream);
+/* y = uint8(clip(clamp(x,0,1)*255 [+ 0.5], 0, 255))  (evaluation.py:81-82 uses plus_half=1) */
+dn_status dn_quantize_u8(const float* x, int64_t n, int plus_half, uint8_t* y, void* stream);
+/* psnr = 10 log10(255^2 / mean((a-b)^2))  (utils_eval.py:49-53) over n uint8 values */
+dn_status dn_psnr_u8(const uint8_t* a, const uint8_t* b, int64_t n, void* part, double* psnr,
+                     void* stream);
+/* mean SSIM (utils_eval.py:19-46): 11x11 Gaussian sigma 1.5, valid region [5,H-5)x[5,W-5),
+   averaged over channels; hwc=1 for [H,W,C] images.  H, W > 10. */
+dn_status dn_ssim_u8(const uint8_t* a, const uint8_t* b, int C, int H, int W, int hwc, void* part,
+                     double* ssim, void* stream);
+/* mean |a - b| (nn.L1Loss, evaluation.py:74) */
+dn_status dn_l1_mean(const float* a, const float* b, int64_t n, void* part, double* l1,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif
