@@ -363,6 +363,92 @@ __global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a, HeadArgs hd) {
   }
 }
 
+// Backward of the fused head (see HeadBwdArgs).  A workgroup loads the two transposed 1x1
+// images once and walks 64*MT-pixel chunks; per 16-pixel fragment the three data gradients
+// stay in registers in the transposed (channel-row) MFMA layout, as in the forward head.
+template <int MT, int NWV>
+__global__ __launch_bounds__(NWV * 64, 2) void k_head_bwd(HeadBwdArgs h) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * HEAD_LW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  for (int p = wave; p < 2 * HEAD_LW / 256; p += NWV) glds16(h.wp + p * 256 + lane * 4, lds + p * 256);
+  __syncthreads();
+  auto ld4 = [](const float* p) { return *reinterpret_cast<const float4*>(p); };
+  auto st4 = [](float* p, const f32x4& v) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  };
+  auto mask = [](f32x4& v, float4 m) {
+    v[0] = m.x > 0.f ? v[0] : v[0] * 0.2f; v[1] = m.y > 0.f ? v[1] : v[1] * 0.2f;
+    v[2] = m.z > 0.f ? v[2] : v[2] * 0.2f; v[3] = m.w > 0.f ? v[3] : v[3] * 0.2f;
+  };
+  const long nchunks = (h.npx + 16 * NWV * MT - 1) / (16 * NWV * MT);
+  for (long ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+#pragma unroll 1
+    for (int m = 0; m < MT; ++m) {
+      // loop-variant zero: keeps the (loop-invariant) LDS weight reads inside the loop
+      // instead of hoisting 144 of them into registers
+      int lz = 0;
+      asm volatile("" : "+v"(lz));
+      const float* wbT = lds + lz;
+      const float* waT = lds + HEAD_LW + lz;
+      const long px = ch * 16 * NWV * MT + (wave * MT + m) * 16 + li;
+      const bool ok = px < h.npx;
+      const long pc = ok ? px : 0;
+      // g_nb (VALU: K = oc)
+      f32x4 t[6];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) t[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int o = 0; o < h.oc; ++o) {
+        const float d = ok ? h.dy[pc * h.dy_stride + o] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          const float4 w = ld4(h.wc + o * 96 + q * 16 + 4 * lg);
+          t[q][0] = fmaf(w.x, d, t[q][0]); t[q][1] = fmaf(w.y, d, t[q][1]);
+          t[q][2] = fmaf(w.z, d, t[q][2]); t[q][3] = fmaf(w.w, d, t[q][3]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        mask(t[q], ld4(h.nb + pc * 96 + q * 16 + 4 * lg));
+        if (ok) st4(h.g_nb + px * 96 + q * 16 + 4 * lg, t[q]);
+      }
+      // g_na = leaky'(na) * Wb^T g_nb
+      f32x4 u[6];
+#pragma unroll
+      for (int f = 0; f < 6; ++f) u[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float* wr = wbT + (q * 16 + 4 * lg + r) * HEAD_WS + li;
+#pragma unroll
+          for (int f = 0; f < 6; ++f) u[f] = mfma4(wr[f * 16], t[q][r], u[f]);
+        }
+#pragma unroll
+      for (int f = 0; f < 6; ++f) {
+        mask(u[f], ld4(h.na + pc * 96 + f * 16 + 4 * lg));
+        if (ok) st4(h.g_na + px * 96 + f * 16 + 4 * lg, u[f]);
+      }
+      // g_d1b = leaky'(d1b) * Wa^T g_na
+#pragma unroll
+      for (int f = 0; f < 6; ++f) t[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float* wr = waT + (q * 16 + 4 * lg + r) * HEAD_WS + li;
+#pragma unroll
+          for (int f = 0; f < 6; ++f) t[f] = mfma4(wr[f * 16], u[q][r], t[f]);
+        }
+#pragma unroll
+      for (int f = 0; f < 6; ++f) {
+        mask(t[f], ld4(h.d1b + pc * 96 + f * 16 + 4 * lg));
+        if (ok) st4(h.g_d1b + px * 96 + f * 16 + 4 * lg, t[f]);
+      }
+    }
+  }
+}
+
 // Weight packing: the per-chunk LDS image [chunk][tap][k][n] (zero padded) of a strided
 // weight view, one image set per blockIdx.z value (deconv forward: one per (a,b)).
 __global__ __launch_bounds__(256) void k_pack(WView wv, int K, int NOUT, int KC, int TAPS, int WNS,
@@ -757,6 +843,14 @@ hipError_t launch_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s) {
   if (a.NOUT != 96 || h.oc < 1) return hipErrorInvalidValue;
   const long tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16);
   return tiles < 1024 ? run_head<1>(a, h, s) : run_head<4>(a, h, s);
+}
+
+hipError_t launch_head_bwd(const HeadBwdArgs& h, hipStream_t s) {
+  if (h.oc < 1 || h.npx < 1) return hipErrorInvalidValue;
+  const long nchunks = (h.npx + 511) / 512;
+  const unsigned grid = (unsigned)(nchunks < 512 ? nchunks : 512);  // 2 per CU, weights loaded once
+  hipLaunchKernelGGL((k_head_bwd<4, 8>), dim3(grid), dim3(512), 0, s, h);
+  return hipGetLastError();
 }
 
 // nin_a / nin_b as two single-chunk images [k][n] with row stride HEAD_WS

@@ -63,6 +63,16 @@ struct HeadArgs {
   float* y;                           // [N, oc, H, W]
   float* d1b; float* na; float* nb;   // optional NHWC (stride 96) saves for the backward
 };
+// Backward of the head: g_nb = leaky'(nb) * (Wc^T dy), g_na = leaky'(na) * (Wb^T g_nb),
+// g_d1b = leaky'(d1b) * (Wa^T g_na) over npx pixels (all NHWC stride 96, dy stride dy_stride)
+struct HeadBwdArgs {
+  const float* wp;                    // packed [nin_b^T | nin_a^T] images, HEAD_LW floats each
+  const float* wc; int oc;            // nin_c weight [oc][96]
+  const float* dy; int dy_stride;
+  const float* nb; const float* na; const float* d1b;
+  float* g_nb; float* g_na; float* g_d1b;
+  long npx;
+};
 constexpr int HEAD_WS = 100;   // k-row stride of a head weight image (conflict-free A reads)
 constexpr int HEAD_LW = 9728;  // 96 * HEAD_WS rounded up to 256 floats
 
@@ -108,6 +118,10 @@ hipError_t launch_ssim(const uint8_t* a, const uint8_t* b, int C, int H, int W, 
                        double* part, double* out, hipStream_t s);
 hipError_t launch_l1(const float* a, const float* b, long n, double* part, double* out,
                      hipStream_t s);
+hipError_t launch_head_bwd(const HeadBwdArgs& h, hipStream_t s);
+int wgrad_thin_splits(long npx);
+hipError_t launch_wgrad_thin(const float* g, int g_stride, int cout, const float* x, long npx,
+                             float* slab, int splits, float* dwb, hipStream_t s);
 hipError_t launch_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);
 hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s);
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);

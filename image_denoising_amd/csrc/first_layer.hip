@@ -1,5 +1,6 @@
-// enc_conv0 (arch_unet.py:116-117, 196: Conv2d(in_nc, 48, 3, padding=1) + LeakyReLU(0.2)) for
-// gfx950.  With in_nc in {1, 3} the layer has 9 or 27 MACs per output channel: as an MFMA
+// Thin layers of the N2N U-Net for gfx950: enc_conv0 (arch_unet.py:116-117, 196:
+// Conv2d(in_nc, 48, 3, padding=1) + LeakyReLU(0.2)) and the weight gradient of nin_c
+// (arch_unet.py:190: Conv2d(96, out_nc, 1)).  With in_nc in {1, 3} the layer has 9 or 27 MACs per output channel: as an MFMA
 // implicit GEMM its K would be padded to 8 (fwd) / 16 (wgrad) channels, so it is written as a
 // direct VALU kernel that is HBM-bound on its 48-channel output instead.
 //
@@ -94,7 +95,7 @@ __global__ __launch_bounds__(192) void k_enc0_wgrad(const float* __restrict__ g,
   const long total = (long)N * H * W, hw = (long)H * W;
   const long pb = (long)blockIdx.x * per;
   const long pe = pb + per < total ? pb + per : total;
-  float acc[KT + 1];
+  float acc[KT + 1];  // (KT + 1 <= 37)
 #pragma unroll
   for (int j = 0; j <= KT; ++j) acc[j] = 0.f;
   for (long p = pb + grp; p < pe; p += 4) {
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(192) void k_enc0_wgrad(const float* __restrict__ g,
 hipError_t launch_enc0_fwd(const float* x, int N, int C, int H, int W, const float* w,
                            const float* b, float* out, float* cat, int cat_stride, int cat_off,
                            int cat_zero_to, hipStream_t s) {
-  if (C < 1 || C > 3) return hipErrorInvalidValue;
+  if (C < 1 || C > 4) return hipErrorInvalidValue;
   const long total = (long)N * H * W;
   const dim3 grid((unsigned)((total + 255) / 256));
   if (C == 1)
@@ -138,8 +139,11 @@ hipError_t launch_enc0_fwd(const float* x, int N, int C, int H, int W, const flo
   else if (C == 2)
     hipLaunchKernelGGL(k_enc0_fwd<2>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
                        cat_off, cat_zero_to);
-  else
+  else if (C == 3)
     hipLaunchKernelGGL(k_enc0_fwd<3>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
+                       cat_off, cat_zero_to);
+  else
+    hipLaunchKernelGGL(k_enc0_fwd<4>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
                        cat_off, cat_zero_to);
   return hipGetLastError();
 }
@@ -154,7 +158,7 @@ int enc0_wgrad_splits(int N, int H, int W) {
 hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int x_stride,
                              int x_off, int N, int C, int H, int W, float* slab, int splits,
                              float* dwb, hipStream_t s) {
-  if (C < 1 || C > 3) return hipErrorInvalidValue;
+  if (C < 1 || C > 4) return hipErrorInvalidValue;
   const long total = (long)N * H * W;
   const long per = (total + splits - 1) / splits;
   if (C == 1)
@@ -163,12 +167,83 @@ hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int x
   else if (C == 2)
     hipLaunchKernelGGL(k_enc0_wgrad<2>, dim3(splits), dim3(192), 0, s, g, g_stride, x, x_stride,
                        x_off, N, H, W, per, slab);
-  else
+  else if (C == 3)
     hipLaunchKernelGGL(k_enc0_wgrad<3>, dim3(splits), dim3(192), 0, s, g, g_stride, x, x_stride,
+                       x_off, N, H, W, per, slab);
+  else
+    hipLaunchKernelGGL(k_enc0_wgrad<4>, dim3(splits), dim3(192), 0, s, g, g_stride, x, x_stride,
                        x_off, N, H, W, per, slab);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const long n_el = (long)E0_CO * 9 * C + E0_CO;
+  return launch_reduce(slab, n_el, splits, n_el, dwb, s);
+}
+
+// ------------------------------------------------------------------------------------
+// Weight gradient of a thin 1x1 conv with 96 input and few output channels (nin_c,
+// arch_unet.py:190): dW[co][ci] = sum_p g[p][co] x[p][ci], db[co] = sum_p g[p][co].
+// 192 threads = 2 pixel groups x 96 input channels; per block a contiguous pixel range;
+// rows of the slab in PyTorch layout (W[co][ci] then b[co]); k_reduce sums them in order.
+template <int CO>
+__global__ __launch_bounds__(192) void k_wgrad_thin(const float* __restrict__ g, int g_stride,
+                                                    const float* __restrict__ x, long npx, long per,
+                                                    float* __restrict__ slab) {
+  __shared__ float red[96][CO + 1];
+  const int tid = threadIdx.x, ci = tid % 96, grp = tid / 96;
+  const long pb = (long)blockIdx.x * per;
+  const long pe = pb + per < npx ? pb + per : npx;
+  float acc[CO], accb[CO];
+#pragma unroll
+  for (int o = 0; o < CO; ++o) acc[o] = accb[o] = 0.f;
+  for (long p = pb + grp; p < pe; p += 2) {
+    const float xv = x[p * 96 + ci];
+#pragma unroll
+    for (int o = 0; o < CO; ++o) {
+      const float gv = g[p * g_stride + o];
+      acc[o] = fmaf(gv, xv, acc[o]);
+      accb[o] += gv;
+    }
+  }
+  if (grp == 1) {
+#pragma unroll
+    for (int o = 0; o < CO; ++o) red[ci][o] = acc[o];
+    if (ci == 0)
+#pragma unroll
+      for (int o = 0; o < CO; ++o) red[o][CO] = accb[o];
+  }
+  __syncthreads();
+  if (grp == 0) {
+    float* row = slab + (long)blockIdx.x * (CO * 96 + CO);
+#pragma unroll
+    for (int o = 0; o < CO; ++o) row[o * 96 + ci] = acc[o] + red[ci][o];
+    if (ci == 0)
+#pragma unroll
+      for (int o = 0; o < CO; ++o) row[CO * 96 + o] = accb[o] + red[o][CO];
+  }
+}
+
+int wgrad_thin_splits(long npx) {
+  long sp = (npx + 1023) / 1024;  // >= 1024 pixels per block
+  if (sp > 1024) sp = 1024;
+  return (int)(sp < 1 ? 1 : sp);
+}
+
+hipError_t launch_wgrad_thin(const float* g, int g_stride, int cout, const float* x, long npx,
+                             float* slab, int splits, float* dwb, hipStream_t s) {
+  const long per = (npx + splits - 1) / splits;
+  if (cout == 1)
+    hipLaunchKernelGGL(k_wgrad_thin<1>, dim3(splits), dim3(192), 0, s, g, g_stride, x, npx, per, slab);
+  else if (cout == 2)
+    hipLaunchKernelGGL(k_wgrad_thin<2>, dim3(splits), dim3(192), 0, s, g, g_stride, x, npx, per, slab);
+  else if (cout == 3)
+    hipLaunchKernelGGL(k_wgrad_thin<3>, dim3(splits), dim3(192), 0, s, g, g_stride, x, npx, per, slab);
+  else if (cout == 4)
+    hipLaunchKernelGGL(k_wgrad_thin<4>, dim3(splits), dim3(192), 0, s, g, g_stride, x, npx, per, slab);
+  else
+    return hipErrorInvalidValue;
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const long n_el = (long)cout * 96 + cout;
   return launch_reduce(slab, n_el, splits, n_el, dwb, s);
 }
 

@@ -155,6 +155,7 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
       }
       p.packB[i] = alloc_f(n);
     }
+    p.packHB = alloc_f(2 * HEAD_LW);
     // slab: max over layers of splits * (W + b)
     long slab = 0;
     for (int i = 0; i < NL; ++i) {
@@ -163,7 +164,9 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
       int KH = H >> lvl, KW = W >> lvl;
       int mode = L.deconv ? W_UP2 : (L.k == 3 ? W_C3 : W_C1);
       if (L.deconv) { KH = H >> (lvl + 1); KW = W >> (lvl + 1); }
-      int sp = i == ENC0 ? enc0_wgrad_splits(N, KH, KW) : wgrad_splits(mode, N, KH, KW, L.cin, L.cout);
+      int sp = i == ENC0   ? enc0_wgrad_splits(N, KH, KW)
+               : (i == NINC && p.OC <= 4) ? wgrad_thin_splits((long)N * KH * KW)
+                           : wgrad_splits(mode, N, KH, KW, L.cin, L.cout);
       p.splits[i] = sp;
       slab = std::max(slab, (long)sp * (L.wcount + L.cout));
     }
@@ -414,7 +417,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   auto G = [&](int i) { return dprm + p.P.L[i].woff; };
   auto V = [&](long off, int stride, int coff = 0) { return View{ws + off, stride, coff}; };
   float* slab = ws + p.slab;
-  for (int i = ENC1; i < NL; ++i) {  // flipped/transposed weight images for the data gradients
+  for (int i = ENC1; i < NINA; ++i) {  // flipped/transposed weight images for the data gradients
     const Layer& L = p.P.L[i];
     const float* w = prm + L.woff;
     if (L.deconv) DN_TRY(pack_deconv_dgrad(w, L.cout, L.cin, ws + p.packB[i], s));
@@ -430,18 +433,29 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     DN_TRY(launch_nchw_to_slice(dy, N, OC, p.H, p.W, ws + p.g_c1, OC, 0, OC, s));
     dyv = V(p.g_c1, OC);
   }
-  // nin_c (1x1, no act): wgrad + dgrad (-> g_nb, masked by nb)
-  DN_TRY(wgrad(W_C1, dyv, V(p.nb, 96), N, H(0), Wd(0), OC, 96, G(NINC), slab, p.splits[NINC], s));
-  DN_TRY(conv_dgrad(dyv, N, H(0), Wd(0), OC, Wt(NINC), 96, 1, EPI_MASK, V(p.nb, 96),
-                    V(p.g_nb, 96), s));
+  // nin_c -> nin_b -> nin_a data gradients in one kernel (g_nb, g_na, g_d1b), then the three
+  // 1x1 weight gradients from them
+  DN_TRY(launch_pack_head(conv_dgrad_view(prm + p.P.L[NINB].woff, 96, 1),
+                          conv_dgrad_view(prm + p.P.L[NINA].woff, 96, 1), ws + p.packHB, s));
+  {
+    HeadBwdArgs h{};
+    h.wp = ws + p.packHB;
+    h.wc = prm + p.P.L[NINC].woff; h.oc = OC;
+    h.dy = dyv.p; h.dy_stride = dyv.stride;
+    h.nb = ws + p.nb; h.na = ws + p.na; h.d1b = ws + p.d1b;
+    h.g_nb = ws + p.g_nb; h.g_na = ws + p.g_na; h.g_d1b = ws + p.g_d1b;
+    h.npx = (long)N * H(0) * Wd(0);
+    DN_TRY(launch_head_bwd(h, s));
+  }
+  if (OC <= 4)
+    DN_TRY(launch_wgrad_thin(dyv.p, dyv.stride, OC, ws + p.nb, (long)N * H(0) * Wd(0), slab,
+                             p.splits[NINC], G(NINC), s));
+  else
+    DN_TRY(wgrad(W_C1, dyv, V(p.nb, 96), N, H(0), Wd(0), OC, 96, G(NINC), slab, p.splits[NINC], s));
   DN_TRY(wgrad(W_C1, V(p.g_nb, 96), V(p.na, 96), N, H(0), Wd(0), 96, 96, G(NINB), slab,
                p.splits[NINB], s));
-  DN_TRY(conv_dgrad(V(p.g_nb, 96), N, H(0), Wd(0), 96, Wt(NINB), 96, 1, EPI_MASK, V(p.na, 96),
-                    V(p.g_na, 96), s));
   DN_TRY(wgrad(W_C1, V(p.g_na, 96), V(p.d1b, 96), N, H(0), Wd(0), 96, 96, G(NINA), slab,
                p.splits[NINA], s));
-  DN_TRY(conv_dgrad(V(p.g_na, 96), N, H(0), Wd(0), 96, Wt(NINA), 96, 1, EPI_MASK,
-                    V(p.d1b, 96), V(p.g_d1b, 96), s));
   DN_TRY(wgrad(W_C3, V(p.g_d1b, 96), V(p.d1a, 96), N, H(0), Wd(0), 96, 96, G(D1B), slab,
                p.splits[D1B], s));
   DN_TRY(conv_dgrad(V(p.g_d1b, 96), N, H(0), Wd(0), 96, Wt(D1B), 96, 3, EPI_MASK,

@@ -51,6 +51,7 @@ struct Plan {
   long g_c[5], g_da[5], g_db[5], g_a[5];
   long g_a6, g_p5, g_a0, g_a1;
   long packB[NL];               // packed data-gradient weight images
+  long packHB;                  // fused head backward: nin_b^T | nin_a^T images
   long slab, slab_floats;
   int splits[NL];
   long total_floats;
