@@ -81,39 +81,59 @@ __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, i
   for (int e = tid; e < npx * (E0_CO / 4); e += 256) o4[e] = s4[e];
 }
 
-// dW/db partials.  192 threads = 4 pixel groups x 48 output channels; a block owns pixels
-// [blk*per, (blk+1)*per) of the flattened N*H*W range, group g takes every 4th of them.
+// dW/db partials.  A block owns a contiguous range of image rows (of the flattened N*H rows)
+// and walks them in 128-pixel segments: the gradient segment [128][48] is staged in LDS with
+// float4 loads, the input rows y-1..y+1 (+1-pixel halo) likewise; then 240 threads = 5 pixel
+// phases x 48 output channels accumulate W[co][ci][t] (and b[co]) from broadcast LDS reads.
 // Slab row layout = the PyTorch parameter layout: W[co][ci][3][3] then b[co].
+constexpr int E0_SEG = 128;
 template <int C>
-__global__ __launch_bounds__(192) void k_enc0_wgrad(const float* __restrict__ g, int g_stride,
+__global__ __launch_bounds__(256) void k_enc0_wgrad(const float* __restrict__ g,
                                                     const float* __restrict__ x, int x_stride,
-                                                    int x_off, int N, int H, int W,
-                                                    long per, float* __restrict__ slab) {
+                                                    int x_off, int N, int H, int W, int rows_per,
+                                                    float* __restrict__ slab) {
   constexpr int KT = 9 * C;
-  __shared__ float red[3][E0_CO][KT + 1];
-  const int tid = threadIdx.x, co = tid % E0_CO, grp = tid / E0_CO;
-  const long total = (long)N * H * W, hw = (long)H * W;
-  const long pb = (long)blockIdx.x * per;
-  const long pe = pb + per < total ? pb + per : total;
-  float acc[KT + 1];  // (KT + 1 <= 37)
+  __shared__ __attribute__((aligned(16))) float gr[E0_SEG * E0_CO];
+  __shared__ float xr[3][C][E0_SEG + 2];
+  __shared__ float red[4][E0_CO][KT + 1];
+  const int tid = threadIdx.x, co = tid % E0_CO, grp = tid / E0_CO;  // grp 5: loader only
+  float acc[KT + 1];
 #pragma unroll
   for (int j = 0; j <= KT; ++j) acc[j] = 0.f;
-  for (long p = pb + grp; p < pe; p += 4) {
-    const float gv = g[p * g_stride + co];
-    const long n = p / hw;
-    const int r = (int)(p - n * hw), y = r / W, xx = r - y * W;
+  const int rb = blockIdx.x * rows_per;
+  const int re = rb + rows_per < N * H ? rb + rows_per : N * H;
+  for (int row = rb; row < re; ++row) {
+    const int n = row / H, y = row - n * H;
+    for (int x0 = 0; x0 < W; x0 += E0_SEG) {
+      const int seg = W - x0 < E0_SEG ? W - x0 : E0_SEG;
+      __syncthreads();
+      const float4* g4 = reinterpret_cast<const float4*>(g + ((long)row * W + x0) * E0_CO);
+      for (int e = tid; e < seg * (E0_CO / 4); e += 256) reinterpret_cast<float4*>(gr)[e] = g4[e];
+      for (int e = tid; e < 3 * C * (seg + 2); e += 256) {
+        const int dy = e / (C * (seg + 2)), r = e - dy * (C * (seg + 2));
+        const int ci = r / (seg + 2), xx = r - ci * (seg + 2);
+        const int gy = y + dy - 1, gx = x0 + xx - 1;
+        xr[dy][ci][xx] = (gy >= 0 && gy < H && gx >= 0 && gx < W)
+                             ? x[((long)(n * H + gy) * W + gx) * x_stride + x_off + ci]
+                             : 0.f;
+      }
+      __syncthreads();
+      if (grp < 5) {
+        for (int px = grp; px < seg; px += 5) {
+          const float gv = gr[px * E0_CO + co];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int yy = y + t / 3 - 1, xc = xx + t % 3 - 1;
-      if (yy >= 0 && yy < H && xc >= 0 && xc < W) {
-        const float* xp = x + ((n * H + yy) * W + xc) * x_stride + x_off;
+          for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-        for (int ci = 0; ci < C; ++ci) acc[ci * 9 + t] = fmaf(gv, xp[ci], acc[ci * 9 + t]);
+            for (int ci = 0; ci < C; ++ci)
+#pragma unroll
+              for (int dx = 0; dx < 3; ++dx)
+                acc[ci * 9 + dy * 3 + dx] = fmaf(gv, xr[dy][ci][px + dx], acc[ci * 9 + dy * 3 + dx]);
+          acc[KT] += gv;
+        }
       }
     }
-    acc[KT] += gv;
   }
-  if (grp > 0)
+  if (grp >= 1 && grp < 5)
 #pragma unroll
     for (int j = 0; j <= KT; ++j) red[grp - 1][co][j] = acc[j];
   __syncthreads();
@@ -122,8 +142,9 @@ __global__ __launch_bounds__(192) void k_enc0_wgrad(const float* __restrict__ g,
     float* row = slab + (long)blockIdx.x * n_el;
 #pragma unroll
     for (int j = 0; j < KT; ++j)
-      row[co * KT + j] = ((acc[j] + red[0][co][j]) + red[1][co][j]) + red[2][co][j];
-    row[E0_CO * KT + co] = ((acc[KT] + red[0][co][KT]) + red[1][co][KT]) + red[2][co][KT];
+      row[co * KT + j] = (((acc[j] + red[0][co][j]) + red[1][co][j]) + red[2][co][j]) + red[3][co][j];
+    row[E0_CO * KT + co] =
+        (((acc[KT] + red[0][co][KT]) + red[1][co][KT]) + red[2][co][KT]) + red[3][co][KT];
   }
 }
 
@@ -149,82 +170,89 @@ hipError_t launch_enc0_fwd(const float* x, int N, int C, int H, int W, const flo
 }
 
 int enc0_wgrad_splits(int N, int H, int W) {
-  const long total = (long)N * H * W;
-  long sp = (total + 511) / 512;  // >= 512 pixels per block
-  if (sp > 1024) sp = 1024;
-  return (int)(sp < 1 ? 1 : sp);
+  (void)W;
+  const int rows = N * H;
+  return rows < 1024 ? rows : 1024;
 }
 
+// g: NHWC [N,H,W,48] contiguous (stride 48); x: NHWC view (stride, offset) with C channels
 hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int x_stride,
                              int x_off, int N, int C, int H, int W, float* slab, int splits,
                              float* dwb, hipStream_t s) {
-  if (C < 1 || C > 4) return hipErrorInvalidValue;
-  const long total = (long)N * H * W;
-  const long per = (total + splits - 1) / splits;
+  if (C < 1 || C > 4 || g_stride != E0_CO) return hipErrorInvalidValue;
+  const int rows = N * H;
+  const int per = (rows + splits - 1) / splits;
+  const int blocks = (rows + per - 1) / per;
   if (C == 1)
-    hipLaunchKernelGGL(k_enc0_wgrad<1>, dim3(splits), dim3(192), 0, s, g, g_stride, x, x_stride,
-                       x_off, N, H, W, per, slab);
+    hipLaunchKernelGGL(k_enc0_wgrad<1>, dim3(blocks), dim3(256), 0, s, g, x, x_stride, x_off, N, H,
+                       W, per, slab);
   else if (C == 2)
-    hipLaunchKernelGGL(k_enc0_wgrad<2>, dim3(splits), dim3(192), 0, s, g, g_stride, x, x_stride,
-                       x_off, N, H, W, per, slab);
+    hipLaunchKernelGGL(k_enc0_wgrad<2>, dim3(blocks), dim3(256), 0, s, g, x, x_stride, x_off, N, H,
+                       W, per, slab);
   else if (C == 3)
-    hipLaunchKernelGGL(k_enc0_wgrad<3>, dim3(splits), dim3(192), 0, s, g, g_stride, x, x_stride,
-                       x_off, N, H, W, per, slab);
+    hipLaunchKernelGGL(k_enc0_wgrad<3>, dim3(blocks), dim3(256), 0, s, g, x, x_stride, x_off, N, H,
+                       W, per, slab);
   else
-    hipLaunchKernelGGL(k_enc0_wgrad<4>, dim3(splits), dim3(192), 0, s, g, g_stride, x, x_stride,
-                       x_off, N, H, W, per, slab);
+    hipLaunchKernelGGL(k_enc0_wgrad<4>, dim3(blocks), dim3(256), 0, s, g, x, x_stride, x_off, N, H,
+                       W, per, slab);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const long n_el = (long)E0_CO * 9 * C + E0_CO;
-  return launch_reduce(slab, n_el, splits, n_el, dwb, s);
+  return launch_reduce(slab, n_el, blocks, n_el, dwb, s);
 }
 
 // ------------------------------------------------------------------------------------
 // Weight gradient of a thin 1x1 conv with 96 input and few output channels (nin_c,
 // arch_unet.py:190): dW[co][ci] = sum_p g[p][co] x[p][ci], db[co] = sum_p g[p][co].
-// 192 threads = 2 pixel groups x 96 input channels; per block a contiguous pixel range;
-// rows of the slab in PyTorch layout (W[co][ci] then b[co]); k_reduce sums them in order.
+// 240 threads = 10 pixel phases x 24 float4 channel quads; per block a contiguous pixel range;
+// the phases are summed in a fixed order into one slab row in PyTorch layout (W[co][ci] then
+// b[co]); k_reduce sums the rows in order.
 template <int CO>
-__global__ __launch_bounds__(192) void k_wgrad_thin(const float* __restrict__ g, int g_stride,
+__global__ __launch_bounds__(256) void k_wgrad_thin(const float* __restrict__ g, int g_stride,
                                                     const float* __restrict__ x, long npx, long per,
                                                     float* __restrict__ slab) {
-  __shared__ float red[96][CO + 1];
-  const int tid = threadIdx.x, ci = tid % 96, grp = tid / 96;
+  constexpr int NE = CO * 96 + CO;
+  __shared__ float red[10][NE];
+  const int tid = threadIdx.x, cq = tid % 24, ph = tid / 24;
   const long pb = (long)blockIdx.x * per;
   const long pe = pb + per < npx ? pb + per : npx;
-  float acc[CO], accb[CO];
+  float4 acc[CO];
+  float accb[CO];
 #pragma unroll
-  for (int o = 0; o < CO; ++o) acc[o] = accb[o] = 0.f;
-  for (long p = pb + grp; p < pe; p += 2) {
-    const float xv = x[p * 96 + ci];
+  for (int o = 0; o < CO; ++o) { acc[o] = make_float4(0.f, 0.f, 0.f, 0.f); accb[o] = 0.f; }
+  if (ph < 10) {
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+#pragma unroll 2
+    for (long p = pb + ph; p < pe; p += 10) {
+      const float4 xv = x4[p * 24 + cq];
+#pragma unroll
+      for (int o = 0; o < CO; ++o) {
+        const float gv = g[p * g_stride + o];
+        acc[o].x = fmaf(gv, xv.x, acc[o].x); acc[o].y = fmaf(gv, xv.y, acc[o].y);
+        acc[o].z = fmaf(gv, xv.z, acc[o].z); acc[o].w = fmaf(gv, xv.w, acc[o].w);
+        accb[o] += gv;
+      }
+    }
 #pragma unroll
     for (int o = 0; o < CO; ++o) {
-      const float gv = g[p * g_stride + o];
-      acc[o] = fmaf(gv, xv, acc[o]);
-      accb[o] += gv;
+      red[ph][o * 96 + 4 * cq] = acc[o].x; red[ph][o * 96 + 4 * cq + 1] = acc[o].y;
+      red[ph][o * 96 + 4 * cq + 2] = acc[o].z; red[ph][o * 96 + 4 * cq + 3] = acc[o].w;
+      if (cq == 0) red[ph][CO * 96 + o] = accb[o];
     }
   }
-  if (grp == 1) {
-#pragma unroll
-    for (int o = 0; o < CO; ++o) red[ci][o] = acc[o];
-    if (ci == 0)
-#pragma unroll
-      for (int o = 0; o < CO; ++o) red[o][CO] = accb[o];
-  }
   __syncthreads();
-  if (grp == 0) {
-    float* row = slab + (long)blockIdx.x * (CO * 96 + CO);
+  float* row = slab + (long)blockIdx.x * NE;
+  for (int e = tid; e < NE; e += 256) {
+    float t = red[0][e];
 #pragma unroll
-    for (int o = 0; o < CO; ++o) row[o * 96 + ci] = acc[o] + red[ci][o];
-    if (ci == 0)
-#pragma unroll
-      for (int o = 0; o < CO; ++o) row[CO * 96 + o] = accb[o] + red[o][CO];
+    for (int q = 1; q < 10; ++q) t += red[q][e];
+    row[e] = t;
   }
 }
 
 int wgrad_thin_splits(long npx) {
-  long sp = (npx + 1023) / 1024;  // >= 1024 pixels per block
-  if (sp > 1024) sp = 1024;
+  long sp = (npx + 511) / 512;  // >= 512 pixels per block
+  if (sp > 2048) sp = 2048;
   return (int)(sp < 1 ? 1 : sp);
 }
 
@@ -232,13 +260,13 @@ hipError_t launch_wgrad_thin(const float* g, int g_stride, int cout, const float
                              float* slab, int splits, float* dwb, hipStream_t s) {
   const long per = (npx + splits - 1) / splits;
   if (cout == 1)
-    hipLaunchKernelGGL(k_wgrad_thin<1>, dim3(splits), dim3(192), 0, s, g, g_stride, x, npx, per, slab);
+    hipLaunchKernelGGL(k_wgrad_thin<1>, dim3(splits), dim3(256), 0, s, g, g_stride, x, npx, per, slab);
   else if (cout == 2)
-    hipLaunchKernelGGL(k_wgrad_thin<2>, dim3(splits), dim3(192), 0, s, g, g_stride, x, npx, per, slab);
+    hipLaunchKernelGGL(k_wgrad_thin<2>, dim3(splits), dim3(256), 0, s, g, g_stride, x, npx, per, slab);
   else if (cout == 3)
-    hipLaunchKernelGGL(k_wgrad_thin<3>, dim3(splits), dim3(192), 0, s, g, g_stride, x, npx, per, slab);
+    hipLaunchKernelGGL(k_wgrad_thin<3>, dim3(splits), dim3(256), 0, s, g, g_stride, x, npx, per, slab);
   else if (cout == 4)
-    hipLaunchKernelGGL(k_wgrad_thin<4>, dim3(splits), dim3(192), 0, s, g, g_stride, x, npx, per, slab);
+    hipLaunchKernelGGL(k_wgrad_thin<4>, dim3(splits), dim3(256), 0, s, g, g_stride, x, npx, per, slab);
   else
     return hipErrorInvalidValue;
   hipError_t e = hipGetLastError();
