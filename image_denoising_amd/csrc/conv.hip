@@ -798,8 +798,11 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad3(WgradArgs a) {
 // out[e] = sum_s slab[s][e] in a fixed order (bit-reproducible): a workgroup owns 64
 // consecutive elements; wave w sums splits w, w+4, w+8, ... in order, then the four wave
 // partials are added in wave order.
+// Element e of the reduced vector goes to out[(e / grp) * ostride + ooff + e % grp] (the
+// identity for grp = n, ooff = 0): a compact slab can fill a strided slice of a gradient.
 __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ slab, long stride,
-                                                int splits, long n, float* __restrict__ out) {
+                                                int splits, long n, float* __restrict__ out,
+                                                long grp, long ostride, long ooff) {
   __shared__ float part[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long e = (long)blockIdx.x * 64 + lane;
@@ -815,7 +818,9 @@ __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ slab, 
   }
   part[wave][lane] = s;
   __syncthreads();
-  if (wave == 0 && e < n) out[e] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+  if (wave == 0 && e < n)
+    out[(e / grp) * ostride + ooff + e % grp] =
+        ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
 }
 
 // ------------------------------------------------------------------------------------
@@ -977,16 +982,17 @@ bool wgrad_supported(int mode, int cout, int cin) {
   return false;
 }
 
-// Splits: enough workgroups for ~one full wave of resident workgroups (about 4 per CU on
-// 256 CUs), at least two pixel chunks each, and a bounded slab.
+// Splits: splits x input-channel blocks fills ONE round of resident workgroups (3 per CU on
+// 256 CUs) without a straggler round (floor, not ceil: 770 workgroups on 768 slots would
+// double the time), at least two pixel chunks each, and a slab of at most 256 MB.
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
   int cin_t, pr, pc;
   wgrad_tile(mode, Cout, cin_t, pr, pc);
   const int taps = mode == W_C3 ? 9 : (mode == W_UP2 ? 4 : 1);
   const long units = (long)N * ((KH + pr - 1) / pr) * ((KW + pc - 1) / pc);
   const long cib = (Cin + cin_t - 1) / cin_t;
-  long want = (768 + cib - 1) / cib;
-  const long slab_cap = (16L << 20) / ((long)Cout * Cin * taps + Cout);  // <= 64 MB of slab
+  long want = 768 / cib;
+  const long slab_cap = (64L << 20) / ((long)Cout * Cin * taps + Cout);  // <= 256 MB of slab
   if (want > slab_cap) want = slab_cap;
   if (want > units / 2) want = units / 2;
   if (want < 1) want = 1;
@@ -1016,7 +1022,15 @@ hipError_t launch_reduce(const float* slab, long slab_stride, int splits, long n
                          hipStream_t s) {
   const long blocks = (n + 63) / 64;
   hipLaunchKernelGGL(k_reduce, dim3((unsigned)blocks), dim3(256), 0, s, slab, slab_stride, splits,
-                     n, out);
+                     n, out, n, 0L, 0L);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce_scatter(const float* slab, long slab_stride, int splits, long n,
+                                 float* out, long grp, long ostride, long ooff, hipStream_t s) {
+  const long blocks = (n + 63) / 64;
+  hipLaunchKernelGGL(k_reduce, dim3((unsigned)blocks), dim3(256), 0, s, slab, slab_stride, splits,
+                     n, out, grp, ostride, ooff);
   return hipGetLastError();
 }
 

@@ -120,12 +120,18 @@ hipError_t launch_l1(const float* a, const float* b, long n, double* part, doubl
                      hipStream_t s);
 hipError_t launch_head_bwd(const HeadBwdArgs& h, hipStream_t s);
 int wgrad_thin_splits(long npx);
+hipError_t launch_wgrad_c3_thin(const float* g, int cout, const float* x, int x_stride, int x_off,
+                                int N, int C, int H, int W, float* slab, long slab_stride,
+                                int cin_total, int ci_base, int with_bias, int splits,
+                                hipStream_t s);
 hipError_t launch_wgrad_thin(const float* g, int g_stride, int cout, const float* x, long npx,
                              float* slab, int splits, float* dwb, hipStream_t s);
 hipError_t launch_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);
 hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s);
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
 hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s);
+hipError_t launch_reduce_scatter(const float* slab, long slab_stride, int splits, long n,
+                                 float* out, long grp, long ostride, long ooff, hipStream_t s);
 hipError_t launch_reduce(const float* slab, long slab_stride, int splits, long n, float* out,
                          hipStream_t s);
 bool fwd_supported(int gather, int nout);

@@ -260,14 +260,39 @@ __global__ __launch_bounds__(256) void k_n2n_loss(const float* __restrict__ out,
   block_store_partials<2>(v, partials);
 }
 
-__global__ void k_n2n_finalize(const double* __restrict__ partials, int nblk, double M,
-                               float lambda, float* __restrict__ loss3) {
-  if (threadIdx.x != 0) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    s1 += partials[b * kLossTerms + 0];
-    s2 += partials[b * kLossTerms + 1];
+// Sum of the first T terms of the block partials by one 256-thread block: thread t adds
+// blocks t, t+256, ... in order, then a fixed tree (deterministic; result valid in thread 0).
+template <int T>
+__device__ __forceinline__ void sum_partials(const double* __restrict__ partials, int nblk,
+                                             double (&out)[T]) {
+  __shared__ double sh[T][256];
+  const int t = threadIdx.x;
+  double v[T];
+#pragma unroll
+  for (int k = 0; k < T; ++k) v[k] = 0.0;
+  for (int b = t; b < nblk; b += 256)
+#pragma unroll
+    for (int k = 0; k < T; ++k) v[k] += partials[b * kLossTerms + k];
+#pragma unroll
+  for (int k = 0; k < T; ++k) sh[k][t] = v[k];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w)
+#pragma unroll
+      for (int k = 0; k < T; ++k) sh[k][t] += sh[k][t + w];
+    __syncthreads();
   }
+#pragma unroll
+  for (int k = 0; k < T; ++k) out[k] = sh[k][0];
+}
+
+__global__ __launch_bounds__(256) void k_n2n_finalize(const double* __restrict__ partials, int nblk,
+                                                      double M, float lambda,
+                                                      float* __restrict__ loss3) {
+  double sums[2];
+  sum_partials<2>(partials, nblk, sums);
+  if (threadIdx.x != 0) return;
+  const double s1 = sums[0], s2 = sums[1];
   const float l1 = (float)(s1 / M);
   const float l2 = lambda * (float)(s2 / M);
   loss3[0] = l1;
@@ -312,13 +337,13 @@ __global__ __launch_bounds__(256) void k_structure_loss(
   block_store_partials<4>(v, partials);
 }
 
-__global__ void k_structure_finalize(const double* __restrict__ partials, int nblk, double M,
-                                     double M1, double M2, float alpha, float beta, float gamma,
-                                     float* __restrict__ loss5) {
+__global__ __launch_bounds__(256) void k_structure_finalize(const double* __restrict__ partials,
+                                                            int nblk, double M, double M1,
+                                                            double M2, float alpha, float beta,
+                                                            float gamma, float* __restrict__ loss5) {
+  double s[4];
+  sum_partials<4>(partials, nblk, s);
   if (threadIdx.x != 0) return;
-  double s[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int b = 0; b < nblk; ++b)
-    for (int t = 0; t < 4; ++t) s[t] += partials[b * kLossTerms + t];
   const float pix = (float)(s[0] / M), tv1 = (float)(s[1] / M1), tv2 = (float)(s[2] / M2),
               cst = (float)(s[3] / M);
   loss5[0] = pix;
@@ -424,7 +449,7 @@ hipError_t launch_n2n_loss(const float* out, const float* sub2, const float* den
                      w, invM, lamM, dout, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_n2n_finalize, dim3(1), dim3(64), 0, s, part, kLossBlocks, M, lambda, loss3);
+  hipLaunchKernelGGL(k_n2n_finalize, dim3(1), dim3(256), 0, s, part, kLossBlocks, M, lambda, loss3);
   return hipGetLastError();
 }
 
@@ -443,7 +468,7 @@ hipError_t launch_structure_loss(const float* pred, const float* pred2, const fl
                      H, W, ga, gtv1, gtv2, gc, dpred, dpred2, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_structure_finalize, dim3(1), dim3(64), 0, s, part, kLossBlocks, M, M1, M2,
+  hipLaunchKernelGGL(k_structure_finalize, dim3(1), dim3(256), 0, s, part, kLossBlocks, M, M1, M2,
                      alpha, beta, gamma, loss5);
   return hipGetLastError();
 }

@@ -197,11 +197,14 @@ __global__ __launch_bounds__(256) void k_ssim_part(const uint8_t* __restrict__ a
 }
 
 // kind 0: PSNR from the squared-error sum; 1: mean (SSIM, L1) of the partials over `count`
-__global__ void k_eval_finalize(const double* __restrict__ part, int nparts, double count, int kind,
-                                double* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  double s = 0.0;
-  for (int i = 0; i < nparts; ++i) s += part[i];
+__global__ __launch_bounds__(256) void k_eval_finalize(const double* __restrict__ part, int nparts,
+                                                       double count, int kind,
+                                                       double* __restrict__ out) {
+  __shared__ double sh[256];
+  double v = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) v += part[i];  // fixed order per thread
+  const double s = block_sum_d(v, sh);
+  if (threadIdx.x != 0) return;
   const double mean = s / count;
   out[0] = kind == 0 ? 10.0 * log10(255.0 * 255.0 / mean) : mean;
 }
@@ -243,7 +246,7 @@ hipError_t launch_psnr(const uint8_t* a, const uint8_t* b, long n, double* part,
                        hipStream_t s) {
   const unsigned nb = blocks_for(n);
   hipLaunchKernelGGL(k_psnr_part, dim3(nb), dim3(256), 0, s, a, b, n, part);
-  hipLaunchKernelGGL(k_eval_finalize, dim3(1), dim3(64), 0, s, part, (int)nb, (double)n, 0, out);
+  hipLaunchKernelGGL(k_eval_finalize, dim3(1), dim3(256), 0, s, part, (int)nb, (double)n, 0, out);
   return hipGetLastError();
 }
 
@@ -252,7 +255,7 @@ hipError_t launch_ssim(const uint8_t* a, const uint8_t* b, int C, int H, int W, 
   const long total = (long)C * (H - 10) * (W - 10);
   const unsigned nb = blocks_for(total);
   hipLaunchKernelGGL(k_ssim_part, dim3(nb), dim3(256), 0, s, a, b, C, H, W, hwc, part);
-  hipLaunchKernelGGL(k_eval_finalize, dim3(1), dim3(64), 0, s, part, (int)nb, (double)total, 1,
+  hipLaunchKernelGGL(k_eval_finalize, dim3(1), dim3(256), 0, s, part, (int)nb, (double)total, 1,
                      out);
   return hipGetLastError();
 }
@@ -261,7 +264,7 @@ hipError_t launch_l1(const float* a, const float* b, long n, double* part, doubl
                      hipStream_t s) {
   const unsigned nb = blocks_for(n);
   hipLaunchKernelGGL(k_l1_part, dim3(nb), dim3(256), 0, s, a, b, n, part);
-  hipLaunchKernelGGL(k_eval_finalize, dim3(1), dim3(64), 0, s, part, (int)nb, (double)n, 1, out);
+  hipLaunchKernelGGL(k_eval_finalize, dim3(1), dim3(256), 0, s, part, (int)nb, (double)n, 1, out);
   return hipGetLastError();
 }
 

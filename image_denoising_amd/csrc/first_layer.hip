@@ -81,35 +81,42 @@ __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, i
   for (int e = tid; e < npx * (E0_CO / 4); e += 256) o4[e] = s4[e];
 }
 
-// dW/db partials.  A block owns a contiguous range of image rows (of the flattened N*H rows)
-// and walks them in 128-pixel segments: the gradient segment [128][48] is staged in LDS with
-// float4 loads, the input rows y-1..y+1 (+1-pixel halo) likewise; then 240 threads = 5 pixel
-// phases x 48 output channels accumulate W[co][ci][t] (and b[co]) from broadcast LDS reads.
-// Slab row layout = the PyTorch parameter layout: W[co][ci][3][3] then b[co].
+// Weight gradient of a 3x3 conv with few input channels C and CO output channels:
+// enc_conv0 (C = in_nc, CO = 48) and the network-input slice of dec_conv1a (C = in_nc,
+// CO = 96, written next to the MFMA kernel's columns of the same slab).  Block b owns image
+// rows [R*b/splits, R*(b+1)/splits) of the flattened N*H rows (possibly none: it then writes
+// zeros, so every slab row is defined) and walks them in 128-pixel segments: the gradient
+// segment [128][CO] is staged in LDS with float4 loads, the input rows y-1..y+1 (+halo)
+// likewise; then NG = 384/CO pixel phases x CO output channels accumulate W[co][ci][t]
+// (and b[co]) from broadcast LDS reads.  Slab row = PyTorch layout W[co][cin_total][3][3]
+// then b[co]; this kernel fills input channels [ci_base, ci_base + C) (+ b if with_bias).
 constexpr int E0_SEG = 128;
-template <int C>
-__global__ __launch_bounds__(256) void k_enc0_wgrad(const float* __restrict__ g,
-                                                    const float* __restrict__ x, int x_stride,
-                                                    int x_off, int N, int H, int W, int rows_per,
-                                                    float* __restrict__ slab) {
-  constexpr int KT = 9 * C;
-  __shared__ __attribute__((aligned(16))) float gr[E0_SEG * E0_CO];
+constexpr int C3T_THREADS = 384;
+template <int C, int CO>
+__global__ __launch_bounds__(C3T_THREADS) void k_wgrad_c3_thin(const float* __restrict__ g,
+                                                       const float* __restrict__ x, int x_stride,
+                                                       int x_off, int N, int H, int W,
+                                                       float* __restrict__ slab, long slab_stride,
+                                                       int cin_total, int ci_base, int with_bias) {
+  constexpr int KT = 9 * C, NG = C3T_THREADS / CO;
+  __shared__ __attribute__((aligned(16))) float gr[E0_SEG * CO];
   __shared__ float xr[3][C][E0_SEG + 2];
-  __shared__ float red[4][E0_CO][KT + 1];
-  const int tid = threadIdx.x, co = tid % E0_CO, grp = tid / E0_CO;  // grp 5: loader only
+  __shared__ float red[NG - 1][CO][KT + 1];
+  const int tid = threadIdx.x, co = tid % CO, grp = tid / CO;
   float acc[KT + 1];
 #pragma unroll
   for (int j = 0; j <= KT; ++j) acc[j] = 0.f;
-  const int rb = blockIdx.x * rows_per;
-  const int re = rb + rows_per < N * H ? rb + rows_per : N * H;
+  const long R = (long)N * H;
+  const int rb = (int)(R * blockIdx.x / gridDim.x), re = (int)(R * (blockIdx.x + 1) / gridDim.x);
   for (int row = rb; row < re; ++row) {
     const int n = row / H, y = row - n * H;
     for (int x0 = 0; x0 < W; x0 += E0_SEG) {
       const int seg = W - x0 < E0_SEG ? W - x0 : E0_SEG;
       __syncthreads();
-      const float4* g4 = reinterpret_cast<const float4*>(g + ((long)row * W + x0) * E0_CO);
-      for (int e = tid; e < seg * (E0_CO / 4); e += 256) reinterpret_cast<float4*>(gr)[e] = g4[e];
-      for (int e = tid; e < 3 * C * (seg + 2); e += 256) {
+      const float4* g4 = reinterpret_cast<const float4*>(g + ((long)row * W + x0) * CO);
+      for (int e = tid; e < seg * (CO / 4); e += C3T_THREADS)
+        reinterpret_cast<float4*>(gr)[e] = g4[e];
+      for (int e = tid; e < 3 * C * (seg + 2); e += C3T_THREADS) {
         const int dy = e / (C * (seg + 2)), r = e - dy * (C * (seg + 2));
         const int ci = r / (seg + 2), xx = r - ci * (seg + 2);
         const int gy = y + dy - 1, gx = x0 + xx - 1;
@@ -118,9 +125,9 @@ __global__ __launch_bounds__(256) void k_enc0_wgrad(const float* __restrict__ g,
                              : 0.f;
       }
       __syncthreads();
-      if (grp < 5) {
-        for (int px = grp; px < seg; px += 5) {
-          const float gv = gr[px * E0_CO + co];
+      {
+        for (int px = grp; px < seg; px += NG) {
+          const float gv = gr[px * CO + co];
 #pragma unroll
           for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
@@ -133,18 +140,21 @@ __global__ __launch_bounds__(256) void k_enc0_wgrad(const float* __restrict__ g,
       }
     }
   }
-  if (grp >= 1 && grp < 5)
+  if (grp >= 1)
 #pragma unroll
     for (int j = 0; j <= KT; ++j) red[grp - 1][co][j] = acc[j];
   __syncthreads();
   if (grp == 0) {
-    const long n_el = (long)E0_CO * KT + E0_CO;
-    float* row = slab + (long)blockIdx.x * n_el;
 #pragma unroll
-    for (int j = 0; j < KT; ++j)
-      row[co * KT + j] = (((acc[j] + red[0][co][j]) + red[1][co][j]) + red[2][co][j]) + red[3][co][j];
-    row[E0_CO * KT + co] =
-        (((acc[KT] + red[0][co][KT]) + red[1][co][KT]) + red[2][co][KT]) + red[3][co][KT];
+    for (int j = 0; j <= KT; ++j)
+#pragma unroll
+      for (int q = 0; q < NG - 1; ++q) acc[j] += red[q][co][j];
+    float* row = slab + (long)blockIdx.x * slab_stride;
+#pragma unroll
+    for (int ci = 0; ci < C; ++ci)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) row[((long)co * cin_total + ci_base + ci) * 9 + t] = acc[ci * 9 + t];
+    if (with_bias) row[(long)CO * cin_total * 9 + co] = acc[KT];
   }
 }
 
@@ -175,30 +185,46 @@ int enc0_wgrad_splits(int N, int H, int W) {
   return rows < 1024 ? rows : 1024;
 }
 
-// g: NHWC [N,H,W,48] contiguous (stride 48); x: NHWC view (stride, offset) with C channels
+template <int CO>
+static hipError_t run_c3_thin(const float* g, const float* x, int x_stride, int x_off, int N, int C,
+                              int H, int W, float* slab, long slab_stride, int cin_total,
+                              int ci_base, int with_bias, int splits, hipStream_t s) {
+#define DN_C3T(CC)                                                                              \
+  hipLaunchKernelGGL((k_wgrad_c3_thin<CC, CO>), dim3(splits), dim3(C3T_THREADS), 0, s, g, x,     \
+                     x_stride, x_off, N, H, W, slab, slab_stride, cin_total, ci_base, with_bias)
+  if (C == 1) DN_C3T(1);
+  else if (C == 2) DN_C3T(2);
+  else if (C == 3) DN_C3T(3);
+  else if (C == 4) DN_C3T(4);
+  else return hipErrorInvalidValue;
+#undef DN_C3T
+  return hipGetLastError();
+}
+
+// g: NHWC [N,H,W,cout] contiguous; x: NHWC view (stride, offset) holding the C channels
+hipError_t launch_wgrad_c3_thin(const float* g, int cout, const float* x, int x_stride, int x_off,
+                                int N, int C, int H, int W, float* slab, long slab_stride,
+                                int cin_total, int ci_base, int with_bias, int splits,
+                                hipStream_t s) {
+  if (C < 1 || C > 4 || splits < 1) return hipErrorInvalidValue;
+  if (cout == 48)
+    return run_c3_thin<48>(g, x, x_stride, x_off, N, C, H, W, slab, slab_stride, cin_total,
+                           ci_base, with_bias, splits, s);
+  if (cout == 96)
+    return run_c3_thin<96>(g, x, x_stride, x_off, N, C, H, W, slab, slab_stride, cin_total,
+                           ci_base, with_bias, splits, s);
+  return hipErrorInvalidValue;
+}
+
 hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int x_stride,
                              int x_off, int N, int C, int H, int W, float* slab, int splits,
                              float* dwb, hipStream_t s) {
-  if (C < 1 || C > 4 || g_stride != E0_CO) return hipErrorInvalidValue;
-  const int rows = N * H;
-  const int per = (rows + splits - 1) / splits;
-  const int blocks = (rows + per - 1) / per;
-  if (C == 1)
-    hipLaunchKernelGGL(k_enc0_wgrad<1>, dim3(blocks), dim3(256), 0, s, g, x, x_stride, x_off, N, H,
-                       W, per, slab);
-  else if (C == 2)
-    hipLaunchKernelGGL(k_enc0_wgrad<2>, dim3(blocks), dim3(256), 0, s, g, x, x_stride, x_off, N, H,
-                       W, per, slab);
-  else if (C == 3)
-    hipLaunchKernelGGL(k_enc0_wgrad<3>, dim3(blocks), dim3(256), 0, s, g, x, x_stride, x_off, N, H,
-                       W, per, slab);
-  else
-    hipLaunchKernelGGL(k_enc0_wgrad<4>, dim3(blocks), dim3(256), 0, s, g, x, x_stride, x_off, N, H,
-                       W, per, slab);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (g_stride != E0_CO) return hipErrorInvalidValue;
   const long n_el = (long)E0_CO * 9 * C + E0_CO;
-  return launch_reduce(slab, n_el, blocks, n_el, dwb, s);
+  hipError_t e = launch_wgrad_c3_thin(g, E0_CO, x, x_stride, x_off, N, C, H, W, slab, n_el, C, 0,
+                                      1, splits, s);
+  if (e != hipSuccess) return e;
+  return launch_reduce(slab, n_el, splits, n_el, dwb, s);
 }
 
 // ------------------------------------------------------------------------------------

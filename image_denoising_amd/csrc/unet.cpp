@@ -166,9 +166,11 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
       if (L.deconv) { KH = H >> (lvl + 1); KW = W >> (lvl + 1); }
       int sp = i == ENC0   ? enc0_wgrad_splits(N, KH, KW)
                : (i == NINC && p.OC <= 4) ? wgrad_thin_splits((long)N * KH * KW)
-                           : wgrad_splits(mode, N, KH, KW, L.cin, L.cout);
+                           : wgrad_splits(mode, N, KH, KW, i == D1A ? 2 * nf : L.cin, L.cout);
       p.splits[i] = sp;
-      slab = std::max(slab, (long)sp * (L.wcount + L.cout));
+      long need = (long)sp * (L.wcount + L.cout);
+      if (i == D1A) need += (long)enc0_wgrad_splits(N, KH, KW) * 96 * p.C * 9;  // input slice
+      slab = std::max(slab, need);
     }
     p.slab = alloc(0, 0);
     off = p.slab + 64 + (slab + 63) / 64 * 64;  // 64 zero floats in front (wgrad DMA padding)
@@ -460,8 +462,28 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                p.splits[D1B], s));
   DN_TRY(conv_dgrad(V(p.g_d1b, 96), N, H(0), Wd(0), 96, Wt(D1B), 96, 3, EPI_MASK,
                     V(p.d1a, 96), V(p.g_d1a, 96), s));
-  DN_TRY(wgrad(W_C3, V(p.g_d1a, 96), V(p.c1, p.c1s), N, H(0), Wd(0), 96, p.c1k, G(D1A), slab,
-               p.splits[D1A], s));
+  // dec_conv1a weight gradient: the MFMA kernel over the up1 channels [0, 2nf) and the thin
+  // kernel over the network-input channels [2nf, 2nf + C), into the same slab rows
+  {
+    const long n = (long)96 * p.c1k * 9 + 96;
+    WgradArgs a{};
+    a.g = ws + p.g_d1a; a.g_stride = 96; a.g_off = 0;
+    a.x = ws + p.c1; a.x_stride = p.c1s; a.x_off = 0;
+    a.N = N; a.KH = H(0); a.KW = Wd(0); a.Cout = 96; a.Cin = 2 * nf;
+    a.zeros = slab; a.slab = slab + 64; a.slab_stride = n;
+    a.wlayout = 0; a.cin_total = p.c1k; a.ci_base = 0; a.bias = 1;
+    DN_TRY(hipMemsetAsync(slab, 0, 64 * sizeof(float), s));
+    DN_TRY(launch_wgrad(W_C3, a, p.splits[D1A], s));
+    DN_TRY(launch_reduce(slab + 64, n, p.splits[D1A], n, G(D1A), s));
+    // input-channel slice: own (compact [co][C][9]) slab after the MFMA kernel's rows, own
+    // split count, then scattered into W[co][2nf + ci][t] (overwrites the unreduced columns)
+    float* thin = slab + 64 + (long)p.splits[D1A] * n;
+    const long nt = 96L * C * 9;
+    const int st = enc0_wgrad_splits(N, H(0), Wd(0));
+    DN_TRY(launch_wgrad_c3_thin(ws + p.g_d1a, 96, ws + p.c1, p.c1s, 2 * nf, N, C, H(0), Wd(0),
+                                thin, nt, C, 0, 0, st, s));
+    DN_TRY(launch_reduce_scatter(thin, nt, st, nt, G(D1A), 9L * C, 9L * p.c1k, 9L * 2 * nf, s));
+  }
   // only the up1 part of the concat needs a gradient (pool0 is the network input)
   DN_TRY(conv_dgrad(V(p.g_d1a, 96), N, H(0), Wd(0), 96, Wt(D1A), 2 * nf, 3, EPI_PLAIN, none,
                     V(p.g_c1, 2 * nf), s));
