@@ -363,8 +363,7 @@ dn_status dn_conv2d_backward_data(const float* dz, int N, int H, int W, int Cout
 
 size_t dn_conv2d_wgrad_slab_size(int N, int H, int W, int Cin, int Cout, int ksize) {
   const int mode = ksize == 3 ? W_C3 : W_C1;
-  const int sp = wgrad_splits(mode, N, H, W, Cin, Cout);
-  return sizeof(float) * (64 + (size_t)sp * ((size_t)Cout * Cin * ksize * ksize + Cout));
+  return sizeof(float) * (64 + (size_t)wgrad_slab_floats(mode, N, H, W, Cin, Cout));
 }
 
 dn_status dn_conv2d_backward_weight(const float* dz, const float* x, int x_stride, int N, int H,
@@ -415,8 +414,7 @@ dn_status dn_deconv2x2_backward_data(const float* dy, int dy_stride, int N, int 
 }
 
 size_t dn_deconv2x2_wgrad_slab_size(int N, int H, int W, int Cin, int Cout) {
-  const int sp = wgrad_splits(W_UP2, N, H, W, Cin, Cout);
-  return sizeof(float) * (64 + (size_t)sp * ((size_t)Cout * Cin * 4 + Cout));
+  return sizeof(float) * (64 + (size_t)wgrad_slab_floats(W_UP2, N, H, W, Cin, Cout));
 }
 
 dn_status dn_deconv2x2_backward_weight(const float* dy, int dy_stride, const float* x, int N, int H,

@@ -795,6 +795,127 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad3(WgradArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// 1x1 / deconv-2x2 weight gradient (nin_a, nin_b: arch_unet.py:186-189; up_k.deconv:
+// arch_unet.py:57).  M = output channels, N = ALL input channels, K = pixels: one workgroup
+// owns the whole Cout x Cin matrix for a contiguous range of 32-pixel row segments, so each
+// operand byte is read from HBM once.  Both operands are copied by per-lane addressed
+// global_load_lds_dwordx4 into double-buffered LDS ([px][Cout] and [px][Cin]), one barrier
+// per stage; the bias rides along as an MFMA against ones.
+//   deconv (up2 != 0): blockIdx.z = (a,b) parity; the gradient operand of low-res pixel
+//   (y, x) is g at (2y+a, 2x+b) of the 2KH x 2KW image.  Slab row r = z*splits + split holds
+//   [W_ab | b_ab] and the launcher reduces per parity (scattered into (in,out,2,2)) and the
+//   bias over all rows.
+// ------------------------------------------------------------------------------------
+template <int CO_FR, int CI_FR, int WM, int WN>
+struct Wg1Cfg {
+  static constexpr int COUT = 16 * CO_FR, CIN = 16 * CI_FR;
+  static constexpr int MFW = CO_FR / WM, NFW = CI_FR / WN;
+  static constexpr int NW = WM * WN, NTHR = 64 * NW;
+  static constexpr int PC = 32;
+  static constexpr int LGF = PC * COUT, LXF = PC * CIN;
+  static constexpr int LGP = LGF / 256, LXP = LXF / 256;
+  static constexpr int LBUF = LGF + LXF;
+  static_assert(LGF % 256 == 0 && LXF % 256 == 0, "whole 1 KiB DMA pieces");
+};
+
+template <int CO_FR, int CI_FR, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad1(WgradArgs a, int up2) {
+  using C = Wg1Cfg<CO_FR, CI_FR, WM, WN>;
+  __shared__ __attribute__((aligned(16))) float lds[2 * C::LBUF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 15, lgp = lane >> 4;
+  const int ux = (a.KW + C::PC - 1) / C::PC;
+  const long U = (long)a.N * a.KH * ux;
+  const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
+  const bool do_bias = wn == 0;
+  const int pa = up2 ? (int)(blockIdx.z >> 1) : 0, pb = up2 ? (int)(blockIdx.z & 1) : 0;
+  const int GH = up2 ? 2 * a.KH : a.KH, GW = up2 ? 2 * a.KW : a.KW, sc = up2 ? 2 : 1;
+
+  f32x4 acc[C::MFW][C::NFW];
+  f32x4 accb[C::MFW];
+#pragma unroll
+  for (int i = 0; i < C::MFW; ++i) {
+    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < C::NFW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  auto issue = [&](long u, float* buf) {
+    const int n = (int)(u / ((long)a.KH * ux));
+    const int rem = (int)(u - (long)n * a.KH * ux);
+    const int py = rem / ux, px0 = (rem % ux) * C::PC;
+    const float* gb = a.g + ((long)n * GH + sc * py + pa) * GW * a.g_stride + a.g_off;
+    for (int p = wave; p < C::LGP; p += C::NW) {
+      const int idx = p * 256 + lane * 4;
+      const int px = idx / C::COUT, co = idx - px * C::COUT;
+      const int gx = px0 + px;
+      const float* src = (gx < a.KW && co < a.Cout) ? gb + (long)(sc * gx + pb) * a.g_stride + co
+                                                     : a.zeros;
+      glds16(src, buf + p * 256);
+    }
+    const float* xb = a.x + ((long)n * a.KH + py) * a.KW * a.x_stride + a.x_off;
+    for (int p = wave; p < C::LXP; p += C::NW) {
+      const int idx = p * 256 + lane * 4;
+      const int px = idx / C::CIN, ci = idx - px * C::CIN;
+      const int gx = px0 + px;
+      const float* src = (gx < a.KW && ci < a.Cin) ? xb + (long)gx * a.x_stride + ci : a.zeros;
+      glds16(src, buf + C::LGF + p * 256);
+    }
+  };
+
+  if (u_beg < u_end) issue(u_beg, lds);
+  __syncthreads();
+  for (long u = u_beg; u < u_end; ++u) {
+    const int cb = (int)((u - u_beg) & 1);
+    const float* lg_ = lds + cb * C::LBUF;
+    const float* lx = lg_ + C::LGF;
+    if (u + 1 < u_end) issue(u + 1, lds + (cb ^ 1) * C::LBUF);
+#pragma unroll 2
+    for (int ks = 0; ks < C::PC / 4; ++ks) {
+      const int pc = 4 * ks + lgp;  // this lane's pixel (k = lane>>4)
+      float av[C::MFW], bv[C::NFW];
+#pragma unroll
+      for (int i = 0; i < C::MFW; ++i) av[i] = lg_[pc * C::COUT + (wm * C::MFW + i) * 16 + li];
+#pragma unroll
+      for (int j = 0; j < C::NFW; ++j) bv[j] = lx[pc * C::CIN + (wn * C::NFW + j) * 16 + li];
+#pragma unroll
+      for (int i = 0; i < C::MFW; ++i)
+#pragma unroll
+        for (int j = 0; j < C::NFW; ++j) acc[i][j] = mfma4(av[i], bv[j], acc[i][j]);
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < C::MFW; ++i) accb[i] = mfma4(av[i], 1.0f, accb[i]);
+      }
+    }
+    __syncthreads();  // next stage landed (vmcnt(0)); everyone done with this buffer
+  }
+
+  const long row = (long)blockIdx.z * gridDim.x + blockIdx.x;
+  float* slab = a.slab + row * a.slab_stride;
+#pragma unroll
+  for (int i = 0; i < C::MFW; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NFW; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = (wm * C::MFW + i) * 16 + 4 * lgp + r;
+        const int ci = (wn * C::NFW + j) * 16 + li;
+        if (co < a.Cout && ci < a.Cin)
+          slab[a.wlayout ? (long)ci * a.Cout + co : (long)co * a.Cin + ci] = acc[i][j][r];
+      }
+  if (do_bias && li == 0) {
+#pragma unroll
+    for (int i = 0; i < C::MFW; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = (wm * C::MFW + i) * 16 + 4 * lgp + r;
+        if (co < a.Cout) slab[(long)a.Cout * a.Cin + co] = accb[i][r];
+      }
+  }
+}
+
 // out[e] = sum_s slab[s][e] in a fixed order (bit-reproducible): a workgroup owns 64
 // consecutive elements; wave w sums splits w, w+4, w+8, ... in order, then the four wave
 // partials are added in wave order.
@@ -1016,6 +1137,60 @@ hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s)
     if (cf == 6) return run_wgrad<W_UP2, 2, 3, 1>(a, splits, s);
   }
   return hipErrorInvalidValue;
+}
+
+// ---- k_wgrad1 routing --------------------------------------------------------------
+static bool wgrad1_shape(int mode, int cin, int cout) {
+  return (mode == W_C1 || mode == W_UP2) && cin == cout && (cin == 96 || cin == 48);
+}
+
+bool wgrad1_ok(int mode, const WgradArgs& a) {
+  if (!wgrad1_shape(mode, a.Cin, a.Cout) || !a.zeros) return false;
+  if ((a.g_stride | a.g_off | a.x_stride | a.x_off) & 3) return false;
+  return a.g_off + a.Cout <= a.g_stride && a.x_off + a.Cin <= a.x_stride;
+}
+
+// one round of resident workgroups (3 per CU) over splits x parities, >= 2 segments each
+int wgrad1_splits(int mode, int N, int KH, int KW) {
+  const int z = mode == W_UP2 ? 4 : 1;
+  const long units = (long)N * KH * ((KW + 31) / 32);
+  long sp = 768 / z;
+  if (sp > units / 2) sp = units / 2;
+  return (int)(sp < 1 ? 1 : sp);
+}
+
+long wgrad_slab_floats(int mode, int N, int KH, int KW, int cin, int cout) {
+  const int taps = mode == W_C3 ? 9 : (mode == W_UP2 ? 4 : 1);
+  long f = (long)wgrad_splits(mode, N, KH, KW, cin, cout) * ((long)cout * cin * taps + cout);
+  if (wgrad1_shape(mode, cin, cout)) {
+    const long f1 = (long)(mode == W_UP2 ? 4 : 1) * wgrad1_splits(mode, N, KH, KW) *
+                    ((long)cout * cin + cout);
+    if (f1 > f) f = f1;
+  }
+  return f;
+}
+
+// k_wgrad1 + its reductions straight into dwb (PyTorch layout, bias after the weight)
+hipError_t launch_wgrad1(int mode, const WgradArgs& a0, float* dwb, hipStream_t s) {
+  const bool up2 = mode == W_UP2;
+  const int sp = wgrad1_splits(mode, a0.N, a0.KH, a0.KW), z = up2 ? 4 : 1;
+  const long W = (long)a0.Cout * a0.Cin, row = W + a0.Cout;
+  WgradArgs a = a0;
+  a.slab_stride = row;
+  a.wlayout = up2 ? 1 : 0;  // deconv weight (in, out, 2, 2): [ci][co] per parity
+  const dim3 grid(sp, 1, z);
+  if (a.Cout == 96)
+    hipLaunchKernelGGL((k_wgrad1<6, 6, 2, 2>), grid, dim3(256), 0, s, a, (int)up2);
+  else
+    hipLaunchKernelGGL((k_wgrad1<3, 3, 1, 3>), grid, dim3(192), 0, s, a, (int)up2);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (!up2) return launch_reduce(a.slab, row, sp, row, dwb, s);
+  for (int ab = 0; ab < 4; ++ab) {  // W[ci][co][a][b]
+    e = launch_reduce_scatter(a.slab + (long)ab * sp * row, row, sp, W, dwb, 1, 4, ab, s);
+    if (e != hipSuccess) return e;
+  }
+  return launch_reduce(a.slab + W, row, 4 * sp, a.Cout, dwb + 4 * W, s);  // bias: all rows
 }
 
 hipError_t launch_reduce(const float* slab, long slab_stride, int splits, long n, float* out,

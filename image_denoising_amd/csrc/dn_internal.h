@@ -130,6 +130,9 @@ hipError_t launch_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);
 hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s);
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
 hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s);
+bool wgrad1_ok(int mode, const WgradArgs& a);
+long wgrad_slab_floats(int mode, int N, int KH, int KW, int cin, int cout);
+hipError_t launch_wgrad1(int mode, const WgradArgs& a, float* dwb, hipStream_t s);
 hipError_t launch_reduce_scatter(const float* slab, long slab_stride, int splits, long n,
                                  float* out, long grp, long ostride, long ooff, hipStream_t s);
 hipError_t launch_reduce(const float* slab, long slab_stride, int splits, long n, float* out,

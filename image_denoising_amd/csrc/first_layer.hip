@@ -83,24 +83,24 @@ __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, i
 
 // Weight gradient of a 3x3 conv with few input channels C and CO output channels:
 // enc_conv0 (C = in_nc, CO = 48) and the network-input slice of dec_conv1a (C = in_nc,
-// CO = 96, written next to the MFMA kernel's columns of the same slab).  Block b owns image
-// rows [R*b/splits, R*(b+1)/splits) of the flattened N*H rows (possibly none: it then writes
-// zeros, so every slab row is defined) and walks them in 128-pixel segments: the gradient
-// segment [128][CO] is staged in LDS with float4 loads, the input rows y-1..y+1 (+halo)
-// likewise; then NG = 384/CO pixel phases x CO output channels accumulate W[co][ci][t]
-// (and b[co]) from broadcast LDS reads.  Slab row = PyTorch layout W[co][cin_total][3][3]
-// then b[co]; this kernel fills input channels [ci_base, ci_base + C) (+ b if with_bias).
-constexpr int E0_SEG = 128;
-constexpr int C3T_THREADS = 384;
+// CO = 96, into its own compact slab).  Block b owns image rows [R*b/splits, R*(b+1)/splits)
+// of the flattened N*H rows (possibly none: it then writes zeros, so every slab row is
+// defined).  Only the input rows y-1..y+1 (+halo, C channels) are staged in LDS; the
+// gradient streams from global memory (the CO threads of a pixel read one contiguous run)
+// with several loads in flight; NG = 192/CO pixel phases x CO output channels accumulate
+// W[co][ci][t] and b[co].  Slab row = W[co][cin_total][3][3] then b[co]; this kernel fills
+// input channels [ci_base, ci_base + C) (+ b if with_bias).
+constexpr int C3T_THREADS = 192, C3T_SEG = 256;
 template <int C, int CO>
 __global__ __launch_bounds__(C3T_THREADS) void k_wgrad_c3_thin(const float* __restrict__ g,
-                                                       const float* __restrict__ x, int x_stride,
-                                                       int x_off, int N, int H, int W,
-                                                       float* __restrict__ slab, long slab_stride,
-                                                       int cin_total, int ci_base, int with_bias) {
+                                                               const float* __restrict__ x,
+                                                               int x_stride, int x_off, int N,
+                                                               int H, int W,
+                                                               float* __restrict__ slab,
+                                                               long slab_stride, int cin_total,
+                                                               int ci_base, int with_bias) {
   constexpr int KT = 9 * C, NG = C3T_THREADS / CO;
-  __shared__ __attribute__((aligned(16))) float gr[E0_SEG * CO];
-  __shared__ float xr[3][C][E0_SEG + 2];
+  __shared__ float xr[3][C][C3T_SEG + 2];
   __shared__ float red[NG - 1][CO][KT + 1];
   const int tid = threadIdx.x, co = tid % CO, grp = tid / CO;
   float acc[KT + 1];
@@ -110,12 +110,9 @@ __global__ __launch_bounds__(C3T_THREADS) void k_wgrad_c3_thin(const float* __re
   const int rb = (int)(R * blockIdx.x / gridDim.x), re = (int)(R * (blockIdx.x + 1) / gridDim.x);
   for (int row = rb; row < re; ++row) {
     const int n = row / H, y = row - n * H;
-    for (int x0 = 0; x0 < W; x0 += E0_SEG) {
-      const int seg = W - x0 < E0_SEG ? W - x0 : E0_SEG;
+    for (int x0 = 0; x0 < W; x0 += C3T_SEG) {
+      const int seg = W - x0 < C3T_SEG ? W - x0 : C3T_SEG;
       __syncthreads();
-      const float4* g4 = reinterpret_cast<const float4*>(g + ((long)row * W + x0) * CO);
-      for (int e = tid; e < seg * (CO / 4); e += C3T_THREADS)
-        reinterpret_cast<float4*>(gr)[e] = g4[e];
       for (int e = tid; e < 3 * C * (seg + 2); e += C3T_THREADS) {
         const int dy = e / (C * (seg + 2)), r = e - dy * (C * (seg + 2));
         const int ci = r / (seg + 2), xx = r - ci * (seg + 2);
@@ -125,18 +122,18 @@ __global__ __launch_bounds__(C3T_THREADS) void k_wgrad_c3_thin(const float* __re
                              : 0.f;
       }
       __syncthreads();
-      {
-        for (int px = grp; px < seg; px += NG) {
-          const float gv = gr[px * CO + co];
+      const float* gp = g + ((long)row * W + x0) * CO + co;
+#pragma unroll 4
+      for (int px = grp; px < seg; px += NG) {
+        const float gv = gp[(long)px * CO];
 #pragma unroll
-          for (int dy = 0; dy < 3; ++dy)
+        for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-            for (int ci = 0; ci < C; ++ci)
+          for (int ci = 0; ci < C; ++ci)
 #pragma unroll
-              for (int dx = 0; dx < 3; ++dx)
-                acc[ci * 9 + dy * 3 + dx] = fmaf(gv, xr[dy][ci][px + dx], acc[ci * 9 + dy * 3 + dx]);
-          acc[KT] += gv;
-        }
+            for (int dx = 0; dx < 3; ++dx)
+              acc[ci * 9 + dy * 3 + dx] = fmaf(gv, xr[dy][ci][px + dx], acc[ci * 9 + dy * 3 + dx]);
+        acc[KT] += gv;
       }
     }
   }

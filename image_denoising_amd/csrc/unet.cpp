@@ -168,7 +168,9 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
                : (i == NINC && p.OC <= 4) ? wgrad_thin_splits((long)N * KH * KW)
                            : wgrad_splits(mode, N, KH, KW, i == D1A ? 2 * nf : L.cin, L.cout);
       p.splits[i] = sp;
-      long need = (long)sp * (L.wcount + L.cout);
+      long need = (i == ENC0 || i == D1A || (i == NINC && p.OC <= 4))
+                      ? (long)sp * (L.wcount + L.cout)
+                      : wgrad_slab_floats(mode, N, KH, KW, L.cin, L.cout);
       if (i == D1A) need += (long)enc0_wgrad_splits(N, KH, KW) * 96 * p.C * 9;  // input slice
       slab = std::max(slab, need);
     }
@@ -316,6 +318,7 @@ hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, 
   a.cin_total = cin; a.ci_base = 0; a.bias = 1;
   hipError_t e = hipMemsetAsync(slab, 0, 64 * sizeof(float), s);
   if (e != hipSuccess) return e;
+  if (wgrad1_ok(mode, a)) return launch_wgrad1(mode, a, dwb, s);  // 1x1 / deconv, own splits
   e = launch_wgrad(mode, a, splits, s);
   if (e != hipSuccess) return e;
   return launch_reduce(slab + 64, n, splits, n, dwb, s);
