@@ -14,6 +14,8 @@
 //
 // Data layout: activations NHWC fp32 (channels contiguous), weights in the reference's
 // PyTorch layout read through a strided view (no repacking pass).
+#include <cstdlib>
+
 #include "dn_internal.h"
 
 namespace dn {
@@ -41,8 +43,10 @@ constexpr int cround(int v, int mod, int res) { return v + (((res - v % mod) % m
 // ------------------------------------------------------------------------------------
 template <int GATHER, int NT, int MT>
 struct FwdCfg {
-  static constexpr int TW = 16, TH = 4 * MT;
-  static constexpr int KC = GATHER == G_C1 ? 32 : (NT >= 9 ? 4 : 8);
+  // G_UP: every wave covers all MT rows of the tile and wave w takes parity (a,b) = w
+  static constexpr int TW = 16, TH = GATHER == G_UP ? MT : 4 * MT;
+  static constexpr int KC = GATHER == G_C1 ? 32 : (GATHER == G_UP ? 16 : (NT >= 9 ? 4 : 8));
+  static constexpr int NZ = GATHER == G_UP ? 4 : 1;  // weight images per chunk in LDS
   static constexpr int TAPS = GATHER == G_C3 ? 9 : (GATHER == G_DN2 ? 4 : 1);
   static constexpr int IH = GATHER == G_C3 ? TH + 2 : (GATHER == G_DN2 ? 2 * TH : TH);
   static constexpr int IW = GATHER == G_C3 ? TW + 2 : (GATHER == G_DN2 ? 2 * TW : TW);
@@ -57,7 +61,7 @@ struct FwdCfg {
   static constexpr int XITEMS = (XQ + 255) / 256;
   static constexpr int PS = NP + 4;             // epilogue staging: pixel stride (floats)
   static constexpr int LST = 4 * 16 * PS;       // 4 waves x 16 pixels x PS
-  static constexpr int LT0 = (LX + 2 * LW) > LST ? (LX + 2 * LW) : LST;
+  static constexpr int LT0 = (LX + 2 * NZ * LW) > LST ? (LX + 2 * NZ * LW) : LST;
   static constexpr int LTOT = LT0 > 2 * HEAD_LW ? LT0 : 2 * HEAD_LW;  // HEAD: both 1x1 images
 };
 
@@ -72,7 +76,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a, HeadArgs hd) {
   __shared__ __attribute__((aligned(16))) float lds[HEAD ? C::LTOT : C::LT0];
   float* lx = lds;
   float* lw0 = lds + C::LX;
-  float* lw1 = lw0 + C::LW;
+  float* lw1 = lw0 + C::NZ * C::LW;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
@@ -133,9 +137,17 @@ __global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a, HeadArgs hd) {
     }
   };
   auto load_w = [&](int c, float* dst) {
-    const float* src = wp + (long)c * C::LW;
+    if constexpr (GATHER == G_UP) {  // the 4 parity images of chunk c, back to back
+      constexpr int PP = C::LW / 256;
 #pragma unroll
-    for (int p = wave; p < C::LW / 256; p += 4) glds16(src + p * 256 + lane * 4, dst + p * 256);
+      for (int p = wave; p < C::NZ * PP; p += 4)
+        glds16(a.wp + (long)(p / PP) * a.wp_z + (long)c * C::LW + (p % PP) * 256 + lane * 4,
+               dst + p * 256);
+    } else {
+      const float* src = wp + (long)c * C::LW;
+#pragma unroll
+      for (int p = wave; p < C::LW / 256; p += 4) glds16(src + p * 256 + lane * 4, dst + p * 256);
+    }
   };
 
   load_w(0, lw0);
@@ -157,7 +169,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a, HeadArgs hd) {
         float av[MT], bv[NT];
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
-          const int r = wave * MT + m;
+          const int r = GATHER == G_UP ? m : wave * MT + m;
           int off;
           if (GATHER == G_C3) off = (r + t / 3) * C::IW + li + t % 3;
           else if (GATHER == G_DN2) off = (2 * r + t / 2) * C::IW + 2 * li + (t & 1);
@@ -165,7 +177,8 @@ __global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a, HeadArgs hd) {
           av[m] = lx[kk * C::XCS + off];
         }
 #pragma unroll
-        for (int q = 0; q < NT; ++q) bv[q] = lw[(t * C::KC + kk) * C::WNS + q * 16 + li];
+        for (int q = 0; q < NT; ++q)
+          bv[q] = lw[(GATHER == G_UP ? wave * C::LW : 0) + (t * C::KC + kk) * C::WNS + q * 16 + li];
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -267,7 +280,8 @@ __global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a, HeadArgs hd) {
   } else {
 
   // epilogue.  C/D map of 16x16 MFMA: col (n) = lane&15, row (pixel x) = 4*(lane>>4) + reg.
-  const int ab = blockIdx.z;
+  const int ab = GATHER == G_UP ? wave : (int)blockIdx.z;
+  const int wrow = GATHER == G_UP ? 0 : wave * MT;  // first tile row of this wave
   const bool vec_out = a.out_layout != OUT_NCHW && ((a.out_stride | a.out_off | a.NOUT) & 3) == 0 &&
                        (a.epi != EPI_MASK || ((a.mask_stride | a.mask_off) & 3) == 0);
   if (vec_out) {
@@ -283,7 +297,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a, HeadArgs hd) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) st[(4 * lg + r) * C::PS + q * 16 + li] = acc[m][q][r];
       __syncthreads();
-      const int gy = ty0 + wave * MT + m;
+      const int gy = ty0 + wrow + m;
       if (gy < a.OH) {
         for (int e = lane; e < 16 * NQ; e += 64) {
           const int p = e / NQ, c = 4 * (e - p * NQ);
@@ -324,7 +338,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a, HeadArgs hd) {
   }
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
-    const int gy = ty0 + wave * MT + m;
+    const int gy = ty0 + wrow + m;
     if (gy >= a.OH) continue;
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
@@ -951,7 +965,7 @@ template <int GATHER, int NT, int MT>
 static hipError_t run_fwd(const FwdArgs& a, hipStream_t s) {
   using C = FwdCfg<GATHER, NT, MT>;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
-  dim3 grid(tx * ty, a.N, a.out_layout == OUT_UP2 ? 4 : 1);
+  dim3 grid(tx * ty, a.N, (a.out_layout == OUT_UP2 && GATHER != G_UP) ? 4 : 1);
   hipLaunchKernelGGL((k_fwd<GATHER, NT, MT>), grid, dim3(256), 0, s, a, HeadArgs{});
   return hipGetLastError();
 }
@@ -998,7 +1012,7 @@ bool fwd_supported(int gather, int nout) {
   const int nt = (nout + 15) / 16;
   if (gather == G_C3) return nt == 3 || nt == 6 || nt == 9;
   if (gather == G_C1) return nt == 1 || nt == 3 || nt == 6;
-  if (gather == G_DN2) return nt == 3 || nt == 6;
+  if (gather == G_DN2 || gather == G_UP) return nt == 3 || nt == 6;
   return false;
 }
 
@@ -1015,6 +1029,9 @@ bool fwd_geometry(int gather, int nout, FwdGeom& g) {
   } else if (gather == G_DN2) {
     if (nt == 3) { geom<G_DN2, 3, 4>(g); return true; }
     if (nt == 6) { geom<G_DN2, 6, 4>(g); return true; }
+  } else if (gather == G_UP) {
+    if (nt == 3) { geom<G_UP, 3, 4>(g); return true; }
+    if (nt == 6) { geom<G_UP, 6, 4>(g); return true; }
   }
   return false;
 }
@@ -1050,9 +1067,18 @@ hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s) {
     if (nt == 6) return small ? run_fwd<G_C3, 6, 1>(a, s) : run_fwd<G_C3, 6, 4>(a, s);
     if (nt == 9) return small ? run_fwd<G_C3, 9, 1>(a, s) : run_fwd<G_C3, 9, 2>(a, s);
   } else if (gather == G_C1) {
+    static const int c1_mt = getenv("DN_C1_MT") ? atoi(getenv("DN_C1_MT")) : 2;  // tuning probe
     if (nt == 1) return run_fwd<G_C1, 1, 4>(a, s);
     if (nt == 3) return small ? run_fwd<G_C1, 3, 1>(a, s) : run_fwd<G_C1, 3, 4>(a, s);
-    if (nt == 6) return small ? run_fwd<G_C1, 6, 1>(a, s) : run_fwd<G_C1, 6, 4>(a, s);
+    if (nt == 6) {
+      if (small || c1_mt == 1) return run_fwd<G_C1, 6, 1>(a, s);
+      if (c1_mt == 2) return run_fwd<G_C1, 6, 2>(a, s);
+      return run_fwd<G_C1, 6, 4>(a, s);
+    }
+  } else if (gather == G_UP) {
+    if (a.out_layout != OUT_UP2) return hipErrorInvalidValue;
+    if (nt == 3) return run_fwd<G_UP, 3, 4>(a, s);
+    if (nt == 6) return run_fwd<G_UP, 6, 4>(a, s);
   } else if (gather == G_DN2) {
     if (nt == 3) return small ? run_fwd<G_DN2, 3, 1>(a, s) : run_fwd<G_DN2, 3, 4>(a, s);
     if (nt == 6) return small ? run_fwd<G_DN2, 6, 1>(a, s) : run_fwd<G_DN2, 6, 4>(a, s);

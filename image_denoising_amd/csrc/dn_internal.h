@@ -11,6 +11,7 @@ enum Gather {
   G_C3 = 0,   // 3x3, stride 1, pad 1: in(y+ky-1, x+kx-1), 9 taps     (conv fwd / conv dgrad)
   G_C1 = 1,   // 1x1: in(y, x), 1 tap                                  (1x1 conv, deconv fwd)
   G_DN2 = 2,  // in(2y+a, 2x+b), 4 taps                                (deconv data-grad)
+  G_UP = 3,   // in(y, x), 1 tap, the 4 waves take the 4 (a,b) parities (deconv forward)
 };
 
 // How the weight-gradient kernel pairs its two operands over the pixel (K) dimension.
@@ -99,11 +100,10 @@ hipError_t launch_pack(int gather, const WView& wv, int K, int nout, int nz, flo
 hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s);
 hipError_t launch_enc0_fwd(const float* x, int N, int C, int H, int W, const float* w,
                            const float* b, float* out, float* cat, int cat_stride, int cat_off,
-                           int cat_zero_to, hipStream_t s);
+                           int cat_zero_to, float* xcopy, hipStream_t s);
 int enc0_wgrad_splits(int N, int H, int W);
-hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int x_stride,
-                             int x_off, int N, int C, int H, int W, float* slab, int splits,
-                             float* dwb, hipStream_t s);
+hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int N, int C, int H,
+                             int W, float* slab, int splits, float* dwb, hipStream_t s);
 constexpr int EVAL_PARTS = 1024;
 hipError_t launch_u8_to_unit(const uint8_t* x, long n, float* y, hipStream_t s);
 hipError_t launch_tile_extract(const uint8_t* img, int C, int H, int W, int ps, int stride,
@@ -120,10 +120,9 @@ hipError_t launch_l1(const float* a, const float* b, long n, double* part, doubl
                      hipStream_t s);
 hipError_t launch_head_bwd(const HeadBwdArgs& h, hipStream_t s);
 int wgrad_thin_splits(long npx);
-hipError_t launch_wgrad_c3_thin(const float* g, int cout, const float* x, int x_stride, int x_off,
-                                int N, int C, int H, int W, float* slab, long slab_stride,
-                                int cin_total, int ci_base, int with_bias, int splits,
-                                hipStream_t s);
+hipError_t launch_wgrad_c3_thin(const float* g, int cout, const float* x, int N, int C, int H,
+                                int W, float* slab, long slab_stride, int cin_total, int ci_base,
+                                int with_bias, int splits, hipStream_t s);
 hipError_t launch_wgrad_thin(const float* g, int g_stride, int cout, const float* x, long npx,
                              float* slab, int splits, float* dwb, hipStream_t s);
 hipError_t launch_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);

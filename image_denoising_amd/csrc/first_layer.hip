@@ -23,7 +23,8 @@ __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, i
                                                   int W, const float* __restrict__ w,
                                                   const float* __restrict__ b,
                                                   float* __restrict__ out, float* __restrict__ cat,
-                                                  int cat_stride, int cat_off, int cat_zero_to) {
+                                                  int cat_stride, int cat_off, int cat_zero_to,
+                                                  float* __restrict__ xcopy) {
   constexpr int KT = 9 * C;
   __shared__ __attribute__((aligned(16))) float wl[(KT + 1) * E0_CO];  // [tap*C+ci | bias][co]
   __shared__ __attribute__((aligned(16))) float st[256 * E0_CO];
@@ -64,7 +65,11 @@ __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, i
       v.z = v.z > 0.f ? v.z : v.z * 0.2f; v.w = v.w > 0.f ? v.w : v.w * 0.2f;
       *reinterpret_cast<float4*>(st + tid * E0_CO + 4 * cq) = v;
     }
-    // the input's slice of the up1 concat buffer (centre tap = the pixel itself)
+    // the input's slice of the up1 concat buffer (centre tap = the pixel itself), and the
+    // compact NCHW copy the weight gradients read (only when a backward follows)
+    if (xcopy)
+#pragma unroll
+      for (int ci = 0; ci < C; ++ci) xcopy[(n * C + ci) * hw + r] = xin[4 * C + ci];
     float* d = cat + p * cat_stride + cat_off;
     if (C == 1 && cat_zero_to - cat_off == 4 && ((cat_stride | cat_off) & 3) == 0) {
       *reinterpret_cast<float4*>(d) = make_float4(xin[4], 0.f, 0.f, 0.f);
@@ -83,61 +88,65 @@ __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, i
 
 // Weight gradient of a 3x3 conv with few input channels C and CO output channels:
 // enc_conv0 (C = in_nc, CO = 48) and the network-input slice of dec_conv1a (C = in_nc,
-// CO = 96, into its own compact slab).  Block b owns image rows [R*b/splits, R*(b+1)/splits)
-// of the flattened N*H rows (possibly none: it then writes zeros, so every slab row is
-// defined).  Only the input rows y-1..y+1 (+halo, C channels) are staged in LDS; the
-// gradient streams from global memory (the CO threads of a pixel read one contiguous run)
-// with several loads in flight; NG = 192/CO pixel phases x CO output channels accumulate
-// W[co][ci][t] and b[co].  Slab row = W[co][cin_total][3][3] then b[co]; this kernel fills
-// input channels [ci_base, ci_base + C) (+ b if with_bias).
-constexpr int C3T_THREADS = 192, C3T_SEG = 256;
+// CO = 96, into its own compact slab).  The input operand is the network input itself, NCHW
+// (a compact copy the forward keeps), so its rows stage with contiguous loads.  Block b owns
+// image rows [R*b/splits, R*(b+1)/splits) of the flattened N*H rows (possibly none: it then
+// writes zeros, so every slab row is defined) and walks them in 128-pixel segments: the
+// gradient segment [128][CO] is staged in LDS with float4 loads, the input rows y-1..y+1
+// (+halo) likewise; then NG = 256/CO pixel phases x CO output channels accumulate
+// W[co][ci][t] and b[co] from broadcast LDS reads (threads past NG*CO only load).
+// Slab row = W[co][cin_total][3][3] then b[co]; this kernel fills input channels
+// [ci_base, ci_base + C) (+ b if with_bias).
+constexpr int E0_SEG = 128;
 template <int C, int CO>
-__global__ __launch_bounds__(C3T_THREADS) void k_wgrad_c3_thin(const float* __restrict__ g,
-                                                               const float* __restrict__ x,
-                                                               int x_stride, int x_off, int N,
-                                                               int H, int W,
-                                                               float* __restrict__ slab,
-                                                               long slab_stride, int cin_total,
-                                                               int ci_base, int with_bias) {
-  constexpr int KT = 9 * C, NG = C3T_THREADS / CO;
-  __shared__ float xr[3][C][C3T_SEG + 2];
+__global__ __launch_bounds__(256) void k_wgrad_c3_thin(const float* __restrict__ g,
+                                                       const float* __restrict__ x, int N, int H,
+                                                       int W, float* __restrict__ slab,
+                                                       long slab_stride, int cin_total,
+                                                       int ci_base, int with_bias) {
+  constexpr int KT = 9 * C, NG = 256 / CO;
+  constexpr int SEG = E0_SEG * 48 / CO;  // 24 KiB gradient stage whatever CO
+  __shared__ __attribute__((aligned(16))) float gr[SEG * CO];
+  __shared__ float xr[3][C][SEG + 2];
   __shared__ float red[NG - 1][CO][KT + 1];
   const int tid = threadIdx.x, co = tid % CO, grp = tid / CO;
   float acc[KT + 1];
 #pragma unroll
   for (int j = 0; j <= KT; ++j) acc[j] = 0.f;
-  const long R = (long)N * H;
+  const long R = (long)N * H, HW = (long)H * W;
   const int rb = (int)(R * blockIdx.x / gridDim.x), re = (int)(R * (blockIdx.x + 1) / gridDim.x);
   for (int row = rb; row < re; ++row) {
     const int n = row / H, y = row - n * H;
-    for (int x0 = 0; x0 < W; x0 += C3T_SEG) {
-      const int seg = W - x0 < C3T_SEG ? W - x0 : C3T_SEG;
+    for (int x0 = 0; x0 < W; x0 += SEG) {
+      const int seg = W - x0 < SEG ? W - x0 : SEG;
       __syncthreads();
-      for (int e = tid; e < 3 * C * (seg + 2); e += C3T_THREADS) {
+      const float4* g4 = reinterpret_cast<const float4*>(g + ((long)row * W + x0) * CO);
+      for (int e = tid; e < seg * (CO / 4); e += 256) reinterpret_cast<float4*>(gr)[e] = g4[e];
+      for (int e = tid; e < 3 * C * (seg + 2); e += 256) {
         const int dy = e / (C * (seg + 2)), r = e - dy * (C * (seg + 2));
         const int ci = r / (seg + 2), xx = r - ci * (seg + 2);
         const int gy = y + dy - 1, gx = x0 + xx - 1;
         xr[dy][ci][xx] = (gy >= 0 && gy < H && gx >= 0 && gx < W)
-                             ? x[((long)(n * H + gy) * W + gx) * x_stride + x_off + ci]
+                             ? x[((long)n * C + ci) * HW + (long)gy * W + gx]
                              : 0.f;
       }
       __syncthreads();
-      const float* gp = g + ((long)row * W + x0) * CO + co;
-#pragma unroll 4
-      for (int px = grp; px < seg; px += NG) {
-        const float gv = gp[(long)px * CO];
+      if (grp < NG) {
+        for (int px = grp; px < seg; px += NG) {
+          const float gv = gr[px * CO + co];
 #pragma unroll
-        for (int dy = 0; dy < 3; ++dy)
+          for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-          for (int ci = 0; ci < C; ++ci)
+            for (int ci = 0; ci < C; ++ci)
 #pragma unroll
-            for (int dx = 0; dx < 3; ++dx)
-              acc[ci * 9 + dy * 3 + dx] = fmaf(gv, xr[dy][ci][px + dx], acc[ci * 9 + dy * 3 + dx]);
-        acc[KT] += gv;
+              for (int dx = 0; dx < 3; ++dx)
+                acc[ci * 9 + dy * 3 + dx] = fmaf(gv, xr[dy][ci][px + dx], acc[ci * 9 + dy * 3 + dx]);
+          acc[KT] += gv;
+        }
       }
     }
   }
-  if (grp >= 1)
+  if (grp >= 1 && grp < NG)
 #pragma unroll
     for (int j = 0; j <= KT; ++j) red[grp - 1][co][j] = acc[j];
   __syncthreads();
@@ -157,22 +166,22 @@ __global__ __launch_bounds__(C3T_THREADS) void k_wgrad_c3_thin(const float* __re
 
 hipError_t launch_enc0_fwd(const float* x, int N, int C, int H, int W, const float* w,
                            const float* b, float* out, float* cat, int cat_stride, int cat_off,
-                           int cat_zero_to, hipStream_t s) {
+                           int cat_zero_to, float* xcopy, hipStream_t s) {
   if (C < 1 || C > 4) return hipErrorInvalidValue;
   const long total = (long)N * H * W;
   const dim3 grid((unsigned)((total + 255) / 256));
   if (C == 1)
     hipLaunchKernelGGL(k_enc0_fwd<1>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
-                       cat_off, cat_zero_to);
+                       cat_off, cat_zero_to, xcopy);
   else if (C == 2)
     hipLaunchKernelGGL(k_enc0_fwd<2>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
-                       cat_off, cat_zero_to);
+                       cat_off, cat_zero_to, xcopy);
   else if (C == 3)
     hipLaunchKernelGGL(k_enc0_fwd<3>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
-                       cat_off, cat_zero_to);
+                       cat_off, cat_zero_to, xcopy);
   else
     hipLaunchKernelGGL(k_enc0_fwd<4>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
-                       cat_off, cat_zero_to);
+                       cat_off, cat_zero_to, xcopy);
   return hipGetLastError();
 }
 
@@ -183,12 +192,12 @@ int enc0_wgrad_splits(int N, int H, int W) {
 }
 
 template <int CO>
-static hipError_t run_c3_thin(const float* g, const float* x, int x_stride, int x_off, int N, int C,
-                              int H, int W, float* slab, long slab_stride, int cin_total,
-                              int ci_base, int with_bias, int splits, hipStream_t s) {
-#define DN_C3T(CC)                                                                              \
-  hipLaunchKernelGGL((k_wgrad_c3_thin<CC, CO>), dim3(splits), dim3(C3T_THREADS), 0, s, g, x,     \
-                     x_stride, x_off, N, H, W, slab, slab_stride, cin_total, ci_base, with_bias)
+static hipError_t run_c3_thin(const float* g, const float* x, int N, int C, int H, int W,
+                              float* slab, long slab_stride, int cin_total, int ci_base,
+                              int with_bias, int splits, hipStream_t s) {
+#define DN_C3T(CC)                                                                          \
+  hipLaunchKernelGGL((k_wgrad_c3_thin<CC, CO>), dim3(splits), dim3(256), 0, s, g, x, N, H, W, \
+                     slab, slab_stride, cin_total, ci_base, with_bias)
   if (C == 1) DN_C3T(1);
   else if (C == 2) DN_C3T(2);
   else if (C == 3) DN_C3T(3);
@@ -198,28 +207,25 @@ static hipError_t run_c3_thin(const float* g, const float* x, int x_stride, int 
   return hipGetLastError();
 }
 
-// g: NHWC [N,H,W,cout] contiguous; x: NHWC view (stride, offset) holding the C channels
-hipError_t launch_wgrad_c3_thin(const float* g, int cout, const float* x, int x_stride, int x_off,
-                                int N, int C, int H, int W, float* slab, long slab_stride,
-                                int cin_total, int ci_base, int with_bias, int splits,
-                                hipStream_t s) {
+// g: NHWC [N,H,W,cout] contiguous; x: NCHW [N,C,H,W] (the network input)
+hipError_t launch_wgrad_c3_thin(const float* g, int cout, const float* x, int N, int C, int H,
+                                int W, float* slab, long slab_stride, int cin_total, int ci_base,
+                                int with_bias, int splits, hipStream_t s) {
   if (C < 1 || C > 4 || splits < 1) return hipErrorInvalidValue;
   if (cout == 48)
-    return run_c3_thin<48>(g, x, x_stride, x_off, N, C, H, W, slab, slab_stride, cin_total,
-                           ci_base, with_bias, splits, s);
+    return run_c3_thin<48>(g, x, N, C, H, W, slab, slab_stride, cin_total, ci_base, with_bias,
+                           splits, s);
   if (cout == 96)
-    return run_c3_thin<96>(g, x, x_stride, x_off, N, C, H, W, slab, slab_stride, cin_total,
-                           ci_base, with_bias, splits, s);
+    return run_c3_thin<96>(g, x, N, C, H, W, slab, slab_stride, cin_total, ci_base, with_bias,
+                           splits, s);
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int x_stride,
-                             int x_off, int N, int C, int H, int W, float* slab, int splits,
-                             float* dwb, hipStream_t s) {
+hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int N, int C, int H,
+                             int W, float* slab, int splits, float* dwb, hipStream_t s) {
   if (g_stride != E0_CO) return hipErrorInvalidValue;
   const long n_el = (long)E0_CO * 9 * C + E0_CO;
-  hipError_t e = launch_wgrad_c3_thin(g, E0_CO, x, x_stride, x_off, N, C, H, W, slab, n_el, C, 0,
-                                      1, splits, s);
+  hipError_t e = launch_wgrad_c3_thin(g, E0_CO, x, N, C, H, W, slab, n_el, C, 0, 1, splits, s);
   if (e != hipSuccess) return e;
   return launch_reduce(slab, n_el, splits, n_el, dwb, s);
 }

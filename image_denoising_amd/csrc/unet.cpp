@@ -143,6 +143,7 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
     p.g_p5 = alloc(5, nf);
     p.g_a0 = alloc(0, nf);
     p.g_a1 = alloc(0, nf);
+    p.xin = alloc(0, p.C);
     for (int i = 0; i < NL; ++i) {  // packed data-gradient weights
       const Layer& L = p.P.L[i];
       long n = 0;
@@ -234,7 +235,7 @@ long conv_fwd_pack_size(int K, int cout, int ksize) {
 long conv_dgrad_pack_size(int cout, int nout, int ksize) {
   return pack_floats(ksize == 3 ? G_C3 : G_C1, nout, cout, 1);
 }
-long deconv_fwd_pack_size(int cin, int cout) { return pack_floats(G_C1, cout, cin, 4); }
+long deconv_fwd_pack_size(int cin, int cout) { return pack_floats(G_UP, cout, cin, 4); }
 long deconv_dgrad_pack_size(int cout, int cin) { return pack_floats(G_DN2, cin, cout, 1); }
 
 hipError_t pack_conv_fwd(const float* w, int K, int cout, int ksize, float* out, hipStream_t s) {
@@ -246,7 +247,7 @@ hipError_t pack_conv_dgrad(const float* w, int cin_total, int nout, int cout, in
                      out, s);
 }
 hipError_t pack_deconv_fwd(const float* w, int cin, int cout, float* out, hipStream_t s) {
-  return launch_pack(G_C1, deconv_fwd_view(w, cout), cin, cout, 4, out, s);
+  return launch_pack(G_UP, deconv_fwd_view(w, cout), cin, cout, 4, out, s);
 }
 hipError_t pack_deconv_dgrad(const float* w, int cout, int cin, float* out, hipStream_t s) {
   return launch_pack(G_DN2, deconv_dgrad_view(w, cout), cout, cin, 1, out, s);
@@ -283,10 +284,10 @@ hipError_t deconv_forward(const View& x, int N, int h, int w, int cin, const flo
   FwdArgs a{};
   a.in = x.p; a.in_stride = x.stride; a.in_off = x.off; a.IHt = h; a.IWt = w;
   a.N = N; a.OH = h; a.OW = w; a.K = cin; a.NOUT = cout;
-  a.wp = wp; a.wp_z = pack_floats(G_C1, cout, cin, 1);
+  a.wp = wp; a.wp_z = pack_floats(G_UP, cout, cin, 1);
   a.bias = b; a.epi = EPI_BIAS;
   a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = OUT_UP2;
-  return launch_fwd(G_C1, a, s);
+  return launch_fwd(G_UP, a, s);
 }
 
 // dx [N,h,w,cin] = sum_{ab,co} dy[2y+a][2x+b][co] * W[ci][co][ab]  (* leaky'(mask));
@@ -344,7 +345,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   }
   // enc_conv0, fused with pool0 = x -> channels [2nf, 2nf+C) of the up1 concat buffer
   DN_TRY(launch_enc0_fwd(x, N, C, p.H, p.W, prm + p.P.L[ENC0].woff, Bs(ENC0), ws + p.a0,
-                         ws + p.c1, p.c1s, 2 * nf, p.c1s, s));
+                         ws + p.c1, p.c1s, 2 * nf, p.c1s, p.with_bwd ? ws + p.xin : nullptr, s));
   DN_TRY(conv_forward(V(p.a0, nf), N, H(0), Wd(0), nf, Wt(ENC1), Bs(ENC1), nf, 3, 1, V(p.a1, nf),
                       OUT_NHWC, s));
   // pool1 -> skip slice of c2
@@ -483,8 +484,8 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     float* thin = slab + 64 + (long)p.splits[D1A] * n;
     const long nt = 96L * C * 9;
     const int st = enc0_wgrad_splits(N, H(0), Wd(0));
-    DN_TRY(launch_wgrad_c3_thin(ws + p.g_d1a, 96, ws + p.c1, p.c1s, 2 * nf, N, C, H(0), Wd(0),
-                                thin, nt, C, 0, 0, st, s));
+    DN_TRY(launch_wgrad_c3_thin(ws + p.g_d1a, 96, ws + p.xin, N, C, H(0), Wd(0), thin, nt, C, 0,
+                                0, st, s));
     DN_TRY(launch_reduce_scatter(thin, nt, st, nt, G(D1A), 9L * C, 9L * p.c1k, 9L * 2 * nf, s));
   }
   // only the up1 part of the concat needs a gradient (pool0 is the network input)
@@ -547,7 +548,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                p.splits[ENC1], s));
   DN_TRY(conv_dgrad(V(p.g_a1, nf), N, H(0), Wd(0), nf, Wt(ENC1), nf, 3, EPI_MASK, V(p.a0, nf),
                     V(p.g_a0, nf), s));
-  DN_TRY(launch_enc0_wgrad(ws + p.g_a0, nf, ws + p.c1, p.c1s, 2 * nf, N, C, H(0), Wd(0), slab,
+  DN_TRY(launch_enc0_wgrad(ws + p.g_a0, nf, ws + p.xin, N, C, H(0), Wd(0), slab,
                            p.splits[ENC0], G(ENC0), s));
   return DN_OK;
 }

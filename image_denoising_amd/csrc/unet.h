@@ -50,6 +50,7 @@ struct Plan {
   long g_nb, g_na, g_d1b, g_d1a, g_c1;
   long g_c[5], g_da[5], g_db[5], g_a[5];
   long g_a6, g_p5, g_a0, g_a1;
+  long xin;                     // compact NCHW copy of the network input (weight gradients)
   long packB[NL];               // packed data-gradient weight images
   long packHB;                  // fused head backward: nin_b^T | nin_a^T images
   long slab, slab_floats;
