@@ -45,7 +45,7 @@ template <int GATHER, int NT, int MT>
 struct FwdCfg {
   // G_UP: every wave covers all MT rows of the tile and wave w takes parity (a,b) = w
   static constexpr int TW = 16, TH = GATHER == G_UP ? MT : 4 * MT;
-  static constexpr int KC = GATHER == G_C1 ? 32 : (GATHER == G_UP ? 16 : (NT >= 9 ? 4 : 8));
+  static constexpr int KC = GATHER == G_C1 ? 32 : (GATHER == G_UP ? 16 : (NT >= 6 ? 4 : 8));
   static constexpr int NZ = GATHER == G_UP ? 4 : 1;  // weight images per chunk in LDS
   static constexpr int TAPS = GATHER == G_C3 ? 9 : (GATHER == G_DN2 ? 4 : 1);
   static constexpr int IH = GATHER == G_C3 ? TH + 2 : (GATHER == G_DN2 ? 2 * TH : TH);
@@ -71,7 +71,7 @@ __device__ __forceinline__ void glds16(const float* g, float* l) {
 }
 
 template <int GATHER, int NT, int MT, bool HEAD = false>
-__global__ __launch_bounds__(256, 2) void k_fwd(FwdArgs a, HeadArgs hd) {
+__global__ __launch_bounds__(256, (GATHER == G_C3 && NT == 6 && !HEAD) ? 3 : 2) void k_fwd(FwdArgs a, HeadArgs hd) {
   using C = FwdCfg<GATHER, NT, MT>;
   __shared__ __attribute__((aligned(16))) float lds[HEAD ? C::LTOT : C::LT0];
   float* lx = lds;
