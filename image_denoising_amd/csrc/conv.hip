@@ -62,7 +62,7 @@ struct FwdCfg {
   static constexpr int PS = NP + 4;             // epilogue staging: pixel stride (floats)
   static constexpr int LST = 4 * 16 * PS;       // 4 waves x 16 pixels x PS
   static constexpr int LT0 = (LX + 2 * NZ * LW) > LST ? (LX + 2 * NZ * LW) : LST;
-  static constexpr int LTOT = LT0 > 2 * HEAD_LW ? LT0 : 2 * HEAD_LW;  // HEAD: both 1x1 images
+  static constexpr int LTOT = LT0 > HEAD_LW ? LT0 : HEAD_LW;  // HEAD: one 1x1 image at a time
 };
 
 __device__ __forceinline__ void glds16(const float* g, float* l) {
@@ -71,7 +71,8 @@ __device__ __forceinline__ void glds16(const float* g, float* l) {
 }
 
 template <int GATHER, int NT, int MT, bool HEAD = false>
-__global__ __launch_bounds__(256, (GATHER == G_C3 && NT == 6 && !HEAD) ? 3 : 2) void k_fwd(FwdArgs a, HeadArgs hd) {
+__global__ __launch_bounds__(256, (GATHER == G_C3 && NT == 6) ? 3 : 2) void k_fwd(
+    FwdArgs a, HeadArgs hd) {
   using C = FwdCfg<GATHER, NT, MT>;
   __shared__ __attribute__((aligned(16))) float lds[HEAD ? C::LTOT : C::LT0];
   float* lx = lds;
@@ -197,7 +198,9 @@ __global__ __launch_bounds__(256, (GATHER == G_C3 && NT == 6 && !HEAD) ? 3 : 2) 
     // supplies k = channel q*16 + 4g + r for lane group g: nin_a/nin_b consume the tile
     // where it is, with the k order permuted the same way in their weight reads.
     static_assert(GATHER == G_C3 && NT == 6, "head fusion is for the 96-channel dec_conv1b");
-    for (int p = wave; p < 2 * HEAD_LW / 256; p += 4) glds16(hd.wp + p * 256 + lane * 4, lds + p * 256);
+    // Two phases through ONE image slot (38 KiB, so three workgroups fit a CU): nin_a for
+    // all rows in place (acc <- na), then nin_b + nin_c.
+    for (int p = wave; p < HEAD_LW / 256; p += 4) glds16(hd.wp + p * 256 + lane * 4, lds + p * 256);
     auto bias_act = [](f32x4& v, float4 b) {
       v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
 #pragma unroll
@@ -205,6 +208,19 @@ __global__ __launch_bounds__(256, (GATHER == G_C3 && NT == 6 && !HEAD) ? 3 : 2) 
     };
     auto save = [&](float* dst, long pix, int q, const f32x4& v) {
       *reinterpret_cast<float4*>(dst + pix * 96 + q * 16 + 4 * lg) = make_float4(v[0], v[1], v[2], v[3]);
+    };
+    // 1x1 GEMM on the transposed tile: out[f] = W^T-image x in (k order = the tile's)
+    auto gemm96 = [&](const float* w, const f32x4 (&in)[NT], f32x4 (&out)[NT]) {
+#pragma unroll
+      for (int f = 0; f < NT; ++f) out[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float* wr = w + (q * 16 + 4 * lg + r) * HEAD_WS + li;
+#pragma unroll
+          for (int f = 0; f < NT; ++f) out[f] = mfma4(wr[f * 16], in[q][r], out[f]);
+        }
     };
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
@@ -222,41 +238,32 @@ __global__ __launch_bounds__(256, (GATHER == G_C3 && NT == 6 && !HEAD) ? 3 : 2) 
           for (int q = 0; q < NT; ++q) save(hd.d1b, ((long)n * a.OH + gy) * a.OW + gx, q, acc[m][q]);
       }
     }
-    __syncthreads();  // nin_a / nin_b images landed
-    const float* wa = lds;
-    const float* wb = lds + HEAD_LW;
+    __syncthreads();  // nin_a image landed
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
+    for (int m = 0; m < MT; ++m) {  // phase 1: acc[m] <- na
       const int gy = ty0 + wave * MT + m;
-      const bool ok = gy < a.OH && gx < a.OW;
-      const long pix = ((long)n * a.OH + gy) * a.OW + gx;
       f32x4 u[NT];
-#pragma unroll
-      for (int f = 0; f < NT; ++f) u[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < NT; ++q)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float* wr = wa + (q * 16 + 4 * lg + r) * HEAD_WS + li;
-#pragma unroll
-          for (int f = 0; f < NT; ++f) u[f] = mfma4(wr[f * 16], acc[m][q][r], u[f]);
-        }
+      gemm96(lds, acc[m], u);
 #pragma unroll
       for (int f = 0; f < NT; ++f) {
         bias_act(u[f], *reinterpret_cast<const float4*>(hd.ba + f * 16 + 4 * lg));
-        if (hd.na && ok) save(hd.na, pix, f, u[f]);
+        acc[m][f] = u[f];
       }
+      if (hd.na && gy < a.OH && gx < a.OW)
+#pragma unroll
+        for (int f = 0; f < NT; ++f) save(hd.na, ((long)n * a.OH + gy) * a.OW + gx, f, acc[m][f]);
+    }
+    __syncthreads();  // everyone done with nin_a
+    for (int p = wave; p < HEAD_LW / 256; p += 4)
+      glds16(hd.wp + HEAD_LW + p * 256 + lane * 4, lds + p * 256);
+    __syncthreads();  // nin_b image landed
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {  // phase 2: nb, then nin_c
+      const int gy = ty0 + wave * MT + m;
+      const bool ok = gy < a.OH && gx < a.OW;
+      const long pix = ((long)n * a.OH + gy) * a.OW + gx;
       f32x4 v[NT];
-#pragma unroll
-      for (int f = 0; f < NT; ++f) v[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < NT; ++q)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float* wr = wb + (q * 16 + 4 * lg + r) * HEAD_WS + li;
-#pragma unroll
-          for (int f = 0; f < NT; ++f) v[f] = mfma4(wr[f * 16], u[q][r], v[f]);
-        }
+      gemm96(lds, acc[m], v);
 #pragma unroll
       for (int f = 0; f < NT; ++f) {
         bias_act(v[f], *reinterpret_cast<const float4*>(hd.bb + f * 16 + 4 * lg));
