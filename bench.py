@@ -129,6 +129,9 @@ def main():
     ap.add_argument("--bs", type=int, default=64, help="patches per GPU")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--channels", type=int, default=1)
+    ap.add_argument("--mode", choices=["n2n", "structure"], default="n2n",
+                    help="n2n: the N2N step (BASELINE metric); structure: train.py's "
+                         "Structure_loss step (two grad forwards at full resolution)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--breakdown", action="store_true", help="per-phase HIP-event timing (stderr)")
     args = ap.parse_args()
@@ -141,23 +144,30 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
 
-    from image_denoising_amd import N2NTrainer, UNet
+    from image_denoising_amd import N2NTrainer, StructureTrainer, UNet
 
     C, H, bs = args.channels, args.size, args.bs
     torch.manual_seed(0)
     net = UNet(in_nc=C, out_nc=C, n_feature=48).to(device)
-    tr = N2NTrainer(net, lr=3e-4, n_epoch=100, increase_ratio=2.0, seed=0)
     clean = synthetic_clean(bs * C, H, H, 1000 + rank, device).view(bs, C, H, H).contiguous()
+    if args.mode == "n2n":
+        tr = N2NTrainer(net, lr=3e-4, n_epoch=100, increase_ratio=2.0, seed=0)
+        step = lambda: tr.train_step(clean, epoch=1)
+    else:
+        tr = StructureTrainer(net, lr=3e-4, n_epoch=100)
+        g = torch.Generator(device="cpu").manual_seed(7 + rank)
+        noisy = (clean + (25.0 / 255.0) * torch.randn(clean.shape, generator=g).to(device)).contiguous()
+        step = lambda: tr.train_step(clean, noisy, epoch=1)
 
     for _ in range(args.warmup):
-        tr.train_step(clean, epoch=1)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = tr.train_step(clean, epoch=1)
+        loss = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -169,7 +179,7 @@ def main():
         elapsed = float(t)
     loss_v = loss.cpu().tolist()
 
-    if args.breakdown and rank == 0:
+    if args.breakdown and rank == 0 and args.mode == "n2n":
         breakdown(tr, clean, device)
 
     if rank == 0:
@@ -177,15 +187,28 @@ def main():
         value = world * bs * args.steps / elapsed
         kms, kflops = time_dominant_kernel(bs, H, H, device)
         achieved = kflops / (kms * 1e-3) / 1e12
-        step_flops = bs * (unet_fwd_flops(H, H, C) + 3 * unet_fwd_flops(H // 2, H // 2, C))
+        if args.mode == "n2n":  # fwd 256 + fwd/bwd 128
+            step_flops = bs * (unet_fwd_flops(H, H, C) + 3 * unet_fwd_flops(H // 2, H // 2, C))
+        else:  # two fwd/bwd at full resolution
+            step_flops = bs * 2 * 3 * unet_fwd_flops(H, H, C)
         traffic, traffic_src = pmc_traffic() if (bs, H, C) == (64, 256, 1) else (None, None)
+        if args.mode == "structure":
+            workload = (f"train.py Structure_loss step (train.py:355-368), UNet(n_feature=48), "
+                        f"{bs}x{C}x{H}x{H} per GPU, Adam lr 3e-4")
+        elif (C, bs) == (3, 32):
+            workload = (f"BASELINE configs[3]: 3-channel N2N step, UNet(n_feature=48), "
+                        f"{bs}x{C}x{H}x{H} per GPU, Adam lr 3e-4")
+        else:
+            workload = (f"BASELINE configs[1]: N2N step, UNet(n_feature=48), "
+                        f"{bs}x{C}x{H}x{H} per GPU, Adam lr 3e-4")
         rec = {
-            "metric": "training patches/sec (256x256x1, bs=64 per GPU, N2N loss + Adam)",
+            "metric": "training patches/sec (256x256x1, bs=64 per GPU, N2N loss + Adam)"
+                      if args.mode == "n2n" and (C, bs, H) == (1, 64, 256)
+                      else f"training patches/sec ({H}x{H}x{C}, bs={bs} per GPU, {args.mode})",
             "value": round(value, 2), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-            "config": {"workload": "BASELINE configs[1]: N2N step, UNet(n_feature=48), "
-                                   f"{bs}x{C}x{H}x{H} per GPU, Adam lr 3e-4",
+            "config": {"workload": workload,
                        "global_batch": bs * world, "patch": [H, H, C], "parallelism": f"dp{world}"},
             "step_tflops": round(step_flops / (ms_step * 1e-3) / 1e12, 2),
             "step_frac_of_fp32_peak": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
@@ -196,7 +219,7 @@ def main():
                          "avg_launch_ms": round(kms, 4), "flops_per_launch": kflops},
             "loss": loss_v,
         }
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.mode == "n2n" and C == 1:
             rec["cpu_baseline"] = cpu_baseline()
         print(json.dumps(rec), flush=True)
     if world > 1:

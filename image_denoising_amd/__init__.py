@@ -8,7 +8,7 @@ from .arch_unet import UNet, reference_init  # noqa: F401
 from .n2n import (AugmentNoise, generate_mask_pair, generate_subimages,  # noqa: F401
                   n2n_loss, n2n_subsample)
 from .optim import FlatAdam, lr_at_epoch  # noqa: F401
-from .trainer import N2NTrainer  # noqa: F401
+from .trainer import N2NTrainer, StructureTrainer  # noqa: F401
 from .util import Structure_loss  # noqa: F401
 
 __version__ = "0.1.0"

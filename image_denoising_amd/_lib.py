@@ -70,6 +70,7 @@ SIGNATURES = {
     "dn_maxpool2x2_forward": (c_int, [_F, c_int, c_int, c_int, c_int, _F, c_int, c_int, c_void_p]),
     "dn_maxpool2x2_backward": (c_int, [_F, c_int, c_int, c_int, c_int, _F, c_int, c_int, c_int, _F,
                                        c_void_p]),
+    "dn_accumulate": (c_int, [_F, _F, c_int64, c_void_p]),
     "dn_eval_partials_size": (c_size_t, []),
     "dn_u8_to_unit": (c_int, [_U8, c_int64, _F, c_void_p]),
     "dn_tile_count": (c_int, [c_int, c_int, c_int]),

@@ -233,6 +233,13 @@ dn_status dn_adam_step(float* param, const float* grad, float* exp_avg, float* e
                     "dn_adam_step");
 }
 
+dn_status dn_accumulate(float* dst, const float* src, int64_t n, void* stream) {
+  if (n < 0) return fail(DN_ERR_ARG, "n < 0");
+  if (n == 0) return DN_OK;
+  if (!dst || !src) return fail(DN_ERR_ARG, "null argument");
+  return hip_status(launch_accumulate(dst, src, n, (hipStream_t)stream), "dn_accumulate");
+}
+
 // ---- evaluation path ----------------------------------------------------------------------
 size_t dn_eval_partials_size(void) { return EVAL_PARTS * sizeof(double); }
 

@@ -125,6 +125,7 @@ hipError_t launch_wgrad_c3_thin(const float* g, int cout, const float* x, int N,
                                 int with_bias, int splits, hipStream_t s);
 hipError_t launch_wgrad_thin(const float* g, int g_stride, int cout, const float* x, long npx,
                              float* slab, int splits, float* dwb, hipStream_t s);
+hipError_t launch_accumulate(float* dst, const float* src, long n, hipStream_t s);
 hipError_t launch_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);
 hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s);
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);

@@ -1,6 +1,8 @@
 // HBM-bound kernels of the N2N training step for gfx950: 2x2 max-pool fwd/bwd, the
 // neighbour sub-sampler, Gaussian noise synthesis, the loss reductions and Adam.
 #include <math.h>
+#include <cstdint>
+
 #include "dn_internal.h"
 #include "philox.h"
 
@@ -470,6 +472,41 @@ hipError_t launch_structure_loss(const float* pred, const float* pred2, const fl
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_structure_finalize, dim3(1), dim3(256), 0, s, part, kLossBlocks, M, M1, M2,
                      alpha, beta, gamma, loss5);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_accumulate_tail(float* __restrict__ dst,
+                                                         const float* __restrict__ src, long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    dst[i] += src[i];
+}
+
+__global__ __launch_bounds__(256) void k_accumulate(float* __restrict__ dst,
+                                                    const float* __restrict__ src, long n) {
+  const long n4 = n >> 2;
+  float4* d4 = reinterpret_cast<float4*>(dst);
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 a = d4[i];
+    const float4 b = s4[i];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    d4[i] = a;
+  }
+  for (long i = 4 * n4 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    dst[i] += src[i];
+}
+
+hipError_t launch_accumulate(float* dst, const float* src, long n, hipStream_t s) {
+  const bool vec = ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0;
+  long blocks = ((vec ? n / 4 : n) + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  if (vec) {
+    hipLaunchKernelGGL(k_accumulate, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, n);
+  } else {  // unaligned views: the scalar tail loop covers everything
+    hipLaunchKernelGGL(k_accumulate, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, 0L);
+    hipLaunchKernelGGL(k_accumulate_tail, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, n);
+  }
   return hipGetLastError();
 }
 

@@ -23,6 +23,7 @@ from . import dist as dp
 from .arch_unet import UNet
 from .n2n import n2n_loss, n2n_subsample
 from .optim import FlatAdam, lr_at_epoch
+from .util import structure_loss
 
 
 class N2NTrainer:
@@ -97,3 +98,64 @@ class N2NTrainer:
         self.opt.step(self.grad, grad_scale=scale)
         self.global_step += 1
         return loss3
+
+
+class StructureTrainer:
+    """The step of the reference's own train.py loop (train.py:355-368), fused:
+
+        pred  = UNet(noisy)   [saved]                 dn_unet_forward   (train.py:361)
+        pred2 = UNet(clean)   [saved]                 dn_unet_forward
+        loss5, dpred, dpred2 = Structure_loss(pred, pred2, clean)
+                                                      dn_structure_loss (util.py:56-70)
+        dW = backward(dpred) + backward(dpred2)       dn_unet_backward x2 + dn_accumulate
+        [data parallel: one RCCL all-reduce(sum) of dW]
+        Adam(W, dW / world)                           dn_adam_step      (train.py:368)
+
+    Inputs are device tensors already scaled to [0, 1] (train.py:357 divides by 255).
+    Returns loss5 = [pixel L1 (= F.l1_loss(pred, clean), train.py:365), tv1, tv2, cst, total].
+    """
+
+    def __init__(self, net: UNet, lr: float = 3e-4, n_epoch: int = 100, gamma: float = 0.5,
+                 alpha_beta_gamma=(1.0, 0.5, 0.5), distributed: bool | None = None):
+        self.net = net
+        self.base_lr, self.n_epoch, self.gamma = lr, n_epoch, gamma
+        self.weights = alpha_beta_gamma
+        self.distributed = dp.is_distributed() if distributed is None else distributed
+        if self.distributed:
+            dp.broadcast_params(net.flat_params)
+        self.opt = FlatAdam(net.flat_params, lr=lr)
+        self.grad = torch.zeros_like(net.flat_params)
+        self.grad2 = torch.zeros_like(net.flat_params)
+        self._bufs = {}
+
+    def _buffers(self, N, H, W, device):
+        key = (N, H, W, device)
+        if key not in self._bufs:
+            f = dict(dtype=torch.float32, device=device)
+            self._bufs = {key: dict(
+                pred=torch.empty((N, self.net.out_nc, H, W), **f),
+                pred2=torch.empty((N, self.net.out_nc, H, W), **f),
+                ws1=self.net._workspace(N, H, W, with_backward=True, fresh=True),
+                ws2=self.net._workspace(N, H, W, with_backward=True, fresh=True))}
+        return self._bufs[key]
+
+    def train_step(self, clean: torch.Tensor, noisy: torch.Tensor, epoch: int = 1) -> torch.Tensor:
+        clean, noisy = clean.contiguous(), noisy.contiguous()
+        if clean.shape != noisy.shape or clean.shape[1] != self.net.in_nc:
+            raise ValueError("clean and noisy must share one [N, in_nc, H, W] shape")
+        if self.net.in_nc != self.net.out_nc:
+            raise ValueError("Structure_loss compares the output with the input: in_nc == out_nc")
+        N, _, H, W = clean.shape
+        b = self._buffers(N, H, W, clean.device)
+        self.net._run_forward(noisy, b["pred"], b["ws1"])
+        self.net._run_forward(clean, b["pred2"], b["ws2"])
+        a, be, g = self.weights
+        loss5, dpred, dpred2 = structure_loss(b["pred"], b["pred2"], clean, a, be, g)
+        self.net._run_backward(dpred, self.grad, b["ws1"], N, H, W)
+        self.net._run_backward(dpred2, self.grad2, b["ws2"], N, H, W)
+        _lib.call("dn_accumulate", _lib.ptr(self.grad), _lib.ptr(self.grad2), self.grad.numel(),
+                  _lib.stream_of(self.grad))
+        scale = dp.allreduce_grads(self.grad) if self.distributed else 1.0
+        self.opt.lr = lr_at_epoch(epoch, self.base_lr, self.n_epoch, self.gamma)
+        self.opt.step(self.grad, grad_scale=scale)
+        return loss5

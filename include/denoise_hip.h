@@ -130,6 +130,10 @@ dn_status dn_adam_step(float* param, const float* grad, float* exp_avg, float* e
                        float lr, float beta1, float beta2, float eps, int64_t step,
                        float grad_scale, void* stream);
 
+/* dst += src over n floats (sums the parameter gradients of several backward passes, e.g.
+   the two network evaluations of the Structure_loss step, train.py:361-367) */
+dn_status dn_accumulate(float* dst, const float* src, int64_t n, void* stream);
+
 /* ---- op-level entry points (NHWC), used by the tests and the tiled-inference path ---- */
 /* The forward-family kernels read weights pre-packed into per-chunk LDS images; the caller
    provides that scratch (pack_ws, pack_bytes >= the *_pack_size query).  backward_data=1
