@@ -126,12 +126,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--bs", type=int, default=64, help="patches per GPU")
-    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--bs", type=int, default=None, help="patches per GPU (64; finetune: 16)")
+    ap.add_argument("--size", type=int, default=None, help="patch edge (256; finetune: 512)")
     ap.add_argument("--channels", type=int, default=1)
-    ap.add_argument("--mode", choices=["n2n", "structure"], default="n2n",
+    ap.add_argument("--mode", choices=["n2n", "structure", "finetune"], default="n2n",
                     help="n2n: the N2N step (BASELINE metric); structure: train.py's "
-                         "Structure_loss step (two grad forwards at full resolution)")
+                         "Structure_loss step (two grad forwards at full resolution); finetune: "
+                         "finetune.py's adapter step (frozen UNet base + OutputAdapter, configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--breakdown", action="store_true", help="per-phase HIP-event timing (stderr)")
     args = ap.parse_args()
@@ -146,11 +147,23 @@ def main():
 
     from image_denoising_amd import N2NTrainer, StructureTrainer, UNet
 
-    C, H, bs = args.channels, args.size, args.bs
+    ft = args.mode == "finetune"
+    C = args.channels
+    H = args.size or (512 if ft else 256)
+    bs = args.bs or (16 if ft else 64)
     torch.manual_seed(0)
     net = UNet(in_nc=C, out_nc=C, n_feature=48).to(device)
     clean = synthetic_clean(bs * C, H, H, 1000 + rank, device).view(bs, C, H, H).contiguous()
-    if args.mode == "n2n":
+    if ft:
+        from image_denoising_amd.adapter import DenoiserWithAdapter
+        from image_denoising_amd.finetune import FinetuneTrainer
+
+        model = DenoiserWithAdapter(net, in_channels=C, hidden_channels=16).to(device)
+        tr = FinetuneTrainer(model, lr=1e-4, lambda_grad=0.1)
+        g = torch.Generator(device="cpu").manual_seed(7 + rank)
+        noisy = (clean + (25.0 / 255.0) * torch.randn(clean.shape, generator=g).to(device)).contiguous()
+        step = lambda: tr.train_step(clean, noisy)
+    elif args.mode == "n2n":
         tr = N2NTrainer(net, lr=3e-4, n_epoch=100, increase_ratio=2.0, seed=0)
         step = lambda: tr.train_step(clean, epoch=1)
     else:
@@ -189,10 +202,16 @@ def main():
         achieved = kflops / (kms * 1e-3) / 1e12
         if args.mode == "n2n":  # fwd 256 + fwd/bwd 128
             step_flops = bs * (unet_fwd_flops(H, H, C) + 3 * unet_fwd_flops(H // 2, H // 2, C))
+        elif ft:  # frozen base forward + adapter fwd (864 flop/px) and bwd (~1728 flop/px, C=1)
+            step_flops = bs * (unet_fwd_flops(H, H, C) + 3 * 864.0 * C * H * H)
         else:  # two fwd/bwd at full resolution
             step_flops = bs * 2 * 3 * unet_fwd_flops(H, H, C)
         traffic, traffic_src = pmc_traffic() if (bs, H, C) == (64, 256, 1) else (None, None)
-        if args.mode == "structure":
+        if ft:
+            workload = (f"BASELINE configs[4]: finetune.py adapter step, frozen UNet(n_feature=48) "
+                        f"base (no_grad) + OutputAdapter(hidden 16), {bs}x{C}x{H}x{H} per GPU, "
+                        f"L1 + 0.1*gradient_loss, Adam lr 1e-4, fp32")
+        elif args.mode == "structure":
             workload = (f"train.py Structure_loss step (train.py:355-368), UNet(n_feature=48), "
                         f"{bs}x{C}x{H}x{H} per GPU, Adam lr 3e-4")
         elif (C, bs) == (3, 32):
@@ -204,7 +223,8 @@ def main():
         rec = {
             "metric": "training patches/sec (256x256x1, bs=64 per GPU, N2N loss + Adam)"
                       if args.mode == "n2n" and (C, bs, H) == (1, 64, 256)
-                      else f"training patches/sec ({H}x{H}x{C}, bs={bs} per GPU, {args.mode})",
+                      else (f"finetune patches/sec ({H}x{H}x{C}, bs={bs} per GPU, frozen base + adapter)"
+                            if ft else f"training patches/sec ({H}x{H}x{C}, bs={bs} per GPU, {args.mode})"),
             "value": round(value, 2), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 BUILD = os.path.join(PKG, "_objs")
 LIB = os.path.join(PKG, "libdenoise_hip.so")
-SOURCES = ["conv.hip", "elementwise.hip", "first_layer.hip", "eval.hip", "unet.cpp", "capi.cpp"]
+SOURCES = ["conv.hip", "elementwise.hip", "first_layer.hip", "eval.hip", "adapter.hip", "unet.cpp", "capi.cpp"]
 HEADERS = ["dn_internal.h", "philox.h", "unet.h"]
 ARCH = os.environ.get("DN_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -455,4 +455,58 @@ dn_status dn_maxpool2x2_backward(const float* x, int N, int H, int W, int C, con
                     "dn_maxpool2x2_backward");
 }
 
+// ---- adapter finetune (adapter.py:5-67, finetune.py:153-162) ---------------------------------
+dn_status dn_adapter_param_count(int in_channels, int hidden_channels, size_t* count) {
+  if (!count) return fail(DN_ERR_ARG, "null argument");
+  if (hidden_channels != 16) return fail(DN_ERR_ARG, "hidden_channels must be 16 (adapter.py default)");
+  const long n = adapter_param_count(in_channels);
+  if (n < 0) return fail(DN_ERR_ARG, "in_channels must be 1 or 3");
+  *count = (size_t)n;
+  return DN_OK;
+}
+
+static dn_status adapter_args(int N, int C, int H, int W, int hidden) {
+  if (hidden != 16) return fail(DN_ERR_ARG, "hidden_channels must be 16 (adapter.py default)");
+  if (C != 1 && C != 3) return fail(DN_ERR_ARG, "in_channels must be 1 or 3");
+  if (N < 1 || H < 1 || W < 1) return fail(DN_ERR_ARG, "empty adapter input");
+  return DN_OK;
+}
+
+size_t dn_adapter_slab_size(int N, int C, int H, int W, int hidden_channels) {
+  if (hidden_channels != 16 || adapter_param_count(C) < 0 || N < 1 || H < 1 || W < 1) return 0;
+  return sizeof(float) * (size_t)adapter_bwd_blocks(N, H, W) * (size_t)adapter_param_count(C);
+}
+
+dn_status dn_adapter_forward(const float* params, const float* noisy, const float* base_out,
+                             float* out, int N, int C, int H, int W, int hidden_channels,
+                             void* stream) {
+  if (!params || !noisy || !base_out || !out) return fail(DN_ERR_ARG, "null argument");
+  if (dn_status st = adapter_args(N, C, H, W, hidden_channels)) return st;
+  return hip_status(launch_adapter_fwd(params, noisy, base_out, N, C, H, W, out, (hipStream_t)stream),
+                    "dn_adapter_forward");
+}
+
+dn_status dn_adapter_backward(const float* params, const float* noisy, const float* base_out,
+                              const float* dout, float* dparams, int N, int C, int H, int W,
+                              int hidden_channels, void* slab, size_t slab_bytes, void* stream) {
+  if (!params || !noisy || !base_out || !dout || !dparams || !slab)
+    return fail(DN_ERR_ARG, "null argument");
+  if (dn_status st = adapter_args(N, C, H, W, hidden_channels)) return st;
+  if (slab_bytes < dn_adapter_slab_size(N, C, H, W, hidden_channels))
+    return fail(DN_ERR_WORKSPACE, "slab smaller than dn_adapter_slab_size()");
+  return hip_status(launch_adapter_bwd(params, noisy, base_out, dout, N, C, H, W, dparams,
+                                       static_cast<float*>(slab), (hipStream_t)stream),
+                    "dn_adapter_backward");
+}
+
+dn_status dn_finetune_loss(const float* pred, const float* target, int N, int C, int H, int W,
+                           float lambda_grad, float* dpred, float* loss3, void* partial_ws,
+                           void* stream) {
+  if (!pred || !target || !dpred || !loss3 || !partial_ws) return fail(DN_ERR_ARG, "null argument");
+  if (N < 1 || C < 1 || H < 2 || W < 2) return fail(DN_ERR_ARG, "gradient_loss needs H, W >= 2");
+  return hip_status(launch_ft_loss(pred, target, N, C, H, W, lambda_grad, dpred, loss3, partial_ws,
+                                   (hipStream_t)stream),
+                    "dn_finetune_loss");
+}
+
 }  // extern "C"

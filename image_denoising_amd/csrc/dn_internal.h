@@ -168,4 +168,15 @@ hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, 
                        float b2, float w2, float step_size, float bc2s, float eps, float gscale,
                        hipStream_t s);
 
+// ---- adapter finetune (adapter.hip) ----
+long adapter_param_count(int C);
+int adapter_bwd_blocks(int N, int H, int W);
+hipError_t launch_adapter_fwd(const float* prm, const float* noisy, const float* base, int N, int C,
+                              int H, int W, float* out, hipStream_t s);
+hipError_t launch_adapter_bwd(const float* prm, const float* noisy, const float* base,
+                              const float* dout, int N, int C, int H, int W, float* dprm,
+                              float* slab, hipStream_t s);
+hipError_t launch_ft_loss(const float* pred, const float* tgt, int N, int C, int H, int W,
+                          float lam, float* dpred, float* loss3, void* partials, hipStream_t s);
+
 }  // namespace dn

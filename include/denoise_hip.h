@@ -207,6 +207,30 @@ dn_status dn_ssim_u8(const uint8_t* a, const uint8_t* b, int C, int H, int W, in
 dn_status dn_l1_mean(const float* a, const float* b, int64_t n, void* part, double* l1,
                      void* stream);
 
+/* ---- adapter finetune: adapter.py:5-67 (OutputAdapter / DenoiserWithAdapter),
+   finetune.py:153-162 (gradient_loss), finetune.py:269-289 (the step) ------------------------
+   Adapter parameters are one flat fp32 buffer in OutputAdapter's state_dict order:
+   net.0.weight [16,2C,3,3], net.0.bias [16], net.2.weight [C,16,3,3], net.2.bias [C]
+   (449 floats for C=1, 1315 for C=3).  Only hidden_channels=16 (adapter.py:13) is built. */
+dn_status dn_adapter_param_count(int in_channels, int hidden_channels, size_t* count);
+/* out = base_out + conv2(relu(conv1(cat[noisy, base_out])))   (adapter.py:22-26); all NCHW */
+dn_status dn_adapter_forward(const float* params, const float* noisy, const float* base_out,
+                             float* out, int N, int C, int H, int W, int hidden_channels,
+                             void* stream);
+/* bytes of slab dn_adapter_backward needs (0 = unsupported arguments) */
+size_t dn_adapter_slab_size(int N, int C, int H, int W, int hidden_channels);
+/* dparams = dL/dparams of the adapter for dout = dL/dout (the base is frozen: no gradient
+   flows into base_out or noisy, finetune.py:255-262).  Overwrites dparams; deterministic. */
+dn_status dn_adapter_backward(const float* params, const float* noisy, const float* base_out,
+                              const float* dout, float* dparams, int N, int C, int H, int W,
+                              int hidden_channels, void* slab, size_t slab_bytes, void* stream);
+/* loss = L1(pred, target) + lambda_grad * gradient_loss(pred, target)  (finetune.py:283-285);
+   writes dpred = dloss/dpred and loss3 = {loss_l1, loss_grad, loss}.  partial_ws holds
+   dn_loss_partials_size() bytes. */
+dn_status dn_finetune_loss(const float* pred, const float* target, int N, int C, int H, int W,
+                           float lambda_grad, float* dpred, float* loss3, void* partial_ws,
+                           void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 OUT = os.path.dirname(os.path.abspath(__file__))
-REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+REF = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "/root/reference"
 
 
 def extract(path: str, names: list[str], ns: dict) -> dict:
@@ -183,5 +183,65 @@ def main():
     print("golden fixtures written to", OUT)
 
 
+def adapter_main():
+    """adapter.py OutputAdapter / DenoiserWithAdapter (imported) and finetune.py's gradient /
+    gradient_loss (AST-extracted: finetune.py imports torchvision, absent here)."""
+    sys.path.insert(0, REF)
+    import adapter  # noqa: E402
+    import arch_unet  # noqa: E402
+
+    ft = extract(os.path.join(REF, "finetune.py"), ["gradient", "gradient_loss"],
+                 {"torch": torch, "F": torch.nn.functional})
+    fx = {}
+    # ---- 6a. OutputAdapter alone, C = 1 and 3: output + parameter grads of the finetune loss
+    for C in (1, 3):
+        torch.manual_seed(10 + C)
+        ad = adapter.OutputAdapter(in_channels=C, hidden_channels=16)
+        g = torch.Generator().manual_seed(20 + C)
+        noisy = torch.rand(2, C, 24, 40, generator=g)
+        base = torch.rand(2, C, 24, 40, generator=g)
+        clean = torch.rand(2, C, 24, 40, generator=g)
+        out = ad(noisy, base)
+        l1 = torch.nn.functional.l1_loss(out, clean)
+        lg = ft["gradient_loss"](out, clean)
+        loss = l1 + 0.1 * lg
+        loss.backward()
+        k = f"c{C}_"
+        fx[k + "params"] = torch.cat([v.reshape(-1) for v in ad.state_dict().values()]).numpy()
+        fx[k + "noisy"], fx[k + "base"], fx[k + "clean"] = noisy.numpy(), base.numpy(), clean.numpy()
+        fx[k + "out"] = out.detach().numpy()
+        fx[k + "loss"] = np.array([l1.item(), lg.item(), loss.item()], np.float32)
+        fx[k + "grad"] = torch.cat([p.grad.reshape(-1) for p in ad.parameters()]).numpy()
+    # ---- 6b. one finetune.py:269-289 step, DenoiserWithAdapter(UNet base), Adam lr 1e-4
+    torch.manual_seed(0)
+    base = arch_unet.UNet(in_nc=1, out_nc=1, n_feature=48)
+    torch.manual_seed(1)
+    model = adapter.DenoiserWithAdapter(base, in_channels=1, hidden_channels=16)
+    g = torch.Generator().manual_seed(30)
+    clean = torch.rand(2, 1, 64, 64, generator=g)
+    noisy = clean + 0.1 * torch.randn(2, 1, 64, 64, generator=g)
+    opt = torch.optim.Adam(filter(lambda p: p.requires_grad, model.parameters()), lr=1e-4)
+    opt.zero_grad()
+    pred = model(noisy)
+    l1 = torch.nn.functional.l1_loss(pred, clean)
+    lg = ft["gradient_loss"](pred, clean)
+    loss = l1 + 0.1 * lg
+    loss.backward()
+    grad = torch.cat([p.grad.reshape(-1) for p in model.adapter.parameters()]).numpy()
+    pre = torch.cat([p.detach().reshape(-1) for p in model.adapter.parameters()]).numpy().copy()
+    opt.step()
+    post = torch.cat([p.detach().reshape(-1) for p in model.adapter.parameters()]).numpy()
+    fx.update(step_noisy=noisy.numpy(), step_clean=clean.numpy(), step_pred=pred.detach().numpy(),
+              step_loss=np.array([l1.item(), lg.item(), loss.item()], np.float32),
+              step_grad=grad, step_pre=pre, step_post=post,
+              step_base_sha=np.array(sha(flat_params(base))))
+    np.savez_compressed(os.path.join(OUT, "adapter.npz"), **fx)
+    print("adapter fixtures written to", OUT)
+
+
 if __name__ == "__main__":
-    main()
+    if "--only" in sys.argv:
+        {"adapter": adapter_main}[sys.argv[sys.argv.index("--only") + 1]]()
+    else:
+        main()
+        adapter_main()
