@@ -80,6 +80,15 @@ SIGNATURES = {
     "dn_psnr_u8": (c_int, [_U8, _U8, c_int64, c_void_p, c_void_p, c_void_p]),
     "dn_ssim_u8": (c_int, [_U8, _U8, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "dn_l1_mean": (c_int, [_F, _F, c_int64, c_void_p, c_void_p, c_void_p]),
+    "dn_iunet_param_count": (c_int, [POINTER(DnCfg), POINTER(c_size_t)]),
+    "dn_iunet_workspace_size": (c_int, [POINTER(DnCfg), c_int, c_int, c_int, c_int,
+                                        POINTER(c_size_t)]),
+    "dn_iunet_forward": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
+                                 c_size_t, c_void_p]),
+    "dn_iunet_backward": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
+                                  c_size_t, c_void_p]),
+    "dn_iunet_debug_buffers": (c_int, [POINTER(DnCfg), c_int, c_int, c_int, c_int,
+                                       POINTER(c_int64), c_int, POINTER(c_int)]),
     "dn_adapter_param_count": (c_int, [c_int, c_int, POINTER(c_size_t)]),
     "dn_adapter_forward": (c_int, [_F, _F, _F, _F, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "dn_adapter_slab_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),

@@ -4,6 +4,7 @@
 #include <cstring>
 #include <string>
 
+#include "iunet.h"
 #include "unet.h"
 
 using namespace dn;
@@ -507,6 +508,105 @@ dn_status dn_finetune_loss(const float* pred, const float* target, int N, int C,
   return hip_status(launch_ft_loss(pred, target, N, C, H, W, lambda_grad, dpred, loss3, partial_ws,
                                    (hipStream_t)stream),
                     "dn_finetune_loss");
+}
+
+// ---- ImprovedUNet (arch_unet.py:421-531) ------------------------------------------------------
+dn_status dn_iunet_param_count(const dn_unet_cfg* cfg, size_t* count) {
+  DN_GUARD_BEGIN
+  if (!cfg || !count) return fail(DN_ERR_ARG, "null argument");
+  IParams P;
+  std::string err;
+  if (!iunet_build_params(*cfg, P, err)) return fail(DN_ERR_ARG, err);
+  *count = (size_t)P.total;
+  return DN_OK;
+  DN_GUARD_END
+}
+
+dn_status dn_iunet_workspace_size(const dn_unet_cfg* cfg, int N, int H, int W, int with_backward,
+                                  size_t* bytes) {
+  DN_GUARD_BEGIN
+  if (!cfg || !bytes) return fail(DN_ERR_ARG, "null argument");
+  IPlan p;
+  std::string err;
+  if (!iunet_build_plan(*cfg, N, H, W, with_backward != 0, p, err)) return fail(DN_ERR_ARG, err);
+  *bytes = (size_t)p.total_floats * sizeof(float);
+  return DN_OK;
+  DN_GUARD_END
+}
+
+dn_status dn_iunet_forward(const dn_unet_cfg* cfg, const float* params, const float* x, float* y,
+                           int N, int H, int W, void* ws, size_t ws_bytes, void* stream) {
+  DN_GUARD_BEGIN
+  if (!cfg || !params || !x || !y || !ws) return fail(DN_ERR_ARG, "null argument");
+  IPlan p;
+  std::string err;
+  // the plan with the backward buffers has the same forward offsets: a workspace that large
+  // makes the forward keep what the backward reads
+  if (!iunet_build_plan(*cfg, N, H, W, true, p, err)) return fail(DN_ERR_ARG, err);
+  if (ws_bytes < (size_t)p.total_floats * sizeof(float) &&
+      !iunet_build_plan(*cfg, N, H, W, false, p, err))
+    return fail(DN_ERR_ARG, err);
+  if (ws_bytes < (size_t)p.total_floats * sizeof(float))
+    return fail(DN_ERR_WORKSPACE, "workspace smaller than dn_iunet_workspace_size()");
+  return iunet_forward(p, params, x, y, static_cast<float*>(ws), (hipStream_t)stream);
+  DN_GUARD_END
+}
+
+dn_status dn_iunet_backward(const dn_unet_cfg* cfg, const float* params, const float* dy,
+                            float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
+                            void* stream) {
+  DN_GUARD_BEGIN
+  if (!cfg || !params || !dy || !dparams || !ws) return fail(DN_ERR_ARG, "null argument");
+  IPlan p;
+  std::string err;
+  if (!iunet_build_plan(*cfg, N, H, W, true, p, err)) return fail(DN_ERR_ARG, err);
+  if (ws_bytes < (size_t)p.total_floats * sizeof(float))
+    return fail(DN_ERR_WORKSPACE, "workspace smaller than dn_iunet_workspace_size(with_backward=1)");
+  return iunet_backward(p, params, dy, dparams, static_cast<float*>(ws), (hipStream_t)stream);
+  DN_GUARD_END
+}
+
+/* (offset_floats, channel_stride, level) of the main ImprovedUNet activations, in the order
+   x0 h | per down level i: F r z1 a1 z2 | bottle: F r z1 a1 z2 | per up k: cc F r z1 a1 z2 | xb cf */
+dn_status dn_iunet_debug_buffers(const dn_unet_cfg* cfg, int N, int H, int W, int with_backward,
+                                 int64_t* desc, int max_entries, int* n_entries) {
+  DN_GUARD_BEGIN
+  if (!cfg || !desc || !n_entries) return fail(DN_ERR_ARG, "null argument");
+  IPlan p;
+  std::string err;
+  if (!iunet_build_plan(*cfg, N, H, W, with_backward != 0, p, err)) return fail(DN_ERR_ARG, err);
+  int n = 0;
+  auto add = [&](long off, int stride, int level) {
+    if (n < max_entries) {
+      desc[3 * n] = off;
+      desc[3 * n + 1] = stride;
+      desc[3 * n + 2] = level;
+    }
+    ++n;
+  };
+  auto blk = [&](const IBlockBufs& b, int ch, int l) {
+    add(b.F, ch + 128, l); add(b.r, ch, l); add(b.z1, ch, l); add(b.a1, ch, l); add(b.z2, ch, l);
+  };
+  add(p.x0, 4, 0); add(p.h, 48, 0);
+  for (int i = 0; i < 4; ++i) blk(p.dl[i], 48 << i, i);
+  blk(p.bb, 384, 4);
+  for (int k = 0; k < 4; ++k) {
+    const int out = p.P.up[k].out;
+    add(p.cc[k], 3 * out, 3 - k);
+    blk(p.ul[k], out, 3 - k);
+  }
+  add(p.xb, 384, 4); add(p.cf, 28, 0);
+  if (with_backward) {  // | per down level: dr dz2 dg1 dz1 | per up k: dcc | dpool
+    for (int i = 0; i < 4; ++i) {
+      const int ch = 48 << i;
+      add(p.dl[i].dr, ch, i); add(p.dl[i].dz2, ch, i); add(p.dl[i].dg1, ch, i);
+      add(p.dl[i].dz1, ch, i);
+    }
+    for (int k = 0; k < 4; ++k) add(p.dcc[k], 3 * p.P.up[k].out, 3 - k);
+  }
+  *n_entries = n;
+  return DN_OK;
+  DN_GUARD_END
 }
 
 }  // extern "C"

@@ -289,14 +289,19 @@ __global__ __launch_bounds__(256, (GATHER == G_C3 && NT == 6) ? 3 : 2) void k_fw
   // epilogue.  C/D map of 16x16 MFMA: col (n) = lane&15, row (pixel x) = 4*(lane>>4) + reg.
   const int ab = GATHER == G_UP ? wave : (int)blockIdx.z;
   const int wrow = GATHER == G_UP ? 0 : wave * MT;  // first tile row of this wave
-  const bool vec_out = a.out_layout != OUT_NCHW && ((a.out_stride | a.out_off | a.NOUT) & 3) == 0 &&
-                       (a.epi != EPI_MASK || ((a.mask_stride | a.mask_off) & 3) == 0);
+  // output-channel block of a wide layer: channels [cz, cz + nout) of NOUT
+  const int cz = a.zc ? (int)blockIdx.z * a.zc : 0;
+  const int nout = a.zc ? min(C::NP, a.NOUT - cz) : a.NOUT;
+  const bool aux = a.epi == EPI_MASK || a.epi == EPI_BIAS_ADD;
+  const bool vec_out = (a.out_layout == OUT_NHWC || a.out_layout == OUT_UP2) &&
+                       ((a.out_stride | a.out_off | a.NOUT) & 3) == 0 &&
+                       (!aux || ((a.mask_stride | a.mask_off) & 3) == 0);
   if (vec_out) {
     // Stage each 16-pixel row of the wave's tile through LDS and write whole pixels
     // (NOUT contiguous channels) as float4: 1 KiB contiguous per wave store instead of
     // 64-byte pieces.  All LDS is free here (the main loop ended on a barrier).
     float* st = lds + wave * 16 * C::PS;
-    const int NQ = a.NOUT >> 2;
+    const int NQ = nout >> 2;
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
 #pragma unroll
@@ -312,22 +317,28 @@ __global__ __launch_bounds__(256, (GATHER == G_C3 && NT == 6) ? 3 : 2) void k_fw
           if (gx >= a.OW) continue;
           float4 v = *reinterpret_cast<const float4*>(st + p * C::PS + c);
           const long pix = ((long)n * a.OH + gy) * a.OW + gx;
-          if (a.epi == EPI_BIAS || a.epi == EPI_BIAS_ACT) {
-            const float4 b = *reinterpret_cast<const float4*>(a.bias + c);
-            v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+          if (a.epi == EPI_BIAS || a.epi == EPI_BIAS_ACT || a.epi == EPI_BIAS_ADD) {
+            if (a.bias) {
+              const float4 b = *reinterpret_cast<const float4*>(a.bias + cz + c);
+              v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+            }
             if (a.epi == EPI_BIAS_ACT) {
               v.x = v.x > 0.f ? v.x : v.x * 0.2f; v.y = v.y > 0.f ? v.y : v.y * 0.2f;
               v.z = v.z > 0.f ? v.z : v.z * 0.2f; v.w = v.w > 0.f ? v.w : v.w * 0.2f;
+            } else if (a.epi == EPI_BIAS_ADD) {
+              const float4 r =
+                  *reinterpret_cast<const float4*>(a.mask + pix * a.mask_stride + a.mask_off + cz + c);
+              v.x = r.x + v.x; v.y = r.y + v.y; v.z = r.z + v.z; v.w = r.w + v.w;
             }
           } else if (a.epi == EPI_MASK) {
             const float4 mk =
-                *reinterpret_cast<const float4*>(a.mask + pix * a.mask_stride + a.mask_off + c);
+                *reinterpret_cast<const float4*>(a.mask + pix * a.mask_stride + a.mask_off + cz + c);
             v.x = mk.x > 0.f ? v.x : v.x * 0.2f; v.y = mk.y > 0.f ? v.y : v.y * 0.2f;
             v.z = mk.z > 0.f ? v.z : v.z * 0.2f; v.w = mk.w > 0.f ? v.w : v.w * 0.2f;
           }
           long oi;
           if (a.out_layout == OUT_NHWC)
-            oi = pix * a.out_stride + a.out_off + c;
+            oi = pix * a.out_stride + a.out_off + cz + c;
           else
             oi = (((long)n * 2 * a.OH + 2 * gy + (ab >> 1)) * 2 * a.OW + 2 * gx + (ab & 1)) *
                      a.out_stride + a.out_off + c;
@@ -350,8 +361,10 @@ __global__ __launch_bounds__(256, (GATHER == G_C3 && NT == 6) ? 3 : 2) void k_fw
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
       const int c = q * 16 + li;
-      if (c >= a.NOUT) continue;
-      const float bias = (a.epi == EPI_BIAS || a.epi == EPI_BIAS_ACT) ? a.bias[c] : 0.f;
+      if (c >= nout) continue;
+      const int cg = cz + c;  // channel of the layer
+      const float bias = ((a.epi == EPI_BIAS || a.epi == EPI_BIAS_ACT || a.epi == EPI_BIAS_ADD) &&
+                          a.bias) ? a.bias[cg] : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int gx = tx0 + 4 * lg + r;
@@ -363,15 +376,20 @@ __global__ __launch_bounds__(256, (GATHER == G_C3 && NT == 6) ? 3 : 2) void k_fw
         } else if (a.epi == EPI_BIAS_ACT) {
           v = v + bias;
           v = v > 0.f ? v : v * 0.2f;
+        } else if (a.epi == EPI_BIAS_ADD) {
+          v = a.mask[pix * a.mask_stride + a.mask_off + cg] + (v + bias);
         } else if (a.epi == EPI_MASK) {
-          const float mk = a.mask[pix * a.mask_stride + a.mask_off + c];
+          const float mk = a.mask[pix * a.mask_stride + a.mask_off + cg];
           v = mk > 0.f ? v : v * 0.2f;
         }
         long oi;
         if (a.out_layout == OUT_NHWC) {
-          oi = pix * a.out_stride + a.out_off + c;
+          oi = pix * a.out_stride + a.out_off + cg;
         } else if (a.out_layout == OUT_NCHW) {
-          oi = (((long)n * a.NOUT + c) * a.OH + gy) * a.OW + gx;
+          oi = (((long)n * a.NOUT + cg) * a.OH + gy) * a.OW + gx;
+        } else if (a.out_layout == OUT_PS) {  // PixelShuffle(2): cg = 4*c' + 2*i + j
+          oi = (((long)n * 2 * a.OH + 2 * gy + ((cg >> 1) & 1)) * 2 * a.OW + 2 * gx + (cg & 1)) *
+                   a.out_stride + a.out_off + (cg >> 2);
         } else {
           oi = (((long)n * 2 * a.OH + 2 * gy + (ab >> 1)) * 2 * a.OW + 2 * gx + (ab & 1)) *
                    a.out_stride + a.out_off + c;
@@ -473,7 +491,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_head_bwd(HeadBwdArgs h) {
 // Weight packing: the per-chunk LDS image [chunk][tap][k][n] (zero padded) of a strided
 // weight view, one image set per blockIdx.z value (deconv forward: one per (a,b)).
 __global__ __launch_bounds__(256) void k_pack(WView wv, int K, int NOUT, int KC, int TAPS, int WNS,
-                                              int LW, int nch, int nz, float* __restrict__ out) {
+                                              int LW, int nch, int nz, float* __restrict__ out,
+                                              int zc, int ntot) {
   const long per_z = (long)nch * LW, total = per_z * nz;
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
     const int z = (int)(e / per_z);
@@ -482,7 +501,7 @@ __global__ __launch_bounds__(256) void k_pack(WView wv, int K, int NOUT, int KC,
     float v = 0.f;
     if (q < TAPS * KC * WNS) {
       const int t = q / (KC * WNS), kk = (q / WNS) % KC, nn = q % WNS, k = c * KC + kk;
-      if (k < K && nn < NOUT) {
+      if (k < K && nn < NOUT && (zc == 0 || z * zc + nn < ntot)) {
         const int tm = wv.flip ? (wv.taps - 1 - t) : t;
         v = wv.w[wv.off + (long)z * wv.sZ + (long)k * wv.sK + (long)nn * wv.sN + (long)tm * wv.sT];
       }
@@ -669,6 +688,7 @@ __global__ __launch_bounds__(NW * 64, MF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a)
   }
 
   float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
+  const int cot = a.cout_total ? a.cout_total : a.Cout;
 #pragma unroll
   for (int i = 0; i < MF; ++i)
 #pragma unroll
@@ -680,8 +700,8 @@ __global__ __launch_bounds__(NW * 64, MF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a)
         const int co = (wave * MF + i) * 16 + 4 * lgp + r;
         if (co < a.Cout && ci < a.Cin) {
           const long widx =
-              a.wlayout == 0 ? ((long)co * a.cin_total + a.ci_base + ci) * C::TAPS + tap
-                             : ((long)(a.ci_base + ci) * a.Cout + co) * C::TAPS + tap;
+              a.wlayout == 0 ? ((long)(a.co_base + co) * a.cin_total + a.ci_base + ci) * C::TAPS + tap
+                             : ((long)(a.ci_base + ci) * cot + a.co_base + co) * C::TAPS + tap;
           slab[widx] = acc[i][f][r];
         }
       }
@@ -692,7 +712,7 @@ __global__ __launch_bounds__(NW * 64, MF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = (wave * MF + i) * 16 + 4 * lgp + r;
-        if (co < a.Cout) slab[(long)a.Cout * a.cin_total * C::TAPS + co] = accb[i][r];
+        if (co < a.Cout) slab[(long)cot * a.cin_total * C::TAPS + a.co_base + co] = accb[i][r];
       }
   }
 }
@@ -795,6 +815,7 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad3(WgradArgs a) {
 
   float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
   const int ci = ci0 + wn * 16 + li;
+  const int cot = a.cout_total ? a.cout_total : a.Cout;
 #pragma unroll
   for (int i = 0; i < C::MFW; ++i)
 #pragma unroll
@@ -803,7 +824,7 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad3(WgradArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int co = (wm * C::MFW + i) * 16 + 4 * lgp + r;
         if (co < a.Cout && ci < a.Cin)
-          slab[((long)co * a.cin_total + a.ci_base + ci) * 9 + t] = acc[i][t][r];
+          slab[((long)(a.co_base + co) * a.cin_total + a.ci_base + ci) * 9 + t] = acc[i][t][r];
       }
   if (do_bias && li == 0) {
 #pragma unroll
@@ -811,7 +832,7 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad3(WgradArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = (wm * C::MFW + i) * 16 + 4 * lgp + r;
-        if (co < a.Cout) slab[(long)a.Cout * a.cin_total * 9 + co] = accb[i][r];
+        if (co < a.Cout) slab[(long)cot * a.cin_total * 9 + a.co_base + co] = accb[i][r];
       }
   }
 }
@@ -972,7 +993,8 @@ template <int GATHER, int NT, int MT>
 static hipError_t run_fwd(const FwdArgs& a, hipStream_t s) {
   using C = FwdCfg<GATHER, NT, MT>;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
-  dim3 grid(tx * ty, a.N, (a.out_layout == OUT_UP2 && GATHER != G_UP) ? 4 : 1);
+  const int nz = a.zc ? (a.NOUT + a.zc - 1) / a.zc : ((a.out_layout == OUT_UP2 && GATHER != G_UP) ? 4 : 1);
+  dim3 grid(tx * ty, a.N, nz);
   hipLaunchKernelGGL((k_fwd<GATHER, NT, MT>), grid, dim3(256), 0, s, a, HeadArgs{});
   return hipGetLastError();
 }
@@ -1003,9 +1025,9 @@ hipError_t launch_head_bwd(const HeadBwdArgs& h, hipStream_t s) {
 // nin_a / nin_b as two single-chunk images [k][n] with row stride HEAD_WS
 hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s) {
   hipLaunchKernelGGL(k_pack, dim3((HEAD_LW + 255) / 256), dim3(256), 0, s, wa, 96, 96, 96, 1,
-                     HEAD_WS, HEAD_LW, 1, 1, out);
+                     HEAD_WS, HEAD_LW, 1, 1, out, 0, 0);
   hipLaunchKernelGGL(k_pack, dim3((HEAD_LW + 255) / 256), dim3(256), 0, s, wb, 96, 96, 96, 1,
-                     HEAD_WS, HEAD_LW, 1, 1, out + HEAD_LW);
+                     HEAD_WS, HEAD_LW, 1, 1, out + HEAD_LW, 0, 0);
   return hipGetLastError();
 }
 
@@ -1017,8 +1039,8 @@ static void geom(FwdGeom& g) {
 
 bool fwd_supported(int gather, int nout) {
   const int nt = (nout + 15) / 16;
-  if (gather == G_C3) return nt == 3 || nt == 6 || nt == 9;
-  if (gather == G_C1) return nt == 1 || nt == 3 || nt == 6;
+  if (gather == G_C3) return nt == 2 || nt == 3 || nt == 6 || nt == 9;
+  if (gather == G_C1) return nt == 1 || nt == 2 || nt == 3 || nt == 6;
   if (gather == G_DN2 || gather == G_UP) return nt == 3 || nt == 6;
   return false;
 }
@@ -1026,11 +1048,13 @@ bool fwd_supported(int gather, int nout) {
 bool fwd_geometry(int gather, int nout, FwdGeom& g) {
   const int nt = (nout + 15) / 16;
   if (gather == G_C3) {
+    if (nt == 2) { geom<G_C3, 2, 4>(g); return true; }
     if (nt == 3) { geom<G_C3, 3, 4>(g); return true; }
     if (nt == 6) { geom<G_C3, 6, 4>(g); return true; }
     if (nt == 9) { geom<G_C3, 9, 2>(g); return true; }
   } else if (gather == G_C1) {
     if (nt == 1) { geom<G_C1, 1, 4>(g); return true; }
+    if (nt == 2) { geom<G_C1, 2, 4>(g); return true; }
     if (nt == 3) { geom<G_C1, 3, 4>(g); return true; }
     if (nt == 6) { geom<G_C1, 6, 4>(g); return true; }
   } else if (gather == G_DN2) {
@@ -1051,7 +1075,7 @@ long pack_floats(int gather, int nout, int K, int nz) {
 }
 
 hipError_t launch_pack(int gather, const WView& wv, int K, int nout, int nz, float* out,
-                       hipStream_t s) {
+                       hipStream_t s, int zc, int ntot) {
   FwdGeom g;
   if (!fwd_geometry(gather, nout, g)) return hipErrorInvalidValue;
   const int nch = (K + g.KC - 1) / g.KC;
@@ -1059,7 +1083,7 @@ hipError_t launch_pack(int gather, const WView& wv, int K, int nout, int nz, flo
   long blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(k_pack, dim3((unsigned)blocks), dim3(256), 0, s, wv, K, nout, g.KC, g.TAPS,
-                     g.WNS, g.LW, nch, nz, out);
+                     g.WNS, g.LW, nch, nz, out, zc, ntot);
   return hipGetLastError();
 }
 
@@ -1089,6 +1113,23 @@ hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s) {
   } else if (gather == G_DN2) {
     if (nt == 3) return small ? run_fwd<G_DN2, 3, 1>(a, s) : run_fwd<G_DN2, 3, 4>(a, s);
     if (nt == 6) return small ? run_fwd<G_DN2, 6, 1>(a, s) : run_fwd<G_DN2, 6, 4>(a, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+// explicit tile width; a.zc must be 16*nt (or 0 for a single block of NOUT <= 16*nt)
+hipError_t launch_fwd_nt(int gather, int nt, const FwdArgs& a, hipStream_t s) {
+  const int nz = a.zc ? (a.NOUT + a.zc - 1) / a.zc : 1;
+  const long big_tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16) * nz;
+  const bool small = big_tiles < 1024;
+  if (gather == G_C3) {
+    if (nt == 2) return small ? run_fwd<G_C3, 2, 1>(a, s) : run_fwd<G_C3, 2, 4>(a, s);
+    if (nt == 3) return small ? run_fwd<G_C3, 3, 1>(a, s) : run_fwd<G_C3, 3, 4>(a, s);
+    if (nt == 6) return small ? run_fwd<G_C3, 6, 1>(a, s) : run_fwd<G_C3, 6, 4>(a, s);
+  } else if (gather == G_C1) {
+    if (nt == 2) return small ? run_fwd<G_C1, 2, 1>(a, s) : run_fwd<G_C1, 2, 4>(a, s);
+    if (nt == 3) return small ? run_fwd<G_C1, 3, 1>(a, s) : run_fwd<G_C1, 3, 4>(a, s);
+    if (nt == 6) return small ? run_fwd<G_C1, 6, 1>(a, s) : run_fwd<G_C1, 6, 2>(a, s);
   }
   return hipErrorInvalidValue;
 }
@@ -1170,6 +1211,63 @@ hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s)
     if (cf == 6) return run_wgrad<W_UP2, 2, 3, 1>(a, splits, s);
   }
   return hipErrorInvalidValue;
+}
+
+// ---- general weight gradient (any Cout via output-channel blocks) ----------------------
+// 3x3: k_wgrad3 in blocks of 96 / 48 / 32 output channels (Cin >= 16, float4-aligned views);
+// 1x1: k_wgrad<W_C1> in blocks of 96 / 48.  Every block of one layer uses the same split count,
+// so each slab row ends up holding the whole [W ; b] image and one k_reduce finishes it.
+static int gw_block(int mode, int cout) {
+  if (mode == W_C3) return cout <= 32 ? 32 : (cout <= 48 ? 48 : 96);
+  return cout <= 48 ? 48 : 96;
+}
+
+int gwgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
+  const int cb = gw_block(mode, Cout);
+  const int nblk = (Cout + cb - 1) / cb;
+  const int cin_t = mode == W_C3 ? (cb == 96 ? 32 : 48) : 96;
+  const long cib = (long)nblk * ((Cin + cin_t - 1) / cin_t);
+  const int taps = mode == W_C3 ? 9 : 1;
+  const int pr = (mode == W_C3 || cb == 96) ? 1 : 2;  // pixel rows per K chunk
+  const long units = (long)N * ((KH + pr - 1) / pr) * ((KW + 31) / 32);
+  long want = 768 / cib;
+  const long slab_cap = (64L << 20) / ((long)Cout * Cin * taps + Cout);
+  if (want > slab_cap) want = slab_cap;
+  if (want > units / 2) want = units / 2;
+  return (int)(want < 1 ? 1 : want);
+}
+
+// operands are read as channel quads: every quad that starts inside [0, C) must lie inside
+// the view's row (padding channels of a wider buffer are fine, they meet masked rows/columns)
+bool gwgrad_ok(int mode, int Cin, int Cout, const View& g, const View& x) {
+  if (mode != W_C3 && mode != W_C1) return false;
+  if ((g.stride | g.off | x.stride | x.off) & 3) return false;
+  if (mode == W_C3 && Cin < 16) return false;
+  if (x.off + ((Cin + 3) & ~3) > x.stride || g.off + ((Cout + 3) & ~3) > g.stride) return false;
+  return Cout >= 1 && Cin >= 1;
+}
+
+hipError_t launch_gwgrad(int mode, const WgradArgs& a0, int splits, hipStream_t s) {
+  const int cb = gw_block(mode, a0.Cout);
+  for (int c0 = 0; c0 < a0.Cout; c0 += cb) {
+    WgradArgs a = a0;
+    a.co_base = c0;
+    a.cout_total = a0.Cout;
+    a.Cout = a0.Cout - c0 < cb ? a0.Cout - c0 : cb;
+    a.g_off = a0.g_off + c0;
+    a.bias = a0.bias;
+    hipError_t e;
+    if (mode == W_C3) {
+      if (cb == 96) e = run_wgrad3<6, 2, 2>(a, splits, s);
+      else if (cb == 48) e = run_wgrad3<3, 1, 3>(a, splits, s);
+      else e = run_wgrad3<2, 1, 3>(a, splits, s);
+    } else {
+      if (cb == 96) e = run_wgrad<W_C1, 2, 3, 6>(a, splits, s);
+      else e = run_wgrad<W_C1, 1, 3, 6>(a, splits, s);
+    }
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // ---- k_wgrad1 routing --------------------------------------------------------------

@@ -27,12 +27,14 @@ enum Epi {
   EPI_PLAIN = 2,     // acc
   EPI_MASK = 3,      // acc * (mask > 0 ? 1 : 0.2)   (LeakyReLU backward through the saved output)
   EPI_ACCUM = 4,     // out += acc
+  EPI_BIAS_ADD = 5,  // acc + bias + res  (residual source read through the mask view)
 };
 
 enum OutLayout {
   OUT_NHWC = 0,  // out[((n*OH+y)*OW+x)*stride + off + c]
   OUT_NCHW = 1,  // out[((n*NOUT+c)*OH+y)*OW+x]
   OUT_UP2 = 2,   // deconv scatter: out[((n*2OH+2y+a)*2OW+2x+b)*stride + off + c], ab = blockIdx.z
+  OUT_PS = 3,    // PixelShuffle(2) of the conv output: channel 4c+2i+j -> pixel (2y+i, 2x+j), channel c
 };
 
 // Strided view of the weight tensor as B[t][k][n] (t = tap, k = reduction channel, n = output).
@@ -52,6 +54,7 @@ struct FwdArgs {
   int epi;
   float* out; int out_stride, out_off; int out_layout;
   const float* mask; int mask_stride, mask_off;
+  int zc;        // > 0: blockIdx.z selects output channels [z*zc, z*zc+zc) (wide layers)
 };
 
 // Fused output head (arch_unet.py:186-190, 253-257): the dec_conv1b kernel keeps its
@@ -87,6 +90,14 @@ struct WgradArgs {
   int cin_total, ci_base;               // weight tensor's Cin and this launch's first ci
   int bias;                             // also produce the bias gradient
   const float* zeros;                   // >= 16 zero bytes (LDS-DMA source for padding)
+  int co_base, cout_total;              // this launch's first output channel / the layer's Cout
+};
+
+// strided NHWC view: element (pixel, c) at p[pixel * stride + off + c]
+struct View {
+  float* p;
+  int stride;
+  int off;
 };
 
 // geometry of the packed per-chunk weight image of the forward-family kernel
@@ -96,7 +107,10 @@ struct FwdGeom { int KC, TAPS, WNS, LW; };
 bool fwd_geometry(int gather, int nout, FwdGeom& g);
 long pack_floats(int gather, int nout, int K, int nz);  // floats of a packed weight set
 hipError_t launch_pack(int gather, const WView& wv, int K, int nout, int nz, float* out,
-                       hipStream_t s);
+                       hipStream_t s, int zc = 0, int ntot = 0);
+// forward-family launch with explicit tile width NT (16*NT output channels per z-block) and
+// a.zc = 16*NT output-channel blocks over blockIdx.z
+hipError_t launch_fwd_nt(int gather, int nt, const FwdArgs& a, hipStream_t s);
 hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s);
 hipError_t launch_enc0_fwd(const float* x, int N, int C, int H, int W, const float* w,
                            const float* b, float* out, float* cat, int cat_stride, int cat_off,
@@ -138,6 +152,9 @@ hipError_t launch_reduce_scatter(const float* slab, long slab_stride, int splits
 hipError_t launch_reduce(const float* slab, long slab_stride, int splits, long n, float* out,
                          hipStream_t s);
 bool fwd_supported(int gather, int nout);
+int gwgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
+bool gwgrad_ok(int mode, int Cin, int Cout, const View& g, const View& x);
+hipError_t launch_gwgrad(int mode, const WgradArgs& a, int splits, hipStream_t s);
 bool wgrad_supported(int mode, int cout, int cin);
 
 // ---- elementwise launchers (elementwise.hip) ----

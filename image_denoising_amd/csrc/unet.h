@@ -25,11 +25,6 @@ struct ParamLayout {
   long total;
 };
 
-struct View {
-  float* p;
-  int stride;
-  int off;
-};
 
 struct Plan {
   ParamLayout P;

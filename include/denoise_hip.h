@@ -231,6 +231,30 @@ dn_status dn_finetune_loss(const float* pred, const float* target, int N, int C,
                            float lambda_grad, float* dpred, float* loss3, void* partial_ws,
                            void* stream);
 
+/* ---- ImprovedUNet: arch_unet.py:421-531 ImprovedUNet(in_nc, out_nc, n_feature=48, depth=4,
+   noise=True) — the model train.sh / evaluation.py default to (train.py:311-313) --------------
+   Same conventions as the UNet entry points: NCHW fp32 at the boundary, ONE flat fp32 parameter
+   buffer in ImprovedUNet's state_dict order (noise_estimator.*, downs.*, bottle.*, ups.*,
+   final.*; GroupNorm weight/bias included), H and W multiples of 16.  cfg->n_feature must be 48
+   (the width train.py:30 uses); in_nc 1..3, out_nc 1..4. */
+dn_status dn_iunet_param_count(const dn_unet_cfg* cfg, size_t* count);
+dn_status dn_iunet_workspace_size(const dn_unet_cfg* cfg, int N, int H, int W, int with_backward,
+                                  size_t* bytes);
+/* y = sigmoid(...) = ImprovedUNet(x); keeps the activations for a backward when ws was sized
+   with with_backward=1 */
+dn_status dn_iunet_forward(const dn_unet_cfg* cfg, const float* params, const float* x, float* y,
+                           int N, int H, int W, void* ws, size_t ws_bytes, void* stream);
+/* dparams = dL/dparams for dy = dL/dy, using the activations the last dn_iunet_forward on ws
+   saved.  Overwrites dparams; deterministic. */
+dn_status dn_iunet_backward(const dn_unet_cfg* cfg, const float* params, const float* dy,
+                            float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
+                            void* stream);
+/* Debug/introspection: (offset_floats, channel_stride, level) of the main NHWC activations:
+   x0 h | down level i = 0..3: F r z1 a1 z2 | bottle: F r z1 a1 z2 | up k = 0..3: cc F r z1 a1 z2 |
+   xb cf */
+dn_status dn_iunet_debug_buffers(const dn_unet_cfg* cfg, int N, int H, int W, int with_backward,
+                                 int64_t* desc, int max_entries, int* n_entries);
+
 #ifdef __cplusplus
 }
 #endif

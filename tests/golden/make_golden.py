@@ -239,9 +239,36 @@ def adapter_main():
     print("adapter fixtures written to", OUT)
 
 
+def iunet_main():
+    """arch_unet.ImprovedUNet (imported): init, forward, parameter gradients of a squared error."""
+    sys.path.insert(0, REF)
+    import arch_unet  # noqa: E402
+
+    for C, N, S, path in ((1, 2, 32, "iunet_c1.npz"), (3, 1, 32, "iunet_c3.npz")):
+        torch.manual_seed(0)
+        net = arch_unet.ImprovedUNet(in_nc=C, out_nc=C, n_feature=48)
+        flat = flat_params(net)
+        g = torch.Generator().manual_seed(1)
+        x = torch.rand(N, C, S, S, generator=g)
+        t = torch.rand(N, C, S, S, generator=g)
+        y = net(x)
+        loss = ((y - t) ** 2).mean()
+        loss.backward()
+        grad = torch.cat([p.grad.reshape(-1) for p in net.parameters()]).numpy()
+        idx = np.random.default_rng(0).choice(grad.size, 16384, replace=False)
+        np.savez_compressed(
+            os.path.join(OUT, path), x=x.numpy(), t=t.numpy(), y=y.detach().numpy(),
+            loss=np.float32(loss.item()), params_sha=np.array(sha(flat)),
+            params_count=np.int64(flat.size), grad_idx=idx, grad_sample=grad[idx],
+            grad_norms=np.array([np.linalg.norm(p.grad.numpy()) for p in net.parameters()]),
+            keys=np.array(list(net.state_dict().keys())))
+    print("ImprovedUNet fixtures written to", OUT)
+
+
 if __name__ == "__main__":
     if "--only" in sys.argv:
-        {"adapter": adapter_main}[sys.argv[sys.argv.index("--only") + 1]]()
+        {"adapter": adapter_main, "iunet": iunet_main}[sys.argv[sys.argv.index("--only") + 1]]()
     else:
         main()
         adapter_main()
+        iunet_main()
