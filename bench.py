@@ -46,6 +46,33 @@ def unet_fwd_flops(H, W, C=1, nf=48):
     return f
 
 
+def iunet_fwd_flops(H, W, C=1, nf=48):
+    """analytic forward FLOPs of arch_unet.ImprovedUNet per image (convs only; GroupNorm,
+    activations, pooling and PixelShuffle are elementwise)"""
+    f = conv_flops(H, W, C, nf, 3) + conv_flops(H, W, nf, 1, 3)  # noise estimator
+
+    def rdb(h, w, ch):
+        return sum(conv_flops(h, w, ch + 32 * j, 32, 3) for j in range(4)) + conv_flops(h, w, ch + 128, ch, 1)
+
+    def res(h, w, ch):
+        return 2 * conv_flops(h, w, ch, ch, 3)
+
+    c, cin = nf, C + 1
+    for i in range(4):
+        h, w = H >> i, W >> i
+        f += conv_flops(h, w, cin, c, 3) + rdb(h, w, c) + res(h, w, c)
+        cin, c = c, 2 * c
+    c //= 2
+    f += rdb(H >> 4, W >> 4, c) + res(H >> 4, W >> 4, c)
+    for k in range(4):
+        o = c // 2
+        h, w = H >> (3 - k), W >> (3 - k)
+        f += conv_flops(h // 2, w // 2, c, 4 * o, 3) + conv_flops(h, w, 3 * o, o, 3)
+        f += rdb(h, w, o) + res(h, w, o)
+        c = o
+    return f + conv_flops(H, W, nf // 2 + C, C, 3)
+
+
 def synthetic_clean(n, H, W, seed, device):
     g = torch.Generator(device="cpu").manual_seed(seed)
     lo = torch.rand(n, 1, H // 8, W // 8, generator=g)
@@ -133,6 +160,8 @@ def main():
                     help="n2n: the N2N step (BASELINE metric); structure: train.py's "
                          "Structure_loss step (two grad forwards at full resolution); finetune: "
                          "finetune.py's adapter step (frozen UNet base + OutputAdapter, configs[4])")
+    ap.add_argument("--arch", choices=["UNet", "UNetImproved"], default="UNet",
+                    help="network (train.py:305-313 / finetune.py --arch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--breakdown", action="store_true", help="per-phase HIP-event timing (stderr)")
     args = ap.parse_args()
@@ -152,7 +181,14 @@ def main():
     H = args.size or (512 if ft else 256)
     bs = args.bs or (16 if ft else 64)
     torch.manual_seed(0)
-    net = UNet(in_nc=C, out_nc=C, n_feature=48).to(device)
+    iu = args.arch == "UNetImproved"
+    if iu:
+        from image_denoising_amd.improved_unet import ImprovedUNet
+
+        net = ImprovedUNet(in_nc=C, out_nc=C, n_feature=48).to(device)
+    else:
+        net = UNet(in_nc=C, out_nc=C, n_feature=48).to(device)
+    fwd_flops = iunet_fwd_flops if iu else unet_fwd_flops
     clean = synthetic_clean(bs * C, H, H, 1000 + rank, device).view(bs, C, H, H).contiguous()
     if ft:
         from image_denoising_amd.adapter import DenoiserWithAdapter
@@ -201,14 +237,18 @@ def main():
         kms, kflops = time_dominant_kernel(bs, H, H, device)
         achieved = kflops / (kms * 1e-3) / 1e12
         if args.mode == "n2n":  # fwd 256 + fwd/bwd 128
-            step_flops = bs * (unet_fwd_flops(H, H, C) + 3 * unet_fwd_flops(H // 2, H // 2, C))
+            step_flops = bs * (fwd_flops(H, H, C) + 3 * fwd_flops(H // 2, H // 2, C))
         elif ft:  # frozen base forward + adapter fwd (864 flop/px) and bwd (~1728 flop/px, C=1)
-            step_flops = bs * (unet_fwd_flops(H, H, C) + 3 * 864.0 * C * H * H)
+            step_flops = bs * (fwd_flops(H, H, C) + 3 * 864.0 * C * H * H)
         else:  # two fwd/bwd at full resolution
-            step_flops = bs * 2 * 3 * unet_fwd_flops(H, H, C)
-        traffic, traffic_src = pmc_traffic() if (bs, H, C) == (64, 256, 1) else (None, None)
-        if ft:
-            workload = (f"BASELINE configs[4]: finetune.py adapter step, frozen UNet(n_feature=48) "
+            step_flops = bs * 2 * 3 * fwd_flops(H, H, C)
+        traffic, traffic_src = pmc_traffic() if (bs, H, C, iu) == (64, 256, 1, False) else (None, None)
+        model = "ImprovedUNet(n_feature=48)" if iu else "UNet(n_feature=48)"
+        if iu and not ft:
+            workload = (f"{args.mode} step with arch_unet.ImprovedUNet(n_feature=48, depth=4, noise=True) "
+                        f"(train.py:311-313), {bs}x{C}x{H}x{H} per GPU, Adam lr 3e-4")
+        elif ft:
+            workload = (f"BASELINE configs[4]: finetune.py adapter step, frozen {model} "
                         f"base (no_grad) + OutputAdapter(hidden 16), {bs}x{C}x{H}x{H} per GPU, "
                         f"L1 + 0.1*gradient_loss, Adam lr 1e-4, fp32")
         elif args.mode == "structure":
@@ -222,9 +262,10 @@ def main():
                         f"{bs}x{C}x{H}x{H} per GPU, Adam lr 3e-4")
         rec = {
             "metric": "training patches/sec (256x256x1, bs=64 per GPU, N2N loss + Adam)"
-                      if args.mode == "n2n" and (C, bs, H) == (1, 64, 256)
+                      if args.mode == "n2n" and (C, bs, H) == (1, 64, 256) and not iu
                       else (f"finetune patches/sec ({H}x{H}x{C}, bs={bs} per GPU, frozen base + adapter)"
-                            if ft else f"training patches/sec ({H}x{H}x{C}, bs={bs} per GPU, {args.mode})"),
+                            if ft else f"training patches/sec ({H}x{H}x{C}, bs={bs} per GPU, {args.mode}"
+                                       f"{', ImprovedUNet' if iu else ''})"),
             "value": round(value, 2), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
@@ -239,7 +280,7 @@ def main():
                          "avg_launch_ms": round(kms, 4), "flops_per_launch": kflops},
             "loss": loss_v,
         }
-        if not args.no_cpu_baseline and world == 1 and args.mode == "n2n" and C == 1:
+        if not args.no_cpu_baseline and world == 1 and args.mode == "n2n" and C == 1 and not iu:
             rec["cpu_baseline"] = cpu_baseline()
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -540,9 +540,21 @@ struct WgCfg {
   static constexpr int GITEMS = (GQ + NTHR - 1) / NTHR, XITEMS = (XQ + NTHR - 1) / NTHR;
 };
 
+// output-channel block of a wide layer (a.zc > 0): blockIdx.z selects channels [z*zc, z*zc+zc)
+__device__ __forceinline__ WgradArgs wg_block(const WgradArgs& a0) {
+  WgradArgs a = a0;
+  if (a0.zc > 0) {
+    a.co_base = (int)blockIdx.z * a0.zc;
+    a.Cout = min(a0.zc, a0.cout_total - a.co_base);
+    a.g_off = a0.g_off + a.co_base;
+  }
+  return a;
+}
+
 template <int MODE, int MF, int NW, int CIF>
-__global__ __launch_bounds__(NW * 64, MF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a) {
+__global__ __launch_bounds__(NW * 64, MF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a0) {
   using C = WgCfg<MODE, MF, NW, CIF>;
+  const WgradArgs a = wg_block(a0);
   __shared__ __attribute__((aligned(16))) float lds[C::LG + C::LX];
   float* lg_ = lds;
   float* lx = lds + C::LG;
@@ -738,8 +750,9 @@ struct Wg3Cfg {
 };
 
 template <int CO_FR, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad3(WgradArgs a) {
+__global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad3(WgradArgs a0) {
   using C = Wg3Cfg<CO_FR, WM, WN>;
+  const WgradArgs a = wg_block(a0);
   __shared__ __attribute__((aligned(16))) float lds[2 * C::LBUF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -862,8 +875,12 @@ struct Wg1Cfg {
 };
 
 template <int CO_FR, int CI_FR, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad1(WgradArgs a, int up2) {
+__global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad1(WgradArgs a0, int up2) {
   using C = Wg1Cfg<CO_FR, CI_FR, WM, WN>;
+  // 1x1 (up2 == 0) with a.zc > 0: blockIdx.z = output-channel block, blockIdx.y = input-channel
+  // block of C::CIN; all blocks of a split write one slab row
+  const WgradArgs a = up2 ? a0 : wg_block(a0);
+  const int ci0 = up2 ? 0 : (int)blockIdx.y * C::CIN;
   __shared__ __attribute__((aligned(16))) float lds[2 * C::LBUF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -871,7 +888,7 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad1(WgradArgs a, int up2
   const int ux = (a.KW + C::PC - 1) / C::PC;
   const long U = (long)a.N * a.KH * ux;
   const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
-  const bool do_bias = wn == 0;
+  const bool do_bias = wn == 0 && blockIdx.y == 0;
   const int pa = up2 ? (int)(blockIdx.z >> 1) : 0, pb = up2 ? (int)(blockIdx.z & 1) : 0;
   const int GH = up2 ? 2 * a.KH : a.KH, GW = up2 ? 2 * a.KW : a.KW, sc = up2 ? 2 : 1;
 
@@ -900,7 +917,7 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad1(WgradArgs a, int up2
     const float* xb = a.x + ((long)n * a.KH + py) * a.KW * a.x_stride + a.x_off;
     for (int p = wave; p < C::LXP; p += C::NW) {
       const int idx = p * 256 + lane * 4;
-      const int px = idx / C::CIN, ci = idx - px * C::CIN;
+      const int px = idx / C::CIN, ci = ci0 + idx - px * C::CIN;
       const int gx = px0 + px;
       const float* src = (gx < a.KW && ci < a.Cin) ? xb + (long)gx * a.x_stride + ci : a.zeros;
       glds16(src, buf + C::LGF + p * 256);
@@ -934,8 +951,9 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad1(WgradArgs a, int up2
     __syncthreads();  // next stage landed (vmcnt(0)); everyone done with this buffer
   }
 
-  const long row = (long)blockIdx.z * gridDim.x + blockIdx.x;
+  const long row = up2 ? (long)blockIdx.z * gridDim.x + blockIdx.x : (long)blockIdx.x;
   float* slab = a.slab + row * a.slab_stride;
+  const int cot = a.zc > 0 ? a.cout_total : a.Cout;
 #pragma unroll
   for (int i = 0; i < C::MFW; ++i)
 #pragma unroll
@@ -943,9 +961,9 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad1(WgradArgs a, int up2
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = (wm * C::MFW + i) * 16 + 4 * lgp + r;
-        const int ci = (wn * C::NFW + j) * 16 + li;
+        const int ci = ci0 + (wn * C::NFW + j) * 16 + li;
         if (co < a.Cout && ci < a.Cin)
-          slab[a.wlayout ? (long)ci * a.Cout + co : (long)co * a.Cin + ci] = acc[i][j][r];
+          slab[a.wlayout ? (long)ci * a.Cout + co : (long)(a.co_base + co) * a.Cin + ci] = acc[i][j][r];
       }
   if (do_bias && li == 0) {
 #pragma unroll
@@ -953,7 +971,7 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad1(WgradArgs a, int up2
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = (wm * C::MFW + i) * 16 + 4 * lgp + r;
-        if (co < a.Cout) slab[(long)a.Cout * a.Cin + co] = accb[i][r];
+        if (co < a.Cout) slab[(long)cot * a.Cin + a.co_base + co] = accb[i][r];
       }
   }
 }
@@ -1123,9 +1141,22 @@ hipError_t launch_fwd_nt(int gather, int nt, const FwdArgs& a, hipStream_t s) {
   const long big_tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16) * nz;
   const bool small = big_tiles < 1024;
   if (gather == G_C3) {
-    if (nt == 2) return small ? run_fwd<G_C3, 2, 1>(a, s) : run_fwd<G_C3, 2, 4>(a, s);
-    if (nt == 3) return small ? run_fwd<G_C3, 3, 1>(a, s) : run_fwd<G_C3, 3, 4>(a, s);
-    if (nt == 6) return small ? run_fwd<G_C3, 6, 1>(a, s) : run_fwd<G_C3, 6, 4>(a, s);
+    // tile height 16/8/4 rows (MT = 4/2/1): the fewest rounds of resident workgroups, weighed
+    // by the per-tile efficiency of the taller tiles (a 1024-tile grid on 768 slots would run
+    // two rounds at 4 rows but 2.7 at 8 rows / 5.3 at 4 rows with less waste per round)
+    const long slots = (nt == 6 ? 3L : 2L) * 256;
+    int mt = 1;
+    double best = 1e30;
+    const int mts[3] = {4, 2, 1};
+    const double eff[3] = {1.0, 1.08, 1.25};
+    for (int i = 0; i < 3; ++i) {
+      const long blocks = (long)a.N * ((a.OH + 4 * mts[i] - 1) / (4 * mts[i])) * ((a.OW + 15) / 16) * nz;
+      const double cost = (double)((blocks + slots - 1) / slots) * mts[i] * eff[i];
+      if (cost < best - 1e-9) { best = cost; mt = mts[i]; }
+    }
+    if (nt == 2) return mt == 4 ? run_fwd<G_C3, 2, 4>(a, s) : mt == 2 ? run_fwd<G_C3, 2, 2>(a, s) : run_fwd<G_C3, 2, 1>(a, s);
+    if (nt == 3) return mt == 4 ? run_fwd<G_C3, 3, 4>(a, s) : mt == 2 ? run_fwd<G_C3, 3, 2>(a, s) : run_fwd<G_C3, 3, 1>(a, s);
+    if (nt == 6) return mt == 4 ? run_fwd<G_C3, 6, 4>(a, s) : mt == 2 ? run_fwd<G_C3, 6, 2>(a, s) : run_fwd<G_C3, 6, 1>(a, s);
   } else if (gather == G_C1) {
     if (nt == 2) return small ? run_fwd<G_C1, 2, 1>(a, s) : run_fwd<G_C1, 2, 4>(a, s);
     if (nt == 3) return small ? run_fwd<G_C1, 3, 1>(a, s) : run_fwd<G_C1, 3, 4>(a, s);
@@ -1137,7 +1168,8 @@ hipError_t launch_fwd_nt(int gather, int nt, const FwdArgs& a, hipStream_t s) {
 template <int MODE, int MF, int NW, int CIF>
 static hipError_t run_wgrad(const WgradArgs& a, int splits, hipStream_t s) {
   using C = WgCfg<MODE, MF, NW, CIF>;
-  dim3 grid(splits, (a.Cin + C::CIN_T - 1) / C::CIN_T, 1);
+  const int nz = a.zc > 0 ? (a.cout_total + a.zc - 1) / a.zc : 1;
+  dim3 grid(splits, (a.Cin + C::CIN_T - 1) / C::CIN_T, nz);
   hipLaunchKernelGGL((k_wgrad<MODE, MF, NW, CIF>), grid, dim3(C::NTHR), 0, s, a);
   return hipGetLastError();
 }
@@ -1145,7 +1177,8 @@ static hipError_t run_wgrad(const WgradArgs& a, int splits, hipStream_t s) {
 template <int CO_FR, int WM, int WN>
 static hipError_t run_wgrad3(const WgradArgs& a, int splits, hipStream_t s) {
   using C = Wg3Cfg<CO_FR, WM, WN>;
-  dim3 grid(splits, (a.Cin + C::CIB - 1) / C::CIB, 1);
+  const int nz = a.zc > 0 ? (a.cout_total + a.zc - 1) / a.zc : 1;
+  dim3 grid(splits, (a.Cin + C::CIB - 1) / C::CIB, nz);
   hipLaunchKernelGGL((k_wgrad3<CO_FR, WM, WN>), grid, dim3(C::NTHR), 0, s, a);
   return hipGetLastError();
 }
@@ -1226,6 +1259,14 @@ int gwgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
   const int cb = gw_block(mode, Cout);
   const int nblk = (Cout + cb - 1) / cb;
   const int cin_t = mode == W_C3 ? (cb == 96 ? 32 : 48) : 96;
+  if (mode == W_C1) {  // k_wgrad1: one 32-pixel row segment per K stage
+    const long units = (long)N * KH * ((KW + 31) / 32);
+    long want = 768 / ((long)nblk * ((Cin + 95) / 96));
+    const long slab_cap = (64L << 20) / ((long)Cout * Cin + Cout);
+    if (want > slab_cap) want = slab_cap;
+    if (want > units / 2) want = units / 2;
+    return (int)(want < 1 ? 1 : want);
+  }
   const long cib = (long)nblk * ((Cin + cin_t - 1) / cin_t);
   const int taps = mode == W_C3 ? 9 : 1;
   const int pr = (mode == W_C3 || cb == 96) ? 1 : 2;  // pixel rows per K chunk
@@ -1249,25 +1290,20 @@ bool gwgrad_ok(int mode, int Cin, int Cout, const View& g, const View& x) {
 
 hipError_t launch_gwgrad(int mode, const WgradArgs& a0, int splits, hipStream_t s) {
   const int cb = gw_block(mode, a0.Cout);
-  for (int c0 = 0; c0 < a0.Cout; c0 += cb) {
-    WgradArgs a = a0;
-    a.co_base = c0;
-    a.cout_total = a0.Cout;
-    a.Cout = a0.Cout - c0 < cb ? a0.Cout - c0 : cb;
-    a.g_off = a0.g_off + c0;
-    a.bias = a0.bias;
-    hipError_t e;
-    if (mode == W_C3) {
-      if (cb == 96) e = run_wgrad3<6, 2, 2>(a, splits, s);
-      else if (cb == 48) e = run_wgrad3<3, 1, 3>(a, splits, s);
-      else e = run_wgrad3<2, 1, 3>(a, splits, s);
-    } else {
-      if (cb == 96) e = run_wgrad<W_C1, 2, 3, 6>(a, splits, s);
-      else e = run_wgrad<W_C1, 1, 3, 6>(a, splits, s);
-    }
-    if (e != hipSuccess) return e;
+  WgradArgs a = a0;  // all output-channel blocks in ONE launch (blockIdx.z)
+  a.zc = cb;
+  a.cout_total = a0.Cout;
+  a.co_base = 0;
+  if (mode == W_C3) {
+    if (cb == 96) return run_wgrad3<6, 2, 2>(a, splits, s);
+    if (cb == 48) return run_wgrad3<3, 1, 3>(a, splits, s);
+    return run_wgrad3<2, 1, 3>(a, splits, s);
   }
-  return hipSuccess;
+  // 1x1: the asynchronous k_wgrad1 tiled over (input-channel block of 96, output-channel block)
+  const dim3 grid(splits, (a.Cin + 95) / 96, (a.Cout + cb - 1) / cb);
+  if (cb == 96) hipLaunchKernelGGL((k_wgrad1<6, 6, 2, 2>), grid, dim3(256), 0, s, a, 0);
+  else hipLaunchKernelGGL((k_wgrad1<3, 6, 1, 3>), grid, dim3(192), 0, s, a, 0);
+  return hipGetLastError();
 }
 
 // ---- k_wgrad1 routing --------------------------------------------------------------

@@ -91,6 +91,7 @@ struct WgradArgs {
   int bias;                             // also produce the bias gradient
   const float* zeros;                   // >= 16 zero bytes (LDS-DMA source for padding)
   int co_base, cout_total;              // this launch's first output channel / the layer's Cout
+  int zc;                               // > 0: blockIdx.z = output-channel block of zc channels
 };
 
 // strided NHWC view: element (pixel, c) at p[pixel * stride + off + c]

@@ -17,6 +17,8 @@
 //     f = leaky(fuse(cc_k)), then ResBlock(RDB(f))      UpBlock, arch_unet.py:454-472
 //   y = sigmoid(final([x_up3 | x]))                      arch_unet.py:530-531
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -55,7 +57,9 @@ struct GGeom {
 bool ggeom(int ksize, int K, int nout, GGeom& g) {
   g.gather = ksize == 3 ? G_C3 : G_C1;
   const int nts[3] = {6, 3, 2};
-  const double eff[3] = {1.0, 1.3, 1.6};  // relative cost per output channel of the tile widths
+  // relative cost per output channel of the tile widths; with few reduction channels (K < 64:
+  // at most 16 four-channel chunks) the 96-wide tile's fixed per-tile cost dominates
+  const double eff[3] = {K < 64 ? 1.6 : 1.0, 1.3, 1.6};
   double best = 1e30;
   for (int i = 0; i < 3; ++i) {
     const int np = 16 * nts[i], nz = (nout + np - 1) / np;
@@ -340,6 +344,53 @@ bool iunet_build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, IPlan
 // ------------------------------------------------------------------------------------
 namespace {
 
+// Optional per-op timing (DN_PROFILE_OPS=1): HIP events around every conv / weight gradient /
+// GroupNorm call, aggregated by shape and printed to stderr at the end of each pass.
+struct OpProf {
+  struct Rec { std::string label; double flops; hipEvent_t a, b; };
+  bool on = getenv("DN_PROFILE_OPS") != nullptr;
+  std::vector<Rec> recs;
+  void flush(const char* pass) {
+    if (!on || recs.empty()) return;
+    hipEventSynchronize(recs.back().b);
+    struct Agg { double ms = 0, flops = 0; int n = 0; };
+    std::vector<std::pair<std::string, Agg>> agg;
+    double total = 0;
+    for (auto& r : recs) {
+      float ms = 0;
+      hipEventElapsedTime(&ms, r.a, r.b);
+      total += ms;
+      auto it = std::find_if(agg.begin(), agg.end(), [&](auto& x) { return x.first == r.label; });
+      if (it == agg.end()) { agg.push_back({r.label, Agg{}}); it = agg.end() - 1; }
+      it->second.ms += ms; it->second.flops += r.flops; it->second.n += 1;
+      hipEventDestroy(r.a); hipEventDestroy(r.b);
+    }
+    std::sort(agg.begin(), agg.end(), [](auto& x, auto& y) { return x.second.ms > y.second.ms; });
+    fprintf(stderr, "[dn ops] %s: %.3f ms in %zu ops\n", pass, total, recs.size());
+    for (auto& [l, a] : agg)
+      fprintf(stderr, "  %8.3f ms  %7.1f TF/s  x%-3d %s\n", a.ms,
+              a.flops > 0 ? a.flops / (a.ms * 1e-3) / 1e12 : 0.0, a.n, l.c_str());
+    recs.clear();
+  }
+};
+OpProf g_prof;
+
+struct OpScope {
+  hipStream_t s;
+  bool on;
+  OpScope(hipStream_t st, const char* kind, int cout, int cin, int k, int h, int w, int N,
+          double flop_mult) : s(st), on(g_prof.on) {
+    if (!on) return;
+    char b[128];
+    snprintf(b, sizeof(b), "%-6s %dx%d k%d @%dx%d", kind, cout, cin, k, h, w);
+    OpProf::Rec r{b, flop_mult * 2.0 * N * h * w * (double)cout * cin * k * k, nullptr, nullptr};
+    hipEventCreate(&r.a); hipEventCreate(&r.b);
+    hipEventRecord(r.a, s);
+    g_prof.recs.push_back(r);
+  }
+  ~OpScope() { if (on) hipEventRecord(g_prof.recs.back().b, s); }
+};
+
 struct Ctx {
   const IPlan& p;
   const float* prm;
@@ -354,6 +405,7 @@ const View kNone{nullptr, 0, 0};
 
 dn_status conv_fwd(const Ctx& c, const IConv& L, const View& in, int h, int w, int epi,
                    const View& out, int layout = OUT_NHWC, const View& aux = kNone) {
+  OpScope prof(c.s, "fwd", L.cout, L.cin, L.k, h, w, c.p.N, 1.0);
   float* pk = c.ws + c.p.pack;
   IU_TRY(gpack_fwd(c.Wt(L), L.k, L.cin, L.cout, pk, c.s));
   IU_TRY(grun(L.k, in, c.p.N, h, w, L.cin, pk, L.cout, c.Bs(L), epi, out, layout, aux, c.s));
@@ -362,6 +414,7 @@ dn_status conv_fwd(const Ctx& c, const IConv& L, const View& in, int h, int w, i
 
 dn_status gn_fwd(const Ctx& c, const IGN& g, const View& z, int h, int w, float* stats, int act,
                  const View* res, const View& out) {
+  OpScope prof(c.s, "gn", g.C, 1, 1, h, w, c.p.N, 0.0);
   const int N = c.p.N;
   const long P = (long)h * w;
   const int S = chan_sums_splits(N, P);
@@ -457,6 +510,7 @@ dn_status iunet_forward(const IPlan& p, const float* prm, const float* x, float*
   if (p.with_bwd)
     IU_TRY(hipMemcpyAsync(ws + p.yout, y, sizeof(float) * (size_t)N * P.OC * H * W,
                           hipMemcpyDeviceToDevice, s));
+  g_prof.flush("iunet forward");
   return DN_OK;
 }
 
@@ -468,6 +522,7 @@ namespace {
 // dW (+ db) of a conv from g = dL/d(conv output) and its input x; written into dprm
 dn_status wgrad_g(const Ctx& c, float* dprm, int mode, const IConv& L, const View& g, const View& x,
                   int h, int w) {
+  OpScope prof(c.s, "wgrad", L.cout, L.cin, L.k, h, w, c.p.N, 1.0);
   const int taps = mode == W_C3 ? 9 : 1;
   const bool bias = L.b >= 0;
   if (bias && L.b != L.w + (long)L.cout * L.cin * taps) {
@@ -496,6 +551,7 @@ dn_status wgrad_g(const Ctx& c, float* dprm, int mode, const IConv& L, const Vie
 // dx (first nout input channels) = conv^T(g) with epilogue epi (aux = mask / residual)
 dn_status dgrad_g(const Ctx& c, const IConv& L, const View& g, int h, int w, int nout, int epi,
                   const View& aux, const View& dx) {
+  OpScope prof(c.s, "dgrad", nout, L.cout, L.k, h, w, c.p.N, 1.0);
   float* pk = c.ws + c.p.pack;
   IU_TRY(gpack_dgrad(c.Wt(L), L.k, L.cin, L.cout, nout, pk, c.s));
   IU_TRY(grun(L.k, g, c.p.N, h, w, L.cout, pk, nout, nullptr, epi, dx, OUT_NHWC, aux, c.s));
@@ -504,6 +560,7 @@ dn_status dgrad_g(const Ctx& c, const IConv& L, const View& g, int h, int w, int
 
 dn_status gn_bwd(const Ctx& c, float* dprm, const IGN& g, const View& dy, const View& z, int h,
                  int w, const float* stats, const View& dz) {
+  OpScope prof(c.s, "gnbwd", g.C, 1, 1, h, w, c.p.N, 0.0);
   const int N = c.p.N;
   const long P = (long)h * w;
   const int S = chan_sums_splits(N, P);
@@ -651,6 +708,7 @@ dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, floa
     IU_TRY(launch_wgrad_c3_thin(ws + p.dh, 48, ws + p.xin, N, C, H, W, slab, n, C, 0, 1, st, s));
     IU_TRY(launch_reduce(slab, n, st, n, dprm + P.ne0.w, s));
   }
+  g_prof.flush("iunet backward");
   return DN_OK;
 }
 

@@ -138,24 +138,30 @@ __global__ __launch_bounds__(256) void k_gn_bwd_fin(const double* __restrict__ p
   }
 }
 
-// one thread per channel: dgamma[c] = sum_n (S2 - mean*S1)*rstd, dbeta[c] = sum_n S1
-__global__ __launch_bounds__(256) void k_gn_dparams(const double* __restrict__ part, int S, int N,
-                                                    int C, int G, const float* __restrict__ stats,
-                                                    float* __restrict__ dgamma,
-                                                    float* __restrict__ dbeta) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+// one 64-lane block per channel: dgamma[c] = sum_n (S2 - mean*S1)*rstd, dbeta[c] = sum_n S1;
+// lane l takes images l, l+64, ... (splits in order), then a fixed xor-tree over the wave
+__global__ __launch_bounds__(64) void k_gn_dparams(const double* __restrict__ part, int S, int N,
+                                                   int C, int G, const float* __restrict__ stats,
+                                                   float* __restrict__ dgamma,
+                                                   float* __restrict__ dbeta) {
+  const int c = blockIdx.x, l = threadIdx.x;
   const int g = c / (C / G);
   double dg = 0.0, dbt = 0.0;
-  for (int n = 0; n < N; ++n) {
+  for (int n = l; n < N; n += 64) {
     double s1, s2;
     split_sum(part, S, C, n, c, s1, s2);
     const double mean = stats[2 * (n * G + g)], rstd = stats[2 * (n * G + g) + 1];
     dg += (s2 - mean * s1) * rstd;
     dbt += s1;
   }
-  dgamma[c] = (float)dg;
-  dbeta[c] = (float)dbt;
+  for (int o = 32; o > 0; o >>= 1) {
+    dg += __shfl_xor(dg, o, 64);
+    dbt += __shfl_xor(dbt, o, 64);
+  }
+  if (l == 0) {
+    dgamma[c] = (float)dg;
+    dbeta[c] = (float)dbt;
+  }
 }
 
 // y = x*A + (x2 ? x2*B : 0) + Cc  (per (n, c) coefficients)  [+ LeakyReLU]  [+ res]
@@ -364,14 +370,30 @@ __global__ __launch_bounds__(256) void k_conv3_thin(const float* __restrict__ in
 #pragma unroll
   for (int o = 0; o < CO; ++o) acc[o] = 0.f;
   const float* inb = in + (long)n * H * W * is + io;
+  // quads must not straddle K: whole quads of real channels, or padding inside the row
+  const bool vec = ((is | io) & 3) == 0 && (K % 4 == 0 || io + ((K + 3) & ~3) <= is);
   for (int k0 = 0; k0 < K; k0 += TKC) {
     const int kc = K - k0 < TKC ? K - k0 : TKC;
-    for (int e = t; e < TKC * 324; e += 256) {
-      const int k = e / 324, r = e % 324;
-      const int gy = ty0 - 1 + r / 18, gx = tx0 - 1 + r % 18;
-      float v = 0.f;
-      if (k < kc && gy >= 0 && gy < H && gx >= 0 && gx < W) v = inb[((long)gy * W + gx) * is + k0 + k];
-      sx[e] = v;
+    if (vec) {  // float4 along channels: consecutive lanes read consecutive quads of a pixel
+      for (int e = t; e < 324 * (TKC / 4); e += 256) {
+        const int r = e / (TKC / 4), q = e % (TKC / 4);
+        const int gy = ty0 - 1 + r / 18, gx = tx0 - 1 + r % 18;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (4 * q < kc && gy >= 0 && gy < H && gx >= 0 && gx < W)
+          v = *reinterpret_cast<const float4*>(inb + ((long)gy * W + gx) * is + k0 + 4 * q);
+        sx[(4 * q) * 324 + r] = v.x;
+        sx[(4 * q + 1) * 324 + r] = v.y;
+        sx[(4 * q + 2) * 324 + r] = v.z;
+        sx[(4 * q + 3) * 324 + r] = v.w;
+      }
+    } else {
+      for (int e = t; e < TKC * 324; e += 256) {
+        const int k = e / 324, r = e % 324;
+        const int gy = ty0 - 1 + r / 18, gx = tx0 - 1 + r % 18;
+        float v = 0.f;
+        if (k < kc && gy >= 0 && gy < H && gx >= 0 && gx < W) v = inb[((long)gy * W + gx) * is + k0 + k];
+        sx[e] = v;
+      }
     }
     for (int e = t; e < CO * TKC * 9; e += 256) {
       const int o = e / (TKC * 9), k = (e / 9) % TKC, tp = e % 9;
@@ -442,8 +464,7 @@ hipError_t launch_gn_bwd_fin(const double* part, int S, int N, int C, int G, lon
                      gamma, stats, ca, cb, cc);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_gn_dparams, dim3((C + 255) / 256), dim3(256), 0, s, part, S, N, C, G, stats,
-                     dgamma, dbeta);
+  hipLaunchKernelGGL(k_gn_dparams, dim3(C), dim3(64), 0, s, part, S, N, C, G, stats, dgamma, dbeta);
   return hipGetLastError();
 }
 
