@@ -169,9 +169,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DN_DIST_BACKEND=gloo rehearses the multi-process path with every rank on the visible GPUs
+    # (round-robin), e.g. 2 ranks on a 1-GPU box; the real runs use RCCL ("nccl"), one GPU each
+    backend = os.environ.get("DN_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
 
     from image_denoising_amd import N2NTrainer, StructureTrainer, UNet
