@@ -148,6 +148,40 @@ def cpu_baseline(seconds_budget=20.0):
                       f"{H}x{H}x1, nf=48, Adam; median of {len(times)} steps after 1 warm-up"}
 
 
+def eval_image(seed=11, size=512):
+    """one synthetic uint8 image pair for the eval-PSNR leg: smooth clean field, gauss25 noise
+    (train.py:84-94 on the [0,255] scale), both clipped to uint8 (evaluation.py reads PNGs)"""
+    import numpy as np
+
+    clean = synthetic_clean(1, size, size, seed, "cpu")[0, 0].numpy()
+    g = torch.Generator().manual_seed(seed + 1)
+    noise = torch.randn(size, size, generator=g).numpy()
+    clean8 = np.clip(clean * 255.0 + 0.5, 0, 255).astype(np.uint8)
+    noisy8 = np.clip(clean8.astype(np.float32) + 25.0 * noise + 0.5, 0, 255).astype(np.uint8)
+    return clean8, noisy8
+
+
+def hip_eval(net, clean8, noisy8):
+    """evaluation.py:66-108 on the HIP path: denoise the full image, PSNR / SSIM on device"""
+    from image_denoising_amd.evaluation import evaluate
+
+    r = evaluate(net, [clean8], [noisy8], tiled=False)
+    return r["avg_psnr"], r["avg_ssim"]
+
+
+def oracle_eval_psnr(flat, clean8, noisy8, in_nc=1):
+    """the same image through the CPU oracle (torch-CPU restatement of the reference UNet and of
+    utils_eval.calculate_psnr) with the same trained weights"""
+    import numpy as np
+
+    from oracle import eval_ref, unet_ref
+
+    x = torch.from_numpy(noisy8.astype(np.float32) / 255.0)[None, None]
+    with torch.no_grad():
+        pred = unet_ref.forward(flat.detach().cpu(), x, in_nc, in_nc)[0, 0].numpy()
+    return float(eval_ref.psnr(eval_ref.quantize_full(pred), clean8))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -288,8 +322,21 @@ def main():
                          "avg_launch_ms": round(kms, 4), "flops_per_launch": kflops},
             "loss": loss_v,
         }
+        if args.mode == "n2n" and C == 1 and not iu:
+            # "eval PSNR vs ref" (BASELINE metric): the trained weights denoise one 512x512 image
+            # on the HIP path; the CPU leg runs the reference restatement on the same weights
+            clean8, noisy8 = eval_image()
+            ps, ss = hip_eval(net, clean8, noisy8)
+            rec["eval"] = {"psnr": round(ps, 4), "ssim": round(ss, 5),
+                           "image": "512x512 synthetic, gauss25, after the timed steps",
+                           "noisy_psnr": round(float(10 * __import__("math").log10(
+                               255.0 ** 2 / float(((noisy8.astype("f8") - clean8) ** 2).mean()))), 4)}
         if not args.no_cpu_baseline and world == 1 and args.mode == "n2n" and C == 1 and not iu:
             rec["cpu_baseline"] = cpu_baseline()
+            ref_ps = oracle_eval_psnr(net.flat_params, clean8, noisy8)
+            rec["cpu_baseline"]["eval_psnr"] = round(ref_ps, 4)
+            rec["eval"]["psnr_ref_cpu"] = round(ref_ps, 4)
+            rec["eval"]["psnr_abs_diff"] = round(abs(ps - ref_ps), 6)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
