@@ -24,6 +24,7 @@ sys.path.insert(0, ROOT)
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector, spec
 PEAK_HBM_GBS = 8000.0
+PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 
 
 def conv_flops(h, w, cin, cout, k):
@@ -104,6 +105,30 @@ def time_dominant_kernel(bs, H, W, device, reps=5):
     flops = bs * conv_flops(H, W, 96, 96, 3)
     del x, y
     return ms, flops
+
+
+def time_dominant_kernel_bf16(bs, H, W, device, reps=5):
+    """the same 96->96 3x3 shape through the bf16 matrix-core kernel (finetune --precision bf16)"""
+    from image_denoising_amd import _lib
+
+    x = torch.randn(bs, H, W, 96, device=device)
+    w = torch.randn(96, 96, 3, 3, device=device) * 0.05
+    b = torch.zeros(96, device=device)
+    y = torch.empty_like(x)
+    s = torch.cuda.current_stream(device)
+    pk = _lib.scratch(_lib.lib().dn_conv2d_bf16_pack_size(96, 96), device)
+    run = lambda: _lib.call("dn_conv2d_forward_bf16", x.data_ptr(), 96, bs, H, W, 96,
+                            w.data_ptr(), b.data_ptr(), 96, 1, y.data_ptr(), 96, pk.data_ptr(),
+                            pk.numel(), s.cuda_stream)
+    run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        run()
+    e1.record(s)
+    e1.synchronize()
+    del x, y
+    return e0.elapsed_time(e1) / reps, bs * conv_flops(H, W, 96, 96, 3)
 
 
 def pmc_traffic():
@@ -194,6 +219,8 @@ def main():
                     help="n2n: the N2N step (BASELINE metric); structure: train.py's "
                          "Structure_loss step (two grad forwards at full resolution); finetune: "
                          "finetune.py's adapter step (frozen UNet base + OutputAdapter, configs[4])")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+                    help="finetune only: bf16 = mixed-precision frozen base (BASELINE configs[4])")
     ap.add_argument("--arch", choices=["UNet", "UNetImproved"], default="UNet",
                     help="network (train.py:305-313 / finetune.py --arch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -237,6 +264,10 @@ def main():
         from image_denoising_amd.finetune import FinetuneTrainer
 
         model = DenoiserWithAdapter(net, in_channels=C, hidden_channels=16).to(device)
+        if args.precision == "bf16":
+            if iu:
+                raise SystemExit("--precision bf16 is built for the UNet base")
+            model.base.set_inference_precision("bf16")
         tr = FinetuneTrainer(model, lr=1e-4, lambda_grad=0.1)
         g = torch.Generator(device="cpu").manual_seed(7 + rank)
         noisy = (clean + (25.0 / 255.0) * torch.randn(clean.shape, generator=g).to(device)).contiguous()
@@ -276,8 +307,10 @@ def main():
     if rank == 0:
         ms_step = 1000.0 * elapsed / args.steps
         value = world * bs * args.steps / elapsed
-        kms, kflops = time_dominant_kernel(bs, H, H, device)
+        bf = ft and args.precision == "bf16"
+        kms, kflops = (time_dominant_kernel_bf16 if bf else time_dominant_kernel)(bs, H, H, device)
         achieved = kflops / (kms * 1e-3) / 1e12
+        peak = PEAK_BF16_TFLOPS if bf else PEAK_FP32_TFLOPS
         if args.mode == "n2n":  # fwd 256 + fwd/bwd 128
             step_flops = bs * (fwd_flops(H, H, C) + 3 * fwd_flops(H // 2, H // 2, C))
         elif ft:  # frozen base forward + adapter fwd (864 flop/px) and bwd (~1728 flop/px, C=1)
@@ -292,7 +325,8 @@ def main():
         elif ft:
             workload = (f"BASELINE configs[4]: finetune.py adapter step, frozen {model} "
                         f"base (no_grad) + OutputAdapter(hidden 16), {bs}x{C}x{H}x{H} per GPU, "
-                        f"L1 + 0.1*gradient_loss, Adam lr 1e-4, fp32")
+                        f"L1 + 0.1*gradient_loss, Adam lr 1e-4, "
+                        f"{'mixed-precision bf16 base' if args.precision == 'bf16' else 'fp32'}")
         elif args.mode == "structure":
             workload = (f"train.py Structure_loss step (train.py:355-368), UNet(n_feature=48), "
                         f"{bs}x{C}x{H}x{H} per GPU, Adam lr 3e-4")
@@ -310,14 +344,18 @@ def main():
                                        f"{', ImprovedUNet' if iu else ''})"),
             "value": round(value, 2), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16 (frozen base 3x3 convs; fp32 accumulate) + fp32 adapter" if bf else "fp32",
+            "data": "synthetic",
             "config": {"workload": workload,
                        "global_batch": bs * world, "patch": [H, H, C], "parallelism": f"dp{world}"},
             "step_tflops": round(step_flops / (ms_step * 1e-3) / 1e12, 2),
             "step_frac_of_fp32_peak": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
-            "roofline": {"bound": "mfma", "kernel": "k_fwd<G_C3,NT=6,MT=4> (dec_conv1b 96->96 3x3 @256^2)",
-                         "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+            "roofline": {"bound": "mfma",
+                         "kernel": ("k_fwd_bf16<NT=6,MT=4> (96->96 3x3, bf16 MFMA)" if bf else
+                                    "k_fwd<G_C3,NT=6,MT=4> (dec_conv1b 96->96 3x3 @256^2)"),
+                         "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": traffic,
                          "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                          "avg_launch_ms": round(kms, 4), "flops_per_launch": kflops},
             "loss": loss_v,

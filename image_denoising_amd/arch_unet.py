@@ -227,6 +227,22 @@ class UNet(nn.Module):
         _lib.call("dn_unet_forward", ctypes.byref(self._cfg), _lib.ptr(self._flat), _lib.ptr(x),
                   _lib.ptr(y), N, H, W, ws.data_ptr(), ws.numel(), _lib.stream_of(x))
 
+    def set_inference_precision(self, dtype: str) -> "UNet":
+        """'fp32' (default, the parity path) or 'bf16': no-grad forwards then multiply
+        bf16-rounded operands on the bf16 matrix cores (fp32 accumulation and storage) —
+        the mixed-precision frozen base of BASELINE configs[4].  Training is always fp32."""
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError("inference precision must be 'fp32' or 'bf16'")
+        self.inference_precision = dtype
+        return self
+
+    def _run_forward_inference(self, x, y, ws):
+        if getattr(self, "inference_precision", "fp32") != "bf16":
+            return self._run_forward(x, y, ws)
+        N, _, H, W = x.shape
+        _lib.call("dn_unet_forward_bf16", ctypes.byref(self._cfg), _lib.ptr(self._flat),
+                  _lib.ptr(x), _lib.ptr(y), N, H, W, ws.data_ptr(), ws.numel(), _lib.stream_of(x))
+
     def _run_backward(self, dy, dflat, ws, N, H, W):
         _lib.call("dn_unet_backward", ctypes.byref(self._cfg), _lib.ptr(self._flat), _lib.ptr(dy),
                   _lib.ptr(dflat), N, H, W, ws.data_ptr(), ws.numel(), _lib.stream_of(dy))
@@ -243,5 +259,5 @@ class UNet(nn.Module):
                 raise NotImplementedError("gradient w.r.t. the network input is not computed")
             return _UNetFunction.apply(x, self, *[p for _, p in self._param_views()])
         y = torch.empty((N, self.out_nc, H, W), dtype=torch.float32, device=x.device)
-        self._run_forward(x, y, self._workspace(N, H, W, with_backward=False))
+        self._run_forward_inference(x, y, self._workspace(N, H, W, with_backward=False))
         return y

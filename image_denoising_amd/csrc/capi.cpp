@@ -99,6 +99,21 @@ dn_status dn_unet_forward(const dn_unet_cfg* cfg, const float* params, const flo
   DN_GUARD_END
 }
 
+dn_status dn_unet_forward_bf16(const dn_unet_cfg* cfg, const float* params, const float* x,
+                               float* y, int N, int H, int W, void* ws, size_t ws_bytes,
+                               void* stream) {
+  DN_GUARD_BEGIN
+  if (!cfg || !params || !x || !y || !ws) return fail(DN_ERR_ARG, "null argument");
+  Plan p;
+  std::string err;
+  if (!build_plan(*cfg, N, H, W, false, p, err)) return fail(DN_ERR_ARG, err);
+  if (ws_bytes < (size_t)p.total_floats * sizeof(float))
+    return fail(DN_ERR_WORKSPACE, "workspace smaller than dn_unet_workspace_size()");
+  p.with_bwd = false;  // inference only: nothing is saved for a backward
+  return unet_forward(p, params, x, y, static_cast<float*>(ws), (hipStream_t)stream, true);
+  DN_GUARD_END
+}
+
 dn_status dn_unet_backward(const dn_unet_cfg* cfg, const float* params, const float* dy,
                            float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
                            void* stream) {
@@ -348,6 +363,33 @@ dn_status dn_conv2d_forward(const float* x, int x_stride, int N, int H, int W, i
     e = conv_forward(View{const_cast<float*>(x), x_stride, 0}, N, H, W, Cin, wp, b, Cout, ksize,
                      act, View{y, y_stride, 0}, OUT_NHWC, s);
   return hip_status(e, "dn_conv2d_forward");
+}
+
+size_t dn_conv2d_bf16_pack_size(int Cin, int Cout) {
+  if (Cin < 1 || Cout < 1) return 0;
+  const long e = bf16_pack_elems(Cin, Cout);
+  return e < 0 ? 0 : 2 * (size_t)e;
+}
+
+dn_status dn_conv2d_forward_bf16(const float* x, int x_stride, int N, int H, int W, int Cin,
+                                 const float* w, const float* b, int Cout, int act, float* y,
+                                 int y_stride, void* pack_ws, size_t pack_bytes, void* stream) {
+  if (!x || !w || !b || !y) return fail(DN_ERR_ARG, "null argument");
+  if (N < 1 || H < 1 || W < 1 || Cin < 1 || x_stride < Cin || y_stride < Cout || (Cout & 3) ||
+      (y_stride & 3))
+    return fail(DN_ERR_ARG, "bad shape (Cout and y_stride must be multiples of 4)");
+  if (dn_status st = need_pack(pack_ws, pack_bytes, dn_conv2d_bf16_pack_size(Cin, Cout))) return st;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = launch_pack_bf16(conv_fwd_view(w, Cin, 3), Cin, Cout, pack_ws, s);
+  if (e == hipSuccess) {
+    FwdArgs a{};
+    a.in = x; a.in_stride = x_stride; a.in_off = 0; a.IHt = H; a.IWt = W;
+    a.N = N; a.OH = H; a.OW = W; a.K = Cin; a.NOUT = Cout;
+    a.wp = static_cast<const float*>(pack_ws); a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
+    a.out = y; a.out_stride = y_stride; a.out_off = 0; a.out_layout = OUT_NHWC;
+    e = launch_fwd_bf16(a, s);
+  }
+  return hip_status(e, "dn_conv2d_forward_bf16");
 }
 
 dn_status dn_conv2d_backward_data(const float* dz, int N, int H, int W, int Cout, const float* w,

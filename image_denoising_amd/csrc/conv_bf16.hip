@@ -1,0 +1,255 @@
+// Mixed-precision 3x3 / 1x1 convolution forward on the gfx950 bf16 matrix cores
+// (v_mfma_f32_16x16x32_bf16): the frozen-base forward of the adapter finetune (BASELINE
+// configs[4], "mixed-precision bf16"; finetune.py:255-262 runs the base under no_grad).
+//
+// Activations stay fp32 NHWC in HBM; each input tile is rounded to bf16 (round-to-nearest-even)
+// as it is staged into LDS, weights are pre-packed in bf16, products accumulate in fp32 and the
+// epilogue (bias, LeakyReLU) and output are fp32 — the numerics of torch.autocast(bfloat16) for
+// a conv, except that the output is not rounded to bf16.
+//
+//   Workgroup = 4 waves, tile = 4*MT rows x 16 pixels x 16*NT output channels; wave w owns rows
+//   [w*MT, w*MT+MT).  K is staged 32 input channels at a time (one MFMA K): the x tile (with
+//   halo) once per chunk, the weights one kernel row (3 taps; 1x1: the single tap) per stage,
+//   double-buffered by global_load_lds.  Per stage a wave issues 3*MT*NT MFMAs of 16x16x32.
+//   LDS rows are 40 bf16 (80 B: 32 + 8 pad) per pixel / per (tap, output channel): a lane's
+//   8-element operand (k = 8*(lane>>4) .. +7) is one ds_read_b128.
+#include "dn_internal.h"
+
+namespace dn {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4b __attribute__((ext_vector_type(4)));
+
+template <int NT, int MT, bool K3 = true>
+struct BCfg {
+  static constexpr int HALO = K3 ? 2 : 0, TPS = K3 ? 3 : 1;  // taps per weight stage
+  static constexpr int SPC = K3 ? 3 : 1;                     // weight stages per K chunk
+  static constexpr int TW = 16, TH = 4 * MT, IH = TH + HALO, IW = TW + HALO;
+  static constexpr int KC = 32;                       // input channels per chunk
+  static constexpr int XS = 40;                       // bf16 per pixel row of the x tile
+  static constexpr int NP = 16 * NT;
+  static constexpr int WS = 40;                       // bf16 per (tap, n) row of a weight stage
+  static constexpr int WST = (TPS * NP * WS + 511) / 512 * 512;  // bf16 per stage, whole KiBs
+  static constexpr int LXB = (IH * IW * XS + 511) / 512 * 512;  // bf16 of the x tile
+  static constexpr int XQ = IH * IW * (KC / 4);       // float4 items of the x tile
+  static constexpr int XITEMS = (XQ + 255) / 256;
+  static constexpr int PS = NP + 4;                   // epilogue staging pixel stride (floats)
+  static constexpr int LST = 4 * 16 * PS;             // floats
+  static constexpr int LBYTES_MAIN = 2 * LXB + 2 * 2 * WST;
+  static constexpr int LBYTES = LBYTES_MAIN > 4 * LST ? LBYTES_MAIN : 4 * LST;
+};
+
+__device__ __forceinline__ void glds16b(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+template <int NT, int MT, bool K3>
+__global__ __launch_bounds__(256, 2) void k_fwd_bf16(FwdArgs a) {
+  using C = BCfg<NT, MT, K3>;
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
+  __bf16* lx = reinterpret_cast<__bf16*>(lds_raw);
+  __bf16* lw0 = lx + C::LXB;
+  __bf16* lw1 = lw0 + C::WST;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int tiles_x = (a.OW + C::TW - 1) / C::TW;
+  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
+  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
+  const int n = blockIdx.y;
+  const int iy0 = ty0 - (K3 ? 1 : 0), ix0 = tx0 - (K3 ? 1 : 0);
+  const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
+  const bool vec = ((a.in_stride | a.in_off) & 3) == 0;
+  const int nch = (a.K + C::KC - 1) / C::KC;
+  const int nst = C::SPC * nch;
+
+  f32x4b acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < NT; ++q) acc[m][q] = f32x4b{0.f, 0.f, 0.f, 0.f};
+
+  float4 xr[C::XITEMS];
+  auto load_x = [&](int k0) {
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * 256;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < C::XQ) {
+        const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+        const int iy = pix / C::IW, ix = pix - iy * C::IW;
+        const int gy = iy0 + iy, gx = ix0 + ix, k = k0 + 4 * q;
+        if (gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt && k < a.K) {
+          const float* p = inb + ((long)gy * a.IWt + gx) * a.in_stride + k;
+          if (vec && k + 4 <= a.K) {
+            v = *reinterpret_cast<const float4*>(p);
+          } else {
+            v.x = p[0];
+            if (k + 1 < a.K) v.y = p[1];
+            if (k + 2 < a.K) v.z = p[2];
+            if (k + 3 < a.K) v.w = p[3];
+          }
+        }
+      }
+      xr[it] = v;
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * 256;
+      if (e < C::XQ) {
+        const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        bf16x4 h;
+        h[0] = (__bf16)xr[it].x; h[1] = (__bf16)xr[it].y;
+        h[2] = (__bf16)xr[it].z; h[3] = (__bf16)xr[it].w;
+        *reinterpret_cast<bf16x4*>(lx + pix * C::XS + 4 * q) = h;
+      }
+    }
+  };
+  auto load_w = [&](int st, __bf16* dst) {  // stage st = chunk * 3 + ky, whole 1 KiB pieces
+    const __bf16* src = reinterpret_cast<const __bf16*>(a.wp) + (long)st * C::WST;
+    for (int p = wave; p < C::WST / 512; p += 4) glds16b(src + p * 512 + lane * 8, dst + p * 512);
+  };
+
+  load_w(0, lw0);
+  load_x(0);
+  store_x();
+  __syncthreads();
+
+  for (int st = 0; st < nst; ++st) {
+    const int c = st / C::SPC, ky = st - C::SPC * c;
+    const __bf16* lw = (st & 1) ? lw1 : lw0;
+    if (st + 1 < nst) load_w(st + 1, (st & 1) ? lw0 : lw1);
+    if (ky == 0 && c + 1 < nch) load_x((c + 1) * C::KC);
+#pragma unroll
+    for (int kx = 0; kx < C::TPS; ++kx) {
+      bf16x8 av[MT], bv[NT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int r = wave * MT + m;
+        av[m] = *reinterpret_cast<const bf16x8*>(lx + ((r + ky) * C::IW + li + kx) * C::XS + 8 * lg);
+      }
+#pragma unroll
+      for (int q = 0; q < NT; ++q)
+        bv[q] = *reinterpret_cast<const bf16x8*>(lw + (kx * C::NP + q * 16 + li) * C::WS + 8 * lg);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int q = 0; q < NT; ++q)
+          acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], bv[q], acc[m][q], 0, 0, 0);
+    }
+    __syncthreads();  // all waves done with this weight stage (and the x tile at ky == 2)
+    if (ky == C::SPC - 1 && c + 1 < nch) store_x();
+    __syncthreads();  // next stage's weights landed (vmcnt(0)), next x tile written
+  }
+
+  // epilogue: stage each 16-pixel row through LDS, write whole pixels as float4 (NHWC)
+  float* stg = reinterpret_cast<float*>(lds_raw) + wave * 16 * C::PS;
+  const int NQ = a.NOUT >> 2;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) stg[(4 * lg + r) * C::PS + q * 16 + li] = acc[m][q][r];
+    __syncthreads();
+    const int gy = ty0 + wave * MT + m;
+    if (gy < a.OH) {
+      for (int e = lane; e < 16 * NQ; e += 64) {
+        const int p = e / NQ, cc = 4 * (e - p * NQ);
+        const int gx = tx0 + p;
+        if (gx >= a.OW) continue;
+        float4 v = *reinterpret_cast<const float4*>(stg + p * C::PS + cc);
+        const float4 b = *reinterpret_cast<const float4*>(a.bias + cc);
+        v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+        if (a.epi == EPI_BIAS_ACT) {
+          v.x = v.x > 0.f ? v.x : v.x * 0.2f; v.y = v.y > 0.f ? v.y : v.y * 0.2f;
+          v.z = v.z > 0.f ? v.z : v.z * 0.2f; v.w = v.w > 0.f ? v.w : v.w * 0.2f;
+        }
+        const long pix = ((long)n * a.OH + gy) * a.OW + gx;
+        *reinterpret_cast<float4*>(a.out + pix * a.out_stride + a.out_off + cc) = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// bf16 weight image: [chunk][ky][kx][n][WS] (k = chunk*32 + kk for kk < 32; zero padded), each
+// (chunk, ky) stage rounded up to whole KiB
+__global__ __launch_bounds__(256) void k_pack_bf16(WView wv, int K, int NOUT, int NP, int WST,
+                                                   int k3, long total, __bf16* __restrict__ out) {
+  const int spc = k3 ? 3 : 1;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long st = e / WST;
+    const int r = (int)(e - st * WST);
+    const int c = (int)(st / spc), ky = (int)(st % spc);
+    float v = 0.f;
+    if (r < spc * NP * 40) {
+      const int kx = r / (NP * 40), nn = (r / 40) % NP, kk = r % 40;
+      const int k = c * 32 + kk;
+      if (kk < 32 && k < K && nn < NOUT) {
+        const int t = k3 ? ky * 3 + kx : 0;
+        const int tm = wv.flip ? wv.taps - 1 - t : t;
+        v = wv.w[wv.off + (long)k * wv.sK + (long)nn * wv.sN + (long)tm * wv.sT];
+      }
+    }
+    out[e] = (__bf16)v;
+  }
+}
+
+template <int NT, int MT, bool K3>
+static hipError_t run_bf16(const FwdArgs& a, hipStream_t s) {
+  using C = BCfg<NT, MT, K3>;
+  const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
+  hipLaunchKernelGGL((k_fwd_bf16<NT, MT, K3>), dim3(tx * ty, a.N, 1), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+static int bf16_nt(int nout) { return nout <= 48 ? 3 : (nout <= 96 ? 6 : 0); }
+
+static long bf16_stage(int nt, int ksize) {
+  if (ksize == 3) return nt == 3 ? BCfg<3, 4, true>::WST : BCfg<6, 4, true>::WST;
+  return nt == 3 ? BCfg<3, 4, false>::WST : BCfg<6, 4, false>::WST;
+}
+
+// bf16 elements of the packed image of a 3x3 (ksize 3) or 1x1 layer (K inputs, nout <= 96)
+long bf16_pack_elems(int K, int nout, int ksize) {
+  const int nt = bf16_nt(nout);
+  if (nt == 0 || (ksize != 1 && ksize != 3)) return -1;
+  return (long)((K + 31) / 32) * (ksize == 3 ? 3 : 1) * bf16_stage(nt, ksize);
+}
+
+hipError_t launch_pack_bf16(const WView& wv, int K, int nout, void* out, hipStream_t s, int ksize) {
+  const int nt = bf16_nt(nout);
+  if (nt == 0) return hipErrorInvalidValue;
+  const long total = bf16_pack_elems(K, nout, ksize);
+  if (total < 0) return hipErrorInvalidValue;
+  long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_pack_bf16, dim3((unsigned)blocks), dim3(256), 0, s, wv, K, nout, 16 * nt,
+                     (int)bf16_stage(nt, ksize), ksize == 3 ? 1 : 0, total,
+                     static_cast<__bf16*>(out));
+  return hipGetLastError();
+}
+
+// a.wp = the launch_pack_bf16 image; epilogue EPI_BIAS / EPI_BIAS_ACT; NHWC fp32 output with
+// float4-aligned views and NOUT % 4 == 0
+hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize) {
+  const int nt = bf16_nt(a.NOUT);
+  if (nt == 0 || (a.NOUT & 3) || ((a.out_stride | a.out_off) & 3) || a.out_layout != OUT_NHWC ||
+      (a.epi != EPI_BIAS && a.epi != EPI_BIAS_ACT) || !a.bias || (ksize != 1 && ksize != 3))
+    return hipErrorInvalidValue;
+  const long tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16);
+  const bool small = tiles < 1024;
+  if (ksize == 1) {
+    if (nt == 3) return small ? run_bf16<3, 1, false>(a, s) : run_bf16<3, 4, false>(a, s);
+    return small ? run_bf16<6, 1, false>(a, s) : run_bf16<6, 4, false>(a, s);
+  }
+  if (nt == 3) return small ? run_bf16<3, 1, true>(a, s) : run_bf16<3, 4, true>(a, s);
+  return small ? run_bf16<6, 1, true>(a, s) : run_bf16<6, 4, true>(a, s);
+}
+
+}  // namespace dn

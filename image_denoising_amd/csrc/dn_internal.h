@@ -186,6 +186,12 @@ hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, 
                        float b2, float w2, float step_size, float bc2s, float eps, float gscale,
                        hipStream_t s);
 
+// ---- mixed-precision (bf16 MFMA) 3x3 forward (conv_bf16.hip) ----
+long bf16_pack_elems(int K, int nout, int ksize = 3);
+hipError_t launch_pack_bf16(const WView& wv, int K, int nout, void* out, hipStream_t s,
+                            int ksize = 3);
+hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize = 3);
+
 // ---- adapter finetune (adapter.hip) ----
 long adapter_param_count(int C);
 int adapter_bwd_blocks(int N, int H, int W);

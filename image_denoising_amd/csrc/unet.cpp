@@ -126,6 +126,17 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
     p.packF[i] = alloc_f(n);
   }
   p.packH = alloc_f(2 * HEAD_LW);
+  for (int i = 0; i < NL; ++i) {  // bf16 images (2 bytes each) of the 3x3 layers
+    const Layer& L = p.P.L[i];
+    p.packBF[i] = -1;
+    if (i == ENC0 || L.deconv || i == NINC) continue;  // 3x3 layers + nin_a / nin_b
+    const long e = bf16_pack_elems(L.cin, L.cout, L.k);
+    if (e < 0) {
+      err = std::string("no bf16 forward tile for layer ") + kNames[i];
+      return false;
+    }
+    p.packBF[i] = alloc_f((e + 1) / 2);
+  }
   p.fwd_floats = off;
   if (bwd) {
     p.g_nb = alloc(0, 96);
@@ -329,18 +340,36 @@ hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, 
 // forward: arch_unet.py:194-260 (non-blind-spot branch)
 // ------------------------------------------------------------------------------------
 dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
-                       hipStream_t s) {
+                       hipStream_t s, bool bf16) {
   const int N = p.N, nf = p.nf, C = p.C;
   auto H = [&](int l) { return p.H >> l; };
   auto Wd = [&](int l) { return p.W >> l; };
   auto Wt = [&](int i) { return ws + p.packF[i]; };  // packed forward weights
   auto Bs = [&](int i) { return prm + p.P.L[i].woff + p.P.L[i].wcount; };
   auto V = [&](long off, int stride, int coff = 0) { return View{ws + off, stride, coff}; };
+  // every 3x3 layer (enc_conv1..dec_conv1b): the fp32 kernel, or the bf16 one (bf16 operands,
+  // fp32 accumulation / bias / activation / storage)
+  auto conv_forward = [&](const View& in, int Nn, int h, int w, int K, const float* wp,
+                          const float* b, int cout, int ksize, int act, const View& out,
+                          int layout, hipStream_t st) -> hipError_t {
+    int i = ENC1;
+    while (i < NL && Wt(i) != wp) ++i;
+    if (!bf16 || i == NL || p.packBF[i] < 0)
+      return dn::conv_forward(in, Nn, h, w, K, wp, b, cout, ksize, act, out, layout, st);
+    FwdArgs a{};
+    a.in = in.p; a.in_stride = in.stride; a.in_off = in.off; a.IHt = h; a.IWt = w;
+    a.N = Nn; a.OH = h; a.OW = w; a.K = K; a.NOUT = cout;
+    a.wp = ws + p.packBF[i]; a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
+    a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = layout;
+    return launch_fwd_bf16(a, st, ksize);
+  };
 
   for (int i = ENC1; i < NINA; ++i) {  // pack the weights into the kernels' per-chunk LDS images
     const Layer& L = p.P.L[i];
     const float* w = prm + L.woff;
     if (L.deconv) DN_TRY(pack_deconv_fwd(w, L.cin, L.cout, ws + p.packF[i], s));
+    else if (bf16) DN_TRY(launch_pack_bf16(conv_fwd_view(w, L.cin, 3), L.cin, L.cout,
+                                           ws + p.packBF[i], s));
     else DN_TRY(pack_conv_fwd(w, L.cin, L.cout, L.k, ws + p.packF[i], s));
   }
   // enc_conv0, fused with pool0 = x -> channels [2nf, 2nf+C) of the up1 concat buffer
@@ -388,6 +417,21 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
                         V(p.c1, p.c1s, 0), s));
   DN_TRY(conv_forward(V(p.c1, p.c1s), N, H(0), Wd(0), p.c1k, Wt(D1A), Bs(D1A), 96, 3, 1,
                       V(p.d1a, 96), OUT_NHWC, s));
+  if (bf16) {  // dec_conv1b, nin_a, nin_b on the bf16 kernel, then nin_c (96 -> out_nc, fp32)
+    DN_TRY(conv_forward(V(p.d1a, 96), N, H(0), Wd(0), 96, Wt(D1B), Bs(D1B), 96, 3, 1,
+                        V(p.d1b, 96), OUT_NHWC, s));
+    for (int i = NINA; i <= NINB; ++i)
+      DN_TRY(launch_pack_bf16(conv_fwd_view(prm + p.P.L[i].woff, 96, 1), 96, 96,
+                              ws + p.packBF[i], s, 1));
+    DN_TRY(pack_conv_fwd(prm + p.P.L[NINC].woff, 96, p.OC, 1, ws + p.packF[NINC], s));
+    DN_TRY(conv_forward(V(p.d1b, 96), N, H(0), Wd(0), 96, Wt(NINA), Bs(NINA), 96, 1, 1,
+                        V(p.na, 96), OUT_NHWC, s));
+    DN_TRY(conv_forward(V(p.na, 96), N, H(0), Wd(0), 96, Wt(NINB), Bs(NINB), 96, 1, 1,
+                        V(p.nb, 96), OUT_NHWC, s));
+    DN_TRY(dn::conv_forward(V(p.nb, 96), N, H(0), Wd(0), 96, Wt(NINC), Bs(NINC), p.OC, 1, 0,
+                            View{y, p.OC, 0}, OUT_NCHW, s));
+    return DN_OK;
+  }
   // dec_conv1b + nin_a + nin_b + nin_c in one kernel (arch_unet.py:251-257); the
   // intermediate activations are written only when a backward will read them
   DN_TRY(launch_pack_head(conv_fwd_view(prm + p.P.L[NINA].woff, 96, 1),

@@ -40,6 +40,7 @@ struct Plan {
   long d1a, d1b, na, nb;
   long packF[NL];               // packed forward weight images
   long packH;                   // fused head: nin_a | nin_b images (2 x HEAD_LW)
+  long packBF[NL];              // bf16 images of the 3x3 layers (mixed-precision forward)
   long fwd_floats;
   // gradients
   long g_nb, g_na, g_d1b, g_d1a, g_c1;
@@ -61,7 +62,7 @@ int dgrad_nout(const Plan& p, int i);
 bool build_params(const dn_unet_cfg& c, ParamLayout& P, std::string& err);
 bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, std::string& err);
 dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
-                       hipStream_t s);
+                       hipStream_t s, bool bf16 = false);
 dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* ws,
                         hipStream_t s);
 

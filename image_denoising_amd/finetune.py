@@ -161,7 +161,8 @@ class FinetuneTrainer:
         base = self.model.base
         if hasattr(base, "_run_forward"):  # HIP base: workspace reused across steps
             N, _, H, W = noisy.shape
-            base._run_forward(noisy, out, base._workspace(N, H, W, with_backward=False))
+            run = getattr(base, "_run_forward_inference", base._run_forward)  # bf16 if set
+            run(noisy, out, base._workspace(N, H, W, with_backward=False))
         else:
             with torch.no_grad():
                 out.copy_(base(noisy))

@@ -67,6 +67,13 @@ dn_status dn_unet_workspace_size(const dn_unet_cfg* cfg, int N, int H, int W, in
    when ws was sized with with_backward=1. */
 dn_status dn_unet_forward(const dn_unet_cfg* cfg, const float* params, const float* x, float* y,
                           int N, int H, int W, void* ws, size_t ws_bytes, void* stream);
+/* Mixed-precision inference forward (the frozen base of the adapter finetune, BASELINE
+   configs[4]): every 3x3 layer multiplies bf16-rounded activations and weights on the bf16
+   matrix cores with fp32 accumulation; bias, activations, 1x1 layers, deconvs and storage stay
+   fp32.  Same workspace as dn_unet_forward; saves nothing for a backward. */
+dn_status dn_unet_forward_bf16(const dn_unet_cfg* cfg, const float* params, const float* x,
+                               float* y, int N, int H, int W, void* ws, size_t ws_bytes,
+                               void* stream);
 /* dparams = dL/dparams given dy = dL/dy, for the activations saved by the last
    dn_unet_forward on the same ws (same N,H,W).  dparams is overwritten (not accumulated). */
 dn_status dn_unet_backward(const dn_unet_cfg* cfg, const float* params, const float* dy,
@@ -146,6 +153,12 @@ size_t dn_deconv2x2_pack_size(int Cin, int Cout, int backward_data);
 dn_status dn_conv2d_forward(const float* x, int x_stride, int N, int H, int W, int Cin,
                             const float* w, const float* b, int Cout, int ksize, int act, float* y,
                             int y_stride, void* pack_ws, size_t pack_bytes, void* stream);
+/* 3x3/pad1 forward on the bf16 matrix cores (bf16-rounded x and w, fp32 accumulate, fp32 bias /
+   LeakyReLU / output); Cout <= 96 and a multiple of 4.  Used by dn_unet_forward_bf16. */
+size_t dn_conv2d_bf16_pack_size(int Cin, int Cout);
+dn_status dn_conv2d_forward_bf16(const float* x, int x_stride, int N, int H, int W, int Cin,
+                                 const float* w, const float* b, int Cout, int act, float* y,
+                                 int y_stride, void* pack_ws, size_t pack_bytes, void* stream);
 /* dx = conv^T(dz) [* leaky'(mask)] : data gradient (mask nullable; mask_stride). If accumulate,
    dx += result.  dx stride dx_stride. */
 dn_status dn_conv2d_backward_data(const float* dz, int N, int H, int W, int Cout, const float* w,
