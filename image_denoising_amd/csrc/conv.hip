@@ -1089,6 +1089,35 @@ hipError_t launch_pack(int gather, const WView& wv, int K, int nout, int nz, flo
   return hipGetLastError();
 }
 
+// Tile height for a G_C3 launch: 16/8/4 rows (MT = 4/2/1) -- the fewest rounds of resident
+// workgroups, each round weighed by its length (occupancy x tile height x per-tile efficiency
+// of the shorter tiles).  E.g. a 1024-tile grid of the 96-channel kernel (3 resident per CU =
+// 768 slots) runs 2 rounds of which the second is a third full at 16 rows, but 2048 tiles of
+// 8 rows fill 2 rounds of 1024 slots.  Occupancy per
+// variant: the compiler's waves/SIMD (one wave of each workgroup per SIMD).
+static int c3_occupancy(int nt, int mt) {
+  if (nt == 6) return mt == 4 ? 3 : 4;
+  if (nt == 9) return 3;
+  if (nt == 3) return mt == 1 ? 5 : 4;
+  return mt == 1 ? 5 : 4;  // nt == 2
+}
+
+static int pick_mt(int nt, const FwdArgs& a, int nz, bool allow4) {
+  const int mts[3] = {4, 2, 1};
+  const double eff[3] = {1.0, 1.08, 1.25};
+  int mt = 1;
+  double best = 1e30;
+  for (int i = allow4 ? 0 : 1; i < 3; ++i) {
+    const long blocks = (long)a.N * ((a.OH + 4 * mts[i] - 1) / (4 * mts[i])) * ((a.OW + 15) / 16) * nz;
+    // a round keeps occ workgroups per CU busy: it lasts ~occ * MT tile-rows of MFMA work
+    const int occ = c3_occupancy(nt, mts[i]);
+    const long slots = 256L * occ;
+    const double cost = (double)((blocks + slots - 1) / slots) * occ * mts[i] * eff[i];
+    if (cost < best - 1e-9) { best = cost; mt = mts[i]; }
+  }
+  return mt;
+}
+
 hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s) {
   const int nt = (a.NOUT + 15) / 16;
   // small images: 4-row tiles so that the grid still fills the chip
@@ -1096,9 +1125,10 @@ hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s) {
                          (a.out_layout == OUT_UP2 ? 4 : 1);
   const bool small = big_tiles < 1024;
   if (gather == G_C3) {
-    if (nt == 3) return small ? run_fwd<G_C3, 3, 1>(a, s) : run_fwd<G_C3, 3, 4>(a, s);
-    if (nt == 6) return small ? run_fwd<G_C3, 6, 1>(a, s) : run_fwd<G_C3, 6, 4>(a, s);
-    if (nt == 9) return small ? run_fwd<G_C3, 9, 1>(a, s) : run_fwd<G_C3, 9, 2>(a, s);
+    const int mt = pick_mt(nt, a, 1, nt != 9);
+    if (nt == 3) return mt == 4 ? run_fwd<G_C3, 3, 4>(a, s) : mt == 2 ? run_fwd<G_C3, 3, 2>(a, s) : run_fwd<G_C3, 3, 1>(a, s);
+    if (nt == 6) return mt == 4 ? run_fwd<G_C3, 6, 4>(a, s) : mt == 2 ? run_fwd<G_C3, 6, 2>(a, s) : run_fwd<G_C3, 6, 1>(a, s);
+    if (nt == 9) return mt == 2 ? run_fwd<G_C3, 9, 2>(a, s) : run_fwd<G_C3, 9, 1>(a, s);
   } else if (gather == G_C1) {
     static const int c1_mt = getenv("DN_C1_MT") ? atoi(getenv("DN_C1_MT")) : 2;  // tuning probe
     if (nt == 1) return run_fwd<G_C1, 1, 4>(a, s);
@@ -1125,19 +1155,7 @@ hipError_t launch_fwd_nt(int gather, int nt, const FwdArgs& a, hipStream_t s) {
   const long big_tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16) * nz;
   const bool small = big_tiles < 1024;
   if (gather == G_C3) {
-    // tile height 16/8/4 rows (MT = 4/2/1): the fewest rounds of resident workgroups, weighed
-    // by the per-tile efficiency of the taller tiles (a 1024-tile grid on 768 slots would run
-    // two rounds at 4 rows but 2.7 at 8 rows / 5.3 at 4 rows with less waste per round)
-    const long slots = (nt == 6 ? 3L : 2L) * 256;
-    int mt = 1;
-    double best = 1e30;
-    const int mts[3] = {4, 2, 1};
-    const double eff[3] = {1.0, 1.08, 1.25};
-    for (int i = 0; i < 3; ++i) {
-      const long blocks = (long)a.N * ((a.OH + 4 * mts[i] - 1) / (4 * mts[i])) * ((a.OW + 15) / 16) * nz;
-      const double cost = (double)((blocks + slots - 1) / slots) * mts[i] * eff[i];
-      if (cost < best - 1e-9) { best = cost; mt = mts[i]; }
-    }
+    const int mt = pick_mt(nt, a, nz, true);
     if (nt == 2) return mt == 4 ? run_fwd<G_C3, 2, 4>(a, s) : mt == 2 ? run_fwd<G_C3, 2, 2>(a, s) : run_fwd<G_C3, 2, 1>(a, s);
     if (nt == 3) return mt == 4 ? run_fwd<G_C3, 3, 4>(a, s) : mt == 2 ? run_fwd<G_C3, 3, 2>(a, s) : run_fwd<G_C3, 3, 1>(a, s);
     if (nt == 6) return mt == 4 ? run_fwd<G_C3, 6, 4>(a, s) : mt == 2 ? run_fwd<G_C3, 6, 2>(a, s) : run_fwd<G_C3, 6, 1>(a, s);
