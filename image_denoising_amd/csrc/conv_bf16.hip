@@ -110,7 +110,9 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16(FwdArgs a) {
     }
   };
   auto load_w = [&](int st, __bf16* dst) {  // stage st = chunk * 3 + ky, whole 1 KiB pieces
-    const __bf16* src = reinterpret_cast<const __bf16*>(a.wp) + (long)st * C::WST;
+    // (deconv: blockIdx.z = output parity (a,b), one image of wp_z bf16 elements each)
+    const __bf16* src = reinterpret_cast<const __bf16*>(a.wp) + (long)blockIdx.z * a.wp_z +
+                        (long)st * C::WST;
     for (int p = wave; p < C::WST / 512; p += 4) glds16b(src + p * 512 + lane * 8, dst + p * 512);
   };
 
@@ -169,8 +171,15 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16(FwdArgs a) {
           v.x = v.x > 0.f ? v.x : v.x * 0.2f; v.y = v.y > 0.f ? v.y : v.y * 0.2f;
           v.z = v.z > 0.f ? v.z : v.z * 0.2f; v.w = v.w > 0.f ? v.w : v.w * 0.2f;
         }
-        const long pix = ((long)n * a.OH + gy) * a.OW + gx;
-        *reinterpret_cast<float4*>(a.out + pix * a.out_stride + a.out_off + cc) = v;
+        long oi;
+        if (a.out_layout == OUT_UP2) {  // ConvTranspose2d(2,2) scatter: pixel (2y+a, 2x+b)
+          const int ab = (int)blockIdx.z;
+          oi = (((long)n * 2 * a.OH + 2 * gy + (ab >> 1)) * 2 * a.OW + 2 * gx + (ab & 1)) *
+                   a.out_stride + a.out_off + cc;
+        } else {
+          oi = (((long)n * a.OH + gy) * a.OW + gx) * a.out_stride + a.out_off + cc;
+        }
+        *reinterpret_cast<float4*>(a.out + oi) = v;
       }
     }
     __syncthreads();
@@ -204,7 +213,8 @@ template <int NT, int MT, bool K3>
 static hipError_t run_bf16(const FwdArgs& a, hipStream_t s) {
   using C = BCfg<NT, MT, K3>;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
-  hipLaunchKernelGGL((k_fwd_bf16<NT, MT, K3>), dim3(tx * ty, a.N, 1), dim3(256), 0, s, a);
+  const int nz = a.out_layout == OUT_UP2 ? 4 : 1;
+  hipLaunchKernelGGL((k_fwd_bf16<NT, MT, K3>), dim3(tx * ty, a.N, nz), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -235,14 +245,30 @@ hipError_t launch_pack_bf16(const WView& wv, int K, int nout, void* out, hipStre
   return hipGetLastError();
 }
 
+// ConvTranspose2d(cin, cout, 2, 2) weight [cin][cout][2][2] as four 1x1 images (one per output
+// parity ab), each bf16_pack_elems(cin, cout, 1) elements
+hipError_t launch_pack_bf16_deconv(const float* w, int cin, int cout, void* out, hipStream_t s) {
+  const long img = bf16_pack_elems(cin, cout, 1);
+  if (img < 0) return hipErrorInvalidValue;
+  for (int ab = 0; ab < 4; ++ab) {
+    WView v{};
+    v.w = w; v.off = ab; v.sK = (long)cout * 4; v.sN = 4; v.sT = 0; v.sZ = 0; v.taps = 1; v.flip = 0;
+    hipError_t e = launch_pack_bf16(v, cin, cout, static_cast<__bf16*>(out) + ab * img, s, 1);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 // a.wp = the launch_pack_bf16 image; epilogue EPI_BIAS / EPI_BIAS_ACT; NHWC fp32 output with
 // float4-aligned views and NOUT % 4 == 0
 hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize) {
   const int nt = bf16_nt(a.NOUT);
-  if (nt == 0 || (a.NOUT & 3) || ((a.out_stride | a.out_off) & 3) || a.out_layout != OUT_NHWC ||
+  if (nt == 0 || (a.NOUT & 3) || ((a.out_stride | a.out_off) & 3) ||
+      (a.out_layout != OUT_NHWC && !(a.out_layout == OUT_UP2 && ksize == 1)) ||
       (a.epi != EPI_BIAS && a.epi != EPI_BIAS_ACT) || !a.bias || (ksize != 1 && ksize != 3))
     return hipErrorInvalidValue;
-  const long tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16);
+  const long tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16) *
+                     (a.out_layout == OUT_UP2 ? 4 : 1);
   const bool small = tiles < 1024;
   if (ksize == 1) {
     if (nt == 3) return small ? run_bf16<3, 1, false>(a, s) : run_bf16<3, 4, false>(a, s);

@@ -191,6 +191,7 @@ long bf16_pack_elems(int K, int nout, int ksize = 3);
 hipError_t launch_pack_bf16(const WView& wv, int K, int nout, void* out, hipStream_t s,
                             int ksize = 3);
 hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize = 3);
+hipError_t launch_pack_bf16_deconv(const float* w, int cin, int cout, void* out, hipStream_t s);
 
 // ---- adapter finetune (adapter.hip) ----
 long adapter_param_count(int C);

@@ -129,8 +129,8 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
   for (int i = 0; i < NL; ++i) {  // bf16 images (2 bytes each) of the 3x3 layers
     const Layer& L = p.P.L[i];
     p.packBF[i] = -1;
-    if (i == ENC0 || L.deconv || i == NINC) continue;  // 3x3 layers + nin_a / nin_b
-    const long e = bf16_pack_elems(L.cin, L.cout, L.k);
+    if (i == ENC0 || i == NINC) continue;  // 3x3 layers, deconvs, nin_a / nin_b
+    const long e = L.deconv ? 4 * bf16_pack_elems(L.cin, L.cout, 1) : bf16_pack_elems(L.cin, L.cout, L.k);
     if (e < 0) {
       err = std::string("no bf16 forward tile for layer ") + kNames[i];
       return false;
@@ -364,10 +364,27 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     return launch_fwd_bf16(a, st, ksize);
   };
 
+  // ConvTranspose2d(2,2): fp32 kernel, or the bf16 1x1 kernel per output parity
+  auto deconv_forward = [&](const View& xin, int Nn, int h, int w, int cin, const float* wp,
+                            const float* b, int cout, const View& out, hipStream_t st) -> hipError_t {
+    int i = ENC1;
+    while (i < NL && Wt(i) != wp) ++i;
+    if (!bf16 || i == NL || p.packBF[i] < 0)
+      return dn::deconv_forward(xin, Nn, h, w, cin, wp, b, cout, out, st);
+    FwdArgs a{};
+    a.in = xin.p; a.in_stride = xin.stride; a.in_off = xin.off; a.IHt = h; a.IWt = w;
+    a.N = Nn; a.OH = h; a.OW = w; a.K = cin; a.NOUT = cout;
+    a.wp = ws + p.packBF[i]; a.wp_z = bf16_pack_elems(cin, cout, 1);
+    a.bias = b; a.epi = EPI_BIAS;
+    a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = OUT_UP2;
+    return launch_fwd_bf16(a, st, 1);
+  };
+
   for (int i = ENC1; i < NINA; ++i) {  // pack the weights into the kernels' per-chunk LDS images
     const Layer& L = p.P.L[i];
     const float* w = prm + L.woff;
-    if (L.deconv) DN_TRY(pack_deconv_fwd(w, L.cin, L.cout, ws + p.packF[i], s));
+    if (L.deconv && bf16) DN_TRY(launch_pack_bf16_deconv(w, L.cin, L.cout, ws + p.packBF[i], s));
+    else if (L.deconv) DN_TRY(pack_deconv_fwd(w, L.cin, L.cout, ws + p.packF[i], s));
     else if (bf16) DN_TRY(launch_pack_bf16(conv_fwd_view(w, L.cin, 3), L.cin, L.cout,
                                            ws + p.packBF[i], s));
     else DN_TRY(pack_conv_fwd(w, L.cin, L.cout, L.k, ws + p.packF[i], s));

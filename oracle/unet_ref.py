@@ -81,8 +81,8 @@ def forward(flat: torch.Tensor, x: torch.Tensor, in_nc: int, out_nc: int, nf: in
     """arch_unet.py:194-260 with the same op order (conv -> LeakyReLU(0.2) -> pool ...).
     `record` (optional) receives the intermediate tensors under the workspace names
     (c1 a0 a1 c2..c5 a2..a5 p5 a6 d2a..d5b d1a d1b na nb) with retain_grad() set.
-    `bf16_3x3` rounds the operands of the 3x3 layers (not enc_conv0) and of nin_a / nin_b to
-    bf16 (the mixed-precision inference path).
+    `bf16_3x3` rounds the operands of the 3x3 layers (not enc_conv0), the deconvs and nin_a /
+    nin_b to bf16 (the mixed-precision inference path).
     `masks` (optional) maps the post-activation names to tensors (e.g. the device's fp32
     activations) that decide LeakyReLU slopes and max-pool routing in the backward, so a
     high-precision backward can be compared with a low-precision one without the slope flips
@@ -90,14 +90,17 @@ def forward(flat: torch.Tensor, x: torch.Tensor, in_nc: int, out_nc: int, nf: in
     P = unflatten(flat, in_nc, out_nc, nf)
 
     def conv(t, n, pad=1):
-        # bf16_3x3 emulates dn_unet_forward_bf16: the 3x3 layers after enc_conv0 and nin_a /
-        # nin_b multiply bf16-rounded activations and weights (exact products), accumulated in
-        # t's precision (the deconvs go through conv_transpose2d, unrounded)
+        # bf16_3x3 emulates dn_unet_forward_bf16: the 3x3 layers after enc_conv0, nin_a / nin_b
+        # and the deconvs multiply bf16-rounded activations and weights (exact products),
+        # accumulated in t's precision
         w = P[n][0]
         if bf16_3x3 and n not in ("enc_conv0", "nin_c"):
             return F.conv2d(_bf16(t), _bf16(w), P[n][1], 1, pad)
         return F.conv2d(t, w, P[n][1], 1, pad)
-    up = lambda t, skip, n: torch.cat([F.conv_transpose2d(t, P[n][0], P[n][1], 2), skip], 1)
+    def up(t, skip, n):
+        w = _bf16(P[n][0]) if bf16_3x3 else P[n][0]
+        t = _bf16(t) if bf16_3x3 else t
+        return torch.cat([F.conv_transpose2d(t, w, P[n][1], 2), skip], 1)
 
     def act(t, name):
         if masks is not None:
