@@ -733,7 +733,7 @@ struct Wg3Cfg {
   static_assert(LGF % 256 == 0, "G stage must be whole 1 KiB pieces");
 };
 
-template <int CO_FR, int WM, int WN>
+template <int CO_FR, int WM, int WN, int SWL = 5>
 __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad3(WgradArgs a0) {
   using C = Wg3Cfg<CO_FR, WM, WN>;
   const WgradArgs a = wg_block(a0);
@@ -742,8 +742,11 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad3(WgradArgs a0) {
   const int wm = wave / WN, wn = wave % WN;
   const int li = lane & 15, lgp = lane >> 4;
   const int ci0 = blockIdx.y * C::CIB;
-  const int ux = (a.KW + C::PC - 1) / C::PC;
-  const long U = (long)a.N * a.KH * ux;
+  // K stage = 32 pixels: one row segment of 32, or (images narrower than 32 with KW a power of
+  // two) a block of 32/KW whole rows, so narrow deep levels do not run 3/4 empty stages
+  constexpr int swl = SWL, sw = 1 << SWL, sh = C::PC >> SWL, xw = sw + 2;
+  const int ux = (a.KW + sw - 1) / sw, uy = (a.KH + sh - 1) / sh;
+  const long U = (long)a.N * uy * ux;
   const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
   const bool do_bias = a.bias && blockIdx.y == 0 && wn == 0;
 
@@ -757,26 +760,26 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad3(WgradArgs a0) {
   }
 
   auto issue = [&](long u, float* buf) {
-    const int n = (int)(u / ((long)a.KH * ux));
-    const int rem = (int)(u - (long)n * a.KH * ux);
-    const int py = rem / ux, px0 = (rem % ux) * C::PC;
+    const int n = (int)(u / ((long)uy * ux));
+    const int rem = (int)(u - (long)n * uy * ux);
+    const int py0 = (rem / ux) * sh, px0 = (rem % ux) * sw;
     const float* gb = a.g + (long)n * a.KH * a.KW * a.g_stride + a.g_off;
     for (int p = wave; p < C::LGP; p += C::NW) {
       const int idx = p * 256 + lane * 4;
       const int px = idx / C::COUT, co = idx - px * C::COUT;
-      const int gx = px0 + px;
-      const float* src = (gx < a.KW && co < a.Cout)
-                             ? gb + ((long)py * a.KW + gx) * a.g_stride + co : a.zeros;
+      const int gy = py0 + (px >> swl), gx = px0 + (px & (sw - 1));
+      const float* src = (gy < a.KH && gx < a.KW && co < a.Cout)
+                             ? gb + ((long)gy * a.KW + gx) * a.g_stride + co : a.zeros;
       glds16(src, buf + p * 256);
     }
     const float* xb = a.x + (long)n * a.KH * a.KW * a.x_stride + a.x_off;
+    const int xpix = (sh + 2) * xw;
     for (int p = wave; p < C::LXP; p += C::NW) {
       const int idx = p * 256 + lane * 4;
       const int px = idx / C::CIB, q = idx - px * C::CIB;
-      const int yy = px / C::XW, xx = px - yy * C::XW;
-      const int gy = py - 1 + yy, gx = px0 - 1 + xx, ci = ci0 + q;
-      const bool ok = px < C::XH * C::XW && gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW &&
-                      ci < a.Cin;
+      const int yy = px / xw, xx = px - yy * xw;
+      const int gy = py0 - 1 + yy, gx = px0 - 1 + xx, ci = ci0 + q;
+      const bool ok = px < xpix && gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW && ci < a.Cin;
       const float* src = ok ? xb + ((long)gy * a.KW + gx) * a.x_stride + ci : a.zeros;
       glds16(src, buf + C::LGF + p * 256);
     }
@@ -792,13 +795,14 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad3(WgradArgs a0) {
 #pragma unroll 2
     for (int ks = 0; ks < C::PC / 4; ++ks) {
       const int pc = 4 * ks + lgp;  // this lane's pixel (k = lane>>4)
+      const int pr = pc >> swl, pcc = pc & (sw - 1);
       float av[C::MFW];
 #pragma unroll
       for (int i = 0; i < C::MFW; ++i)
         av[i] = lg_[pc * C::COUT + (wm * C::MFW + i) * 16 + li];
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const float bv = lx[((t / 3) * C::XW + pc + t % 3) * C::CIB + wn * 16 + li];
+        const float bv = lx[((pr + t / 3) * xw + pcc + t % 3) * C::CIB + wn * 16 + li];
 #pragma unroll
         for (int i = 0; i < C::MFW; ++i) acc[i][t] = mfma4(av[i], bv, acc[i][t]);
       }
@@ -1181,7 +1185,11 @@ static hipError_t run_wgrad3(const WgradArgs& a, int splits, hipStream_t s) {
   using C = Wg3Cfg<CO_FR, WM, WN>;
   const int nz = a.zc > 0 ? (a.cout_total + a.zc - 1) / a.zc : 1;
   dim3 grid(splits, (a.Cin + C::CIB - 1) / C::CIB, nz);
-  hipLaunchKernelGGL((k_wgrad3<CO_FR, WM, WN>), grid, dim3(C::NTHR), 0, s, a);
+  // K stage width: 32-pixel row segments, or 16 / 8 / 4 pixels x 2 / 4 / 8 rows for narrow images
+  if (a.KW >= 32) hipLaunchKernelGGL((k_wgrad3<CO_FR, WM, WN, 5>), grid, dim3(C::NTHR), 0, s, a);
+  else if (a.KW >= 16) hipLaunchKernelGGL((k_wgrad3<CO_FR, WM, WN, 4>), grid, dim3(C::NTHR), 0, s, a);
+  else if (a.KW >= 8) hipLaunchKernelGGL((k_wgrad3<CO_FR, WM, WN, 3>), grid, dim3(C::NTHR), 0, s, a);
+  else hipLaunchKernelGGL((k_wgrad3<CO_FR, WM, WN, 2>), grid, dim3(C::NTHR), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1219,7 +1227,11 @@ int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
   int cin_t, pr, pc;
   wgrad_tile(mode, Cout, cin_t, pr, pc);
   const int taps = mode == W_C3 ? 9 : (mode == W_UP2 ? 4 : 1);
-  const long units = (long)N * ((KH + pr - 1) / pr) * ((KW + pc - 1) / pc);
+  long units = (long)N * ((KH + pr - 1) / pr) * ((KW + pc - 1) / pc);
+  if (mode == W_C3 && KW < 32) {  // k_wgrad3 stages rows of narrow images together
+    const int sw = KW >= 16 ? 16 : (KW >= 8 ? 8 : 4), sh = 32 / sw;
+    units = (long)N * ((KH + sh - 1) / sh) * ((KW + sw - 1) / sw);
+  }
   const long cib = (Cin + cin_t - 1) / cin_t;
   long want = 768 / cib;
   const long slab_cap = (64L << 20) / ((long)Cout * Cin * taps + Cout);  // <= 256 MB of slab
@@ -1271,8 +1283,9 @@ int gwgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
   }
   const long cib = (long)nblk * ((Cin + cin_t - 1) / cin_t);
   const int taps = mode == W_C3 ? 9 : 1;
-  const int pr = (mode == W_C3 || cb == 96) ? 1 : 2;  // pixel rows per K chunk
-  const long units = (long)N * ((KH + pr - 1) / pr) * ((KW + 31) / 32);
+  const int sw = KW >= 32 ? 32 : (KW >= 16 ? 16 : (KW >= 8 ? 8 : 4));  // k_wgrad3 segments
+  const long units = mode == W_C3 ? (long)N * ((KH + 32 / sw - 1) / (32 / sw)) * ((KW + sw - 1) / sw)
+                                  : (long)N * ((KH + (cb == 96 ? 0 : 1)) / (cb == 96 ? 1 : 2)) * ((KW + 31) / 32);
   long want = 768 / cib;
   const long slab_cap = (64L << 20) / ((long)Cout * Cin * taps + Cout);
   if (want > slab_cap) want = slab_cap;
