@@ -1269,10 +1269,25 @@ static int gw_block(int mode, int cout) {
   return cout <= 48 ? 48 : 96;
 }
 
+// input channels per workgroup of the 3x3 kernel: 32 for 96-wide output blocks; for 32-wide
+// blocks (RDB growth convs, 24-channel layers) 32 / 48 / 64, whichever pads Cin least (ties:
+// the wider block, fewer workgroups re-reading the gradient operand); else 48
+static int gw_cin_t(int cb, int Cin) {
+  if (cb == 96) return 32;
+  if (cb == 48) return 48;
+  int best = 48;
+  long pad = 1L << 30;
+  for (int t : {64, 48, 32}) {
+    const long p = (long)(Cin + t - 1) / t * t;
+    if (p < pad) { pad = p; best = t; }
+  }
+  return best;
+}
+
 int gwgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
   const int cb = gw_block(mode, Cout);
   const int nblk = (Cout + cb - 1) / cb;
-  const int cin_t = mode == W_C3 ? (cb == 96 ? 32 : 48) : 96;
+  const int cin_t = mode == W_C3 ? gw_cin_t(cb, Cin) : 96;
   if (mode == W_C1) {  // k_wgrad1: one 32-pixel row segment per K stage
     const long units = (long)N * KH * ((KW + 31) / 32);
     long want = 768 / ((long)nblk * ((Cin + 95) / 96));
@@ -1312,6 +1327,9 @@ hipError_t launch_gwgrad(int mode, const WgradArgs& a0, int splits, hipStream_t 
   if (mode == W_C3) {
     if (cb == 96) return run_wgrad3<6, 2, 2>(a, splits, s);
     if (cb == 48) return run_wgrad3<3, 1, 3>(a, splits, s);
+    const int ct = gw_cin_t(cb, a.Cin);
+    if (ct == 64) return run_wgrad3<2, 1, 4>(a, splits, s);
+    if (ct == 32) return run_wgrad3<2, 1, 2>(a, splits, s);
     return run_wgrad3<2, 1, 3>(a, splits, s);
   }
   // 1x1: the asynchronous k_wgrad1 tiled over (input-channel block of 96, output-channel block)
