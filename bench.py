@@ -25,6 +25,8 @@ sys.path.insert(0, ROOT)
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector, spec
 PEAK_HBM_GBS = 8000.0
 PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
+# fp32 by three-way bf16 splitting: 6 bf16 MFMA products per fp32 product
+PEAK_X6_TFLOPS = PEAK_BF16_TFLOPS / 6
 
 
 def conv_flops(h, w, cin, cout, k):
@@ -107,6 +109,30 @@ def time_dominant_kernel(bs, H, W, device, reps=5):
     return ms, flops
 
 
+def time_dominant_kernel_x6(bs, H, W, device, reps=5):
+    """the same 96->96 3x3 shape through the split-bf16 fp32 kernel (--conv-precision fp32_x6)"""
+    from image_denoising_amd import _lib
+
+    x = torch.randn(bs, H, W, 96, device=device)
+    w = torch.randn(96, 96, 3, 3, device=device) * 0.05
+    b = torch.zeros(96, device=device)
+    y = torch.empty_like(x)
+    s = torch.cuda.current_stream(device)
+    pk = _lib.scratch(_lib.lib().dn_conv2d_x6_pack_size(96, 96, 0), device)
+    run = lambda: _lib.call("dn_conv2d_forward_x6", x.data_ptr(), 96, bs, H, W, 96,
+                            w.data_ptr(), b.data_ptr(), 96, 1, y.data_ptr(), 96, pk.data_ptr(),
+                            pk.numel(), s.cuda_stream)
+    run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        run()
+    e1.record(s)
+    e1.synchronize()
+    del x, y
+    return e0.elapsed_time(e1) / reps, bs * conv_flops(H, W, 96, 96, 3)
+
+
 def time_dominant_kernel_bf16(bs, H, W, device, reps=5):
     """the same 96->96 3x3 shape through the bf16 matrix-core kernel (finetune --precision bf16)"""
     from image_denoising_amd import _lib
@@ -131,12 +157,13 @@ def time_dominant_kernel_bf16(bs, H, W, device, reps=5):
     return e0.elapsed_time(e1) / reps, bs * conv_flops(H, W, 96, 96, 3)
 
 
-def pmc_traffic():
+def pmc_traffic(tag=""):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
     (tools/pmc.sh + tools/pmc_summary.py; FETCH_SIZE x2 gfx950 correction), or None."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_dominant.json")))
+    pat = f"*_pmc_dominant_{tag}.json" if tag else "*_pmc_dominant.json"
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pat)))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -221,6 +248,9 @@ def main():
                          "finetune.py's adapter step (frozen UNet base + OutputAdapter, configs[4])")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                     help="finetune only: bf16 = mixed-precision frozen base (BASELINE configs[4])")
+    ap.add_argument("--conv-precision", choices=["fp32", "fp32_x6"], default="fp32",
+                    help="UNet 3x3 convs: fp32 matrix cores, or fp32 operands split into three "
+                         "bf16 pieces on the bf16 matrix cores (fp32-accurate, DESIGN.md §11)")
     ap.add_argument("--arch", choices=["UNet", "UNetImproved"], default="UNet",
                     help="network (train.py:305-313 / finetune.py --arch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -256,7 +286,8 @@ def main():
 
         net = ImprovedUNet(in_nc=C, out_nc=C, n_feature=48).to(device)
     else:
-        net = UNet(in_nc=C, out_nc=C, n_feature=48).to(device)
+        net = UNet(in_nc=C, out_nc=C, n_feature=48).to(device).set_precision(args.conv_precision)
+    x6 = args.conv_precision == "fp32_x6" and not iu
     fwd_flops = iunet_fwd_flops if iu else unet_fwd_flops
     clean = synthetic_clean(bs * C, H, H, 1000 + rank, device).view(bs, C, H, H).contiguous()
     if ft:
@@ -308,16 +339,19 @@ def main():
         ms_step = 1000.0 * elapsed / args.steps
         value = world * bs * args.steps / elapsed
         bf = ft and args.precision == "bf16"
-        kms, kflops = (time_dominant_kernel_bf16 if bf else time_dominant_kernel)(bs, H, H, device)
+        timer = (time_dominant_kernel_bf16 if bf else
+                 time_dominant_kernel_x6 if x6 else time_dominant_kernel)
+        kms, kflops = timer(bs, H, H, device)
         achieved = kflops / (kms * 1e-3) / 1e12
-        peak = PEAK_BF16_TFLOPS if bf else PEAK_FP32_TFLOPS
+        peak = PEAK_BF16_TFLOPS if bf else (PEAK_X6_TFLOPS if x6 else PEAK_FP32_TFLOPS)
         if args.mode == "n2n":  # fwd 256 + fwd/bwd 128
             step_flops = bs * (fwd_flops(H, H, C) + 3 * fwd_flops(H // 2, H // 2, C))
         elif ft:  # frozen base forward + adapter fwd (864 flop/px) and bwd (~1728 flop/px, C=1)
             step_flops = bs * (fwd_flops(H, H, C) + 3 * 864.0 * C * H * H)
         else:  # two fwd/bwd at full resolution
             step_flops = bs * 2 * 3 * fwd_flops(H, H, C)
-        traffic, traffic_src = pmc_traffic() if (bs, H, C, iu) == (64, 256, 1, False) else (None, None)
+        traffic, traffic_src = (pmc_traffic("x6" if x6 else "") if (bs, H, C, iu, bf) == (64, 256, 1, False, False)
+                                else (None, None))
         model = "ImprovedUNet(n_feature=48)" if iu else "UNet(n_feature=48)"
         if iu and not ft:
             workload = (f"{args.mode} step with arch_unet.ImprovedUNet(n_feature=48, depth=4, noise=True) "
@@ -345,7 +379,9 @@ def main():
             "value": round(value, 2), "unit": "patches/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16 (frozen base 3x3 convs; fp32 accumulate) + fp32 adapter" if bf else "fp32",
+            "dtype": ("bf16 (frozen base 3x3 convs; fp32 accumulate) + fp32 adapter" if bf else
+                      "fp32 (3x3 convs: exact 3-piece bf16 split, 6 products, fp32 accumulate)"
+                      if x6 else "fp32"),
             "data": "synthetic",
             "config": {"workload": workload,
                        "global_batch": bs * world, "patch": [H, H, C], "parallelism": f"dp{world}"},
@@ -353,6 +389,8 @@ def main():
             "step_frac_of_fp32_peak": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
             "roofline": {"bound": "mfma",
                          "kernel": ("k_fwd_bf16<NT=6,MT=4> (96->96 3x3, bf16 MFMA)" if bf else
+                                    "k_c3x6<NT=6,MT=2> (dec_conv1b 96->96 3x3 @256^2, fp32 via "
+                                    "bf16x6; peak = bf16 dense / 6)" if x6 else
                                     "k_fwd<G_C3,NT=6,MT=4> (dec_conv1b 96->96 3x3 @256^2)"),
                          "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic,

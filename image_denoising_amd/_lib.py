@@ -38,6 +38,10 @@ SIGNATURES = {
                                  c_size_t, c_void_p]),
     "dn_unet_forward_bf16": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
                                      c_size_t, c_void_p]),
+    "dn_unet_forward_prec": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
+                                     c_size_t, c_int, c_void_p]),
+    "dn_unet_backward_prec": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
+                                      c_size_t, c_int, c_void_p]),
     "dn_unet_debug_buffers": (c_int, [POINTER(DnCfg), c_int, c_int, c_int, c_int,
                                       POINTER(c_int64), c_int, POINTER(c_int)]),
     "dn_n2n_subsample": (c_int, [_F, c_int, c_int, c_int, c_int, _U8, c_uint64, c_uint64, c_uint64,
@@ -60,6 +64,11 @@ SIGNATURES = {
     "dn_conv2d_bf16_pack_size": (c_size_t, [c_int, c_int]),
     "dn_conv2d_forward_bf16": (c_int, [_F, c_int, c_int, c_int, c_int, c_int, _F, _F, c_int, c_int,
                                        _F, c_int, c_void_p, c_size_t, c_void_p]),
+    "dn_conv2d_x6_pack_size": (c_size_t, [c_int, c_int, c_int]),
+    "dn_conv2d_forward_x6": (c_int, [_F, c_int, c_int, c_int, c_int, c_int, _F, _F, c_int, c_int,
+                                     _F, c_int, c_void_p, c_size_t, c_void_p]),
+    "dn_conv2d_backward_data_x6": (c_int, [_F, c_int, c_int, c_int, c_int, _F, c_int, _F, c_int,
+                                           c_int, _F, c_int, c_void_p, c_size_t, c_void_p]),
     "dn_conv2d_backward_data": (c_int, [_F, c_int, c_int, c_int, c_int, _F, c_int, c_int, _F,
                                         c_int, c_int, _F, c_int, c_void_p, c_size_t, c_void_p]),
     "dn_conv2d_wgrad_slab_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),

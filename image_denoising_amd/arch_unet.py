@@ -222,10 +222,28 @@ class UNet(nn.Module):
         if self._flat.device != x.device:
             raise RuntimeError("module parameters and input are on different devices")
 
+    # arithmetic of the 3x3 convolutions (include/denoise_hip.h DN_PREC_*)
+    _PRECISIONS = {"fp32": 0, "fp32_x6": 2}
+
+    def set_precision(self, mode: str) -> "UNet":
+        """Arithmetic of the 3x3 convolutions in training and fp32 inference:
+        'fp32'    fp32 operands on the fp32 matrix cores (v_mfma_f32_16x16x4_f32);
+        'fp32_x6' fp32 operands split exactly into three bf16 pieces, the six piece products
+                  of order <= 2 on the bf16 matrix cores, fp32 accumulation -- the rounding
+                  error of an fp32 dot product at 2.67x the matrix-core peak."""
+        if mode not in self._PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(self._PRECISIONS)}")
+        self.precision = mode
+        return self
+
+    def _prec(self) -> int:
+        return self._PRECISIONS[getattr(self, "precision", "fp32")]
+
     def _run_forward(self, x, y, ws):
         N, _, H, W = x.shape
-        _lib.call("dn_unet_forward", ctypes.byref(self._cfg), _lib.ptr(self._flat), _lib.ptr(x),
-                  _lib.ptr(y), N, H, W, ws.data_ptr(), ws.numel(), _lib.stream_of(x))
+        _lib.call("dn_unet_forward_prec", ctypes.byref(self._cfg), _lib.ptr(self._flat),
+                  _lib.ptr(x), _lib.ptr(y), N, H, W, ws.data_ptr(), ws.numel(), self._prec(),
+                  _lib.stream_of(x))
 
     def set_inference_precision(self, dtype: str) -> "UNet":
         """'fp32' (default, the parity path) or 'bf16': no-grad forwards then multiply
@@ -244,8 +262,9 @@ class UNet(nn.Module):
                   _lib.ptr(x), _lib.ptr(y), N, H, W, ws.data_ptr(), ws.numel(), _lib.stream_of(x))
 
     def _run_backward(self, dy, dflat, ws, N, H, W):
-        _lib.call("dn_unet_backward", ctypes.byref(self._cfg), _lib.ptr(self._flat), _lib.ptr(dy),
-                  _lib.ptr(dflat), N, H, W, ws.data_ptr(), ws.numel(), _lib.stream_of(dy))
+        _lib.call("dn_unet_backward_prec", ctypes.byref(self._cfg), _lib.ptr(self._flat),
+                  _lib.ptr(dy), _lib.ptr(dflat), N, H, W, ws.data_ptr(), ws.numel(), self._prec(),
+                  _lib.stream_of(dy))
 
     # ---- nn.Module API ----------------------------------------------------------------
     def forward(self, x: torch.Tensor) -> torch.Tensor:

@@ -83,7 +83,17 @@ dn_status dn_unet_workspace_size(const dn_unet_cfg* cfg, int N, int H, int W, in
 
 dn_status dn_unet_forward(const dn_unet_cfg* cfg, const float* params, const float* x, float* y,
                           int N, int H, int W, void* ws, size_t ws_bytes, void* stream) {
+  return dn_unet_forward_prec(cfg, params, x, y, N, H, W, ws, ws_bytes, DN_PREC_FP32, stream);
+}
+
+dn_status dn_unet_forward_prec(const dn_unet_cfg* cfg, const float* params, const float* x,
+                               float* y, int N, int H, int W, void* ws, size_t ws_bytes,
+                               int precision, void* stream) {
   DN_GUARD_BEGIN
+  if (precision == DN_PREC_BF16)
+    return dn_unet_forward_bf16(cfg, params, x, y, N, H, W, ws, ws_bytes, stream);
+  if (precision != DN_PREC_FP32 && precision != DN_PREC_FP32_X6)
+    return fail(DN_ERR_ARG, "unknown precision");
   if (!cfg || !params || !x || !y || !ws) return fail(DN_ERR_ARG, "null argument");
   Plan p;
   std::string err;
@@ -95,7 +105,7 @@ dn_status dn_unet_forward(const dn_unet_cfg* cfg, const float* params, const flo
     return fail(DN_ERR_ARG, err);
   if (ws_bytes < (size_t)p.total_floats * sizeof(float))
     return fail(DN_ERR_WORKSPACE, "workspace smaller than dn_unet_workspace_size()");
-  return unet_forward(p, params, x, y, static_cast<float*>(ws), (hipStream_t)stream);
+  return unet_forward(p, params, x, y, static_cast<float*>(ws), (hipStream_t)stream, precision);
   DN_GUARD_END
 }
 
@@ -110,14 +120,24 @@ dn_status dn_unet_forward_bf16(const dn_unet_cfg* cfg, const float* params, cons
   if (ws_bytes < (size_t)p.total_floats * sizeof(float))
     return fail(DN_ERR_WORKSPACE, "workspace smaller than dn_unet_workspace_size()");
   p.with_bwd = false;  // inference only: nothing is saved for a backward
-  return unet_forward(p, params, x, y, static_cast<float*>(ws), (hipStream_t)stream, true);
+  return unet_forward(p, params, x, y, static_cast<float*>(ws), (hipStream_t)stream,
+                      DN_PREC_BF16);
   DN_GUARD_END
 }
 
 dn_status dn_unet_backward(const dn_unet_cfg* cfg, const float* params, const float* dy,
                            float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
                            void* stream) {
+  return dn_unet_backward_prec(cfg, params, dy, dparams, N, H, W, ws, ws_bytes, DN_PREC_FP32,
+                               stream);
+}
+
+dn_status dn_unet_backward_prec(const dn_unet_cfg* cfg, const float* params, const float* dy,
+                                float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
+                                int precision, void* stream) {
   DN_GUARD_BEGIN
+  if (precision != DN_PREC_FP32 && precision != DN_PREC_FP32_X6)
+    return fail(DN_ERR_ARG, "backward precision must be DN_PREC_FP32 or DN_PREC_FP32_X6");
   if (!cfg || !params || !dy || !dparams || !ws) return fail(DN_ERR_ARG, "null argument");
   Plan p;
   std::string err;
@@ -125,7 +145,8 @@ dn_status dn_unet_backward(const dn_unet_cfg* cfg, const float* params, const fl
   if (ws_bytes < (size_t)p.total_floats * sizeof(float))
     return fail(DN_ERR_WORKSPACE,
                 "workspace smaller than dn_unet_workspace_size(with_backward=1)");
-  return unet_backward(p, params, dy, dparams, static_cast<float*>(ws), (hipStream_t)stream);
+  return unet_backward(p, params, dy, dparams, static_cast<float*>(ws), (hipStream_t)stream,
+                       precision);
   DN_GUARD_END
 }
 
@@ -390,6 +411,63 @@ dn_status dn_conv2d_forward_bf16(const float* x, int x_stride, int N, int H, int
     e = launch_fwd_bf16(a, s);
   }
   return hip_status(e, "dn_conv2d_forward_bf16");
+}
+
+size_t dn_conv2d_x6_pack_size(int Cin, int Cout, int backward_data) {
+  if (Cin < 1 || Cout < 1) return 0;
+  const long e = backward_data ? x6_pack_elems(Cout, Cin, x6_dgrad_zc(Cin))
+                               : x6_pack_elems(Cin, Cout, 0);
+  return e < 0 ? 0 : 2 * (size_t)e;
+}
+
+dn_status dn_conv2d_forward_x6(const float* x, int x_stride, int N, int H, int W, int Cin,
+                               const float* w, const float* b, int Cout, int act, float* y,
+                               int y_stride, void* pack_ws, size_t pack_bytes, void* stream) {
+  if (!x || !w || !b || !y) return fail(DN_ERR_ARG, "null argument");
+  if (N < 1 || H < 1 || W < 1 || Cin < 1 || x_stride < Cin || y_stride < Cout)
+    return fail(DN_ERR_ARG, "bad shape");
+  const size_t need = dn_conv2d_x6_pack_size(Cin, Cout, 0);
+  if (need == 0) return fail(DN_ERR_ARG, "bf16x6 forward supports Cout <= 96");
+  if (dn_status st = need_pack(pack_ws, pack_bytes, need)) return st;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = launch_pack_x6(conv_fwd_view(w, Cin, 3), Cin, Cout, 0, pack_ws, s);
+  if (e == hipSuccess) {
+    FwdArgs a{};
+    a.in = x; a.in_stride = x_stride; a.in_off = 0; a.IHt = H; a.IWt = W;
+    a.N = N; a.OH = H; a.OW = W; a.K = Cin; a.NOUT = Cout;
+    a.wp = static_cast<const float*>(pack_ws); a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
+    a.out = y; a.out_stride = y_stride; a.out_off = 0; a.out_layout = OUT_NHWC;
+    e = launch_fwd_x6(a, s);
+  }
+  return hip_status(e, "dn_conv2d_forward_x6");
+}
+
+dn_status dn_conv2d_backward_data_x6(const float* dz, int N, int H, int W, int Cout,
+                                     const float* w, int Cin, const float* mask, int mask_stride,
+                                     int accumulate, float* dx, int dx_stride, void* pack_ws,
+                                     size_t pack_bytes, void* stream) {
+  if (!dz || !w || !dx) return fail(DN_ERR_ARG, "null argument");
+  if (N < 1 || H < 1 || W < 1 || Cout < 1 || dx_stride < Cin) return fail(DN_ERR_ARG, "bad shape");
+  if (mask && accumulate) return fail(DN_ERR_ARG, "mask and accumulate are exclusive");
+  const size_t need = dn_conv2d_x6_pack_size(Cin, Cout, 1);
+  if (need == 0) return fail(DN_ERR_ARG, "bf16x6 data gradient: unsupported Cin");
+  if (dn_status st = need_pack(pack_ws, pack_bytes, need)) return st;
+  hipStream_t s = (hipStream_t)stream;
+  const int zc = x6_dgrad_zc(Cin);
+  hipError_t e = launch_pack_x6(conv_dgrad_view(w, Cin, 3), Cout, Cin, zc, pack_ws, s);
+  if (e == hipSuccess) {
+    FwdArgs a{};
+    a.in = dz; a.in_stride = Cout; a.in_off = 0; a.IHt = H; a.IWt = W;
+    a.N = N; a.OH = H; a.OW = W; a.K = Cout; a.NOUT = Cin;
+    a.zc = zc;
+    a.wp = static_cast<const float*>(pack_ws);
+    a.wp_z = zc ? x6_pack_elems(Cout, Cin, zc) / ((Cin + zc - 1) / zc) : 0;
+    a.epi = mask ? EPI_MASK : (accumulate ? EPI_ACCUM : EPI_PLAIN);
+    a.out = dx; a.out_stride = dx_stride; a.out_off = 0; a.out_layout = OUT_NHWC;
+    a.mask = mask; a.mask_stride = mask_stride; a.mask_off = 0;
+    e = launch_fwd_x6(a, s);
+  }
+  return hip_status(e, "dn_conv2d_backward_data_x6");
 }
 
 dn_status dn_conv2d_backward_data(const float* dz, int N, int H, int W, int Cout, const float* w,

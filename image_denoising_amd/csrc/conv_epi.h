@@ -1,0 +1,119 @@
+// Output epilogue shared by the output-stationary conv kernels (k_fwd in conv.hip, the split-bf16
+// fp32 kernel in conv_x6.hip).  Both keep a wave's tile as acc[m][q] in the 16x16 MFMA C/D map
+// (col = lane&15 -> output channel q*16 + col, row = 4*(lane>>4) + reg -> pixel x of tile row m),
+// so one LDS-staged epilogue serves every layout and fused op (FwdArgs::epi / out_layout).
+#pragma once
+
+#include "dn_internal.h"
+
+namespace dn {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Stage each 16-pixel row of the wave's tile through LDS, then write whole pixels: as float4
+// (NOUT contiguous channels, 1 KiB contiguous per wave store) when the layout allows, else
+// element by element (NCHW, PixelShuffle, unaligned views).  `lds` must hold 4*16*PS floats and
+// be free (the caller's main loop ended on a barrier).  UP: deconv forward, wave = parity (a,b)
+// and every wave covers all MT rows; else wave w owns rows [w*MT, w*MT+MT) and blockIdx.z is
+// the output-channel block (zc) or the scatter parity.
+template <int NT, int MT, int PS, bool UP>
+__device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, const f32x4 (&acc)[MT][NT],
+                                             float* lds, int ty0, int tx0, int n) {
+  constexpr int NP = 16 * NT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int ab = UP ? wave : (int)blockIdx.z;
+  const int wrow = UP ? 0 : wave * MT;  // first tile row of this wave
+  // output-channel block of a wide layer: channels [cz, cz + nout) of NOUT
+  const int cz = a.zc ? (int)blockIdx.z * a.zc : 0;
+  const int nout = a.zc ? min(NP, a.NOUT - cz) : a.NOUT;
+  const bool aux = a.epi == EPI_MASK || a.epi == EPI_BIAS_ADD;
+  const bool vec_out = (a.out_layout == OUT_NHWC || a.out_layout == OUT_UP2) &&
+                       ((a.out_stride | a.out_off | a.NOUT) & 3) == 0 &&
+                       (!aux || ((a.mask_stride | a.mask_off) & 3) == 0);
+  float* st = lds + wave * 16 * PS;
+  const bool bias_epi = (a.epi == EPI_BIAS || a.epi == EPI_BIAS_ACT || a.epi == EPI_BIAS_ADD) &&
+                        a.bias != nullptr;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) st[(4 * lg + r) * PS + q * 16 + li] = acc[m][q][r];
+    __syncthreads();
+    const int gy = ty0 + wrow + m;
+    if (gy < a.OH && vec_out) {
+      const int NQ = nout >> 2;
+      for (int e = lane; e < 16 * NQ; e += 64) {
+        const int p = e / NQ, c = 4 * (e - p * NQ);
+        const int gx = tx0 + p;
+        if (gx >= a.OW) continue;
+        float4 v = *reinterpret_cast<const float4*>(st + p * PS + c);
+        const long pix = ((long)n * a.OH + gy) * a.OW + gx;
+        if (bias_epi) {
+          const float4 b = *reinterpret_cast<const float4*>(a.bias + cz + c);
+          v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+        }
+        if (a.epi == EPI_BIAS_ACT) {
+          v.x = v.x > 0.f ? v.x : v.x * 0.2f; v.y = v.y > 0.f ? v.y : v.y * 0.2f;
+          v.z = v.z > 0.f ? v.z : v.z * 0.2f; v.w = v.w > 0.f ? v.w : v.w * 0.2f;
+        } else if (aux) {
+          const float4 r =
+              *reinterpret_cast<const float4*>(a.mask + pix * a.mask_stride + a.mask_off + cz + c);
+          if (a.epi == EPI_BIAS_ADD) {
+            v.x = r.x + v.x; v.y = r.y + v.y; v.z = r.z + v.z; v.w = r.w + v.w;
+          } else {
+            v.x = r.x > 0.f ? v.x : v.x * 0.2f; v.y = r.y > 0.f ? v.y : v.y * 0.2f;
+            v.z = r.z > 0.f ? v.z : v.z * 0.2f; v.w = r.w > 0.f ? v.w : v.w * 0.2f;
+          }
+        }
+        long oi;
+        if (a.out_layout == OUT_NHWC)
+          oi = pix * a.out_stride + a.out_off + cz + c;
+        else
+          oi = (((long)n * 2 * a.OH + 2 * gy + (ab >> 1)) * 2 * a.OW + 2 * gx + (ab & 1)) *
+                   a.out_stride + a.out_off + c;
+        float4* o = reinterpret_cast<float4*>(a.out + oi);
+        if (a.epi == EPI_ACCUM) {
+          const float4 old = *o;
+          v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
+        }
+        *o = v;
+      }
+    } else if (gy < a.OH) {
+      for (int e = lane; e < 16 * nout; e += 64) {
+        const int p = e / nout, c = e - p * nout;
+        const int gx = tx0 + p;
+        if (gx >= a.OW) continue;
+        const int cg = cz + c;  // channel of the layer
+        float v = st[p * PS + c];
+        const long pix = ((long)n * a.OH + gy) * a.OW + gx;
+        if (bias_epi) v = v + a.bias[cg];
+        if (a.epi == EPI_BIAS_ACT) {
+          v = v > 0.f ? v : v * 0.2f;
+        } else if (a.epi == EPI_BIAS_ADD) {
+          v = a.mask[pix * a.mask_stride + a.mask_off + cg] + v;
+        } else if (a.epi == EPI_MASK) {
+          v = a.mask[pix * a.mask_stride + a.mask_off + cg] > 0.f ? v : v * 0.2f;
+        }
+        long oi;
+        if (a.out_layout == OUT_NHWC) {
+          oi = pix * a.out_stride + a.out_off + cg;
+        } else if (a.out_layout == OUT_NCHW) {
+          oi = (((long)n * a.NOUT + cg) * a.OH + gy) * a.OW + gx;
+        } else if (a.out_layout == OUT_PS) {  // PixelShuffle(2): cg = 4*c' + 2*i + j
+          oi = (((long)n * 2 * a.OH + 2 * gy + ((cg >> 1) & 1)) * 2 * a.OW + 2 * gx + (cg & 1)) *
+                   a.out_stride + a.out_off + (cg >> 2);
+        } else {
+          oi = (((long)n * 2 * a.OH + 2 * gy + (ab >> 1)) * 2 * a.OW + 2 * gx + (ab & 1)) *
+                   a.out_stride + a.out_off + c;
+        }
+        if (a.epi == EPI_ACCUM) v += a.out[oi];
+        a.out[oi] = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace dn

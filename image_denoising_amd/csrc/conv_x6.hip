@@ -1,0 +1,513 @@
+// fp32 3x3 convolution on the gfx950 bf16 matrix cores by three-way operand splitting
+// ("bf16x6"): the training-path conv forward / data gradient at fp32 accuracy.
+//
+// Every fp32 operand v is split exactly into three bf16 pieces, v = v0 + v1 + v2 (each piece
+// is the round-to-nearest-even bf16 of what the previous ones left; 3 x 8 significand bits
+// cover fp32's 24).  A product a*b is the sum of the nine piece products a_i*b_j of weight
+// 2^-8(i+j); the six with i+j <= 2 are kept (a0b0, a0b1, a1b0, a0b2, a1b1, a2b0), the dropped
+// three are below 2^-23 |ab|, i.e. one fp32 rounding.  Each piece product is exact in the
+// MFMA's fp32 accumulator, so the result has the error of an fp32 dot product (measured
+// against fp64: the same rms error as the fp32 MFMA path).  Six
+// v_mfma_f32_16x16x32_bf16 (16 cycles each) replace eight v_mfma_f32_16x16x4_f32 (32 cycles)
+// per 16x16x32 block: a 2.67x higher matrix-core ceiling for the same fp32-accurate result.
+//
+//   Workgroup = 4 waves, tile = 4*MT rows x 16 pixels x 16*NT output channels; wave w owns
+//   rows [w*MT, w*MT+MT).  K is staged 32 input channels (one MFMA K) at a time: the x tile
+//   (with halo) is split as it is staged (fp32 registers -> three bf16 planes in LDS, once
+//   per chunk), the pre-split weights arrive one tap per stage by global_load_lds, double
+//   buffered, one barrier per stage.  LDS rows are 32 bf16 (64 B) with the 16-B quad index
+//   XOR-swizzled by (row >> 1) & 3, which makes the per-lane ds_read_b128 operand reads
+//   conflict-free for every tap offset.
+#include <cstdlib>
+
+#include "conv_epi.h"
+
+namespace dn {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// 16-B quad q of LDS row `row` lives at quad q ^ ((row >> 1) & 3)
+__device__ __forceinline__ int x6_swz(int row, int q) { return q ^ ((row >> 1) & 3); }
+
+// v = h + m + l exactly (normal fp32 v); each step's remainder is exact in fp32
+__device__ __forceinline__ void split3(float v, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)v;
+  const float r = v - (float)h;
+  m = (__bf16)r;
+  l = (__bf16)(r - (float)m);
+}
+
+__device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// One 16x16x32 block of every fragment of a wave: acc[m][q] += sum_k A[m] B[q] at fp32 accuracy.
+// The leading product a0*b0 and the five corrections are summed by the matrix core from zero
+// (hi, lo) and only then added to the running fp32 sum with a round-to-nearest VALU add: the
+// matrix core's internal alignment rounds toward -inf, which on a long running sum (6 x 27
+// MFMAs per output for K = 96) leaves a small negative bias that the weight-gradient sums over
+// ~1e5 pixels would turn into a visible error; on a fresh 32-term block it is ~50x smaller.
+// QG output-channel fragments are processed together (temporaries 8*MT*QG registers) so that
+// the lo chain has MT*QG - 1 independent MFMAs between dependent ones.
+// fragment-group width: >= 4 independent lo chains within the register budget
+constexpr int x6_qg(int mt, int nt) { return mt >= 4 ? 1 : (mt == 2 ? (nt % 2 ? 3 : 2) : nt); }
+
+template <int MT, int NT, int QG>
+__device__ __forceinline__ void x6_block(f32x4 (&acc)[MT][NT], const bf16x8 (&av)[3][MT],
+                                         const bf16x8 (&bv)[3][NT]) {
+  static_assert(NT % QG == 0, "whole fragment groups");
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  constexpr int PA[4] = {1, 0, 1, 2}, PB[4] = {0, 2, 1, 0};
+#pragma unroll
+  for (int q0 = 0; q0 < NT; q0 += QG) {
+    f32x4 hi[MT][QG], lo[MT][QG];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int g = 0; g < QG; ++g) hi[m][g] = mfma_bf16(av[0][m], bv[0][q0 + g], z);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int g = 0; g < QG; ++g) lo[m][g] = mfma_bf16(av[0][m], bv[1][q0 + g], z);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int g = 0; g < QG; ++g)
+          lo[m][g] = mfma_bf16(av[PA[j]][m], bv[PB[j]][q0 + g], lo[m][g]);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int g = 0; g < QG; ++g) acc[m][q0 + g] += hi[m][g] + lo[m][g];
+  }
+}
+
+// bf16 elements of one weight stage (one tap, three planes of NP x 32) in the packed image,
+// padded to whole rounds of the pipelined kernel's DMA (8 waves x 1 KiB global_load_lds_dwordx4;
+// the 12-byte form would fit 18 KiB exactly, but it writes lane x 16 B in LDS, not lane x 12)
+__host__ __device__ constexpr int x6_wst(int np) {
+  return (3 * np * 32 * 2 + 8191) / 8192 * 8192 / 2;
+}
+
+template <int NT, int MT>
+struct XCfg {
+  static constexpr int TW = 16, TH = 4 * MT, IH = TH + 2, IW = TW + 2, KC = 32, NP = 16 * NT;
+  static constexpr int XPIX = IH * IW;
+  static constexpr int XPL = XPIX * KC;        // bf16 per plane of the x tile
+  static constexpr int WPL = NP * KC;          // bf16 per plane of a weight stage
+  static constexpr int WST = 3 * WPL;          // bf16 per stage (one tap, three planes)
+  static constexpr int WSTP = x6_wst(NP);      // stage stride in the packed image
+  static_assert(WST % 512 == 0, "weight stages are copied in whole KiBs");
+  static constexpr int XQ = XPIX * (KC / 4);   // float4 items of the x tile
+  static constexpr int XITEMS = (XQ + 255) / 256;
+  static constexpr int PS = NP + 4;            // epilogue staging pixel stride (floats)
+  static constexpr int LBYTES_MAIN = 2 * 3 * XPL + 2 * 2 * WST;
+  static constexpr int LBYTES = LBYTES_MAIN > 4 * 4 * 16 * PS ? LBYTES_MAIN : 4 * 4 * 16 * PS;
+  // resident workgroups per CU (LDS-limited; the register budget allows 2 waves per SIMD)
+  static constexpr int OCC = (163840 / LBYTES) < 2 ? (163840 / LBYTES) : 2;
+};
+
+template <int NT, int MT>
+__global__ __launch_bounds__(256, 2) void k_c3x6(FwdArgs a) {
+  using C = XCfg<NT, MT>;
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
+  __bf16* lx = reinterpret_cast<__bf16*>(lds_raw);
+  __bf16* lw0 = lx + 3 * C::XPL;
+  __bf16* lw1 = lw0 + C::WST;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int tiles_x = (a.OW + C::TW - 1) / C::TW;
+  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
+  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
+  const int n = blockIdx.y;
+  const int iy0 = ty0 - 1, ix0 = tx0 - 1;
+  const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
+  const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp) + (long)blockIdx.z * a.wp_z;
+  const bool vec = ((a.in_stride | a.in_off) & 3) == 0;
+  const int nch = (a.K + C::KC - 1) / C::KC;
+  const int nst = 9 * nch;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < NT; ++q) acc[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float4 xr[C::XITEMS];
+  auto load_x = [&](int k0) {
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * 256;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < C::XQ) {
+        const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+        const int iy = pix / C::IW, ix = pix - iy * C::IW;
+        const int gy = iy0 + iy, gx = ix0 + ix, k = k0 + 4 * q;
+        if (gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt && k < a.K) {
+          const float* p = inb + ((long)gy * a.IWt + gx) * a.in_stride + k;
+          if (vec && k + 4 <= a.K) {
+            v = *reinterpret_cast<const float4*>(p);
+          } else {
+            v.x = p[0];
+            if (k + 1 < a.K) v.y = p[1];
+            if (k + 2 < a.K) v.z = p[2];
+            if (k + 3 < a.K) v.w = p[3];
+          }
+        }
+      }
+      xr[it] = v;
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * 256;
+      if (e < C::XQ) {
+        const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+        const float f[4] = {xr[it].x, xr[it].y, xr[it].z, xr[it].w};
+        bf16x4 h, m, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          __bf16 hj, mj, lj;
+          split3(f[j], hj, mj, lj);
+          h[j] = hj; m[j] = mj; l[j] = lj;
+        }
+        const int off = pix * C::KC + x6_swz(pix, q >> 1) * 8 + (q & 1) * 4;
+        *reinterpret_cast<bf16x4*>(lx + off) = h;
+        *reinterpret_cast<bf16x4*>(lx + C::XPL + off) = m;
+        *reinterpret_cast<bf16x4*>(lx + 2 * C::XPL + off) = l;
+      }
+    }
+  };
+  auto load_w = [&](int st, __bf16* dst) {  // stage st = chunk * 9 + tap, whole KiB pieces
+    const __bf16* src = wimg + (long)st * C::WSTP;
+#pragma unroll
+    for (int p = wave; p < C::WST / 512; p += 4) {
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(src + p * 512 + lane * 8),
+          (__attribute__((address_space(3))) void*)(dst + p * 512), 16, 0, 0);
+    }
+  };
+
+  load_w(0, lw0);
+  load_x(0);
+  store_x();
+  __syncthreads();
+
+  for (int st = 0; st < nst; ++st) {
+    const int c = st / 9, t = st - 9 * c, ky = t / 3, kx = t - 3 * ky;
+    const __bf16* lw = (st & 1) ? lw1 : lw0;
+    // the buffer of stage st+1 was last read in stage st-1, which every wave has left
+    if (st + 1 < nst) load_w(st + 1, (st & 1) ? lw0 : lw1);
+    if (t == 0 && c + 1 < nch) load_x((c + 1) * C::KC);
+    bf16x8 av[3][MT], bv[3][NT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int pix = (wave * MT + m + ky) * C::IW + li + kx;
+      const int off = pix * C::KC + x6_swz(pix, lg) * 8;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) av[p][m] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
+    }
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      const int row = q * 16 + li;
+      const int off = row * C::KC + x6_swz(row, lg) * 8;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bv[p][q] = *reinterpret_cast<const bf16x8*>(lw + p * C::WPL + off);
+    }
+    x6_block<MT, NT, x6_qg(MT, NT)>(acc, av, bv);
+    if (t == 8 && c + 1 < nch) {  // every wave is done with this chunk's x tile
+      __syncthreads();
+      store_x();
+    }
+    __syncthreads();  // next stage's weights landed (vmcnt(0)); next x tile written
+  }
+  fwd_epilogue<NT, MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
+}
+
+// ------------------------------------------------------------------------------------
+// Pipelined variant for large grids: 8 waves (2 per SIMD) share one 16 x 16 x 16*NT tile
+// (wave w: rows 2w, 2w+1), one workgroup per CU.  The weight stages stream through an
+// S-deep LDS ring by 1 KiB DMAs (global_load_lds_dwordx4, PPW per wave per stage),
+// so a stage's weights are requested S-2 stages (~2 us) before they are read; the wait before
+// each stage's barrier counts only this wave's own DMAs (s_waitcnt vmcnt(N)), not the next
+// chunk's x tile, which is loaded into registers when a chunk starts and split into the
+// three LDS planes when it ends.  Requires float4-aligned input views with K % 4 == 0.
+// ------------------------------------------------------------------------------------
+template <int NT>
+struct PCfg {
+  static constexpr int WAVES = 8, MT = 2, S = 4;
+  static constexpr int TW = 16, TH = WAVES * MT, IH = TH + 2, IW = TW + 2, KC = 32, NP = 16 * NT;
+  static constexpr int XPIX = IH * IW;
+  static constexpr int XPL = XPIX * KC;
+  static constexpr int WPL = NP * KC;
+  static constexpr int WSTP = x6_wst(NP);              // bf16 per stage (padded)
+  static constexpr int PPW = WSTP * 2 / (WAVES * 1024);  // 1 KiB DMAs per wave per stage
+  static_assert(PPW * WAVES * 1024 == WSTP * 2, "stage = whole DMA rounds");
+  static constexpr int XQ = XPIX * (KC / 4);
+  static constexpr int XITEMS = (XQ + WAVES * 64 - 1) / (WAVES * 64);
+  static constexpr int PS = NP + 4;
+  static constexpr int LBYTES_MAIN = 2 * 3 * XPL + 2 * S * WSTP;
+  static constexpr int LEPI = 4 * WAVES * 16 * PS;
+  static constexpr int LBYTES = LBYTES_MAIN > LEPI ? LBYTES_MAIN : LEPI;
+  static_assert(LBYTES <= 163840, "one workgroup per CU");
+};
+
+#define X6_WAITCNT_VM(n) \
+  __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
+
+__device__ __forceinline__ void x6_barrier() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no compiler motion of LDS accesses across it
+  __builtin_amdgcn_s_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+template <int NT>
+__global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
+  using C = PCfg<NT>;
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
+  __bf16* lx = reinterpret_cast<__bf16*>(lds_raw);
+  __bf16* ring = lx + 3 * C::XPL;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int tiles_x = (a.OW + C::TW - 1) / C::TW;
+  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
+  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
+  const int n = blockIdx.y;
+  const int iy0 = ty0 - 1, ix0 = tx0 - 1;
+  const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
+  const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp) + (long)blockIdx.z * a.wp_z;
+  const int nch = (a.K + C::KC - 1) / C::KC;
+  const int nst = 9 * nch;
+
+  f32x4 acc[C::MT][NT];
+#pragma unroll
+  for (int m = 0; m < C::MT; ++m)
+#pragma unroll
+    for (int q = 0; q < NT; ++q) acc[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Exactly XITEMS buffer loads per thread per chunk (items outside the tile or the image get
+  // an out-of-range offset, for which the buffer unit returns zeros) and exactly PPW DMAs per
+  // wave per stage (past the last stage: a harmless re-load into a retired ring slot), so the
+  // vmcnt counts below are compile-time constants.
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(inb), (short)0, a.IHt * a.IWt * a.in_stride * 4, 0x00020000);
+  f32x4 xr[C::XITEMS];
+  auto load_x = [&](int k0) {
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * C::WAVES * 64;
+      const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+      const int iy = pix / C::IW, ix = pix - iy * C::IW;
+      const int gy = iy0 + iy, gx = ix0 + ix, k = k0 + 4 * q;
+      const bool ok = e < C::XQ && gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt && k < a.K;
+      const int off = ok ? ((gy * a.IWt + gx) * a.in_stride + k) * 4 : 0x7fffffff;
+      xr[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * C::WAVES * 64;
+      if (e < C::XQ) {
+        const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+        const float f[4] = {xr[it][0], xr[it][1], xr[it][2], xr[it][3]};
+        bf16x4 h, m, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          __bf16 hj, mj, lj;
+          split3(f[j], hj, mj, lj);
+          h[j] = hj; m[j] = mj; l[j] = lj;
+        }
+        const int off = pix * C::KC + x6_swz(pix, q >> 1) * 8 + (q & 1) * 4;
+        *reinterpret_cast<bf16x4*>(lx + off) = h;
+        *reinterpret_cast<bf16x4*>(lx + C::XPL + off) = m;
+        *reinterpret_cast<bf16x4*>(lx + 2 * C::XPL + off) = l;
+      }
+    }
+  };
+  // weights of stage `src_st` into ring slot `slot`: PPW DMAs of 1 KiB per wave
+  auto load_w = [&](int src_st, int slot) {
+    const unsigned char* src = reinterpret_cast<const unsigned char*>(wimg + (long)src_st * C::WSTP);
+    unsigned char* dst = reinterpret_cast<unsigned char*>(ring + slot * C::WSTP);
+#pragma unroll
+    for (int j = 0; j < C::PPW; ++j) {
+      const int piece = wave * C::PPW + j;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(src + piece * 1024 + lane * 16),
+          (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16, 0, 0);
+    }
+  };
+
+  // prologue: x tile of chunk 0 split into LDS, chunk 1's x in registers, weight stages
+  // 0 .. S-2 in flight
+  load_x(0);
+  store_x();
+  load_x((nch > 1 ? 1 : 0) * C::KC);
+#pragma unroll
+  for (int j = 0; j < C::S - 1; ++j) load_w(j < nst ? j : nst - 1, j);
+  X6_WAITCNT_VM(C::PPW * (C::S - 2));  // own DMAs of stage 0 landed
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
+  x6_barrier();
+
+  // Stage st computes from ring slot st % S, then (after the chunk's last tap: splits the next
+  // chunk's x tile into LDS and loads the one after into registers) requests stage st+S-1 into
+  // slot (st-1) % S, which every wave left at the previous barrier.  The compiler's own waits
+  // for the x registers then only ever cover DMAs issued a stage or more earlier.
+  for (int c = 0; c < nch; ++c) {
+    const bool more = c + 1 < nch;
+#pragma unroll 1
+    for (int t = 0; t < 9; ++t) {
+      const int st = 9 * c + t;
+      const __bf16* lw = ring + (st % C::S) * C::WSTP;
+      const int ky = t / 3, kx = t - 3 * ky;
+      bf16x8 av[3][C::MT], bv[3][NT];
+#pragma unroll
+      for (int m = 0; m < C::MT; ++m) {
+        const int pix = (wave * C::MT + m + ky) * C::IW + li + kx;
+        const int off = pix * C::KC + x6_swz(pix, lg) * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          av[p][m] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
+      }
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        const int row = q * 16 + li;
+        const int off = row * C::KC + x6_swz(row, lg) * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bv[p][q] = *reinterpret_cast<const bf16x8*>(lw + p * C::WPL + off);
+      }
+      x6_block<C::MT, NT, x6_qg(C::MT, NT)>(acc, av, bv);
+      const bool xstep = t == 8 && more;
+      if (xstep) {
+        x6_barrier();  // every wave is done with this chunk's x tile
+        store_x();
+        load_x((c + 2 < nch ? c + 2 : nch - 1) * C::KC);  // uniform count: re-load at the end
+      }
+      load_w(st + C::S - 1 < nst ? st + C::S - 1 : nst - 1, (st + C::S - 1) % C::S);
+      // own DMAs of stage st+1 landed: issued after them are those of stages st+2, st+S-1 and,
+      // in a chunk's first stage, the x loads issued at the previous chunk's end
+      if (t == 0 && c > 0) X6_WAITCNT_VM(C::PPW * (C::S - 2) + C::XITEMS);
+      else X6_WAITCNT_VM(C::PPW * (C::S - 2));
+      if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
+      x6_barrier();
+    }
+  }
+  X6_WAITCNT_VM(0);  // the trailing re-load DMAs must land before the LDS is reused
+  x6_barrier();
+  fwd_epilogue<NT, C::MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
+}
+
+// Pre-split weight image, one per output-channel block z: [chunk][tap][piece][n < NP][32 k],
+// bf16, 16-B quads swizzled by n (see x6_swz); zero padded past K / NOUT.
+// Each stage is x6_wst(NP) elements (the tail past 3*NP*32 is zero).
+__global__ __launch_bounds__(256) void k_pack_x6(WView wv, int K, int NOUT, int NP, int nch,
+                                                 int nz, int zc, int ntot, __bf16* __restrict__ out) {
+  const int wst = x6_wst(NP), pad = wst - 3 * NP * 32;
+  const long per_z = (long)nch * 9 * NP * 32, total = per_z * nz;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int z = (int)(e / per_z);
+    const long r = e - (long)z * per_z;
+    const int kk = (int)(r % 32), nn = (int)((r / 32) % NP);
+    const int ct = (int)(r / (32L * NP)), t = ct % 9, c = ct / 9, k = c * 32 + kk;
+    float v = 0.f;
+    if (k < K && nn < NOUT && (zc == 0 || z * zc + nn < ntot)) {
+      const int tm = wv.flip ? wv.taps - 1 - t : t;
+      v = wv.w[wv.off + (long)z * wv.sZ + (long)k * wv.sK + (long)nn * wv.sN + (long)tm * wv.sT];
+    }
+    __bf16 h, m, l;
+    split3(v, h, m, l);
+    __bf16* st = out + ((long)z * nch * 9 + ct) * wst;
+    const int o = nn * 32 + x6_swz(nn, kk >> 3) * 8 + (kk & 7);
+    st[o] = h;
+    st[NP * 32 + o] = m;
+    st[2 * NP * 32 + o] = l;
+    if ((int)(r % (32L * NP)) < pad) st[3 * NP * 32 + (int)(r % (32L * NP))] = (__bf16)0.f;
+  }
+}
+
+template <int NT, int MT>
+static hipError_t run_x6(const FwdArgs& a, int nz, hipStream_t s) {
+  using C = XCfg<NT, MT>;
+  const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
+  hipLaunchKernelGGL((k_c3x6<NT, MT>), dim3(tx * ty, a.N, nz), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// output channels per workgroup: 48 or 96 (wider layers run zc-blocks of 48 or 96)
+static int x6_np(int nout, int zc) {
+  const int np = zc > 0 ? zc : nout;
+  return np <= 48 ? 48 : (np <= 96 ? 96 : 0);
+}
+
+long x6_pack_elems(int K, int nout, int zc) {
+  const int np = x6_np(nout, zc);
+  if (np == 0 || (zc > 0 && zc != np)) return -1;
+  const int nz = zc > 0 ? (nout + zc - 1) / zc : 1;
+  return (long)nz * ((K + 31) / 32) * 9 * x6_wst(np);
+}
+
+hipError_t launch_pack_x6(const WView& wv, int K, int nout, int zc, void* out, hipStream_t s) {
+  const long total = x6_pack_elems(K, nout, zc);
+  if (total < 0 || wv.taps != 9) return hipErrorInvalidValue;
+  const int np = x6_np(nout, zc);
+  const int nz = zc > 0 ? (nout + zc - 1) / zc : 1;
+  WView v = wv;
+  if (zc > 0) v.sZ = (long)zc * wv.sN;  // block z = output channels [z*zc, z*zc + zc)
+  long blocks = ((long)nz * ((K + 31) / 32) * 9 * np * 32 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_pack_x6, dim3((unsigned)blocks), dim3(256), 0, s, v, K,
+                     zc > 0 ? zc : nout, np, (K + 31) / 32, nz, zc, nout,
+                     static_cast<__bf16*>(out));
+  return hipGetLastError();
+}
+
+// Tile height 8/4 rows: the fewest rounds of resident workgroups, each weighed by its length
+// (as pick_mt in conv.hip; per-tile efficiency of the shorter tiles from the halo overhead).
+template <int NT>
+static int x6_pick_mt(const FwdArgs& a, int nz) {
+  const int mts[2] = {2, 1};
+  const int occ[2] = {XCfg<NT, 2>::OCC, XCfg<NT, 1>::OCC};
+  const double eff[2] = {1.0, 1.2};
+  int mt = 1;
+  double best = 1e30;
+  for (int i = 0; i < 2; ++i) {
+    const long blocks = (long)a.N * ((a.OH + 4 * mts[i] - 1) / (4 * mts[i])) * ((a.OW + 15) / 16) * nz;
+    const long slots = 256L * occ[i];
+    const double cost = (double)((blocks + slots - 1) / slots) * occ[i] * mts[i] * eff[i];
+    if (cost < best - 1e-9) { best = cost; mt = mts[i]; }
+  }
+  return mt;
+}
+
+template <int NT>
+static hipError_t run_x6p(const FwdArgs& a, int nz, hipStream_t s) {
+  using C = PCfg<NT>;
+  const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
+  hipLaunchKernelGGL((k_c3x6p<NT>), dim3(tx * ty, a.N, nz), dim3(C::WAVES * 64), 0, s, a);
+  return hipGetLastError();
+}
+
+// a.wp = the launch_pack_x6 image (a.wp_z = its per-block size when a.zc > 0); every epilogue
+// and output layout of k_fwd
+hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
+  const int np = x6_np(a.NOUT, a.zc);
+  if (np == 0 || (a.zc > 0 && a.zc != np)) return hipErrorInvalidValue;
+  const int nz = a.zc > 0 ? (a.NOUT + a.zc - 1) / a.zc : 1;
+  // large grids: the pipelined 16-row kernel (one workgroup per CU, >= 2 rounds of tiles)
+  const long tiles16 = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16) * nz;
+  static const bool no_pipe = getenv("DN_X6_NOPIPE") != nullptr;  // A/B probe
+  if (!no_pipe && tiles16 >= 512 && ((a.in_stride | a.in_off | a.K) & 3) == 0)
+    return np == 48 ? run_x6p<3>(a, nz, s) : run_x6p<6>(a, nz, s);
+  if (np == 48) {
+    return x6_pick_mt<3>(a, nz) == 2 ? run_x6<3, 2>(a, nz, s) : run_x6<3, 1>(a, nz, s);
+  }
+  return x6_pick_mt<6>(a, nz) == 2 ? run_x6<6, 2>(a, nz, s) : run_x6<6, 1>(a, nz, s);
+}
+
+}  // namespace dn

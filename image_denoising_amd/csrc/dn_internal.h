@@ -188,6 +188,10 @@ hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, 
 
 // ---- mixed-precision (bf16 MFMA) 3x3 forward (conv_bf16.hip) ----
 long bf16_pack_elems(int K, int nout, int ksize = 3);
+// ---- fp32 3x3 conv on the bf16 matrix cores by three-way operand splitting (conv_x6.hip) ----
+long x6_pack_elems(int K, int nout, int zc);  // bf16 elements of a pre-split weight image
+hipError_t launch_pack_x6(const WView& wv, int K, int nout, int zc, void* out, hipStream_t s);
+hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s);
 hipError_t launch_pack_bf16(const WView& wv, int K, int nout, void* out, hipStream_t s,
                             int ksize = 3);
 hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize = 3);

@@ -137,6 +137,17 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
     }
     p.packBF[i] = alloc_f((e + 1) / 2);
   }
+  for (int i = 0; i < NL; ++i) {  // bf16x6 (split fp32) images of the 3x3 layers
+    const Layer& L = p.P.L[i];
+    p.packX[i] = -1;
+    if (i == ENC0 || L.deconv || L.k != 3) continue;
+    const long e = x6_pack_elems(L.cin, L.cout, 0);
+    if (e < 0) {
+      err = std::string("no bf16x6 forward tile for layer ") + kNames[i];
+      return false;
+    }
+    p.packX[i] = alloc_f((e + 1) / 2);
+  }
   p.fwd_floats = off;
   if (bwd) {
     p.g_nb = alloc(0, 96);
@@ -168,6 +179,18 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
       p.packB[i] = alloc_f(n);
     }
     p.packHB = alloc_f(2 * HEAD_LW);
+    for (int i = 0; i < NL; ++i) {  // bf16x6 data-gradient images of the 3x3 layers
+      const Layer& L = p.P.L[i];
+      p.packXB[i] = -1;
+      if (i == ENC0 || L.deconv || L.k != 3) continue;
+      const int nout = dgrad_nout(p, i);
+      const long e = x6_pack_elems(L.cout, nout, x6_dgrad_zc(nout));
+      if (e < 0) {
+        err = std::string("no bf16x6 data-gradient tile for layer ") + kNames[i];
+        return false;
+      }
+      p.packXB[i] = alloc_f((e + 1) / 2);
+    }
     // slab: max over layers of splits * (W + b)
     long slab = 0;
     for (int i = 0; i < NL; ++i) {
@@ -194,6 +217,8 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
   p.with_bwd = bwd;
   return true;
 }
+
+int x6_dgrad_zc(int nout) { return nout <= 96 ? 0 : 48; }
 
 // channels of the data gradient a layer's backward must produce
 int dgrad_nout(const Plan& p, int i) {
@@ -340,20 +365,33 @@ hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, 
 // forward: arch_unet.py:194-260 (non-blind-spot branch)
 // ------------------------------------------------------------------------------------
 dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
-                       hipStream_t s, bool bf16) {
+                       hipStream_t s, int prec) {
+  const bool bf16 = prec == DN_PREC_BF16, x6 = prec == DN_PREC_FP32_X6;
   const int N = p.N, nf = p.nf, C = p.C;
   auto H = [&](int l) { return p.H >> l; };
   auto Wd = [&](int l) { return p.W >> l; };
   auto Wt = [&](int i) { return ws + p.packF[i]; };  // packed forward weights
   auto Bs = [&](int i) { return prm + p.P.L[i].woff + p.P.L[i].wcount; };
   auto V = [&](long off, int stride, int coff = 0) { return View{ws + off, stride, coff}; };
-  // every 3x3 layer (enc_conv1..dec_conv1b): the fp32 kernel, or the bf16 one (bf16 operands,
-  // fp32 accumulation / bias / activation / storage)
+  // every 3x3 layer (enc_conv1..dec_conv1b): the fp32 kernel, the bf16x6 one (split fp32
+  // operands on the bf16 matrix cores), or the bf16 one (bf16 operands, fp32 accumulation /
+  // bias / activation / storage)
   auto conv_forward = [&](const View& in, int Nn, int h, int w, int K, const float* wp,
                           const float* b, int cout, int ksize, int act, const View& out,
                           int layout, hipStream_t st) -> hipError_t {
     int i = ENC1;
     while (i < NL && Wt(i) != wp) ++i;
+    if (x6 && i < NL && p.packX[i] >= 0) {
+      FwdArgs a{};
+      a.in = in.p; a.in_stride = in.stride; a.in_off = in.off; a.IHt = h; a.IWt = w;
+      a.N = Nn; a.OH = h; a.OW = w; a.K = K; a.NOUT = cout;
+      // dec_conv1a reads [up1 | x | zero pad] (c1s = c1k rounded to 4): taking the zero pad
+      // channel as a reduction channel (its packed weights are zero) keeps K % 4 == 0
+      if (i == D1A) a.K = p.c1s;
+      a.wp = ws + p.packX[i]; a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
+      a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = layout;
+      return launch_fwd_x6(a, st);
+    }
     if (!bf16 || i == NL || p.packBF[i] < 0)
       return dn::conv_forward(in, Nn, h, w, K, wp, b, cout, ksize, act, out, layout, st);
     FwdArgs a{};
@@ -387,6 +425,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     else if (L.deconv) DN_TRY(pack_deconv_fwd(w, L.cin, L.cout, ws + p.packF[i], s));
     else if (bf16) DN_TRY(launch_pack_bf16(conv_fwd_view(w, L.cin, 3), L.cin, L.cout,
                                            ws + p.packBF[i], s));
+    else if (x6) DN_TRY(launch_pack_x6(conv_fwd_view(w, L.cin, 3), L.cin, L.cout, 0,
+                                       ws + p.packX[i], s));
     else DN_TRY(pack_conv_fwd(w, L.cin, L.cout, L.k, ws + p.packF[i], s));
   }
   // enc_conv0, fused with pool0 = x -> channels [2nf, 2nf+C) of the up1 concat buffer
@@ -449,6 +489,19 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
                             View{y, p.OC, 0}, OUT_NCHW, s));
     return DN_OK;
   }
+  if (x6) {  // dec_conv1b on the bf16x6 kernel, then nin_a, nin_b, nin_c on the fp32 1x1 kernel
+    DN_TRY(conv_forward(V(p.d1a, 96), N, H(0), Wd(0), 96, Wt(D1B), Bs(D1B), 96, 3, 1,
+                        V(p.d1b, 96), OUT_NHWC, s));
+    for (int i = NINA; i <= NINC; ++i)
+      DN_TRY(pack_conv_fwd(prm + p.P.L[i].woff, 96, p.P.L[i].cout, 1, ws + p.packF[i], s));
+    DN_TRY(dn::conv_forward(V(p.d1b, 96), N, H(0), Wd(0), 96, Wt(NINA), Bs(NINA), 96, 1, 1,
+                            V(p.na, 96), OUT_NHWC, s));
+    DN_TRY(dn::conv_forward(V(p.na, 96), N, H(0), Wd(0), 96, Wt(NINB), Bs(NINB), 96, 1, 1,
+                            V(p.nb, 96), OUT_NHWC, s));
+    DN_TRY(dn::conv_forward(V(p.nb, 96), N, H(0), Wd(0), 96, Wt(NINC), Bs(NINC), p.OC, 1, 0,
+                            View{y, p.OC, 0}, OUT_NCHW, s));
+    return DN_OK;
+  }
   // dec_conv1b + nin_a + nin_b + nin_c in one kernel (arch_unet.py:251-257); the
   // intermediate activations are written only when a backward will read them
   DN_TRY(launch_pack_head(conv_fwd_view(prm + p.P.L[NINA].woff, 96, 1),
@@ -476,7 +529,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
 // post-activation output); skip gradients are accumulated into the concat-gradient buffers.
 // ------------------------------------------------------------------------------------
 dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* ws,
-                        hipStream_t s) {
+                        hipStream_t s, int prec) {
+  const bool x6 = prec == DN_PREC_FP32_X6;
   const int N = p.N, nf = p.nf, C = p.C;
   auto H = [&](int l) { return p.H >> l; };
   auto Wd = [&](int l) { return p.W >> l; };
@@ -487,9 +541,35 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   for (int i = ENC1; i < NINA; ++i) {  // flipped/transposed weight images for the data gradients
     const Layer& L = p.P.L[i];
     const float* w = prm + L.woff;
-    if (L.deconv) DN_TRY(pack_deconv_dgrad(w, L.cout, L.cin, ws + p.packB[i], s));
-    else DN_TRY(pack_conv_dgrad(w, L.cin, dgrad_nout(p, i), L.cout, L.k, ws + p.packB[i], s));
+    if (L.deconv) {
+      DN_TRY(pack_deconv_dgrad(w, L.cout, L.cin, ws + p.packB[i], s));
+    } else if (x6 && p.packXB[i] >= 0) {
+      const int nout = dgrad_nout(p, i);
+      DN_TRY(launch_pack_x6(conv_dgrad_view(w, L.cin, 3), L.cout, nout, x6_dgrad_zc(nout),
+                            ws + p.packXB[i], s));
+    } else {
+      DN_TRY(pack_conv_dgrad(w, L.cin, dgrad_nout(p, i), L.cout, L.k, ws + p.packB[i], s));
+    }
   }
+  // 3x3 data gradients: the fp32 kernel or the bf16x6 one
+  auto conv_dgrad = [&](const View& dz, int Nn, int h, int w, int cout, const float* wp, int nout,
+                        int ksize, int epi, const View& mask, const View& dx,
+                        hipStream_t st) -> hipError_t {
+    int i = ENC1;
+    while (i < NL && Wt(i) != wp) ++i;
+    if (!x6 || i == NL || p.packXB[i] < 0 || ksize != 3)
+      return dn::conv_dgrad(dz, Nn, h, w, cout, wp, nout, ksize, epi, mask, dx, st);
+    FwdArgs a{};
+    a.in = dz.p; a.in_stride = dz.stride; a.in_off = dz.off; a.IHt = h; a.IWt = w;
+    a.N = Nn; a.OH = h; a.OW = w; a.K = cout; a.NOUT = nout;
+    a.zc = x6_dgrad_zc(nout);
+    a.wp = ws + p.packXB[i];
+    a.wp_z = a.zc ? x6_pack_elems(cout, nout, a.zc) / ((nout + a.zc - 1) / a.zc) : 0;
+    a.bias = nullptr; a.epi = epi;
+    a.out = dx.p; a.out_stride = dx.stride; a.out_off = dx.off; a.out_layout = OUT_NHWC;
+    a.mask = mask.p; a.mask_stride = mask.stride; a.mask_off = mask.off;
+    return launch_fwd_x6(a, st);
+  };
   const View none{nullptr, 0, 0};
   const int OC = p.OC;
 

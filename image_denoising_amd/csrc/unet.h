@@ -41,6 +41,7 @@ struct Plan {
   long packF[NL];               // packed forward weight images
   long packH;                   // fused head: nin_a | nin_b images (2 x HEAD_LW)
   long packBF[NL];              // bf16 images of the 3x3 layers (mixed-precision forward)
+  long packX[NL];               // pre-split bf16x6 images of the 3x3 layers (forward)
   long fwd_floats;
   // gradients
   long g_nb, g_na, g_d1b, g_d1a, g_c1;
@@ -48,6 +49,7 @@ struct Plan {
   long g_a6, g_p5, g_a0, g_a1;
   long xin;                     // compact NCHW copy of the network input (weight gradients)
   long packB[NL];               // packed data-gradient weight images
+  long packXB[NL];              // pre-split bf16x6 data-gradient images of the 3x3 layers
   long packHB;                  // fused head backward: nin_b^T | nin_a^T images
   long slab, slab_floats;
   int splits[NL];
@@ -61,10 +63,14 @@ int layer_level(int i);
 int dgrad_nout(const Plan& p, int i);
 bool build_params(const dn_unet_cfg& c, ParamLayout& P, std::string& err);
 bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, std::string& err);
+// prec: DN_PREC_FP32 (fp32 matrix cores), DN_PREC_FP32_X6 (3x3 layers on the bf16 matrix cores
+// by three-way operand splitting, fp32-accurate), DN_PREC_BF16 (forward only, bf16 operands)
 dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
-                       hipStream_t s, bool bf16 = false);
+                       hipStream_t s, int prec = DN_PREC_FP32);
 dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* ws,
-                        hipStream_t s);
+                        hipStream_t s, int prec = DN_PREC_FP32);
+// zc of the bf16x6 data gradient of a 3x3 layer producing nout channels (0: one block)
+int x6_dgrad_zc(int nout);
 
 WView conv_fwd_view(const float* w, int K, int ksize);
 WView conv_dgrad_view(const float* w, int cin_total, int ksize);

@@ -38,6 +38,16 @@ typedef int dn_status;
 #define DN_ERR_WORKSPACE (-2)   /* workspace too small */
 #define DN_ERR_HIP (-3)         /* a HIP runtime call failed */
 
+/* Arithmetic of the U-Net's 3x3 convolutions (dn_unet_forward_prec / dn_unet_backward_prec):
+   DN_PREC_FP32     fp32 operands on the fp32 matrix cores (v_mfma_f32_16x16x4_f32);
+   DN_PREC_FP32_X6  fp32 operands split exactly into three bf16 pieces, the six piece products of
+                    order <= 2 on the bf16 matrix cores with fp32 accumulation: fp32-accurate
+                    (error of an fp32 dot product), 2.67x the matrix-core ceiling;
+   DN_PREC_BF16     forward only: bf16-rounded operands (the adapter-finetune frozen base). */
+#define DN_PREC_FP32 0
+#define DN_PREC_BF16 1
+#define DN_PREC_FP32_X6 2
+
 /* U-Net configuration: arch_unet.py:101-106 UNet(in_nc, out_nc, n_feature, blindspot=False). */
 typedef struct dn_unet_cfg {
   int in_nc;      /* input channels  (1 or 3)  */
@@ -79,6 +89,14 @@ dn_status dn_unet_forward_bf16(const dn_unet_cfg* cfg, const float* params, cons
 dn_status dn_unet_backward(const dn_unet_cfg* cfg, const float* params, const float* dy,
                            float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
                            void* stream);
+/* dn_unet_forward / dn_unet_backward with the 3x3 convolutions' arithmetic chosen by
+   precision (DN_PREC_*; the backward takes DN_PREC_FP32 or DN_PREC_FP32_X6). */
+dn_status dn_unet_forward_prec(const dn_unet_cfg* cfg, const float* params, const float* x,
+                               float* y, int N, int H, int W, void* ws, size_t ws_bytes,
+                               int precision, void* stream);
+dn_status dn_unet_backward_prec(const dn_unet_cfg* cfg, const float* params, const float* dy,
+                                float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
+                                int precision, void* stream);
 
 /* Debug/introspection: (offset_floats, channel_stride, level) of every NHWC buffer of the
    workspace plan, in the order c1 a0 a1 c2..c5 a2..a5 p5 a6 d{2..5}a d{2..5}b d1a d1b nin_a nin_b
@@ -159,6 +177,18 @@ size_t dn_conv2d_bf16_pack_size(int Cin, int Cout);
 dn_status dn_conv2d_forward_bf16(const float* x, int x_stride, int N, int H, int W, int Cin,
                                  const float* w, const float* b, int Cout, int act, float* y,
                                  int y_stride, void* pack_ws, size_t pack_bytes, void* stream);
+/* 3x3/pad1 forward and data gradient at fp32 accuracy on the bf16 matrix cores (DN_PREC_FP32_X6:
+   operands split exactly into three bf16 pieces, six piece products accumulated in fp32).
+   Forward: Cout <= 96.  Data gradient: any Cin (blocks of 48 channels past 96).  Same argument
+   meaning as dn_conv2d_forward (ksize 3) / dn_conv2d_backward_data. */
+size_t dn_conv2d_x6_pack_size(int Cin, int Cout, int backward_data);
+dn_status dn_conv2d_forward_x6(const float* x, int x_stride, int N, int H, int W, int Cin,
+                               const float* w, const float* b, int Cout, int act, float* y,
+                               int y_stride, void* pack_ws, size_t pack_bytes, void* stream);
+dn_status dn_conv2d_backward_data_x6(const float* dz, int N, int H, int W, int Cout,
+                                     const float* w, int Cin, const float* mask, int mask_stride,
+                                     int accumulate, float* dx, int dx_stride, void* pack_ws,
+                                     size_t pack_bytes, void* stream);
 /* dx = conv^T(dz) [* leaky'(mask)] : data gradient (mask nullable; mask_stride). If accumulate,
    dx += result.  dx stride dx_stride. */
 dn_status dn_conv2d_backward_data(const float* dz, int N, int H, int W, int Cout, const float* w,

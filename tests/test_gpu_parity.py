@@ -267,21 +267,27 @@ def test_maxpool_forward_backward(ties):
 # ---------------------------------------------------------------------------------------
 # whole U-Net vs reference fixtures
 # ---------------------------------------------------------------------------------------
-def _net(C):
+def _net(C, prec="fp32"):
     from image_denoising_amd import UNet
 
     torch.manual_seed(0)
-    return UNet(in_nc=C, out_nc=C, n_feature=48).to(DEV)
+    return UNet(in_nc=C, out_nc=C, n_feature=48).to(DEV).set_precision(prec)
 
 
+# the whole-network parity tests run both 3x3-conv arithmetics (DN_PREC_*): fp32 on the fp32
+# matrix cores and the split-bf16 fp32 ("fp32_x6") on the bf16 ones, at the same tolerances
+PRECS = ["fp32", "fp32_x6"]
+
+
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("C,name", [(1, "unet_c1.npz"), (3, "unet_c3.npz")])
-def test_unet_forward_backward_vs_reference(golden, C, name):
+def test_unet_forward_backward_vs_reference(golden, C, name, prec):
     """Output within 1e-4 of the reference; parameter gradients as close to the exact (fp64)
     gradient as the reference's own fp32 gradients are."""
     from oracle.unet_ref import forward, layer_table
 
     g = golden(name)
-    net = _net(C)
+    net = _net(C, prec)
     x = torch.from_numpy(g["x"]).to(DEV)
     with torch.no_grad():
         y0 = net(x)
@@ -365,15 +371,16 @@ def _device_activations(net, x, r):
     return y.cpu(), dflat.cpu(), acts
 
 
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("C,N,H,W", [(1, 2, 64, 64), (1, 1, 32, 32), (1, 3, 32, 96),
                                      (3, 2, 64, 32), (1, 2, 128, 128)])
-def test_unet_unit_gain_fwd_bwd_vs_fp64(C, N, H, W):
+def test_unet_unit_gain_fwd_bwd_vs_fp64(C, N, H, W, prec):
     """Every level contributes O(1) (unit-gain weights).  Forward vs fp64 within 1e-4; all 50
     parameter gradients vs an fp64 backward that takes LeakyReLU slopes and pool routing from
     the device's own fp32 activations (so only the rounding of the linear ops remains)."""
     from oracle.unet_ref import forward, layer_table
 
-    net = _net(C)
+    net = _net(C, prec)
     _unit_gain(net)
     x = torch.rand(N, C, H, W, generator=torch.Generator().manual_seed(1))
     r = torch.randn(N, C, H, W, generator=torch.Generator().manual_seed(2))
@@ -459,12 +466,13 @@ def test_adam_matches_torch_adam():
     assert float((pg.cpu() != pt.detach()).float().mean()) < 0.05
 
 
-def test_n2n_step_vs_reference(golden):
+@pytest.mark.parametrize("prec", PRECS)
+def test_n2n_step_vs_reference(golden, prec):
     from image_denoising_amd import N2NTrainer
     from image_denoising_amd.arch_unet import reference_init
 
     g = golden("n2n_step.npz")
-    net = _net(1)
+    net = _net(1, prec)
     torch.manual_seed(0)
     pre = reference_init(1, 1, 48).numpy()
     tr = N2NTrainer(net, lr=3e-4, n_epoch=100, increase_ratio=2.0)
@@ -482,13 +490,14 @@ def test_n2n_step_vs_reference(golden):
     assert np.abs(upd - ref_upd).max() <= 6.1e-4  # never more than 2*lr apart
 
 
-def test_n2n_step_deterministic():
+@pytest.mark.parametrize("prec", PRECS)
+def test_n2n_step_deterministic(prec):
     from image_denoising_amd import N2NTrainer
 
     clean = torch.rand(4, 1, 64, 64, device=DEV)
     res = []
     for _ in range(2):
-        net = _net(1)
+        net = _net(1, prec)
         tr = N2NTrainer(net, seed=3)
         for e in range(2):
             tr.train_step(clean, epoch=1)
@@ -496,13 +505,14 @@ def test_n2n_step_deterministic():
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
-def test_config1_full_size_step_properties():
+@pytest.mark.parametrize("prec", PRECS)
+def test_config1_full_size_step_properties(prec):
     """BASELINE config 1 (bs=64, 256x256x1): one full N2N step; per-image independence lets a
     single image be checked against the oracle at full resolution."""
     from image_denoising_amd import N2NTrainer
     from oracle import unet_ref
 
-    net = _net(1)
+    net = _net(1, prec)
     g = torch.Generator(device="cpu").manual_seed(0)
     clean = F.interpolate(torch.rand(64, 1, 32, 32, generator=g), size=(256, 256),
                           mode="bilinear", align_corners=False).to(DEV)

@@ -1,0 +1,140 @@
+"""The split-bf16 fp32 3x3 convolution (DN_PREC_FP32_X6, csrc/conv_x6.hip) vs an fp64 reference,
+through the C-ABI.  The claim under test is fp32 accuracy: its error against fp64 must be of the
+size of the fp32 matrix-core kernel's own (same shapes, same inputs), and within the 1e-4
+north-star tolerance by two orders of magnitude.  Needs an MI355X."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+# |err| / max|ref| against fp64; an fp32 dot product of K ~ 1e3 terms lands near 1e-7
+X6_TOL = 2e-6
+
+
+def rel_err(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def L():
+    from image_denoising_amd import _lib
+
+    return _lib
+
+
+def S():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+def _forward(x, w, b, act, x6):
+    _lib = L()
+    N, cin, H, W = x.shape
+    cout = w.shape[0]
+    xg, wg, bg = nhwc(x).to(DEV), w.to(DEV), b.to(DEV)
+    y = torch.empty(N, H, W, cout, device=DEV)
+    if x6:
+        pk = _lib.scratch(_lib.lib().dn_conv2d_x6_pack_size(cin, cout, 0), DEV)
+        _lib.call("dn_conv2d_forward_x6", xg.data_ptr(), cin, N, H, W, cin, wg.data_ptr(),
+                  bg.data_ptr(), cout, act, y.data_ptr(), cout, pk.data_ptr(), pk.numel(), S())
+    else:
+        pk = _lib.scratch(_lib.lib().dn_conv2d_pack_size(cin, cout, 3, 0), DEV)
+        _lib.call("dn_conv2d_forward", xg.data_ptr(), cin, N, H, W, cin, wg.data_ptr(),
+                  bg.data_ptr(), cout, 3, act, y.data_ptr(), cout, pk.data_ptr(), pk.numel(), S())
+    return nchw(y.cpu())
+
+
+@pytest.mark.parametrize("cin,cout,N,H,W", [
+    (48, 48, 2, 32, 32), (48, 96, 1, 20, 36), (96, 96, 2, 16, 16), (96, 96, 2, 64, 64),
+    (144, 96, 2, 16, 32), (99, 96, 2, 32, 32), (97, 48, 1, 8, 8), (3, 48, 2, 32, 32),
+    (96, 96, 64, 32, 32), (48, 48, 8, 4, 4),
+    # >= 512 16x16 tiles: the pipelined 8-wave kernel (k_c3x6p)
+    (96, 96, 8, 128, 128), (48, 48, 8, 128, 128), (144, 96, 8, 128, 128), (3, 48, 2, 256, 256),
+])
+@pytest.mark.parametrize("act", [0, 1])
+def test_x6_forward_vs_fp64(cin, cout, N, H, W, act):
+    g = torch.Generator().manual_seed(cin * 1000 + cout + H)
+    x = torch.randn(N, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * 0.1
+    b = torch.randn(cout, generator=g) * 0.1
+    y6 = _forward(x, w, b, act, True)
+    y32 = _forward(x, w, b, act, False)
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1)
+    if act:
+        ref = F.leaky_relu(ref, 0.2)
+    e6, e32 = rel_err(y6.numpy(), ref.numpy()), rel_err(y32.numpy(), ref.numpy())
+    assert e6 < X6_TOL, (e6, e32)
+    assert e6 < 4 * e32 + 1e-7, (e6, e32)  # fp32-class, not bf16-class (~4e-3)
+
+
+def _dgrad(dz, w, cin, mode, mask, base, x6):
+    _lib = L()
+    N, cout, H, W = dz.shape
+    dx = nhwc(base).to(DEV) if mode == "accum" else torch.zeros(N, H, W, cin, device=DEV)
+    mg, dzg, wg = nhwc(mask).to(DEV), nhwc(dz).to(DEV), w.to(DEV)
+    name = "dn_conv2d_backward_data_x6" if x6 else "dn_conv2d_backward_data"
+    size = (_lib.lib().dn_conv2d_x6_pack_size(cin, cout, 1) if x6
+            else _lib.lib().dn_conv2d_pack_size(cin, cout, 3, 1))
+    pk = _lib.scratch(size, DEV)
+    args = [dzg.data_ptr(), N, H, W, cout, wg.data_ptr(), cin]
+    if not x6:
+        args.append(3)
+    args += [mg.data_ptr() if mode == "mask" else None, cin, 1 if mode == "accum" else 0,
+             dx.data_ptr(), cin, pk.data_ptr(), pk.numel(), S()]
+    _lib.call(name, *args)
+    return nchw(dx.cpu())
+
+
+@pytest.mark.parametrize("cin,cout,N,H,W", [
+    (48, 48, 2, 32, 32), (96, 96, 2, 16, 16), (144, 96, 2, 16, 16), (48, 96, 2, 8, 8),
+    (96, 48, 1, 20, 36), (144, 96, 1, 64, 32),
+    (96, 96, 8, 128, 128), (144, 96, 3, 128, 112), (48, 48, 8, 128, 128),  # pipelined kernel
+])
+@pytest.mark.parametrize("mode", ["plain", "mask", "accum"])
+def test_x6_backward_data_vs_fp64(cin, cout, N, H, W, mode):
+    g = torch.Generator().manual_seed(cin + 7 * cout + H)
+    x = torch.randn(N, cin, H, W, generator=g).double().requires_grad_(True)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * 0.1
+    dz = torch.randn(N, cout, H, W, generator=g)
+    mask = torch.randn(N, cin, H, W, generator=g)
+    base = torch.randn(N, cin, H, W, generator=g)
+    F.conv2d(x, w.double(), None, padding=1).backward(dz.double())
+    ref = x.grad
+    if mode == "mask":
+        ref = torch.where(mask.double() > 0, ref, ref * 0.2)
+    if mode == "accum":
+        ref = ref + base.double()
+    d6 = _dgrad(dz, w, cin, mode, mask, base, True)
+    d32 = _dgrad(dz, w, cin, mode, mask, base, False)
+    e6, e32 = rel_err(d6.numpy(), ref.numpy()), rel_err(d32.numpy(), ref.numpy())
+    assert e6 < X6_TOL, (e6, e32)
+    assert e6 < 4 * e32 + 1e-7, (e6, e32)
+
+
+def test_x6_exact_on_bf16_representable_inputs():
+    """Operands that are exact in bf16 leave pieces 1 and 2 zero: the result is then the exact
+    product sum rounded once per MFMA accumulation, equal to fp64 to fp32 rounding."""
+    g = torch.Generator().manual_seed(5)
+    q = lambda t: t.to(torch.bfloat16).float()
+    x = q(torch.randn(1, 96, 16, 16, generator=g))
+    w = q(torch.randn(96, 96, 3, 3, generator=g) * 0.1)
+    b = torch.zeros(96)
+    y6 = _forward(x, w, b, 0, True)
+    ref = F.conv2d(x.double(), w.double(), None, padding=1)
+    assert rel_err(y6.numpy(), ref.numpy()) < 1e-6
