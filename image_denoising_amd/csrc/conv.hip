@@ -68,6 +68,112 @@ __device__ __forceinline__ void glds16(const float* g, float* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
+// Tail of the fused output head (arch_unet.py:251-257) for k_nin_head: acc holds a 4*MT x
+// 16-pixel tile of the 96 dec_conv1b channels in the 16x16 MFMA C/D map (PRE_ACT: before its
+// bias + LeakyReLU, which are applied here and optionally saved to hd.d1b; else the activated
+// values).  lds must hold HEAD_LW floats and be free.  k_fwd<..., HEAD> keeps its own inline copy
+// of the PRE_ACT form: through this function its 168-register budget (3 workgroups per CU)
+// spills.
+template <int MT, bool PRE_ACT>
+__device__ __forceinline__ void head_tail(const FwdArgs& a, const HeadArgs& hd,
+                                          f32x4 (&acc)[MT][6], float* lds, int ty0, int tx0,
+                                          int n) {
+  constexpr int NT = 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+    // acc[m][q][r] = dec_conv1b pre-activation at pixel (row m, x = li), channel
+    // q*16 + 4*lg + r.  As the B operand of the next 16x16x4 MFMA, register r of fragment q
+    // supplies k = channel q*16 + 4g + r for lane group g: nin_a/nin_b consume the tile
+    // where it is, with the k order permuted the same way in their weight reads.
+    // Two phases through ONE image slot (38 KiB, so three workgroups fit a CU): nin_a for
+    // all rows in place (acc <- na), then nin_b + nin_c.
+    for (int p = wave; p < HEAD_LW / 256; p += 4) glds16(hd.wp + p * 256 + lane * 4, lds + p * 256);
+    auto bias_act = [](f32x4& v, float4 b) {
+      v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * 0.2f;
+    };
+    auto save = [&](float* dst, long pix, int q, const f32x4& v) {
+      *reinterpret_cast<float4*>(dst + pix * 96 + q * 16 + 4 * lg) = make_float4(v[0], v[1], v[2], v[3]);
+    };
+    // 1x1 GEMM on the transposed tile: out[f] = W^T-image x in (k order = the tile's)
+    auto gemm96 = [&](const float* w, const f32x4 (&in)[NT], f32x4 (&out)[NT]) {
+#pragma unroll
+      for (int f = 0; f < NT; ++f) out[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float* wr = w + (q * 16 + 4 * lg + r) * HEAD_WS + li;
+#pragma unroll
+          for (int f = 0; f < NT; ++f) out[f] = mfma4(wr[f * 16], in[q][r], out[f]);
+        }
+    };
+    if (PRE_ACT) {
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        const float4 b = *reinterpret_cast<const float4*>(a.bias + q * 16 + 4 * lg);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) bias_act(acc[m][q], b);
+      }
+    }
+    const int gx = tx0 + li;
+    if (PRE_ACT && hd.d1b) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int gy = ty0 + wave * MT + m;
+        if (gy < a.OH && gx < a.OW)
+#pragma unroll
+          for (int q = 0; q < NT; ++q) save(hd.d1b, ((long)n * a.OH + gy) * a.OW + gx, q, acc[m][q]);
+      }
+    }
+    __syncthreads();  // nin_a image landed
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {  // phase 1: acc[m] <- na
+      const int gy = ty0 + wave * MT + m;
+      f32x4 u[NT];
+      gemm96(lds, acc[m], u);
+#pragma unroll
+      for (int f = 0; f < NT; ++f) {
+        bias_act(u[f], *reinterpret_cast<const float4*>(hd.ba + f * 16 + 4 * lg));
+        acc[m][f] = u[f];
+      }
+      if (hd.na && gy < a.OH && gx < a.OW)
+#pragma unroll
+        for (int f = 0; f < NT; ++f) save(hd.na, ((long)n * a.OH + gy) * a.OW + gx, f, acc[m][f]);
+    }
+    __syncthreads();  // everyone done with nin_a
+    for (int p = wave; p < HEAD_LW / 256; p += 4)
+      glds16(hd.wp + HEAD_LW + p * 256 + lane * 4, lds + p * 256);
+    __syncthreads();  // nin_b image landed
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {  // phase 2: nb, then nin_c
+      const int gy = ty0 + wave * MT + m;
+      const bool ok = gy < a.OH && gx < a.OW;
+      const long pix = ((long)n * a.OH + gy) * a.OW + gx;
+      f32x4 v[NT];
+      gemm96(lds, acc[m], v);
+#pragma unroll
+      for (int f = 0; f < NT; ++f) {
+        bias_act(v[f], *reinterpret_cast<const float4*>(hd.bb + f * 16 + 4 * lg));
+        if (hd.nb && ok) save(hd.nb, pix, f, v[f]);
+      }
+      // nin_c: per-lane partial over its 24 channels, then across the 4 lane groups
+      for (int o = 0; o < hd.oc; ++o) {
+        float t = 0.f;
+#pragma unroll
+        for (int f = 0; f < NT; ++f) {
+          const float4 w = *reinterpret_cast<const float4*>(hd.wc + o * 96 + f * 16 + 4 * lg);
+          t = fmaf(w.x, v[f][0], t); t = fmaf(w.y, v[f][1], t);
+          t = fmaf(w.z, v[f][2], t); t = fmaf(w.w, v[f][3], t);
+        }
+        t += __shfl_xor(t, 16);
+        t += __shfl_xor(t, 32);
+        if (lg == 0 && ok) hd.y[(((long)n * hd.oc + o) * a.OH + gy) * a.OW + gx] = t + hd.bc[o];
+      }
+    }
+}
+
 template <int GATHER, int NT, int MT, bool HEAD = false>
 __global__ __launch_bounds__(256, (GATHER == G_C3 && NT == 6) ? 3 : 2) void k_fwd(
     FwdArgs a, HeadArgs hd) {
@@ -285,6 +391,31 @@ __global__ __launch_bounds__(256, (GATHER == G_C3 && NT == 6) ? 3 : 2) void k_fw
   } else {
     fwd_epilogue<NT, MT, C::PS, GATHER == G_UP>(a, acc, lds, ty0, tx0, n);
   }
+}
+
+// The same head on an already activated dec_conv1b output (hd.d1b ignored; a.in = d1b NHWC,
+// stride 96): the head of a forward whose dec_conv1b ran on another kernel (bf16x6).
+template <int MT>
+__global__ __launch_bounds__(256, 2) void k_nin_head(FwdArgs a, HeadArgs hd) {
+  __shared__ __attribute__((aligned(16))) float lds[HEAD_LW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int tiles_x = (a.OW + 15) / 16;
+  const int ty0 = (blockIdx.x / tiles_x) * 4 * MT, tx0 = (blockIdx.x % tiles_x) * 16;
+  const int n = blockIdx.y, gx = tx0 + li;
+  f32x4 acc[MT][6];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int gy = ty0 + wave * MT + m;
+    const bool ok = gy < a.OH && gx < a.OW;
+    const float* p = a.in + (((long)n * a.IHt + gy) * a.IWt + gx) * a.in_stride + a.in_off + 4 * lg;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const float4 v = ok ? *reinterpret_cast<const float4*>(p + q * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+      acc[m][q] = f32x4{v.x, v.y, v.z, v.w};
+    }
+  }
+  head_tail<MT, false>(a, hd, acc, lds, ty0, tx0, n);
 }
 
 // Backward of the fused head (see HeadBwdArgs).  A workgroup loads the two transposed 1x1
@@ -919,6 +1050,16 @@ hipError_t launch_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s) {
   if (a.NOUT != 96 || h.oc < 1) return hipErrorInvalidValue;
   const long tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16);
   return tiles < 1024 ? run_head<1>(a, h, s) : run_head<4>(a, h, s);
+}
+
+hipError_t launch_nin_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s) {
+  if (a.K != 96 || h.oc < 1 || ((a.in_stride | a.in_off) & 3)) return hipErrorInvalidValue;
+  const long tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16);
+  const int mt = tiles < 1024 ? 1 : 2;
+  const dim3 grid(((a.OW + 15) / 16) * ((a.OH + 4 * mt - 1) / (4 * mt)), a.N, 1);
+  if (mt == 1) hipLaunchKernelGGL((k_nin_head<1>), grid, dim3(256), 0, s, a, h);
+  else hipLaunchKernelGGL((k_nin_head<2>), grid, dim3(256), 0, s, a, h);
+  return hipGetLastError();
 }
 
 hipError_t launch_head_bwd(const HeadBwdArgs& h, hipStream_t s) {

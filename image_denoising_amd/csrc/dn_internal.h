@@ -142,6 +142,8 @@ hipError_t launch_wgrad_thin(const float* g, int g_stride, int cout, const float
                              float* slab, int splits, float* dwb, hipStream_t s);
 hipError_t launch_accumulate(float* dst, const float* src, long n, hipStream_t s);
 hipError_t launch_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);
+// nin_a -> nin_b -> nin_c on an activated dec_conv1b output (a.in, a.K = 96); h.d1b unused
+hipError_t launch_nin_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);
 hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s);
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
 hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s);

@@ -489,17 +489,21 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
                             View{y, p.OC, 0}, OUT_NCHW, s));
     return DN_OK;
   }
-  if (x6) {  // dec_conv1b on the bf16x6 kernel, then nin_a, nin_b, nin_c on the fp32 1x1 kernel
+  if (x6) {  // dec_conv1b on the bf16x6 kernel, then the fused nin_a -> nin_b -> nin_c head
     DN_TRY(conv_forward(V(p.d1a, 96), N, H(0), Wd(0), 96, Wt(D1B), Bs(D1B), 96, 3, 1,
                         V(p.d1b, 96), OUT_NHWC, s));
-    for (int i = NINA; i <= NINC; ++i)
-      DN_TRY(pack_conv_fwd(prm + p.P.L[i].woff, 96, p.P.L[i].cout, 1, ws + p.packF[i], s));
-    DN_TRY(dn::conv_forward(V(p.d1b, 96), N, H(0), Wd(0), 96, Wt(NINA), Bs(NINA), 96, 1, 1,
-                            V(p.na, 96), OUT_NHWC, s));
-    DN_TRY(dn::conv_forward(V(p.na, 96), N, H(0), Wd(0), 96, Wt(NINB), Bs(NINB), 96, 1, 1,
-                            V(p.nb, 96), OUT_NHWC, s));
-    DN_TRY(dn::conv_forward(V(p.nb, 96), N, H(0), Wd(0), 96, Wt(NINC), Bs(NINC), p.OC, 1, 0,
-                            View{y, p.OC, 0}, OUT_NCHW, s));
+    DN_TRY(launch_pack_head(conv_fwd_view(prm + p.P.L[NINA].woff, 96, 1),
+                            conv_fwd_view(prm + p.P.L[NINB].woff, 96, 1), ws + p.packH, s));
+    FwdArgs a{};
+    a.in = ws + p.d1b; a.in_stride = 96; a.in_off = 0; a.IHt = H(0); a.IWt = Wd(0);
+    a.N = N; a.OH = H(0); a.OW = Wd(0); a.K = 96; a.NOUT = 96;
+    HeadArgs h{};
+    h.wp = ws + p.packH;
+    h.ba = Bs(NINA); h.bb = Bs(NINB);
+    h.wc = prm + p.P.L[NINC].woff; h.bc = Bs(NINC); h.oc = p.OC;
+    h.y = y;
+    if (p.with_bwd) { h.na = ws + p.na; h.nb = ws + p.nb; }
+    DN_TRY(launch_nin_head(a, h, s));
     return DN_OK;
   }
   // dec_conv1b + nin_a + nin_b + nin_c in one kernel (arch_unet.py:251-257); the
