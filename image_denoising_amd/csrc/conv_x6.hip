@@ -117,7 +117,8 @@ __global__ __launch_bounds__(256, 2) void k_c3x6(FwdArgs a) {
   __bf16* lw0 = lx + 3 * C::XPL;
   __bf16* lw1 = lw0 + C::WST;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int li = lane & 15, lg = lane >> 4;
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
   const int ty0 = (blockIdx.x / tiles_x) * C::TH;
@@ -272,7 +273,8 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   __bf16* lx = reinterpret_cast<__bf16*>(lds_raw);
   __bf16* ring = lx + 3 * C::XPL;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int li = lane & 15, lg = lane >> 4;
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
   const int ty0 = (blockIdx.x / tiles_x) * C::TH;
