@@ -248,9 +248,10 @@ def main():
                          "finetune.py's adapter step (frozen UNet base + OutputAdapter, configs[4])")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                     help="finetune only: bf16 = mixed-precision frozen base (BASELINE configs[4])")
-    ap.add_argument("--conv-precision", choices=["fp32", "fp32_x6"], default="fp32",
-                    help="UNet 3x3 convs: fp32 matrix cores, or fp32 operands split into three "
-                         "bf16 pieces on the bf16 matrix cores (fp32-accurate, DESIGN.md §11)")
+    ap.add_argument("--conv-precision", choices=["fp32", "fp32_x6"], default="fp32_x6",
+                    help="UNet 3x3 convs: fp32 operands split exactly into three bf16 pieces on "
+                         "the bf16 matrix cores (fp32_x6, default: fp32-accurate, DESIGN.md §11), "
+                         "or fp32 operands on the fp32 matrix cores")
     ap.add_argument("--arch", choices=["UNet", "UNetImproved"], default="UNet",
                     help="network (train.py:305-313 / finetune.py --arch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -389,8 +390,8 @@ def main():
             "step_frac_of_fp32_peak": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
             "roofline": {"bound": "mfma",
                          "kernel": ("k_fwd_bf16<NT=6,MT=4> (96->96 3x3, bf16 MFMA)" if bf else
-                                    "k_c3x6<NT=6,MT=2> (dec_conv1b 96->96 3x3 @256^2, fp32 via "
-                                    "bf16x6; peak = bf16 dense / 6)" if x6 else
+                                    "k_c3x6p<NT=6> (dec_conv1b 96->96 3x3 @256^2, fp32 as 6 "
+                                    "split-bf16 products; peak = bf16 dense / 6)" if x6 else
                                     "k_fwd<G_C3,NT=6,MT=4> (dec_conv1b 96->96 3x3 @256^2)"),
                          "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic,

@@ -1,5 +1,6 @@
 #!/bin/bash
 # HBM traffic of the dominant kernel: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes
+# (KERNEL=x6: the split-bf16 fp32 kernel of --conv-precision fp32_x6)
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
