@@ -12,10 +12,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Stage each 16-pixel row of the wave's tile through LDS, then write whole pixels: as float4
 // (NOUT contiguous channels, 1 KiB contiguous per wave store) when the layout allows, else
-// element by element (NCHW, PixelShuffle, unaligned views).  `lds` must hold 4*16*PS floats and
-// be free (the caller's main loop ended on a barrier).  UP: deconv forward, wave = parity (a,b)
-// and every wave covers all MT rows; else wave w owns rows [w*MT, w*MT+MT) and blockIdx.z is
-// the output-channel block (zc) or the scatter parity.
+// element by element (NCHW, PixelShuffle, unaligned views).  `lds` must hold waves*16*PS floats
+// and be free (the caller's main loop ended on a barrier); each wave uses only its own 16*PS.
+// UP: deconv forward, wave = parity (a,b) and every wave covers all MT rows; else wave w owns
+// rows [w*MT, w*MT+MT) and blockIdx.z is the output-channel block (zc) or the scatter parity.
 template <int NT, int MT, int PS, bool UP>
 __device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, const f32x4 (&acc)[MT][NT],
                                              float* lds, int ty0, int tx0, int n) {
@@ -40,7 +40,8 @@ __device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, const f32x4 (&acc
     for (int q = 0; q < NT; ++q)
 #pragma unroll
       for (int r = 0; r < 4; ++r) st[(4 * lg + r) * PS + q * 16 + li] = acc[m][q][r];
-    __syncthreads();
+    // st is this wave's own staging area and a wave's LDS accesses complete in order: no
+    // barrier (a __syncthreads here would also drain the previous row's global stores)
     const int gy = ty0 + wrow + m;
     if (gy < a.OH && vec_out) {
       const int NQ = nout >> 2;
@@ -112,7 +113,6 @@ __device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, const f32x4 (&acc
         a.out[oi] = v;
       }
     }
-    __syncthreads();
   }
 }
 

@@ -45,15 +45,16 @@ def dgrad(cin, cout, H, x6):  # dx [N,H,H,cin] from dz [N,H,H,cout]
     return timeit(f)
 
 
-shapes = [("fwd", 48, 48, H) for H in (256, 128, 64, 32, 16, 8)] + \
-         [("fwd", 96, 96, H) for H in (256, 128, 64, 32, 16)] + \
-         [("fwd", 144, 96, H) for H in (128, 64, 32, 16)] + [("fwd", 100, 96, 256), ("fwd", 100, 96, 128)] + \
-         [("dgrad", 48, 48, H) for H in (128, 64, 32, 16, 8, 4)] + \
-         [("dgrad", 96, 96, H) for H in (128, 64, 32, 16, 8)] + \
-         [("dgrad", 144, 96, H) for H in (64, 32, 16, 8)]
-for op, cin, cout, H in shapes:
-    fl = 2.0 * N * H * H * cin * cout * 9
-    f = fwd if op == "fwd" else dgrad
-    a, b = f(cin, cout, H, False), f(cin, cout, H, True)
-    print(f"{op:5s} {cin:3d}->{cout:3d} H{H:4d}  fp32 {a:7.3f} ms {fl/a/1e9:6.1f} TF/s   x6 {b:7.3f} ms "
-          f"{fl/b/1e9:6.1f} TF/s   {'x6' if b < a else 'fp32'}", flush=True)
+if __name__ == "__main__":
+    shapes = [("fwd", 48, 48, H) for H in (256, 128, 64, 32, 16, 8)] + \
+             [("fwd", 96, 96, H) for H in (256, 128, 64, 32, 16)] + \
+             [("fwd", 144, 96, H) for H in (128, 64, 32, 16)] + [("fwd", 100, 96, 256), ("fwd", 100, 96, 128)] + \
+             [("dgrad", 48, 48, H) for H in (128, 64, 32, 16, 8, 4)] + \
+             [("dgrad", 96, 96, H) for H in (128, 64, 32, 16, 8)] + \
+             [("dgrad", 144, 96, H) for H in (64, 32, 16, 8)]
+    for op, cin, cout, H in shapes:
+        fl = 2.0 * N * H * H * cin * cout * 9
+        f = fwd if op == "fwd" else dgrad
+        a, b = f(cin, cout, H, False), f(cin, cout, H, True)
+        print(f"{op:5s} {cin:3d}->{cout:3d} H{H:4d}  fp32 {a:7.3f} ms {fl/a/1e9:6.1f} TF/s   x6 {b:7.3f} ms "
+              f"{fl/b/1e9:6.1f} TF/s   {'x6' if b < a else 'fp32'}", flush=True)
