@@ -19,7 +19,6 @@
 //   XOR-swizzled by (row >> 1) & 3, which makes the per-lane ds_read_b128 operand reads
 //   conflict-free for every tap offset.
 #include <cstdlib>
-#include <type_traits>
 
 #include "conv_epi.h"
 
@@ -241,20 +240,18 @@ __global__ __launch_bounds__(256, 2) void k_c3x6(FwdArgs a) {
 // ------------------------------------------------------------------------------------
 template <int NT>
 struct PCfg {
-  static constexpr int WAVES = 8, MT = 2, S = 5;
+  static constexpr int WAVES = 8, MT = 2, S = 4;
   static constexpr int TW = 16, TH = WAVES * MT, IH = TH + 2, IW = TW + 2, KC = 32, NP = 16 * NT;
   static constexpr int XPIX = IH * IW;
   static constexpr int XPL = XPIX * KC;
   static constexpr int WPL = NP * KC;
-  static constexpr int WSTP = x6_wst(NP);              // stage stride in the packed image
-  static constexpr int WST = 3 * WPL;                  // bf16 per stage in LDS (no padding)
-  static constexpr int PIECES = WST * 2 / 1024;        // 1 KiB DMAs per stage
-  static_assert(PIECES * 1024 == WST * 2, "stage = whole KiBs");
-  static constexpr int PPW = (PIECES + WAVES - 1) / WAVES;  // DMAs of the busiest wave
+  static constexpr int WSTP = x6_wst(NP);              // bf16 per stage (padded)
+  static constexpr int PPW = WSTP * 2 / (WAVES * 1024);  // 1 KiB DMAs per wave per stage
+  static_assert(PPW * WAVES * 1024 == WSTP * 2, "stage = whole DMA rounds");
   static constexpr int XQ = XPIX * (KC / 4);
   static constexpr int XITEMS = (XQ + WAVES * 64 - 1) / (WAVES * 64);
   static constexpr int PS = NP + 4;
-  static constexpr int LBYTES_MAIN = 2 * 3 * XPL + 2 * S * WST;
+  static constexpr int LBYTES_MAIN = 2 * 3 * XPL + 2 * S * WSTP;
   static constexpr int LEPI = 4 * WAVES * 16 * PS;
   static constexpr int LBYTES = LBYTES_MAIN > LEPI ? LBYTES_MAIN : LEPI;
   static_assert(LBYTES <= 163840, "one workgroup per CU");
@@ -338,25 +335,14 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   // weights of stage `src_st` into ring slot `slot`: PPW DMAs of 1 KiB per wave
   auto load_w = [&](int src_st, int slot) {
     const unsigned char* src = reinterpret_cast<const unsigned char*>(wimg + (long)src_st * C::WSTP);
-    unsigned char* dst = reinterpret_cast<unsigned char*>(ring + slot * C::WST);
+    unsigned char* dst = reinterpret_cast<unsigned char*>(ring + slot * C::WSTP);
 #pragma unroll
     for (int j = 0; j < C::PPW; ++j) {
       const int piece = wave * C::PPW + j;
-      if (piece < C::PIECES)  // wave-uniform: the last waves issue fewer (or no) DMAs
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(src + piece * 1024 + lane * 16),
-            (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(src + piece * 1024 + lane * 16),
+          (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16, 0, 0);
     }
-  };
-  // s_waitcnt vmcnt(own DMAs per stage x `stages` + `extra`): own DMAs of one stage landed
-  const int nw = C::PIECES - wave * C::PPW < 0 ? 0
-                 : (C::PIECES - wave * C::PPW > C::PPW ? C::PPW : C::PIECES - wave * C::PPW);
-  auto wait_dma = [&](auto stages, auto extra) {
-    constexpr int ST = decltype(stages)::value, EX = decltype(extra)::value;
-    if (nw == C::PPW) X6_WAITCNT_VM(C::PPW * ST + EX);
-    else if (nw == C::PPW - 1) X6_WAITCNT_VM((C::PPW - 1 > 0 ? C::PPW - 1 : 0) * ST + EX);
-    else if (nw == C::PPW - 2) X6_WAITCNT_VM((C::PPW - 2 > 0 ? C::PPW - 2 : 0) * ST + EX);
-    else X6_WAITCNT_VM(EX);
   };
 
   // prologue: x tile of chunk 0 split into LDS, chunk 1's x in registers, weight stages
@@ -366,8 +352,7 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   load_x((nch > 1 ? 1 : 0) * C::KC);
 #pragma unroll
   for (int j = 0; j < C::S - 1; ++j) load_w(j < nst ? j : nst - 1, j);
-  static_assert(C::PPW <= 3, "wait_dma covers 0 .. 3 DMAs per wave and stage");
-  wait_dma(std::integral_constant<int, C::S - 2>{}, std::integral_constant<int, 0>{});
+  X6_WAITCNT_VM(C::PPW * (C::S - 2));  // own DMAs of stage 0 landed
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
   x6_barrier();
 
@@ -380,7 +365,7 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
 #pragma unroll 1
     for (int t = 0; t < 9; ++t) {
       const int st = 9 * c + t;
-      const __bf16* lw = ring + (st % C::S) * C::WST;
+      const __bf16* lw = ring + (st % C::S) * C::WSTP;
       const int ky = t / 3, kx = t - 3 * ky;
       bf16x8 av[3][C::MT], bv[3][NT];
 #pragma unroll
@@ -407,12 +392,10 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
         load_x((c + 2 < nch ? c + 2 : nch - 1) * C::KC);  // uniform count: re-load at the end
       }
       load_w(st + C::S - 1 < nst ? st + C::S - 1 : nst - 1, (st + C::S - 1) % C::S);
-      // own DMAs of stage st+1 landed: issued after them are those of stages st+2 .. st+S-1
-      // and, in a chunk's first S-3 stages, the x loads issued at the previous chunk's end
-      if (t <= C::S - 4 && c > 0)  // the x loads went out before the DMAs of stage 9c + S - 2
-        wait_dma(std::integral_constant<int, C::S - 2>{}, std::integral_constant<int, C::XITEMS>{});
-      else
-        wait_dma(std::integral_constant<int, C::S - 2>{}, std::integral_constant<int, 0>{});
+      // own DMAs of stage st+1 landed: issued after them are those of stages st+2, st+S-1 and,
+      // in a chunk's first stage, the x loads issued at the previous chunk's end
+      if (t == 0 && c > 0) X6_WAITCNT_VM(C::PPW * (C::S - 2) + C::XITEMS);
+      else X6_WAITCNT_VM(C::PPW * (C::S - 2));
       if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
       x6_barrier();
     }
