@@ -556,17 +556,6 @@ struct WgCfg {
   static constexpr int GITEMS = (GQ + NTHR - 1) / NTHR, XITEMS = (XQ + NTHR - 1) / NTHR;
 };
 
-// output-channel block of a wide layer (a.zc > 0): blockIdx.z selects channels [z*zc, z*zc+zc)
-__device__ __forceinline__ WgradArgs wg_block(const WgradArgs& a0) {
-  WgradArgs a = a0;
-  if (a0.zc > 0) {
-    a.co_base = (int)blockIdx.z * a0.zc;
-    a.Cout = min(a0.zc, a0.cout_total - a.co_base);
-    a.g_off = a0.g_off + a.co_base;
-  }
-  return a;
-}
-
 template <int MODE, int MF, int NW, int CIF>
 __global__ __launch_bounds__(NW * 64, MF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a0) {
   using C = WgCfg<MODE, MF, NW, CIF>;

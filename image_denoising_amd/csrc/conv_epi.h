@@ -1,5 +1,6 @@
-// Output epilogue shared by the output-stationary conv kernels (k_fwd in conv.hip, the split-bf16
-// fp32 kernel in conv_x6.hip).  Both keep a wave's tile as acc[m][q] in the 16x16 MFMA C/D map
+// Device helpers shared by the conv kernels (conv.hip, conv_x6.hip): the weight-gradient
+// output-channel blocking and the output epilogue of the output-stationary kernels (k_fwd and
+// the split-bf16 fp32 kernels).  Those keep a wave's tile as acc[m][q] in the 16x16 MFMA C/D map
 // (col = lane&15 -> output channel q*16 + col, row = 4*(lane>>4) + reg -> pixel x of tile row m),
 // so one LDS-staged epilogue serves every layout and fused op (FwdArgs::epi / out_layout).
 #pragma once
@@ -9,6 +10,18 @@
 namespace dn {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// weight gradients: output-channel block of a wide layer (a.zc > 0): blockIdx.z selects
+// channels [z*zc, z*zc+zc)
+__device__ __forceinline__ WgradArgs wg_block(const WgradArgs& a0) {
+  WgradArgs a = a0;
+  if (a0.zc > 0) {
+    a.co_base = (int)blockIdx.z * a0.zc;
+    a.Cout = min(a0.zc, a0.cout_total - a.co_base);
+    a.g_off = a0.g_off + a.co_base;
+  }
+  return a;
+}
 
 // Stage each 16-pixel row of the wave's tile through LDS, then write whole pixels: as float4
 // (NOUT contiguous channels, 1 KiB contiguous per wave store) when the layout allows, else
