@@ -284,7 +284,8 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
   const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp) + (long)blockIdx.z * a.wp_z;
   const int nch = (a.K + C::KC - 1) / C::KC;
-  const int nst = 9 * nch;
+  const bool tail = a.x6_tail != 0;       // last chunk: 2 im2col stages instead of 9 taps
+  const int nst = 9 * nch - (tail ? 7 : 0);
 
   f32x4 acc[C::MT][NT];
 #pragma unroll
@@ -362,19 +363,43 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   // for the x registers then only ever cover DMAs issued a stage or more earlier.
   for (int c = 0; c < nch; ++c) {
     const bool more = c + 1 < nch;
+    const bool thin = tail && !more;
 #pragma unroll 1
-    for (int t = 0; t < 9; ++t) {
+    for (int t = 0; t < (thin ? 2 : 9); ++t) {
       const int st = 9 * c + t;
       const __bf16* lw = ring + (st % C::S) * C::WSTP;
-      const int ky = t / 3, kx = t - 3 * ky;
       bf16x8 av[3][C::MT], bv[3][NT];
+      if (thin) {
+        // im2col stage t: lane group lg holds k = 8lg..8lg+7 = channels 0..3 of taps
+        // 8t+2lg and 8t+2lg+1 (taps past 8 are zero), read as 8 B from quad 0 of the pixel
+        const int ta = 8 * t + 2 * lg, tb = ta + 1;
+        const int ca = ta < 9 ? ta : 8, cb = tb < 9 ? tb : 8;
+        const int da = (ca / 3) * C::IW + ca % 3, db = (cb / 3) * C::IW + cb % 3;
+        const bf16x4 z4 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
 #pragma unroll
-      for (int m = 0; m < C::MT; ++m) {
-        const int pix = (wave * C::MT + m + ky) * C::IW + li + kx;
-        const int off = pix * C::KC + x6_swz(pix, lg) * 8;
+        for (int m = 0; m < C::MT; ++m) {
+          const int p0 = (wave * C::MT + m) * C::IW + li;
+          const int pa = p0 + da, pb = p0 + db;
+          const int oa = pa * C::KC + x6_swz(pa, 0) * 8, ob = pb * C::KC + x6_swz(pb, 0) * 8;
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
-          av[p][m] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
+          for (int p = 0; p < 3; ++p) {
+            bf16x4 va = *reinterpret_cast<const bf16x4*>(lx + p * C::XPL + oa);
+            bf16x4 vb = *reinterpret_cast<const bf16x4*>(lx + p * C::XPL + ob);
+            if (ta > 8) va = z4;
+            if (tb > 8) vb = z4;
+            av[p][m] = __builtin_shufflevector(va, vb, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+        }
+      } else {
+        const int ky = t / 3, kx = t - 3 * ky;
+#pragma unroll
+        for (int m = 0; m < C::MT; ++m) {
+          const int pix = (wave * C::MT + m + ky) * C::IW + li + kx;
+          const int off = pix * C::KC + x6_swz(pix, lg) * 8;
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            av[p][m] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
+        }
       }
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
@@ -408,17 +433,28 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
 // Pre-split weight image, one per output-channel block z: [chunk][tap][piece][n < NP][32 k],
 // bf16, 16-B quads swizzled by n (see x6_swz); zero padded past K / NOUT.
 // Each stage is x6_wst(NP) elements (the tail past 3*NP*32 is zero).
+// tail != 0: the last chunk's (<= 4) channels are packed im2col in its first two stages, k =
+// 4*tap + channel (stage 0: taps 0..7, stage 1: tap 8), for k_c3x6p's x6_tail mode.
 __global__ __launch_bounds__(256) void k_pack_x6(WView wv, int K, int NOUT, int NP, int nch,
-                                                 int nz, int zc, int ntot, __bf16* __restrict__ out) {
+                                                 int nz, int zc, int ntot, int tail,
+                                                 __bf16* __restrict__ out) {
   const int wst = x6_wst(NP), pad = wst - 3 * NP * 32;
   const long per_z = (long)nch * 9 * NP * 32, total = per_z * nz;
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
     const int z = (int)(e / per_z);
     const long r = e - (long)z * per_z;
     const int kk = (int)(r % 32), nn = (int)((r / 32) % NP);
-    const int ct = (int)(r / (32L * NP)), t = ct % 9, c = ct / 9, k = c * 32 + kk;
+    const int ct = (int)(r / (32L * NP)), c = ct / 9;
+    int t = ct % 9, k = c * 32 + kk;
+    bool live = true;
+    if (tail && c == nch - 1) {
+      const int kg = 32 * t + kk;  // im2col index of the tail stage
+      live = t < 2 && kg < 36;
+      t = kg >> 2;
+      k = c * 32 + (kg & 3);
+    }
     float v = 0.f;
-    if (k < K && nn < NOUT && (zc == 0 || z * zc + nn < ntot)) {
+    if (live && k < K && nn < NOUT && (zc == 0 || z * zc + nn < ntot)) {
       const int tm = wv.flip ? wv.taps - 1 - t : t;
       v = wv.w[wv.off + (long)z * wv.sZ + (long)k * wv.sK + (long)nn * wv.sN + (long)tm * wv.sT];
     }
@@ -454,9 +490,12 @@ long x6_pack_elems(int K, int nout, int zc) {
   return (long)nz * ((K + 31) / 32) * 9 * x6_wst(np);
 }
 
-hipError_t launch_pack_x6(const WView& wv, int K, int nout, int zc, void* out, hipStream_t s) {
+bool x6_tail_ok(int K) { return K % 32 >= 1 && K % 32 <= 4; }
+
+hipError_t launch_pack_x6(const WView& wv, int K, int nout, int zc, void* out, hipStream_t s,
+                          bool tail) {
   const long total = x6_pack_elems(K, nout, zc);
-  if (total < 0 || wv.taps != 9) return hipErrorInvalidValue;
+  if (total < 0 || wv.taps != 9 || (tail && !x6_tail_ok(K))) return hipErrorInvalidValue;
   const int np = x6_np(nout, zc);
   const int nz = zc > 0 ? (nout + zc - 1) / zc : 1;
   WView v = wv;
@@ -464,7 +503,7 @@ hipError_t launch_pack_x6(const WView& wv, int K, int nout, int zc, void* out, h
   long blocks = ((long)nz * ((K + 31) / 32) * 9 * np * 32 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(k_pack_x6, dim3((unsigned)blocks), dim3(256), 0, s, v, K,
-                     zc > 0 ? zc : nout, np, (K + 31) / 32, nz, zc, nout,
+                     zc > 0 ? zc : nout, np, (K + 31) / 32, nz, zc, nout, tail ? 1 : 0,
                      static_cast<__bf16*>(out));
   return hipGetLastError();
 }
@@ -504,7 +543,12 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
   // large grids: the pipelined 16-row kernel (one workgroup per CU, >= 2 rounds of tiles)
   const long tiles16 = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16) * nz;
   static const bool no_pipe = getenv("DN_X6_NOPIPE") != nullptr;  // A/B probe
-  if (!no_pipe && tiles16 >= 512 && ((a.in_stride | a.in_off | a.K) & 3) == 0)
+  const bool aligned = ((a.in_stride | a.in_off | a.K) & 3) == 0;
+  if (a.x6_tail) {  // im2col-packed tail chunk: only the pipelined kernel reads it
+    if (!aligned || !x6_tail_ok(a.K)) return hipErrorInvalidValue;
+    return np == 48 ? run_x6p<3>(a, nz, s) : run_x6p<6>(a, nz, s);
+  }
+  if (!no_pipe && tiles16 >= 512 && aligned)
     return np == 48 ? run_x6p<3>(a, nz, s) : run_x6p<6>(a, nz, s);
   if (np == 48) {
     return x6_pick_mt<3>(a, nz) == 2 ? run_x6<3, 2>(a, nz, s) : run_x6<3, 1>(a, nz, s);

@@ -55,6 +55,7 @@ struct FwdArgs {
   float* out; int out_stride, out_off; int out_layout;
   const float* mask; int mask_stride, mask_off;
   int zc;        // > 0: blockIdx.z selects output channels [z*zc, z*zc+zc) (wide layers)
+  int x6_tail;   // split-bf16 kernels: the last K chunk (<= 4 channels) is packed im2col
 };
 
 // Fused output head (arch_unet.py:186-190, 253-257): the dec_conv1b kernel keeps its
@@ -192,7 +193,9 @@ hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, 
 long bf16_pack_elems(int K, int nout, int ksize = 3);
 // ---- fp32 3x3 conv on the bf16 matrix cores by three-way operand splitting (conv_x6.hip) ----
 long x6_pack_elems(int K, int nout, int zc);  // bf16 elements of a pre-split weight image
-hipError_t launch_pack_x6(const WView& wv, int K, int nout, int zc, void* out, hipStream_t s);
+hipError_t launch_pack_x6(const WView& wv, int K, int nout, int zc, void* out, hipStream_t s,
+                          bool tail = false);
+bool x6_tail_ok(int K);  // K's last 32-channel chunk holds 1..4 channels (im2col tail packing)
 hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s);
 hipError_t launch_pack_bf16(const WView& wv, int K, int nout, void* out, hipStream_t s,
                             int ksize = 3);

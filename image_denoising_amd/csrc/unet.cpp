@@ -387,7 +387,10 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
       a.N = Nn; a.OH = h; a.OW = w; a.K = K; a.NOUT = cout;
       // dec_conv1a reads [up1 | x | zero pad] (c1s = c1k rounded to 4): taking the zero pad
       // channel as a reduction channel (its packed weights are zero) keeps K % 4 == 0
-      if (i == D1A) a.K = p.c1s;
+      if (i == D1A) {
+        a.K = p.c1s;
+        a.x6_tail = x6_tail_ok(p.c1s);  // the few x channels: im2col stages (see the pack)
+      }
       a.wp = ws + p.packX[i]; a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
       a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = layout;
       return launch_fwd_x6(a, st);
@@ -426,7 +429,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     else if (bf16) DN_TRY(launch_pack_bf16(conv_fwd_view(w, L.cin, 3), L.cin, L.cout,
                                            ws + p.packBF[i], s));
     else if (x6) DN_TRY(launch_pack_x6(conv_fwd_view(w, L.cin, 3), L.cin, L.cout, 0,
-                                       ws + p.packX[i], s));
+                                       ws + p.packX[i], s, i == D1A && x6_tail_ok(p.c1s)));
     else DN_TRY(pack_conv_fwd(w, L.cin, L.cout, L.k, ws + p.packF[i], s));
   }
   // enc_conv0, fused with pool0 = x -> channels [2nf, 2nf+C) of the up1 concat buffer

@@ -15,6 +15,8 @@ def main():
     ap.add_argument("--csv")
     ap.add_argument("--shapes")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--seq", help="print the last --last dispatches matching this, in order")
+    ap.add_argument("--last", type=int, default=40)
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, duration, grid_x, grid_y, grid_z, workgroup_x, vgpr_count, "
@@ -34,6 +36,12 @@ def main():
     for n, (k, t, mn, mx) in out[:a.top]:
         print(f"{t/1e6:9.2f} ms {k:6d} {t/k/1e3:9.1f} us {100*t/tot:5.1f}% {n[:100]}")
     print(f"total {tot/1e6:.2f} ms")
+    if a.seq:
+        seq = c.execute("select name, duration, grid_x, grid_y, grid_z, workgroup_x from kernels "
+                        "order by start").fetchall()
+        seq = [r for r in seq if a.seq in r[0]][-a.last:]
+        for name, d, gx, gy, gz, wx in seq:
+            print(f"{d/1e3:9.1f} us  blocks {gx // max(wx, 1):6d} x {gy:3d} x {gz}  {name[:60]}")
     if a.shapes:
         shp = collections.defaultdict(lambda: [0, 0.0])
         for name, d, gx, gy, gz, wx, v, av, lds in rows:
