@@ -286,9 +286,10 @@ def main():
         from image_denoising_amd.improved_unet import ImprovedUNet
 
         net = ImprovedUNet(in_nc=C, out_nc=C, n_feature=48).to(device)
+        net.set_precision(args.conv_precision)
     else:
         net = UNet(in_nc=C, out_nc=C, n_feature=48).to(device).set_precision(args.conv_precision)
-    x6 = args.conv_precision == "fp32_x6" and not iu
+    x6 = args.conv_precision == "fp32_x6"
     fwd_flops = iunet_fwd_flops if iu else unet_fwd_flops
     clean = synthetic_clean(bs * C, H, H, 1000 + rank, device).view(bs, C, H, H).contiguous()
     if ft:

@@ -101,6 +101,10 @@ SIGNATURES = {
                                  c_size_t, c_void_p]),
     "dn_iunet_backward": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
                                   c_size_t, c_void_p]),
+    "dn_iunet_forward_prec": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
+                                      c_size_t, c_int, c_void_p]),
+    "dn_iunet_backward_prec": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
+                                       c_size_t, c_int, c_void_p]),
     "dn_iunet_debug_buffers": (c_int, [POINTER(DnCfg), c_int, c_int, c_int, c_int,
                                        POINTER(c_int64), c_int, POINTER(c_int)]),
     "dn_adapter_param_count": (c_int, [c_int, c_int, POINTER(c_size_t)]),

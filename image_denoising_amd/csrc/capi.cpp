@@ -656,7 +656,15 @@ dn_status dn_iunet_workspace_size(const dn_unet_cfg* cfg, int N, int H, int W, i
 
 dn_status dn_iunet_forward(const dn_unet_cfg* cfg, const float* params, const float* x, float* y,
                            int N, int H, int W, void* ws, size_t ws_bytes, void* stream) {
+  return dn_iunet_forward_prec(cfg, params, x, y, N, H, W, ws, ws_bytes, DN_PREC_FP32, stream);
+}
+
+dn_status dn_iunet_forward_prec(const dn_unet_cfg* cfg, const float* params, const float* x,
+                                float* y, int N, int H, int W, void* ws, size_t ws_bytes,
+                                int precision, void* stream) {
   DN_GUARD_BEGIN
+  if (precision != DN_PREC_FP32 && precision != DN_PREC_FP32_X6)
+    return fail(DN_ERR_ARG, "ImprovedUNet precision must be DN_PREC_FP32 or DN_PREC_FP32_X6");
   if (!cfg || !params || !x || !y || !ws) return fail(DN_ERR_ARG, "null argument");
   IPlan p;
   std::string err;
@@ -668,21 +676,31 @@ dn_status dn_iunet_forward(const dn_unet_cfg* cfg, const float* params, const fl
     return fail(DN_ERR_ARG, err);
   if (ws_bytes < (size_t)p.total_floats * sizeof(float))
     return fail(DN_ERR_WORKSPACE, "workspace smaller than dn_iunet_workspace_size()");
-  return iunet_forward(p, params, x, y, static_cast<float*>(ws), (hipStream_t)stream);
+  return iunet_forward(p, params, x, y, static_cast<float*>(ws), (hipStream_t)stream, precision);
   DN_GUARD_END
 }
 
 dn_status dn_iunet_backward(const dn_unet_cfg* cfg, const float* params, const float* dy,
                             float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
                             void* stream) {
+  return dn_iunet_backward_prec(cfg, params, dy, dparams, N, H, W, ws, ws_bytes, DN_PREC_FP32,
+                                stream);
+}
+
+dn_status dn_iunet_backward_prec(const dn_unet_cfg* cfg, const float* params, const float* dy,
+                                 float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
+                                 int precision, void* stream) {
   DN_GUARD_BEGIN
+  if (precision != DN_PREC_FP32 && precision != DN_PREC_FP32_X6)
+    return fail(DN_ERR_ARG, "ImprovedUNet precision must be DN_PREC_FP32 or DN_PREC_FP32_X6");
   if (!cfg || !params || !dy || !dparams || !ws) return fail(DN_ERR_ARG, "null argument");
   IPlan p;
   std::string err;
   if (!iunet_build_plan(*cfg, N, H, W, true, p, err)) return fail(DN_ERR_ARG, err);
   if (ws_bytes < (size_t)p.total_floats * sizeof(float))
     return fail(DN_ERR_WORKSPACE, "workspace smaller than dn_iunet_workspace_size(with_backward=1)");
-  return iunet_backward(p, params, dy, dparams, static_cast<float*>(ws), (hipStream_t)stream);
+  return iunet_backward(p, params, dy, dparams, static_cast<float*>(ws), (hipStream_t)stream,
+                        precision);
   DN_GUARD_END
 }
 

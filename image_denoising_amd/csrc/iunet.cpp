@@ -70,6 +70,16 @@ bool ggeom(int ksize, int K, int nout, GGeom& g) {
   return g.img > 0;
 }
 
+// split-bf16 (DN_PREC_FP32_X6) 3x3 convs: the kernels tile 48 or 96 output channels and 32
+// reduction channels, so they take the convs that fill those tiles (measured per shape in
+// the 32-output RDB growth convs, the 24-channel level and K = 48 stay on the
+// fp32 kernels, where the padding would cost more than the faster matrix cores give)
+bool x6_takes(int K, int nout) {
+  return nout % 48 == 0 && (K % 32 == 0 || K >= 128) && (K > 32 || nout % 96 == 0);
+}
+// output-channel blocks of the wide layers: 96, or 48 where 96 would pad (144 = 3 x 48)
+int x6_zc(int nout) { return nout <= 96 ? 0 : (nout % 96 == 0 ? 96 : 48); }
+
 long gpack_floats(int ksize, int K, int nout) {
   GGeom g;
   if (!ggeom(ksize, K, nout, g)) return -1;
@@ -109,6 +119,21 @@ hipError_t grun(int ksize, const View& in, int N, int H, int W, int K, const flo
   a.mask = aux.p; a.mask_stride = aux.stride; a.mask_off = aux.off;
   a.zc = g.np;
   return launch_fwd_nt(g.gather, g.nt, a, s);
+}
+
+// the same 3x3 conv on the split-bf16 kernels (image from launch_pack_x6 with zc = x6_zc(nout))
+hipError_t x6run(const View& in, int N, int H, int W, int K, const float* wp, int nout,
+                 const float* bias, int epi, const View& out, int layout, const View& aux,
+                 hipStream_t s) {
+  FwdArgs a{};
+  a.in = in.p; a.in_stride = in.stride; a.in_off = in.off; a.IHt = H; a.IWt = W;
+  a.N = N; a.OH = H; a.OW = W; a.K = K; a.NOUT = nout;
+  a.zc = x6_zc(nout);
+  a.wp = wp; a.wp_z = a.zc ? x6_pack_elems(K, nout, a.zc) / ((nout + a.zc - 1) / a.zc) : 0;
+  a.bias = bias; a.epi = epi;
+  a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = layout;
+  a.mask = aux.p; a.mask_stride = aux.stride; a.mask_off = aux.off;
+  return launch_fwd_x6(a, s);
 }
 
 // ---- parameter layout (state_dict order of ImprovedUNet) ---------------------------------
@@ -270,7 +295,12 @@ bool iunet_build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, IPlan
   p.gpart = allocf(2L * 2 * std::max(2048L, (long)N) * 384);  // N*S splits x 384 ch x 2 doubles
   // packed-weight scratch: max over every conv (forward and data-gradient images)
   long pk = 0;
-  auto pf = [&](int k, int K, int nout) { pk = std::max(pk, gpack_floats(k, K, nout)); };
+  long x6max = 0;
+  auto pf = [&](int k, int K, int nout) {
+    pk = std::max(pk, gpack_floats(k, K, nout));
+    if (k == 3 && x6_takes(K, nout))
+      x6max = std::max(x6max, (x6_pack_elems(K, nout, x6_zc(nout)) + 1) / 2);
+  };
   for (int i = 0; i < 4; ++i) {
     const ILevel& L = P.down[i];
     pf(3, L.conv.cin, L.conv.cout);
@@ -291,6 +321,7 @@ bool iunet_build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, IPlan
   }
   pf(3, 1, 48);         // ne2 data gradient
   pf(3, P.OC, 24);      // final data gradient (x_up3 part)
+  pk = std::max(pk, x6max);  // the split-bf16 images of the same 3x3 convs
   p.pack = allocf(pk);
   p.pack_floats = pk;
   if (bwd) {
@@ -396,6 +427,7 @@ struct Ctx {
   const float* prm;
   float* ws;
   hipStream_t s;
+  int prec;
   View V(long o, int stride, int off = 0) const { return View{ws + o, stride, off}; }
   const float* Wt(const IConv& c) const { return prm + c.w; }
   const float* Bs(const IConv& c) const { return c.b >= 0 ? prm + c.b : nullptr; }
@@ -407,6 +439,12 @@ dn_status conv_fwd(const Ctx& c, const IConv& L, const View& in, int h, int w, i
                    const View& out, int layout = OUT_NHWC, const View& aux = kNone) {
   OpScope prof(c.s, "fwd", L.cout, L.cin, L.k, h, w, c.p.N, 1.0);
   float* pk = c.ws + c.p.pack;
+  if (c.prec == DN_PREC_FP32_X6 && L.k == 3 && x6_takes(L.cin, L.cout)) {
+    IU_TRY(launch_pack_x6(conv_fwd_view(c.Wt(L), L.cin, 3), L.cin, L.cout, x6_zc(L.cout), pk,
+                          c.s));
+    IU_TRY(x6run(in, c.p.N, h, w, L.cin, pk, L.cout, c.Bs(L), epi, out, layout, aux, c.s));
+    return DN_OK;
+  }
   IU_TRY(gpack_fwd(c.Wt(L), L.k, L.cin, L.cout, pk, c.s));
   IU_TRY(grun(L.k, in, c.p.N, h, w, L.cin, pk, L.cout, c.Bs(L), epi, out, layout, aux, c.s));
   return DN_OK;
@@ -456,8 +494,9 @@ WView thin_view(const float* w, int cin) {  // weight [o][cin][3][3] as W(o, k, 
 }  // namespace
 
 dn_status iunet_forward(const IPlan& p, const float* prm, const float* x, float* y, float* ws,
-                        hipStream_t s) {
-  const Ctx c{p, prm, ws, s};
+                        hipStream_t s, int prec) {
+  if (prec != DN_PREC_FP32 && prec != DN_PREC_FP32_X6) return DN_ERR_ARG;
+  const Ctx c{p, prm, ws, s, prec};
   const IParams& P = p.P;
   const int N = p.N, H = p.H, W = p.W, C = P.C;
   // noise estimator: h = leaky(ne0(x)) (also writes x into x0[:, :C], zeros x0[:, C:4])
@@ -553,6 +592,12 @@ dn_status dgrad_g(const Ctx& c, const IConv& L, const View& g, int h, int w, int
                   const View& aux, const View& dx) {
   OpScope prof(c.s, "dgrad", nout, L.cout, L.k, h, w, c.p.N, 1.0);
   float* pk = c.ws + c.p.pack;
+  if (c.prec == DN_PREC_FP32_X6 && L.k == 3 && x6_takes(L.cout, nout)) {
+    IU_TRY(launch_pack_x6(conv_dgrad_view(c.Wt(L), L.cin, 3), L.cout, nout, x6_zc(nout), pk,
+                          c.s));
+    IU_TRY(x6run(g, c.p.N, h, w, L.cout, pk, nout, nullptr, epi, dx, OUT_NHWC, aux, c.s));
+    return DN_OK;
+  }
   IU_TRY(gpack_dgrad(c.Wt(L), L.k, L.cin, L.cout, nout, pk, c.s));
   IU_TRY(grun(L.k, g, c.p.N, h, w, L.cout, pk, nout, nullptr, epi, dx, OUT_NHWC, aux, c.s));
   return DN_OK;
@@ -613,8 +658,9 @@ dn_status rdb_bwd(const Ctx& c, float* dprm, const IRdb& R, const IBlockBufs& b,
 }  // namespace
 
 dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, float* dprm, float* ws,
-                         hipStream_t s) {
-  const Ctx c{p, prm, ws, s};
+                         hipStream_t s, int prec) {
+  if (prec != DN_PREC_FP32 && prec != DN_PREC_FP32_X6) return DN_ERR_ARG;
+  const Ctx c{p, prm, ws, s, prec};
   const IParams& P = p.P;
   const int N = p.N, H = p.H, W = p.W, C = P.C, OC = P.OC;
   const long HW = (long)H * W;

@@ -61,9 +61,11 @@ struct IPlan {
 bool iunet_build_params(const dn_unet_cfg& c, IParams& P, std::string& err);
 bool iunet_build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, IPlan& p,
                       std::string& err);
+// prec: DN_PREC_FP32, or DN_PREC_FP32_X6 (the 3x3 convs' forward and data gradient as split
+// bf16 products, conv_x6.hip)
 dn_status iunet_forward(const IPlan& p, const float* prm, const float* x, float* y, float* ws,
-                        hipStream_t s);
+                        hipStream_t s, int prec = DN_PREC_FP32);
 dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, float* dprm,
-                         float* ws, hipStream_t s);
+                         float* ws, hipStream_t s, int prec = DN_PREC_FP32);
 
 }  // namespace dn

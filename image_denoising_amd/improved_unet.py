@@ -158,14 +158,30 @@ class ImprovedUNet(nn.Module):
             self._ws_cache = {key: ws}
         return ws
 
+    # arithmetic of the 3x3 convolutions (include/denoise_hip.h DN_PREC_*)
+    _PRECISIONS = {"fp32": 0, "fp32_x6": 2}
+
+    def set_precision(self, mode: str) -> "ImprovedUNet":
+        """Arithmetic of the 3x3 convolutions' forward and data gradient: 'fp32' (fp32 matrix
+        cores) or 'fp32_x6' (exact three-piece bf16 split, six products, fp32 accumulation;
+        DESIGN.md §11).  Weight gradients and the 1x1 / noise-estimator convs stay fp32."""
+        if mode not in self._PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(self._PRECISIONS)}")
+        self.precision = mode
+        return self
+
+    def _prec(self) -> int:
+        return self._PRECISIONS[getattr(self, "precision", "fp32")]
+
     def _run_forward(self, x, y, ws):
         N, _, H, W = x.shape
-        _lib.call("dn_iunet_forward", ctypes.byref(self._cfg), _lib.ptr(self._flat), _lib.ptr(x),
-                  _lib.ptr(y), N, H, W, ws.data_ptr(), ws.numel(), _lib.stream_of(x))
+        _lib.call("dn_iunet_forward_prec", ctypes.byref(self._cfg), _lib.ptr(self._flat),
+                  _lib.ptr(x), _lib.ptr(y), N, H, W, ws.data_ptr(), ws.numel(), self._prec(),
+                  _lib.stream_of(x))
 
     def _run_backward(self, dy, dflat, ws, N, H, W):
-        _lib.call("dn_iunet_backward", ctypes.byref(self._cfg), _lib.ptr(self._flat),
-                  _lib.ptr(dy), _lib.ptr(dflat), N, H, W, ws.data_ptr(), ws.numel(),
+        _lib.call("dn_iunet_backward_prec", ctypes.byref(self._cfg), _lib.ptr(self._flat),
+                  _lib.ptr(dy), _lib.ptr(dflat), N, H, W, ws.data_ptr(), ws.numel(), self._prec(),
                   _lib.stream_of(dy))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

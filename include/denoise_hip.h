@@ -292,6 +292,15 @@ dn_status dn_iunet_forward(const dn_unet_cfg* cfg, const float* params, const fl
 dn_status dn_iunet_backward(const dn_unet_cfg* cfg, const float* params, const float* dy,
                             float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
                             void* stream);
+/* dn_iunet_forward / dn_iunet_backward with the 3x3 convolutions' arithmetic chosen by
+   precision: DN_PREC_FP32 or DN_PREC_FP32_X6 (forward and data gradient as exact split-bf16
+   products; weight gradients, 1x1 convs and the noise estimator stay on the fp32 kernels). */
+dn_status dn_iunet_forward_prec(const dn_unet_cfg* cfg, const float* params, const float* x,
+                                float* y, int N, int H, int W, void* ws, size_t ws_bytes,
+                                int precision, void* stream);
+dn_status dn_iunet_backward_prec(const dn_unet_cfg* cfg, const float* params, const float* dy,
+                                 float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
+                                 int precision, void* stream);
 /* Debug/introspection: (offset_floats, channel_stride, level) of the main NHWC activations:
    x0 h | down level i = 0..3: F r z1 a1 z2 | bottle: F r z1 a1 z2 | up k = 0..3: cc F r z1 a1 z2 |
    xb cf */

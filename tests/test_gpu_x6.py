@@ -105,6 +105,9 @@ def _dgrad(dz, w, cin, mode, mask, base, x6):
     (48, 48, 2, 32, 32), (96, 96, 2, 16, 16), (144, 96, 2, 16, 16), (48, 96, 2, 8, 8),
     (96, 48, 1, 20, 36), (144, 96, 1, 64, 32),
     (96, 96, 8, 128, 128), (144, 96, 3, 128, 112), (48, 48, 8, 128, 128),  # pipelined kernel
+    # ImprovedUNet shapes: final conv (K = out_nc), RDB growth convs (K = 32, wide outputs)
+    (24, 3, 1, 32, 32), (24, 1, 2, 32, 32), (144, 32, 1, 16, 16), (112, 32, 1, 16, 16),
+    (80, 32, 2, 16, 16), (120, 32, 1, 32, 32), (72, 24, 1, 32, 32),
 ])
 @pytest.mark.parametrize("mode", ["plain", "mask", "accum"])
 def test_x6_backward_data_vs_fp64(cin, cout, N, H, W, mode):
@@ -121,8 +124,13 @@ def test_x6_backward_data_vs_fp64(cin, cout, N, H, W, mode):
     if mode == "accum":
         ref = ref + base.double()
     d6 = _dgrad(dz, w, cin, mode, mask, base, True)
-    d32 = _dgrad(dz, w, cin, mode, mask, base, False)
-    e6, e32 = rel_err(d6.numpy(), ref.numpy()), rel_err(d32.numpy(), ref.numpy())
+    e6 = rel_err(d6.numpy(), ref.numpy())
+    try:
+        d32 = _dgrad(dz, w, cin, mode, mask, base, False)
+    except L().DenoiseHipError:  # channel counts the fp32 op kernels are not built for
+        assert e6 < X6_TOL, e6
+        return
+    e32 = rel_err(d32.numpy(), ref.numpy())
     assert e6 < X6_TOL, (e6, e32)
     assert e6 < 4 * e32 + 1e-7, (e6, e32)
 
