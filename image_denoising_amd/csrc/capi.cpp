@@ -430,9 +430,13 @@ dn_status dn_conv2d_forward_x6(const float* x, int x_stride, int N, int H, int W
   if (need == 0) return fail(DN_ERR_ARG, "bf16x6 forward supports Cout <= 96");
   if (dn_status st = need_pack(pack_ws, pack_bytes, need)) return st;
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = launch_pack_x6(conv_fwd_view(w, Cin, 3), Cin, Cout, 0, pack_ws, s);
+  // large grids with a partial last 32-channel chunk: the pipelined kernel's tail packing
+  const int tail = (x_stride % 4 == 0 && Cin % 4 == 0 && x6_pipelined(N, H, W, Cout, 0))
+                       ? x6_tail_mode(Cin) : 0;
+  hipError_t e = launch_pack_x6(conv_fwd_view(w, Cin, 3), Cin, Cout, 0, pack_ws, s, tail);
   if (e == hipSuccess) {
     FwdArgs a{};
+    a.x6_tail = tail;
     a.in = x; a.in_stride = x_stride; a.in_off = 0; a.IHt = H; a.IWt = W;
     a.N = N; a.OH = H; a.OW = W; a.K = Cin; a.NOUT = Cout;
     a.wp = static_cast<const float*>(pack_ws); a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
@@ -454,9 +458,11 @@ dn_status dn_conv2d_backward_data_x6(const float* dz, int N, int H, int W, int C
   if (dn_status st = need_pack(pack_ws, pack_bytes, need)) return st;
   hipStream_t s = (hipStream_t)stream;
   const int zc = x6_dgrad_zc(Cin);
-  hipError_t e = launch_pack_x6(conv_dgrad_view(w, Cin, 3), Cout, Cin, zc, pack_ws, s);
+  const int tail = (Cout % 4 == 0 && x6_pipelined(N, H, W, Cin, zc)) ? x6_tail_mode(Cout) : 0;
+  hipError_t e = launch_pack_x6(conv_dgrad_view(w, Cin, 3), Cout, Cin, zc, pack_ws, s, tail);
   if (e == hipSuccess) {
     FwdArgs a{};
+    a.x6_tail = tail;
     a.in = dz; a.in_stride = Cout; a.in_off = 0; a.IHt = H; a.IWt = W;
     a.N = N; a.OH = H; a.OW = W; a.K = Cout; a.NOUT = Cin;
     a.zc = zc;

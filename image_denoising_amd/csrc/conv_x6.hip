@@ -284,8 +284,10 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
   const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp) + (long)blockIdx.z * a.wp_z;
   const int nch = (a.K + C::KC - 1) / C::KC;
-  const bool tail = a.x6_tail != 0;       // last chunk: 2 im2col stages instead of 9 taps
-  const int nst = 9 * nch - (tail ? 7 : 0);
+  // last chunk packed by x6_tail_mode: 2 im2col stages (mode 1) or 5 tap-pair stages (mode 2)
+  const int tail = a.x6_tail;
+  const int tail_st = tail == 1 ? 2 : 5;
+  const int nst = 9 * nch - (tail ? 9 - tail_st : 0);
 
   f32x4 acc[C::MT][NT];
 #pragma unroll
@@ -365,11 +367,11 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     const bool more = c + 1 < nch;
     const bool thin = tail && !more;
 #pragma unroll 1
-    for (int t = 0; t < (thin ? 2 : 9); ++t) {
+    for (int t = 0; t < (thin ? tail_st : 9); ++t) {
       const int st = 9 * c + t;
       const __bf16* lw = ring + (st % C::S) * C::WSTP;
       bf16x8 av[3][C::MT], bv[3][NT];
-      if (thin) {
+      if (thin && tail == 1) {
         // im2col stage t: lane group lg holds k = 8lg..8lg+7 = channels 0..3 of taps
         // 8t+2lg and 8t+2lg+1 (taps past 8 are zero), read as 8 B from quad 0 of the pixel
         const int ta = 8 * t + 2 * lg, tb = ta + 1;
@@ -388,6 +390,23 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
             if (ta > 8) va = z4;
             if (tb > 8) vb = z4;
             av[p][m] = __builtin_shufflevector(va, vb, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+        }
+      } else if (thin) {
+        // tap-pair stage t: lane groups 0,1 hold channels 0..15 of tap 2t, groups 2,3 those of
+        // tap 2t+1 (zero past tap 8): quad lg & 1 of the pixel at that tap
+        const int ta = 2 * t + (lg >> 1);
+        const int ca = ta < 9 ? ta : 8;
+        const int da = (ca / 3) * C::IW + ca % 3;
+        const bf16x8 z8 = {};
+#pragma unroll
+        for (int m = 0; m < C::MT; ++m) {
+          const int pa = (wave * C::MT + m) * C::IW + li + da;
+          const int oa = pa * C::KC + x6_swz(pa, lg & 1) * 8;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const bf16x8 v = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + oa);
+            av[p][m] = ta > 8 ? z8 : v;
           }
         }
       } else {
@@ -433,8 +452,9 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
 // Pre-split weight image, one per output-channel block z: [chunk][tap][piece][n < NP][32 k],
 // bf16, 16-B quads swizzled by n (see x6_swz); zero padded past K / NOUT.
 // Each stage is x6_wst(NP) elements (the tail past 3*NP*32 is zero).
-// tail != 0: the last chunk's (<= 4) channels are packed im2col in its first two stages, k =
-// 4*tap + channel (stage 0: taps 0..7, stage 1: tap 8), for k_c3x6p's x6_tail mode.
+// tail (x6_tail_mode, for k_c3x6p): the last chunk's channels packed over its first stages:
+// 1: (<= 4 channels) im2col, k = 4*tap + channel (stage 0: taps 0..7, stage 1: tap 8);
+// 2: (<= 16 channels) two taps per stage, k = 16*(tap - 2*stage) + channel (5 stages).
 __global__ __launch_bounds__(256) void k_pack_x6(WView wv, int K, int NOUT, int NP, int nch,
                                                  int nz, int zc, int ntot, int tail,
                                                  __bf16* __restrict__ out) {
@@ -447,11 +467,16 @@ __global__ __launch_bounds__(256) void k_pack_x6(WView wv, int K, int NOUT, int 
     const int ct = (int)(r / (32L * NP)), c = ct / 9;
     int t = ct % 9, k = c * 32 + kk;
     bool live = true;
-    if (tail && c == nch - 1) {
-      const int kg = 32 * t + kk;  // im2col index of the tail stage
+    if (tail == 1 && c == nch - 1) {
+      const int kg = 32 * t + kk;  // im2col index of the tail stage: 4 * tap + channel
       live = t < 2 && kg < 36;
       t = kg >> 2;
       k = c * 32 + (kg & 3);
+    } else if (tail == 2 && c == nch - 1) {  // tap pair: 16 * (tap - 2t) + channel
+      const int tap = 2 * t + (kk >> 4);
+      live = t < 5 && tap < 9;
+      t = tap < 9 ? tap : 8;
+      k = c * 32 + (kk & 15);
     }
     float v = 0.f;
     if (live && k < K && nn < NOUT && (zc == 0 || z * zc + nn < ntot)) {
@@ -490,12 +515,16 @@ long x6_pack_elems(int K, int nout, int zc) {
   return (long)nz * ((K + 31) / 32) * 9 * x6_wst(np);
 }
 
-bool x6_tail_ok(int K) { return K % 32 >= 1 && K % 32 <= 4; }
+int x6_tail_mode(int K) {
+  const int r = K % 32;
+  return r == 0 ? 0 : (r <= 4 ? 1 : (r <= 16 ? 2 : 0));
+}
 
 hipError_t launch_pack_x6(const WView& wv, int K, int nout, int zc, void* out, hipStream_t s,
-                          bool tail) {
+                          int tail) {
   const long total = x6_pack_elems(K, nout, zc);
-  if (total < 0 || wv.taps != 9 || (tail && !x6_tail_ok(K))) return hipErrorInvalidValue;
+  if (total < 0 || wv.taps != 9 || (tail && tail != x6_tail_mode(K)))
+    return hipErrorInvalidValue;
   const int np = x6_np(nout, zc);
   const int nz = zc > 0 ? (nout + zc - 1) / zc : 1;
   WView v = wv;
@@ -503,7 +532,7 @@ hipError_t launch_pack_x6(const WView& wv, int K, int nout, int zc, void* out, h
   long blocks = ((long)nz * ((K + 31) / 32) * 9 * np * 32 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(k_pack_x6, dim3((unsigned)blocks), dim3(256), 0, s, v, K,
-                     zc > 0 ? zc : nout, np, (K + 31) / 32, nz, zc, nout, tail ? 1 : 0,
+                     zc > 0 ? zc : nout, np, (K + 31) / 32, nz, zc, nout, tail,
                      static_cast<__bf16*>(out));
   return hipGetLastError();
 }
@@ -534,6 +563,11 @@ static hipError_t run_x6p(const FwdArgs& a, int nz, hipStream_t s) {
   return hipGetLastError();
 }
 
+bool x6_pipelined(int N, int H, int W, int nout, int zc) {
+  const int nz = zc > 0 ? (nout + zc - 1) / zc : 1;
+  return (long)N * ((H + 15) / 16) * ((W + 15) / 16) * nz >= 512;
+}
+
 // a.wp = the launch_pack_x6 image (a.wp_z = its per-block size when a.zc > 0); every epilogue
 // and output layout of k_fwd
 hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
@@ -541,14 +575,13 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
   if (np == 0 || (a.zc > 0 && a.zc != np)) return hipErrorInvalidValue;
   const int nz = a.zc > 0 ? (a.NOUT + a.zc - 1) / a.zc : 1;
   // large grids: the pipelined 16-row kernel (one workgroup per CU, >= 2 rounds of tiles)
-  const long tiles16 = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16) * nz;
   static const bool no_pipe = getenv("DN_X6_NOPIPE") != nullptr;  // A/B probe
   const bool aligned = ((a.in_stride | a.in_off | a.K) & 3) == 0;
-  if (a.x6_tail) {  // im2col-packed tail chunk: only the pipelined kernel reads it
-    if (!aligned || !x6_tail_ok(a.K)) return hipErrorInvalidValue;
+  if (a.x6_tail) {  // tail-packed last chunk: only the pipelined kernel reads it
+    if (!aligned || a.x6_tail != x6_tail_mode(a.K)) return hipErrorInvalidValue;
     return np == 48 ? run_x6p<3>(a, nz, s) : run_x6p<6>(a, nz, s);
   }
-  if (!no_pipe && tiles16 >= 512 && aligned)
+  if (!no_pipe && x6_pipelined(a.N, a.OH, a.OW, a.NOUT, a.zc) && aligned)
     return np == 48 ? run_x6p<3>(a, nz, s) : run_x6p<6>(a, nz, s);
   if (np == 48) {
     return x6_pick_mt<3>(a, nz) == 2 ? run_x6<3, 2>(a, nz, s) : run_x6<3, 1>(a, nz, s);

@@ -55,7 +55,7 @@ struct FwdArgs {
   float* out; int out_stride, out_off; int out_layout;
   const float* mask; int mask_stride, mask_off;
   int zc;        // > 0: blockIdx.z selects output channels [z*zc, z*zc+zc) (wide layers)
-  int x6_tail;   // split-bf16 kernels: the last K chunk (<= 4 channels) is packed im2col
+  int x6_tail;   // split-bf16 kernels: packing of the last K chunk, x6_tail_mode(K) (0: plain)
 };
 
 // Fused output head (arch_unet.py:186-190, 253-257): the dec_conv1b kernel keeps its
@@ -194,8 +194,12 @@ long bf16_pack_elems(int K, int nout, int ksize = 3);
 // ---- fp32 3x3 conv on the bf16 matrix cores by three-way operand splitting (conv_x6.hip) ----
 long x6_pack_elems(int K, int nout, int zc);  // bf16 elements of a pre-split weight image
 hipError_t launch_pack_x6(const WView& wv, int K, int nout, int zc, void* out, hipStream_t s,
-                          bool tail = false);
-bool x6_tail_ok(int K);  // K's last 32-channel chunk holds 1..4 channels (im2col tail packing)
+                          int tail = 0);
+// packing of a partial last 32-channel chunk for the pipelined kernel: 1 = <= 4 channels,
+// im2col over the 9 taps (2 stages); 2 = <= 16 channels, two taps per stage (5 stages); else 0
+int x6_tail_mode(int K);
+// the launch takes the pipelined kernel (large grid), so a tail-packed image may be used
+bool x6_pipelined(int N, int H, int W, int nout, int zc);
 hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s);
 hipError_t launch_pack_bf16(const WView& wv, int K, int nout, void* out, hipStream_t s,
                             int ksize = 3);

@@ -376,6 +376,13 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // every 3x3 layer (enc_conv1..dec_conv1b): the fp32 kernel, the bf16x6 one (split fp32
   // operands on the bf16 matrix cores), or the bf16 one (bf16 operands, fp32 accumulation /
   // bias / activation / storage)
+  // the pipelined split-bf16 kernel takes a partial last K chunk (dec_conv1a's x channels,
+  // the 48-channel encoder's second chunk) packed over fewer stages (x6_tail_mode)
+  auto x6_tail_f = [&](int i) -> int {
+    const Layer& L = p.P.L[i];
+    const int l = layer_level(i);
+    return x6_pipelined(N, H(l), Wd(l), L.cout, 0) ? x6_tail_mode(i == D1A ? p.c1s : L.cin) : 0;
+  };
   auto conv_forward = [&](const View& in, int Nn, int h, int w, int K, const float* wp,
                           const float* b, int cout, int ksize, int act, const View& out,
                           int layout, hipStream_t st) -> hipError_t {
@@ -387,10 +394,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
       a.N = Nn; a.OH = h; a.OW = w; a.K = K; a.NOUT = cout;
       // dec_conv1a reads [up1 | x | zero pad] (c1s = c1k rounded to 4): taking the zero pad
       // channel as a reduction channel (its packed weights are zero) keeps K % 4 == 0
-      if (i == D1A) {
-        a.K = p.c1s;
-        a.x6_tail = x6_tail_ok(p.c1s);  // the few x channels: im2col stages (see the pack)
-      }
+      if (i == D1A) a.K = p.c1s;
+      a.x6_tail = x6_tail_f(i);  // a partial last K chunk packed over fewer stages
       a.wp = ws + p.packX[i]; a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
       a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = layout;
       return launch_fwd_x6(a, st);
@@ -429,7 +434,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     else if (bf16) DN_TRY(launch_pack_bf16(conv_fwd_view(w, L.cin, 3), L.cin, L.cout,
                                            ws + p.packBF[i], s));
     else if (x6) DN_TRY(launch_pack_x6(conv_fwd_view(w, L.cin, 3), L.cin, L.cout, 0,
-                                       ws + p.packX[i], s, i == D1A && x6_tail_ok(p.c1s)));
+                                       ws + p.packX[i], s, x6_tail_f(i)));
     else DN_TRY(pack_conv_fwd(w, L.cin, L.cout, L.k, ws + p.packF[i], s));
   }
   // enc_conv0, fused with pool0 = x -> channels [2nf, 2nf+C) of the up1 concat buffer
@@ -545,6 +550,11 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   auto G = [&](int i) { return dprm + p.P.L[i].woff; };
   auto V = [&](long off, int stride, int coff = 0) { return View{ws + off, stride, coff}; };
   float* slab = ws + p.slab;
+  auto x6_tail_b = [&](int i) -> int {  // as x6_tail_f in the forward, for the data gradients
+    const int l = layer_level(i), nout = dgrad_nout(p, i);
+    return x6_pipelined(N, H(l), Wd(l), nout, x6_dgrad_zc(nout)) ? x6_tail_mode(p.P.L[i].cout)
+                                                                  : 0;
+  };
   for (int i = ENC1; i < NINA; ++i) {  // flipped/transposed weight images for the data gradients
     const Layer& L = p.P.L[i];
     const float* w = prm + L.woff;
@@ -553,7 +563,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     } else if (x6 && p.packXB[i] >= 0) {
       const int nout = dgrad_nout(p, i);
       DN_TRY(launch_pack_x6(conv_dgrad_view(w, L.cin, 3), L.cout, nout, x6_dgrad_zc(nout),
-                            ws + p.packXB[i], s));
+                            ws + p.packXB[i], s, x6_tail_b(i)));
     } else {
       DN_TRY(pack_conv_dgrad(w, L.cin, dgrad_nout(p, i), L.cout, L.k, ws + p.packB[i], s));
     }
@@ -575,6 +585,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     a.bias = nullptr; a.epi = epi;
     a.out = dx.p; a.out_stride = dx.stride; a.out_off = dx.off; a.out_layout = OUT_NHWC;
     a.mask = mask.p; a.mask_stride = mask.stride; a.mask_off = mask.off;
+    a.x6_tail = x6_tail_b(i);
     return launch_fwd_x6(a, st);
   };
   const View none{nullptr, 0, 0};

@@ -66,6 +66,8 @@ def _forward(x, w, b, act, x6):
     (96, 96, 64, 32, 32), (48, 48, 8, 4, 4),
     # >= 512 16x16 tiles: the pipelined 8-wave kernel (k_c3x6p)
     (96, 96, 8, 128, 128), (48, 48, 8, 128, 128), (144, 96, 8, 128, 128), (3, 48, 2, 256, 256),
+    # pipelined with a partial last chunk packed over fewer stages (x6_tail_mode 1 / 2)
+    (100, 96, 2, 256, 256), (36, 48, 4, 128, 128), (80, 96, 8, 128, 128), (16, 48, 8, 128, 128),
 ])
 @pytest.mark.parametrize("act", [0, 1])
 def test_x6_forward_vs_fp64(cin, cout, N, H, W, act):
@@ -105,6 +107,7 @@ def _dgrad(dz, w, cin, mode, mask, base, x6):
     (48, 48, 2, 32, 32), (96, 96, 2, 16, 16), (144, 96, 2, 16, 16), (48, 96, 2, 8, 8),
     (96, 48, 1, 20, 36), (144, 96, 1, 64, 32),
     (96, 96, 8, 128, 128), (144, 96, 3, 128, 112), (48, 48, 8, 128, 128),  # pipelined kernel
+    (96, 80, 8, 128, 128), (48, 16, 8, 128, 128), (96, 4, 8, 128, 128),  # ... with a tail chunk
     # ImprovedUNet shapes: final conv (K = out_nc), RDB growth convs (K = 32, wide outputs)
     (24, 3, 1, 32, 32), (24, 1, 2, 32, 32), (144, 32, 1, 16, 16), (112, 32, 1, 16, 16),
     (80, 32, 2, 16, 16), (120, 32, 1, 32, 32), (72, 24, 1, 32, 32),
