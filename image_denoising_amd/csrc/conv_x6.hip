@@ -502,10 +502,10 @@ static hipError_t run_x6(const FwdArgs& a, int nz, hipStream_t s) {
   return hipGetLastError();
 }
 
-// output channels per workgroup: 48 or 96 (wider layers run zc-blocks of 48 or 96)
+// output channels per workgroup: 32, 48 or 96 (wider layers run zc-blocks of 48 or 96)
 static int x6_np(int nout, int zc) {
   const int np = zc > 0 ? zc : nout;
-  return np <= 48 ? 48 : (np <= 96 ? 96 : 0);
+  return np <= 32 ? 32 : (np <= 48 ? 48 : (np <= 96 ? 96 : 0));
 }
 
 long x6_pack_elems(int K, int nout, int zc) {
@@ -577,15 +577,18 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
   // large grids: the pipelined 16-row kernel (one workgroup per CU, >= 2 rounds of tiles)
   static const bool no_pipe = getenv("DN_X6_NOPIPE") != nullptr;  // A/B probe
   const bool aligned = ((a.in_stride | a.in_off | a.K) & 3) == 0;
+  auto pipe = [&]() {
+    return np == 32 ? run_x6p<2>(a, nz, s) : (np == 48 ? run_x6p<3>(a, nz, s) : run_x6p<6>(a, nz, s));
+  };
   if (a.x6_tail) {  // tail-packed last chunk: only the pipelined kernel reads it
     if (!aligned || a.x6_tail != x6_tail_mode(a.K)) return hipErrorInvalidValue;
-    return np == 48 ? run_x6p<3>(a, nz, s) : run_x6p<6>(a, nz, s);
+    return pipe();
   }
-  if (!no_pipe && x6_pipelined(a.N, a.OH, a.OW, a.NOUT, a.zc) && aligned)
-    return np == 48 ? run_x6p<3>(a, nz, s) : run_x6p<6>(a, nz, s);
-  if (np == 48) {
+  if (!no_pipe && x6_pipelined(a.N, a.OH, a.OW, a.NOUT, a.zc) && aligned) return pipe();
+  if (np == 32)
+    return x6_pick_mt<2>(a, nz) == 2 ? run_x6<2, 2>(a, nz, s) : run_x6<2, 1>(a, nz, s);
+  if (np == 48)
     return x6_pick_mt<3>(a, nz) == 2 ? run_x6<3, 2>(a, nz, s) : run_x6<3, 1>(a, nz, s);
-  }
   return x6_pick_mt<6>(a, nz) == 2 ? run_x6<6, 2>(a, nz, s) : run_x6<6, 1>(a, nz, s);
 }
 

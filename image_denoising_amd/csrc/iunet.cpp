@@ -70,12 +70,15 @@ bool ggeom(int ksize, int K, int nout, GGeom& g) {
   return g.img > 0;
 }
 
-// split-bf16 (DN_PREC_FP32_X6) 3x3 convs: the kernels tile 48 or 96 output channels and 32
-// reduction channels, so they take the convs that fill those tiles (measured per shape in
-// the 32-output RDB growth convs, the 24-channel level and K = 48 stay on the
-// fp32 kernels, where the padding would cost more than the faster matrix cores give)
-bool x6_takes(int K, int nout) {
-  return nout % 48 == 0 && (K % 32 == 0 || K >= 128) && (K > 32 || nout % 96 == 0);
+// split-bf16 (DN_PREC_FP32_X6) 3x3 convs: the kernels tile 32, 48 or 96 output channels and
+// 32 reduction channels (on large grids a partial last chunk of <= 16 channels costs 5 of 9
+// stages, `tail`), so they take the convs that fill those tiles; the 24-channel level and
+// small-grid K = 48 stay on the fp32 kernels, where the padding would cost more than the
+// faster matrix cores give (measured per shape)
+bool x6_shape(int nout) { return nout == 32 || nout % 48 == 0; }
+bool x6_takes(int K, int nout, int tail) {
+  if (nout == 32 && K < 80) return false;  // 32-wide tiles: staging-bound, no gain (32x48, 32x56)
+  return x6_shape(nout) && (K % 32 == 0 || K >= 128 || tail) && (K > 32 || nout % 96 == 0);
 }
 // output-channel blocks of the wide layers: 96, or 48 where 96 would pad (144 = 3 x 48)
 int x6_zc(int nout) { return nout <= 96 ? 0 : (nout % 96 == 0 ? 96 : 48); }
@@ -122,10 +125,17 @@ hipError_t grun(int ksize, const View& in, int N, int H, int W, int K, const flo
 }
 
 // the same 3x3 conv on the split-bf16 kernels (image from launch_pack_x6 with zc = x6_zc(nout))
+// tail packing of a partial last K chunk when the launch takes the pipelined kernel
+int x6_tail_for(const View& in, int N, int H, int W, int K, int nout) {
+  const bool aligned = ((in.stride | in.off | K) & 3) == 0;
+  return aligned && x6_pipelined(N, H, W, nout, x6_zc(nout)) ? x6_tail_mode(K) : 0;
+}
+
 hipError_t x6run(const View& in, int N, int H, int W, int K, const float* wp, int nout,
                  const float* bias, int epi, const View& out, int layout, const View& aux,
-                 hipStream_t s) {
+                 int tail, hipStream_t s) {
   FwdArgs a{};
+  a.x6_tail = tail;
   a.in = in.p; a.in_stride = in.stride; a.in_off = in.off; a.IHt = H; a.IWt = W;
   a.N = N; a.OH = H; a.OW = W; a.K = K; a.NOUT = nout;
   a.zc = x6_zc(nout);
@@ -298,7 +308,7 @@ bool iunet_build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, IPlan
   long x6max = 0;
   auto pf = [&](int k, int K, int nout) {
     pk = std::max(pk, gpack_floats(k, K, nout));
-    if (k == 3 && x6_takes(K, nout))
+    if (k == 3 && x6_shape(nout))
       x6max = std::max(x6max, (x6_pack_elems(K, nout, x6_zc(nout)) + 1) / 2);
   };
   for (int i = 0; i < 4; ++i) {
@@ -439,10 +449,11 @@ dn_status conv_fwd(const Ctx& c, const IConv& L, const View& in, int h, int w, i
                    const View& out, int layout = OUT_NHWC, const View& aux = kNone) {
   OpScope prof(c.s, "fwd", L.cout, L.cin, L.k, h, w, c.p.N, 1.0);
   float* pk = c.ws + c.p.pack;
-  if (c.prec == DN_PREC_FP32_X6 && L.k == 3 && x6_takes(L.cin, L.cout)) {
+  const int tail = x6_tail_for(in, c.p.N, h, w, L.cin, L.cout);
+  if (c.prec == DN_PREC_FP32_X6 && L.k == 3 && x6_takes(L.cin, L.cout, tail)) {
     IU_TRY(launch_pack_x6(conv_fwd_view(c.Wt(L), L.cin, 3), L.cin, L.cout, x6_zc(L.cout), pk,
-                          c.s));
-    IU_TRY(x6run(in, c.p.N, h, w, L.cin, pk, L.cout, c.Bs(L), epi, out, layout, aux, c.s));
+                          c.s, tail));
+    IU_TRY(x6run(in, c.p.N, h, w, L.cin, pk, L.cout, c.Bs(L), epi, out, layout, aux, tail, c.s));
     return DN_OK;
   }
   IU_TRY(gpack_fwd(c.Wt(L), L.k, L.cin, L.cout, pk, c.s));
@@ -592,10 +603,11 @@ dn_status dgrad_g(const Ctx& c, const IConv& L, const View& g, int h, int w, int
                   const View& aux, const View& dx) {
   OpScope prof(c.s, "dgrad", nout, L.cout, L.k, h, w, c.p.N, 1.0);
   float* pk = c.ws + c.p.pack;
-  if (c.prec == DN_PREC_FP32_X6 && L.k == 3 && x6_takes(L.cout, nout)) {
+  const int tail = x6_tail_for(g, c.p.N, h, w, L.cout, nout);
+  if (c.prec == DN_PREC_FP32_X6 && L.k == 3 && x6_takes(L.cout, nout, tail)) {
     IU_TRY(launch_pack_x6(conv_dgrad_view(c.Wt(L), L.cin, 3), L.cout, nout, x6_zc(nout), pk,
-                          c.s));
-    IU_TRY(x6run(g, c.p.N, h, w, L.cout, pk, nout, nullptr, epi, dx, OUT_NHWC, aux, c.s));
+                          c.s, tail));
+    IU_TRY(x6run(g, c.p.N, h, w, L.cout, pk, nout, nullptr, epi, dx, OUT_NHWC, aux, tail, c.s));
     return DN_OK;
   }
   IU_TRY(gpack_dgrad(c.Wt(L), L.k, L.cin, L.cout, nout, pk, c.s));

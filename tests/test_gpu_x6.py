@@ -68,6 +68,8 @@ def _forward(x, w, b, act, x6):
     (96, 96, 8, 128, 128), (48, 48, 8, 128, 128), (144, 96, 8, 128, 128), (3, 48, 2, 256, 256),
     # pipelined with a partial last chunk packed over fewer stages (x6_tail_mode 1 / 2)
     (100, 96, 2, 256, 256), (36, 48, 4, 128, 128), (80, 96, 8, 128, 128), (16, 48, 8, 128, 128),
+    # 32 outputs (ImprovedUNet RDB growth convs): 4-wave and pipelined (+ tail)
+    (48, 32, 2, 32, 32), (144, 32, 1, 24, 40), (80, 32, 8, 128, 128), (112, 32, 8, 128, 128),
 ])
 @pytest.mark.parametrize("act", [0, 1])
 def test_x6_forward_vs_fp64(cin, cout, N, H, W, act):
@@ -76,11 +78,16 @@ def test_x6_forward_vs_fp64(cin, cout, N, H, W, act):
     w = torch.randn(cout, cin, 3, 3, generator=g) * 0.1
     b = torch.randn(cout, generator=g) * 0.1
     y6 = _forward(x, w, b, act, True)
-    y32 = _forward(x, w, b, act, False)
     ref = F.conv2d(x.double(), w.double(), b.double(), padding=1)
     if act:
         ref = F.leaky_relu(ref, 0.2)
-    e6, e32 = rel_err(y6.numpy(), ref.numpy()), rel_err(y32.numpy(), ref.numpy())
+    e6 = rel_err(y6.numpy(), ref.numpy())
+    try:
+        y32 = _forward(x, w, b, act, False)
+    except L().DenoiseHipError:  # channel counts the fp32 op kernels are not built for
+        assert e6 < X6_TOL, e6
+        return
+    e32 = rel_err(y32.numpy(), ref.numpy())
     assert e6 < X6_TOL, (e6, e32)
     assert e6 < 4 * e32 + 1e-7, (e6, e32)  # fp32-class, not bf16-class (~4e-3)
 
@@ -108,6 +115,7 @@ def _dgrad(dz, w, cin, mode, mask, base, x6):
     (96, 48, 1, 20, 36), (144, 96, 1, 64, 32),
     (96, 96, 8, 128, 128), (144, 96, 3, 128, 112), (48, 48, 8, 128, 128),  # pipelined kernel
     (96, 80, 8, 128, 128), (48, 16, 8, 128, 128), (96, 4, 8, 128, 128),  # ... with a tail chunk
+    (32, 96, 2, 32, 32), (32, 48, 8, 128, 128),  # 32 outputs
     # ImprovedUNet shapes: final conv (K = out_nc), RDB growth convs (K = 32, wide outputs)
     (24, 3, 1, 32, 32), (24, 1, 2, 32, 32), (144, 32, 1, 16, 16), (112, 32, 1, 16, 16),
     (80, 32, 2, 16, 16), (120, 32, 1, 32, 32), (72, 24, 1, 32, 32),
