@@ -17,7 +17,7 @@ BUILD = os.path.join(PKG, "_objs")
 LIB = os.path.join(PKG, "libdenoise_hip.so")
 SOURCES = ["conv.hip", "conv_bf16.hip", "conv_x6.hip", "elementwise.hip", "first_layer.hip", "eval.hip", "adapter.hip", "iunet_ops.hip", "unet.cpp",
            "iunet.cpp", "capi.cpp"]
-HEADERS = ["dn_internal.h", "conv_epi.h", "philox.h", "unet.h", "iunet.h", "iunet_ops.h"]
+HEADERS = ["dn_internal.h", "conv_epi.h", "x6_core.h", "philox.h", "unet.h", "iunet.h", "iunet_ops.h"]
 ARCH = os.environ.get("DN_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",

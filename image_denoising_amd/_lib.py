@@ -74,6 +74,8 @@ SIGNATURES = {
     "dn_conv2d_wgrad_slab_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "dn_conv2d_backward_weight": (c_int, [_F, _F, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                           _F, c_void_p, c_void_p]),
+    "dn_conv2d_backward_weight_x6": (c_int, [_F, _F, c_int, c_int, c_int, c_int, c_int, c_int,
+                                             _F, c_void_p, c_void_p]),
     "dn_deconv2x2_forward": (c_int, [_F, c_int, c_int, c_int, c_int, _F, _F, c_int, _F, c_int,
                                      c_int, c_void_p, c_size_t, c_void_p]),
     "dn_deconv2x2_backward_data": (c_int, [_F, c_int, c_int, c_int, c_int, c_int, _F, c_int, _F,

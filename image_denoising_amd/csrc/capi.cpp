@@ -515,6 +515,18 @@ dn_status dn_conv2d_backward_weight(const float* dz, const float* x, int x_strid
                     "dn_conv2d_backward_weight");
 }
 
+dn_status dn_conv2d_backward_weight_x6(const float* dz, const float* x, int x_stride, int N,
+                                       int H, int W, int Cin, int Cout, float* dwb, void* slab,
+                                       void* stream) {
+  if (!dz || !x || !dwb || !slab) return fail(DN_ERR_ARG, "null argument");
+  if (!wgrad_supported(W_C3, Cout, Cin)) return fail(DN_ERR_ARG, "unsupported Cout");
+  const int sp = wgrad_splits(W_C3, N, H, W, Cin, Cout);
+  return hip_status(wgrad(W_C3, View{const_cast<float*>(dz), Cout, 0},
+                          View{const_cast<float*>(x), x_stride, 0}, N, H, W, Cout, Cin, dwb,
+                          static_cast<float*>(slab), sp, (hipStream_t)stream, true),
+                    "dn_conv2d_backward_weight_x6");
+}
+
 dn_status dn_deconv2x2_forward(const float* x, int N, int H, int W, int Cin, const float* w,
                                const float* b, int Cout, float* y, int y_stride, int y_off,
                                void* pack_ws, size_t pack_bytes, void* stream) {

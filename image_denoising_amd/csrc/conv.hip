@@ -1272,8 +1272,9 @@ int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
   return (int)want;
 }
 
-hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s) {
+hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s, bool x6) {
   const int cf = (a.Cout + 15) / 16;
+  if (x6 && mode == W_C3 && wgrad3_x6_ok(a)) return launch_wgrad3_x6(a, splits, s);
   if (mode == W_C3 && wgrad3_ok(a)) {
     if (cf == 6) return run_wgrad3<6, 2, 2>(a, splits, s);
     if (cf == 3) return run_wgrad3<3, 1, 3>(a, splits, s);

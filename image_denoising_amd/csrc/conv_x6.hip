@@ -21,68 +21,9 @@
 #include <cstdlib>
 
 #include "conv_epi.h"
+#include "x6_core.h"
 
 namespace dn {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-
-// 16-B quad q of LDS row `row` lives at quad q ^ ((row >> 1) & 3)
-__device__ __forceinline__ int x6_swz(int row, int q) { return q ^ ((row >> 1) & 3); }
-
-// v = h + m + l exactly (normal fp32 v); each step's remainder is exact in fp32
-__device__ __forceinline__ void split3(float v, __bf16& h, __bf16& m, __bf16& l) {
-  h = (__bf16)v;
-  const float r = v - (float)h;
-  m = (__bf16)r;
-  l = (__bf16)(r - (float)m);
-}
-
-__device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-// One 16x16x32 block of every fragment of a wave: acc[m][q] += sum_k A[m] B[q] at fp32 accuracy.
-// The leading product a0*b0 and the five corrections are summed by the matrix core from zero
-// (hi, lo) and only then added to the running fp32 sum with a round-to-nearest VALU add: the
-// matrix core's internal alignment rounds toward -inf, which on a long running sum (6 x 27
-// MFMAs per output for K = 96) leaves a small negative bias that the weight-gradient sums over
-// ~1e5 pixels would turn into a visible error; on a fresh 32-term block it is ~50x smaller.
-// QG output-channel fragments are processed together (temporaries 8*MT*QG registers) so that
-// the lo chain has MT*QG - 1 independent MFMAs between dependent ones.
-// fragment-group width: >= 4 independent lo chains within the register budget
-constexpr int x6_qg(int mt, int nt) { return mt >= 4 ? 1 : (mt == 2 ? (nt % 2 ? 3 : 2) : nt); }
-
-template <int MT, int NT, int QG>
-__device__ __forceinline__ void x6_block(f32x4 (&acc)[MT][NT], const bf16x8 (&av)[3][MT],
-                                         const bf16x8 (&bv)[3][NT]) {
-  static_assert(NT % QG == 0, "whole fragment groups");
-  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-  constexpr int PA[4] = {1, 0, 1, 2}, PB[4] = {0, 2, 1, 0};
-#pragma unroll
-  for (int q0 = 0; q0 < NT; q0 += QG) {
-    f32x4 hi[MT][QG], lo[MT][QG];
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int g = 0; g < QG; ++g) hi[m][g] = mfma_bf16(av[0][m], bv[0][q0 + g], z);
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int g = 0; g < QG; ++g) lo[m][g] = mfma_bf16(av[0][m], bv[1][q0 + g], z);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int g = 0; g < QG; ++g)
-          lo[m][g] = mfma_bf16(av[PA[j]][m], bv[PB[j]][q0 + g], lo[m][g]);
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int g = 0; g < QG; ++g) acc[m][q0 + g] += hi[m][g] + lo[m][g];
-  }
-}
 
 // bf16 elements of one weight stage (one tap, three planes of NP x 32) in the packed image,
 // padded to whole rounds of the pipelined kernel's DMA (8 waves x 1 KiB global_load_lds_dwordx4;
@@ -590,6 +531,233 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
   if (np == 48)
     return x6_pick_mt<3>(a, nz) == 2 ? run_x6<3, 2>(a, nz, s) : run_x6<3, 1>(a, nz, s);
   return x6_pick_mt<6>(a, nz) == 2 ? run_x6<6, 2>(a, nz, s) : run_x6<6, 1>(a, nz, s);
+}
+
+
+// ------------------------------------------------------------------------------------
+// 3x3 weight gradient at fp32 accuracy on the bf16 matrix cores (96 output channels).
+// GEMM M = 96 output channels, N = 32 input channels x 9 taps, K = pixels; workgroup = 3 x 2
+// waves, wave (wm, wn) owns output fragments {2wm, 2wm+1} x input channels [16wn, 16wn+16)
+// x 9 taps.  One K stage = 32 pixels (a 32-wide row segment, or 2 / 4 rows of 16 / 8 pixels)
+// = ONE v_mfma_f32_16x16x32_bf16 K block: lane group g holds stage pixels 8g..8g+7.
+// Operands are loaded into registers (float4 along channels) one stage ahead, then split once
+// into three bf16 planes and transposed into LDS with the pixel index contiguous:
+//   G  [plane][co][k]                          (64-B rows, 16-B quads XOR-swizzled)
+//   X  [dx][plane][row][ci][col]  col = k - dx  (one copy per horizontal tap, so every
+//                                                operand read is one aligned ds_read_b128)
+// and each (fragment, tap) runs the six piece products of x6_block, summed from zero and
+// added to the fp32 accumulators (no long-sum rounding bias; see x6_block).
+// ------------------------------------------------------------------------------------
+template <int SWL>
+struct Wx6Cfg {
+  static constexpr int SW = 1 << SWL, SH = 32 >> SWL, RH = SH + 2, XW = SW + 2;
+  static constexpr int COUT = 96, CIB = 32, MFW = 2, WM = 3, WN = 2, NTHR = 64 * WM * WN;
+  static constexpr int GPL = COUT * 32;                  // bf16 per G plane
+  static constexpr int XPL = RH * CIB * SW;              // bf16 per X plane (one dx copy)
+  static constexpr int XITEMS = (CIB / 4) * RH * (XW / 2);  // (ci quad, row, column pair)
+  static constexpr int XI = (XITEMS + NTHR - 1) / NTHR;
+  static constexpr int LBYTES = 2 * (3 * GPL + 9 * XPL);
+  static_assert(16 * (COUT / 4) == NTHR, "one G item (channel quad, pixel pair) per thread");
+};
+
+template <int SWL>
+__global__ __launch_bounds__(384, 3) void k_wgrad3x6(WgradArgs a0) {
+  using C = Wx6Cfg<SWL>;
+  const WgradArgs a = wg_block(a0);
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
+  __bf16* lg = reinterpret_cast<__bf16*>(lds_raw);
+  __bf16* lx = lg + 3 * C::GPL;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  const int li = lane & 15, lgp = lane >> 4;
+  const int ci0 = blockIdx.y * C::CIB;
+  constexpr int sw = C::SW, sh = C::SH;
+  const int ux = (a.KW + sw - 1) / sw, uy = (a.KH + sh - 1) / sh;
+  const long U = (long)a.N * uy * ux;
+  const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
+  const bool do_bias = a.bias && blockIdx.y == 0 && wn == 0;
+
+  f32x4 acc[9][C::MFW][1];
+  f32x4 accb[C::MFW];
+#pragma unroll
+  for (int i = 0; i < C::MFW; ++i) {
+    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t][i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // this thread's G item: output-channel quad gq, stage pixel pair (2gk, 2gk+1)
+  const int gq = tid % (C::COUT / 4), gk = tid / (C::COUT / 4);
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 rg[2], rx[C::XI][2];
+
+  auto load = [&](long u) {
+    const int n = (int)(u / ((long)uy * ux));
+    const int rem = (int)(u - (long)n * uy * ux);
+    const int py0 = (rem / ux) * sh, px0 = (rem % ux) * sw;
+    const float* gb = a.g + (long)n * a.KH * a.KW * a.g_stride + a.g_off + 4 * gq;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = 2 * gk + j;
+      const int gy = py0 + (k >> SWL), gx = px0 + (k & (sw - 1));
+      rg[j] = (gy < a.KH && gx < a.KW)
+                  ? *reinterpret_cast<const f32x4*>(gb + ((long)gy * a.KW + gx) * a.g_stride)
+                  : z4;
+    }
+    const float* xb = a.x + (long)n * a.KH * a.KW * a.x_stride + a.x_off;
+#pragma unroll
+    for (int q = 0; q < C::XI; ++q) {
+      const int it = tid + q * C::NTHR;
+      const int cq = it % (C::CIB / 4), rest = it / (C::CIB / 4);
+      const int r = rest / (C::XW / 2), cp = rest % (C::XW / 2);
+      const int gy = py0 - 1 + r, ci = ci0 + 4 * cq;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int gx = px0 - 1 + 2 * cp + j;
+        const bool ok = it < C::XITEMS && gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW &&
+                        ci < a.Cin;
+        rx[q][j] = ok ? *reinterpret_cast<const f32x4*>(xb + ((long)gy * a.KW + gx) * a.x_stride + ci)
+                      : z4;
+      }
+    }
+  };
+
+  auto store = [&]() {
+    unsigned* lgw = reinterpret_cast<unsigned*>(lg);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {  // G: [plane][co][k], pair (2gk, 2gk+1) = one 32-bit word
+      const int co = 4 * gq + c, k = 2 * gk;
+      unsigned w[3];
+      split3x2(rg[0][c], rg[1][c], w[0], w[1], w[2]);
+      const int off = co * 32 + x6_swz(co, k >> 3) * 8 + (k & 7);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) lgw[(p * C::GPL + off) >> 1] = w[p];
+    }
+#pragma unroll
+    for (int q = 0; q < C::XI; ++q) {
+      const int it = tid + q * C::NTHR;
+      if (it >= C::XITEMS) continue;
+      const int cq = it % (C::CIB / 4), rest = it / (C::CIB / 4);
+      const int r = rest / (C::XW / 2), cp = rest % (C::XW / 2);
+      const int c0 = 2 * cp;  // halo columns c0, c0 + 1 -> k = c - dx in copy dx
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int row = r * C::CIB + 4 * cq + c;
+        unsigned w[3];
+        split3x2(rx[q][0][c], rx[q][1][c], w[0], w[1], w[2]);
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            __bf16* dst = lx + (dx * 3 + p) * C::XPL;
+            const int k0 = c0 - dx;  // even for dx = 0, 2
+            auto at = [&](int k) {
+              return SWL == 5 ? row * 32 + x6_swz(row, k >> 3) * 8 + (k & 7) : row * sw + k;
+            };
+            if (dx != 1) {
+              if (k0 >= 0 && k0 + 1 < sw) reinterpret_cast<unsigned*>(dst)[at(k0) >> 1] = w[p];
+            } else {
+              const unsigned short lo = (unsigned short)(w[p] & 0xffffu);
+              const unsigned short hi = (unsigned short)(w[p] >> 16);
+              if (k0 >= 0) reinterpret_cast<unsigned short*>(dst)[at(k0)] = lo;
+              if (k0 + 1 < sw) reinterpret_cast<unsigned short*>(dst)[at(k0 + 1)] = hi;
+            }
+          }
+        }
+      }
+    }
+  };
+
+  if (u_beg < u_end) load(u_beg);
+  for (long u = u_beg; u < u_end; ++u) {
+    __syncthreads();  // everyone done reading the previous stage
+    store();
+    __syncthreads();
+    bf16x8 av[3][C::MFW];
+#pragma unroll
+    for (int i = 0; i < C::MFW; ++i) {
+      const int co = (wm * C::MFW + i) * 16 + li;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        av[p][i] = *reinterpret_cast<const bf16x8*>(lg + p * C::GPL + co * 32 + x6_swz(co, lgp) * 8);
+    }
+    if (do_bias) {  // sum over pixels: the G pieces against ones (exact in bf16)
+      bf16x8 one;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) one[e] = (__bf16)1.0f;
+#pragma unroll
+      for (int i = 0; i < C::MFW; ++i) {
+        const f32x4 hi = mfma_bf16(av[0][i], one, z4);
+        f32x4 lo = mfma_bf16(av[1][i], one, z4);
+        lo = mfma_bf16(av[2][i], one, lo);
+        accb[i] += hi + lo;
+      }
+    }
+    // lane group lgp holds stage pixels 8lgp..8lgp+7: row r0, columns c0.. (within one row)
+    const int k0 = 8 * lgp, r0 = k0 >> SWL, c0 = k0 & (sw - 1);
+    const int ci = wn * 16 + li;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int row = (r0 + t / 3) * C::CIB + ci;
+      const int off = SWL == 5 ? row * 32 + x6_swz(row, lgp) * 8 : row * sw + c0;
+      bf16x8 bv[3][1];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        bv[p][0] = *reinterpret_cast<const bf16x8*>(lx + ((t % 3) * 3 + p) * C::XPL + off);
+      x6_block<C::MFW, 1, 1>(acc[t], av, bv);
+      // keep the scheduler from interleaving taps: each tap's fresh hi / lo sums would stay
+      // live across the others and spill (two lo chains per tap are enough in flight)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (u + 1 < u_end) load(u + 1);  // in flight while the other workgroup computes
+  }
+
+  float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
+  const int cio = ci0 + wn * 16 + li;
+  const int cot = a.cout_total ? a.cout_total : a.Cout;
+#pragma unroll
+  for (int i = 0; i < C::MFW; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = (wm * C::MFW + i) * 16 + 4 * lgp + r;
+        if (cio < a.Cin)
+          slab[((long)(a.co_base + co) * a.cin_total + a.ci_base + cio) * 9 + t] = acc[t][i][0][r];
+      }
+  if (do_bias && li == 0) {
+#pragma unroll
+    for (int i = 0; i < C::MFW; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = (wm * C::MFW + i) * 16 + 4 * lgp + r;
+        slab[(long)cot * a.cin_total * 9 + a.co_base + co] = accb[i][r];
+      }
+  }
+}
+
+// 96 output channels, 16-byte aligned NHWC views whose channel quads stay inside each pixel,
+// rows at least 8 wide (a lane's 8 K values must lie in one row)
+bool wgrad3_x6_ok(const WgradArgs& a) {
+  if (a.Cout != 96 || a.Cin < 32 || a.KW < 8 || !a.zeros) return false;
+  if ((a.g_stride | a.g_off | a.x_stride | a.x_off) & 3) return false;
+  return a.x_off + ((a.Cin + 3) & ~3) <= a.x_stride && a.g_off + 96 <= a.g_stride;
+}
+
+// two workgroups per CU: splits x input-channel blocks fill one round of 512
+int wgrad_splits_x6(const WgradArgs& a, int splits) {
+  if (!wgrad3_x6_ok(a)) return splits;
+  const int cap = 512 / ((a.Cin + 31) / 32);
+  return splits < cap ? splits : (cap < 1 ? 1 : cap);
+}
+
+hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s) {
+  const dim3 grid(splits, (a.Cin + 31) / 32, 1);
+  if (a.KW >= 32) hipLaunchKernelGGL(k_wgrad3x6<5>, grid, dim3(384), 0, s, a);
+  else if (a.KW >= 16) hipLaunchKernelGGL(k_wgrad3x6<4>, grid, dim3(384), 0, s, a);
+  else hipLaunchKernelGGL(k_wgrad3x6<3>, grid, dim3(384), 0, s, a);
+  return hipGetLastError();
 }
 
 }  // namespace dn

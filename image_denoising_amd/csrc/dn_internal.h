@@ -147,7 +147,11 @@ hipError_t launch_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);
 hipError_t launch_nin_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);
 hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s);
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
-hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s);
+hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s, bool x6 = false);
+// bf16x6 3x3 weight gradient (conv_x6.hip): 96 outputs, Cin >= 32, rows >= 8 wide
+bool wgrad3_x6_ok(const WgradArgs& a);
+int wgrad_splits_x6(const WgradArgs& a, int splits);  // split count when the x6 kernel is taken
+hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s);
 bool wgrad1_ok(int mode, const WgradArgs& a);
 long wgrad_slab_floats(int mode, int N, int KH, int KW, int cin, int cout);
 hipError_t launch_wgrad1(int mode, const WgradArgs& a, float* dwb, hipStream_t s);

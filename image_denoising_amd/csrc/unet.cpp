@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace dn {
@@ -341,7 +342,7 @@ hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const flo
 }
 
 hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, int cout, int cin,
-                 float* dwb, float* slab, int splits, hipStream_t s) {
+                 float* dwb, float* slab, int splits, hipStream_t s, bool x6) {
   WgradArgs a{};
   a.g = g.p; a.g_stride = g.stride; a.g_off = g.off;
   a.x = x.p; a.x_stride = x.stride; a.x_off = x.off;
@@ -356,7 +357,8 @@ hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, 
   hipError_t e = hipMemsetAsync(slab, 0, 64 * sizeof(float), s);
   if (e != hipSuccess) return e;
   if (wgrad1_ok(mode, a)) return launch_wgrad1(mode, a, dwb, s);  // 1x1 / deconv, own splits
-  e = launch_wgrad(mode, a, splits, s);
+  if (x6 && mode == W_C3) splits = wgrad_splits_x6(a, splits);
+  e = launch_wgrad(mode, a, splits, s, x6);
   if (e != hipSuccess) return e;
   return launch_reduce(slab + 64, n, splits, n, dwb, s);
 }
@@ -543,6 +545,10 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
 dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* ws,
                         hipStream_t s, int prec) {
   const bool x6 = prec == DN_PREC_FP32_X6;
+  // bf16x6 3x3 weight gradients (k_wgrad3x6) only on request (DN_X6_WGRAD=1): measured slower
+  // than the fp32 k_wgrad3 in the step (37.5 vs 33.2 ms)
+  static const bool x6w_env = getenv("DN_X6_WGRAD") && atoi(getenv("DN_X6_WGRAD")) != 0;
+  const bool x6w = x6 && x6w_env;
   const int N = p.N, nf = p.nf, C = p.C;
   auto H = [&](int l) { return p.H >> l; };
   auto Wd = [&](int l) { return p.W >> l; };
@@ -622,7 +628,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   DN_TRY(wgrad(W_C1, V(p.g_na, 96), V(p.d1b, 96), N, H(0), Wd(0), 96, 96, G(NINA), slab,
                p.splits[NINA], s));
   DN_TRY(wgrad(W_C3, V(p.g_d1b, 96), V(p.d1a, 96), N, H(0), Wd(0), 96, 96, G(D1B), slab,
-               p.splits[D1B], s));
+               p.splits[D1B], s, x6w));
   DN_TRY(conv_dgrad(V(p.g_d1b, 96), N, H(0), Wd(0), 96, Wt(D1B), 96, 3, EPI_MASK,
                     V(p.d1a, 96), V(p.g_d1a, 96), s));
   // dec_conv1a weight gradient: the MFMA kernel over the up1 channels [0, 2nf) and the thin
@@ -636,8 +642,9 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     a.zeros = slab; a.slab = slab + 64; a.slab_stride = n;
     a.wlayout = 0; a.cin_total = p.c1k; a.ci_base = 0; a.bias = 1;
     DN_TRY(hipMemsetAsync(slab, 0, 64 * sizeof(float), s));
-    DN_TRY(launch_wgrad(W_C3, a, p.splits[D1A], s));
-    DN_TRY(launch_reduce(slab + 64, n, p.splits[D1A], n, G(D1A), s));
+    const int sp = x6w ? wgrad_splits_x6(a, p.splits[D1A]) : p.splits[D1A];
+    DN_TRY(launch_wgrad(W_C3, a, sp, s, x6w));
+    DN_TRY(launch_reduce(slab + 64, n, sp, n, G(D1A), s));
     // input-channel slice: own (compact [co][C][9]) slab after the MFMA kernel's rows, own
     // split count, then scattered into W[co][2nf + ci][t] (overwrites the unreduced columns)
     float* thin = slab + 64 + (long)p.splits[D1A] * n;
@@ -664,11 +671,11 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                         V(p.g_db[l], 2 * nf), s));
     const int ia = da_idx[l], ib = ia + 1;
     DN_TRY(wgrad(W_C3, V(p.g_db[l], 2 * nf), V(p.da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, 2 * nf,
-                 G(ib), slab, p.splits[ib], s));
+                 G(ib), slab, p.splits[ib], s, x6w));
     DN_TRY(conv_dgrad(V(p.g_db[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ib), 2 * nf, 3,
                       EPI_MASK, V(p.da[l], 2 * nf), V(p.g_da[l], 2 * nf), s));
     DN_TRY(wgrad(W_C3, V(p.g_da[l], 2 * nf), V(p.c[l], p.cs[l]), N, H(l), Wd(l), 2 * nf, p.cs[l],
-                 G(ia), slab, p.splits[ia], s));
+                 G(ia), slab, p.splits[ia], s, x6w));
     DN_TRY(conv_dgrad(V(p.g_da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ia), p.cs[l], 3,
                       EPI_PLAIN, none, V(p.g_c[l], p.cs[l]), s));
     dU = V(p.g_c[l], p.cs[l], 0);  // [u_{l+1} grad | skip grad]
@@ -680,7 +687,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                       EPI_MASK, V(p.g_a6, nf), s));
   // enc_conv6 (input p5, level 5)
   DN_TRY(wgrad(W_C3, V(p.g_a6, nf), V(p.p5, nf), N, H(5), Wd(5), nf, nf, G(ENC6), slab,
-               p.splits[ENC6], s));
+               p.splits[ENC6], s, x6w));
   DN_TRY(conv_dgrad(V(p.g_a6, nf), N, H(5), Wd(5), nf, Wt(ENC6), nf, 3, EPI_PLAIN, none,
                     V(p.g_p5, nf), s));
   // pool5 backward -> g_a5 (level 4)
@@ -690,7 +697,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     const int li = ENC2 + (l - 1);
     const int skip = (l == 4) ? nf : 2 * nf;
     DN_TRY(wgrad(W_C3, V(p.g_a[l], nf), V(p.c[l], p.cs[l], skip), N, H(l), Wd(l), nf, nf, G(li),
-                 slab, p.splits[li], s));
+                 slab, p.splits[li], s, x6w));
     DN_TRY(conv_dgrad(V(p.g_a[l], nf), N, H(l), Wd(l), nf, Wt(li), nf, 3, EPI_ACCUM, none,
                       V(p.g_c[l], p.cs[l], skip), s));
     // pool_l backward: d p_l (skip slice) -> gradient of the level l-1 activation
@@ -704,7 +711,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   }
   // enc_conv1 (input a0), enc_conv0 (input x = c1 slice; no data gradient needed)
   DN_TRY(wgrad(W_C3, V(p.g_a1, nf), V(p.a0, nf), N, H(0), Wd(0), nf, nf, G(ENC1), slab,
-               p.splits[ENC1], s));
+               p.splits[ENC1], s, x6w));
   DN_TRY(conv_dgrad(V(p.g_a1, nf), N, H(0), Wd(0), nf, Wt(ENC1), nf, 3, EPI_MASK, V(p.a0, nf),
                     V(p.g_a0, nf), s));
   DN_TRY(launch_enc0_wgrad(ws + p.g_a0, nf, ws + p.xin, N, C, H(0), Wd(0), slab,

@@ -95,6 +95,6 @@ hipError_t deconv_forward(const View& x, int N, int h, int w, int cin, const flo
 hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const float* wp, int cin,
                         const View& mask, int epi, const View& dx, hipStream_t s);
 hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, int cout, int cin,
-                 float* dwb, float* slab, int splits, hipStream_t s);
+                 float* dwb, float* slab, int splits, hipStream_t s, bool x6 = false);
 
 }  // namespace dn

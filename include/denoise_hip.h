@@ -201,6 +201,12 @@ size_t dn_conv2d_wgrad_slab_size(int N, int H, int W, int Cin, int Cout, int ksi
 dn_status dn_conv2d_backward_weight(const float* dz, const float* x, int x_stride, int N, int H,
                                     int W, int Cin, int Cout, int ksize, float* dwb, void* slab,
                                     void* stream);
+/* The same 3x3 weight gradient at fp32 accuracy on the bf16 matrix cores (DN_PREC_FP32_X6: each
+   32-pixel K block as six split-bf16 products, summed from zero, added in fp32).  96 output
+   channels with Cin >= 32 take the split kernel; other shapes run the fp32 kernel.  Same slab. */
+dn_status dn_conv2d_backward_weight_x6(const float* dz, const float* x, int x_stride, int N,
+                                       int H, int W, int Cin, int Cout, float* dwb, void* slab,
+                                       void* stream);
 /* ConvTranspose2d(Cin, Cout, 2, 2) (arch_unet.py:57): x [N,H,W,Cin] -> y [N,2H,2W,*]
    (written at channel offset y_off of stride y_stride, i.e. directly into a concat buffer). */
 dn_status dn_deconv2x2_forward(const float* x, int N, int H, int W, int Cin, const float* w,

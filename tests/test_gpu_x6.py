@@ -157,3 +157,44 @@ def test_x6_exact_on_bf16_representable_inputs():
     y6 = _forward(x, w, b, 0, True)
     ref = F.conv2d(x.double(), w.double(), None, padding=1)
     assert rel_err(y6.numpy(), ref.numpy()) < 1e-6
+
+
+def _wgrad(dz, x, x6):
+    _lib = L()
+    N, cout, H, W = dz.shape
+    cin = x.shape[1]
+    nbytes = _lib.lib().dn_conv2d_wgrad_slab_size(N, H, W, cin, cout, 3)
+    slab = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    dwb = torch.full((cout * cin * 9 + cout,), float("nan"), device=DEV)
+    dzg, xg = nhwc(dz).to(DEV), nhwc(x).to(DEV)
+    if x6:
+        _lib.call("dn_conv2d_backward_weight_x6", dzg.data_ptr(), xg.data_ptr(), cin, N, H, W,
+                  cin, cout, dwb.data_ptr(), slab.data_ptr(), S())
+    else:
+        _lib.call("dn_conv2d_backward_weight", dzg.data_ptr(), xg.data_ptr(), cin, N, H, W, cin,
+                  cout, 3, dwb.data_ptr(), slab.data_ptr(), S())
+    return dwb.cpu().numpy()
+
+
+# k_wgrad3<6, 3, 2, *, X6>: 96 outputs; 32-wide rows and the 16/8/4-wide multi-row K stages;
+# Cin 96 / 144 (concat) / 48 / 97 (a partial 32-channel block); long pixel sums (64 x 128^2)
+@pytest.mark.parametrize("cin,cout,N,H,W", [
+    (96, 96, 2, 32, 32), (144, 96, 2, 16, 32), (48, 96, 2, 64, 64), (97, 96, 1, 32, 32),
+    (96, 96, 4, 16, 16), (96, 96, 8, 8, 8), (96, 96, 16, 4, 4), (96, 96, 64, 128, 128),
+    (48, 48, 2, 32, 32),  # 48 outputs: the fp32 kernel behind the same entry point
+])
+def test_x6_backward_weight_vs_fp64(cin, cout, N, H, W):
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(N, cin, H, W, generator=g)
+    dz = torch.randn(N, cout, H, W, generator=g)
+    w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    b = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x.double(), w, b, padding=1).backward(dz.double())
+    nw = cout * cin * 9
+    ref_w, ref_b = w.grad.numpy().reshape(-1), b.grad.numpy()
+    o6, o32 = _wgrad(dz, x, True), _wgrad(dz, x, False)
+    assert np.isfinite(o6).all()
+    e6, e32 = rel_err(o6[:nw], ref_w), rel_err(o32[:nw], ref_w)
+    assert e6 < X6_TOL, (e6, e32)
+    assert e6 < 4 * e32 + 1e-7, (e6, e32)
+    assert rel_err(o6[nw:], ref_b) < X6_TOL
