@@ -760,4 +760,149 @@ hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------
+// The nin head (nin_a -> nin_b -> nin_c, arch_unet.py:186-190, 257-259) on the activated
+// dec_conv1b output, with the two 96x96 1x1 GEMMs in the bf16x6 arithmetic.  As in k_nin_head
+// the tile lives in the 16x16 MFMA C/D map (rows = channels, columns = 16 pixels), which is
+// directly the B operand of the next GEMM: for K block b (32 channels) lane group g supplies
+// channels {32b + 4g + r, 32b + 16 + 4g + r} (r < 4) = registers 2b and 2b+1 of its tile
+// fragment, split into three bf16x8 planes in registers.  The weight images are pre-split
+// in the same permuted K order (k_pack_head_x6: [plane][b][out][32], 64-B rows, quads
+// swizzled) and DMA'd into one 54 KiB LDS slot per layer.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pack_head_x6(const float* __restrict__ wa,
+                                                      const float* __restrict__ wb,
+                                                      __bf16* __restrict__ out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= 2 * X6_HEAD_BF) return;
+  const int layer = e / X6_HEAD_BF, r0 = e % X6_HEAD_BF;
+  const int p = r0 / (3 * 96 * 32), row = (r0 / 32) % (3 * 96), k = r0 % 32;  // row = b*96 + o
+  const int b = row / 96, o = row % 96, g = k >> 3, j = k & 7;
+  const int ch = 32 * b + (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4));
+  __bf16 h, m, l;
+  split3((layer ? wb : wa)[o * 96 + ch], h, m, l);
+  out[layer * X6_HEAD_BF + (p * 3 * 96 + row) * 32 + x6_swz(row, g) * 8 + j] = p == 0 ? h : (p == 1 ? m : l);
+}
+
+template <int MT>
+__global__ __launch_bounds__(256, 2) void k_nin_head_x6(FwdArgs a, HeadArgs hd, const __bf16* wimg) {
+  __shared__ __attribute__((aligned(16))) __bf16 lw[X6_HEAD_BF];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int tiles_x = (a.OW + 15) / 16;
+  const int ty0 = (blockIdx.x / tiles_x) * 4 * MT, tx0 = (blockIdx.x % tiles_x) * 16;
+  const int n = blockIdx.y, gx = tx0 + li;
+  auto dma = [&](const __bf16* src) {  // 54 KiB = 54 x (4 waves ... ) 1 KiB wave copies
+    for (int q = wave; q < X6_HEAD_BF * 2 / 1024; q += 4)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(src + q * 512 + lane * 8),
+          (__attribute__((address_space(3))) void*)(lw + q * 512), 16, 0, 0);
+  };
+  dma(wimg);
+  f32x4 acc[MT][6];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int gy = ty0 + wave * MT + m;
+    const bool ok = gy < a.OH && gx < a.OW;
+    const float* p = a.in + (((long)n * a.IHt + gy) * a.IWt + gx) * a.in_stride + a.in_off + 4 * lg;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const float4 v = ok ? *reinterpret_cast<const float4*>(p + q * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+      acc[m][q] = f32x4{v.x, v.y, v.z, v.w};
+    }
+  }
+  auto bias_act = [](f32x4& v, float4 b) {
+    v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * 0.2f;
+  };
+  auto save = [&](float* dst, long pix, int q, const f32x4& v) {
+    *reinterpret_cast<float4*>(dst + pix * 96 + q * 16 + 4 * lg) = make_float4(v[0], v[1], v[2], v[3]);
+  };
+  // out = W (LDS image) x in, three 32-channel K blocks of six split products each
+  auto gemm96 = [&](const f32x4 (&in)[6], f32x4 (&out)[6][1]) {
+#pragma unroll
+    for (int f = 0; f < 6; ++f) out[f][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      bf16x8 xv[3][1];
+      const float v8[8] = {in[2 * b][0], in[2 * b][1], in[2 * b][2], in[2 * b][3],
+                           in[2 * b + 1][0], in[2 * b + 1][1], in[2 * b + 1][2], in[2 * b + 1][3]};
+      split3x8(v8, xv[0][0], xv[1][0], xv[2][0]);
+      bf16x8 wv[3][6];
+#pragma unroll
+      for (int f = 0; f < 6; ++f) {
+        const int row = b * 96 + f * 16 + li;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          wv[pl][f] = *reinterpret_cast<const bf16x8*>(lw + (pl * 3 * 96 + row) * 32 + x6_swz(row, lg) * 8);
+      }
+      x6_block<6, 1, 1>(out, wv, xv);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  __syncthreads();  // nin_a image landed (the DMA's vmcnt is drained by the barrier)
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {  // phase 1: acc[m] <- na
+    const int gy = ty0 + wave * MT + m;
+    f32x4 u[6][1];
+    gemm96(acc[m], u);
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+      bias_act(u[f][0], *reinterpret_cast<const float4*>(hd.ba + f * 16 + 4 * lg));
+      acc[m][f] = u[f][0];
+    }
+    if (hd.na && gy < a.OH && gx < a.OW)
+#pragma unroll
+      for (int f = 0; f < 6; ++f) save(hd.na, ((long)n * a.OH + gy) * a.OW + gx, f, acc[m][f]);
+  }
+  __syncthreads();  // everyone done with nin_a
+  dma(wimg + X6_HEAD_BF);
+  __syncthreads();  // nin_b image landed
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {  // phase 2: nb, then nin_c
+    const int gy = ty0 + wave * MT + m;
+    const bool ok = gy < a.OH && gx < a.OW;
+    const long pix = ((long)n * a.OH + gy) * a.OW + gx;
+    f32x4 v[6][1];
+    gemm96(acc[m], v);
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+      bias_act(v[f][0], *reinterpret_cast<const float4*>(hd.bb + f * 16 + 4 * lg));
+      if (hd.nb && ok) save(hd.nb, pix, f, v[f][0]);
+    }
+    // nin_c (fp32 VALU): per-lane partial over its 24 channels, then across the lane groups
+    for (int o = 0; o < hd.oc; ++o) {
+      float t = 0.f;
+#pragma unroll
+      for (int f = 0; f < 6; ++f) {
+        const float4 w = *reinterpret_cast<const float4*>(hd.wc + o * 96 + f * 16 + 4 * lg);
+        t = fmaf(w.x, v[f][0][0], t); t = fmaf(w.y, v[f][0][1], t);
+        t = fmaf(w.z, v[f][0][2], t); t = fmaf(w.w, v[f][0][3], t);
+      }
+      t += __shfl_xor(t, 16);
+      t += __shfl_xor(t, 32);
+      if (lg == 0 && ok) hd.y[(((long)n * hd.oc + o) * a.OH + gy) * a.OW + gx] = t + hd.bc[o];
+    }
+  }
+}
+
+// nin_a / nin_b weights (OIHW 96x96x1x1, contiguous) -> the two pre-split head images
+hipError_t launch_pack_head_x6(const float* wa, const float* wb, void* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_pack_head_x6, dim3((2 * X6_HEAD_BF + 255) / 256), dim3(256), 0, s, wa, wb,
+                     static_cast<__bf16*>(out));
+  return hipGetLastError();
+}
+
+hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* wimg, hipStream_t s) {
+  if (a.K != 96 || h.oc < 1 || ((a.in_stride | a.in_off) & 3)) return hipErrorInvalidValue;
+  const long tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16);
+  const int mt = tiles < 1024 ? 1 : 2;
+  const dim3 grid(((a.OW + 15) / 16) * ((a.OH + 4 * mt - 1) / (4 * mt)), a.N, 1);
+  const __bf16* w = static_cast<const __bf16*>(wimg);
+  if (mt == 1) hipLaunchKernelGGL((k_nin_head_x6<1>), grid, dim3(256), 0, s, a, h, w);
+  else hipLaunchKernelGGL((k_nin_head_x6<2>), grid, dim3(256), 0, s, a, h, w);
+  return hipGetLastError();
+}
+
 }  // namespace dn

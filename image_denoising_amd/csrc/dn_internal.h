@@ -80,6 +80,7 @@ struct HeadBwdArgs {
 };
 constexpr int HEAD_WS = 100;   // k-row stride of a head weight image (conflict-free A reads)
 constexpr int HEAD_LW = 9728;  // 96 * HEAD_WS rounded up to 256 floats
+constexpr int X6_HEAD_BF = 3 * 3 * 96 * 32;  // bf16 per layer of the bf16x6 head image (54 KiB)
 
 struct WgradArgs {
   const float* g; int g_stride, g_off;  // gradient operand (rows = co), NHWC
@@ -146,6 +147,9 @@ hipError_t launch_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);
 // nin_a -> nin_b -> nin_c on an activated dec_conv1b output (a.in, a.K = 96); h.d1b unused
 hipError_t launch_nin_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);
 hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s);
+// bf16x6 nin head (conv_x6.hip): pre-split nin_a | nin_b images (2 x X6_HEAD_BF bf16)
+hipError_t launch_pack_head_x6(const float* wa, const float* wb, void* out, hipStream_t s);
+hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* wimg, hipStream_t s);
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
 hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s, bool x6 = false);
 // bf16x6 3x3 weight gradient (conv_x6.hip): 96 outputs, Cin >= 32, rows >= 8 wide

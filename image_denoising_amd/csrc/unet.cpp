@@ -126,7 +126,7 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
     }
     p.packF[i] = alloc_f(n);
   }
-  p.packH = alloc_f(2 * HEAD_LW);
+  p.packH = alloc_f(2 * HEAD_LW > X6_HEAD_BF ? 2 * HEAD_LW : X6_HEAD_BF);  // fp32 | bf16x6 head images
   for (int i = 0; i < NL; ++i) {  // bf16 images (2 bytes each) of the 3x3 layers
     const Layer& L = p.P.L[i];
     p.packBF[i] = -1;
@@ -502,8 +502,13 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   if (x6) {  // dec_conv1b on the bf16x6 kernel, then the fused nin_a -> nin_b -> nin_c head
     DN_TRY(conv_forward(V(p.d1a, 96), N, H(0), Wd(0), 96, Wt(D1B), Bs(D1B), 96, 3, 1,
                         V(p.d1b, 96), OUT_NHWC, s));
-    DN_TRY(launch_pack_head(conv_fwd_view(prm + p.P.L[NINA].woff, 96, 1),
-                            conv_fwd_view(prm + p.P.L[NINB].woff, 96, 1), ws + p.packH, s));
+    // DN_X6_HEAD=0: the fp32 nin head (A/B)
+    static const bool head_x6 = !getenv("DN_X6_HEAD") || atoi(getenv("DN_X6_HEAD")) != 0;
+    if (head_x6)
+      DN_TRY(launch_pack_head_x6(prm + p.P.L[NINA].woff, prm + p.P.L[NINB].woff, ws + p.packH, s));
+    else
+      DN_TRY(launch_pack_head(conv_fwd_view(prm + p.P.L[NINA].woff, 96, 1),
+                              conv_fwd_view(prm + p.P.L[NINB].woff, 96, 1), ws + p.packH, s));
     FwdArgs a{};
     a.in = ws + p.d1b; a.in_stride = 96; a.in_off = 0; a.IHt = H(0); a.IWt = Wd(0);
     a.N = N; a.OH = H(0); a.OW = Wd(0); a.K = 96; a.NOUT = 96;
@@ -513,7 +518,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     h.wc = prm + p.P.L[NINC].woff; h.bc = Bs(NINC); h.oc = p.OC;
     h.y = y;
     if (p.with_bwd) { h.na = ws + p.na; h.nb = ws + p.nb; }
-    DN_TRY(launch_nin_head(a, h, s));
+    DN_TRY(head_x6 ? launch_nin_head_x6(a, h, ws + p.packH, s) : launch_nin_head(a, h, s));
     return DN_OK;
   }
   // dec_conv1b + nin_a + nin_b + nin_c in one kernel (arch_unet.py:251-257); the
