@@ -905,4 +905,110 @@ hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* w
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------
+// ConvTranspose2d(96, 96, 2, 2) forward (UpsampleCat's deconv, arch_unet.py:51-62) in the
+// bf16x6 arithmetic: out(2y+a, 2x+b, co) = bias[co] + sum_ci x(y, x, ci) W[ci][co][a][b].
+// Workgroup = one output parity (a, b) x 4 waves x MT low-res rows of 16 pixels; the parity's
+// 96x96 weight matrix is pre-split ([plane][K block][co][32 ci], 64-B rows, swizzled quads;
+// 54 KiB) and DMA'd into LDS.  A lane's B operand is 8 consecutive input channels of its
+// pixel (two float4 loads, split in registers); the 16x16 C/D tile (rows = output channels,
+// columns = pixels) is stored as float4 channel quads at the scattered output pixel.  The
+// four parity workgroups of a tile are 8 block indices apart, i.e. on one XCD, so three of
+// the four input reads hit that XCD's L2.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pack_deconv_x6(const float* __restrict__ w,
+                                                        __bf16* __restrict__ out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= 4 * X6_HEAD_BF) return;
+  const int par = e / X6_HEAD_BF, r0 = e % X6_HEAD_BF;
+  const int p = r0 / (3 * 96 * 32), row = (r0 / 32) % (3 * 96), k = r0 % 32;  // row = b*96 + co
+  const int b = row / 96, co = row % 96;
+  __bf16 h, m, l;
+  split3(w[((32 * b + k) * 96 + co) * 4 + par], h, m, l);  // W[ci][co][a][b], par = 2a + b
+  out[par * X6_HEAD_BF + (p * 3 * 96 + row) * 32 + x6_swz(row, k >> 3) * 8 + (k & 7)] =
+      p == 0 ? h : (p == 1 ? m : l);
+}
+
+template <int MT>
+__global__ __launch_bounds__(256, 2) void k_deconv_x6(FwdArgs a, const __bf16* wimg, int ntiles) {
+  __shared__ __attribute__((aligned(16))) __bf16 lw[X6_HEAD_BF];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int bx = blockIdx.x;
+  const int par = (bx >> 3) & 3, tile = ((bx >> 5) << 3) | (bx & 7);
+  if (tile >= ntiles) return;
+  const int tiles_x = (a.OW + 15) / 16, tiles_y = (a.OH + 4 * MT - 1) / (4 * MT);
+  const int n = tile / (tiles_x * tiles_y), rt = tile % (tiles_x * tiles_y);
+  const int ty0 = (rt / tiles_x) * 4 * MT, tx0 = (rt % tiles_x) * 16, gx = tx0 + li;
+  const int pa = par >> 1, pb = par & 1;
+  const __bf16* src = wimg + par * X6_HEAD_BF;
+  for (int q = wave; q < X6_HEAD_BF * 2 / 1024; q += 4)
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(src + q * 512 + lane * 8),
+        (__attribute__((address_space(3))) void*)(lw + q * 512), 16, 0, 0);
+  __syncthreads();  // weight image landed
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int gy = ty0 + wave * MT + m;
+    const bool ok = gy < a.OH && gx < a.OW;
+    const float* xp = a.in + (((long)n * a.IHt + gy) * a.IWt + gx) * a.in_stride + a.in_off + 8 * lg;
+    f32x4 out[6][1];
+#pragma unroll
+    for (int f = 0; f < 6; ++f) out[f][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      float v8[8];
+      const float4 u0 = ok ? *reinterpret_cast<const float4*>(xp + 32 * b) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 u1 = ok ? *reinterpret_cast<const float4*>(xp + 32 * b + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v8[0] = u0.x; v8[1] = u0.y; v8[2] = u0.z; v8[3] = u0.w;
+      v8[4] = u1.x; v8[5] = u1.y; v8[6] = u1.z; v8[7] = u1.w;
+      bf16x8 xv[3][1];
+      split3x8(v8, xv[0][0], xv[1][0], xv[2][0]);
+      bf16x8 wv[3][6];
+#pragma unroll
+      for (int f = 0; f < 6; ++f) {
+        const int row = b * 96 + f * 16 + li;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          wv[pl][f] = *reinterpret_cast<const bf16x8*>(lw + (pl * 3 * 96 + row) * 32 + x6_swz(row, lg) * 8);
+      }
+      x6_block<6, 1, 1>(out, wv, xv);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (ok) {
+      float* op = a.out + (((long)n * 2 * a.OH + 2 * gy + pa) * 2 * a.OW + 2 * gx + pb) * a.out_stride + a.out_off;
+#pragma unroll
+      for (int f = 0; f < 6; ++f) {
+        const float4 bb = *reinterpret_cast<const float4*>(a.bias + f * 16 + 4 * lg);
+        *reinterpret_cast<float4*>(op + f * 16 + 4 * lg) =
+            make_float4(out[f][0][0] + bb.x, out[f][0][1] + bb.y, out[f][0][2] + bb.z, out[f][0][3] + bb.w);
+      }
+    }
+  }
+}
+
+bool deconv_x6_ok(const FwdArgs& a) {
+  return a.K == 96 && a.NOUT == 96 && !((a.in_stride | a.in_off | a.out_stride | a.out_off) & 3);
+}
+
+// raw deconv weight (96, 96, 2, 2) -> four pre-split parity images (4 x X6_HEAD_BF bf16)
+hipError_t launch_pack_deconv_x6(const float* w, void* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_pack_deconv_x6, dim3((4 * X6_HEAD_BF + 255) / 256), dim3(256), 0, s, w,
+                     static_cast<__bf16*>(out));
+  return hipGetLastError();
+}
+
+// a: in = x (IHt = OH = h, IWt = OW = w), out = the 2h x 2w view, bias; K = NOUT = 96
+hipError_t launch_deconv_x6(const FwdArgs& a, const void* wimg, hipStream_t s) {
+  if (!deconv_x6_ok(a)) return hipErrorInvalidValue;
+  const long tiles1 = (long)a.N * ((a.OH + 3) / 4) * ((a.OW + 15) / 16);
+  const int mt = tiles1 < 2048 ? 1 : 2;
+  const long nt = (long)a.N * ((a.OH + 4 * mt - 1) / (4 * mt)) * ((a.OW + 15) / 16);
+  const dim3 grid((unsigned)((nt + 7) / 8 * 32));
+  const __bf16* w = static_cast<const __bf16*>(wimg);
+  if (mt == 1) hipLaunchKernelGGL((k_deconv_x6<1>), grid, dim3(256), 0, s, a, w, (int)nt);
+  else hipLaunchKernelGGL((k_deconv_x6<2>), grid, dim3(256), 0, s, a, w, (int)nt);
+  return hipGetLastError();
+}
+
 }  // namespace dn

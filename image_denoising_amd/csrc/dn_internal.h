@@ -150,6 +150,10 @@ hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStr
 // bf16x6 nin head (conv_x6.hip): pre-split nin_a | nin_b images (2 x X6_HEAD_BF bf16)
 hipError_t launch_pack_head_x6(const float* wa, const float* wb, void* out, hipStream_t s);
 hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* wimg, hipStream_t s);
+// bf16x6 ConvTranspose2d(96, 96, 2, 2) forward: four pre-split parity images (4 x X6_HEAD_BF bf16)
+bool deconv_x6_ok(const FwdArgs& a);
+hipError_t launch_pack_deconv_x6(const float* w, void* out, hipStream_t s);
+hipError_t launch_deconv_x6(const FwdArgs& a, const void* wimg, hipStream_t s);
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
 hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s, bool x6 = false);
 // bf16x6 3x3 weight gradient (conv_x6.hip): 96 outputs, Cin >= 32, rows >= 8 wide

@@ -127,6 +127,7 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
     p.packF[i] = alloc_f(n);
   }
   p.packH = alloc_f(2 * HEAD_LW > X6_HEAD_BF ? 2 * HEAD_LW : X6_HEAD_BF);  // fp32 | bf16x6 head images
+  p.packUX = alloc_f(2 * X6_HEAD_BF);  // 4 x X6_HEAD_BF bf16
   for (int i = 0; i < NL; ++i) {  // bf16 images (2 bytes each) of the 3x3 layers
     const Layer& L = p.P.L[i];
     p.packBF[i] = -1;
@@ -369,6 +370,8 @@ hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, 
 dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
                        hipStream_t s, int prec) {
   const bool bf16 = prec == DN_PREC_BF16, x6 = prec == DN_PREC_FP32_X6;
+  // bf16x6 96-channel deconvs (k_deconv_x6); DN_X6_DECONV=0 keeps the fp32 kernel (A/B)
+  static const bool x6_deconv = !getenv("DN_X6_DECONV") || atoi(getenv("DN_X6_DECONV")) != 0;
   const int N = p.N, nf = p.nf, C = p.C;
   auto H = [&](int l) { return p.H >> l; };
   auto Wd = [&](int l) { return p.W >> l; };
@@ -417,6 +420,17 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
                             const float* b, int cout, const View& out, hipStream_t st) -> hipError_t {
     int i = ENC1;
     while (i < NL && Wt(i) != wp) ++i;
+    if (x6 && x6_deconv && i < NL && cin == 96 && cout == 96) {
+      // bf16x6 parity GEMMs; the pre-split image is rebuilt per layer (stream-ordered reuse)
+      FwdArgs a{};
+      a.in = xin.p; a.in_stride = xin.stride; a.in_off = xin.off; a.IHt = h; a.IWt = w;
+      a.N = Nn; a.OH = h; a.OW = w; a.K = cin; a.NOUT = cout; a.bias = b;
+      a.out = out.p; a.out_stride = out.stride; a.out_off = out.off;
+      if (deconv_x6_ok(a)) {
+        hipError_t e = launch_pack_deconv_x6(prm + p.P.L[i].woff, ws + p.packUX, st);
+        return e != hipSuccess ? e : launch_deconv_x6(a, ws + p.packUX, st);
+      }
+    }
     if (!bf16 || i == NL || p.packBF[i] < 0)
       return dn::deconv_forward(xin, Nn, h, w, cin, wp, b, cout, out, st);
     FwdArgs a{};

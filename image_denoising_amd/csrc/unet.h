@@ -40,6 +40,7 @@ struct Plan {
   long d1a, d1b, na, nb;
   long packF[NL];               // packed forward weight images
   long packH;                   // fused head: nin_a | nin_b images (2 x HEAD_LW)
+  long packUX;                  // bf16x6 deconv parity images (one layer at a time)
   long packBF[NL];              // bf16 images of the 3x3 layers (mixed-precision forward)
   long packX[NL];               // pre-split bf16x6 images of the 3x3 layers (forward)
   long fwd_floats;
