@@ -569,7 +569,8 @@ def test_structure_step_vs_oracle(C):
 
 
 @pytest.mark.parametrize("prec", PRECS)
-def test_n2n_trajectory_vs_oracle(prec):
+@pytest.mark.parametrize("C", [1, 3])
+def test_n2n_trajectory_vs_oracle(C, prec):
     """SURVEY §8d eval parity: several N2N steps (train.py:356-368) with the same inputs and
     rd_idx stream on the HIP path and on the oracle (torch.optim.Adam state carried across
     steps), then the denoised image of a held-out input (evaluation.py:74) compared at the
@@ -581,12 +582,12 @@ def test_n2n_trajectory_vs_oracle(prec):
     from oracle import unet_ref
 
     steps, N, H = 4, 2, 64
-    net = _net(1, prec)
+    net = _net(C, prec)
     torch.manual_seed(0)
-    flat = reference_init(1, 1, 48)
+    flat = reference_init(C, C, 48)
     assert torch.equal(net.flat_params.detach().cpu(), flat)
     g = torch.Generator(device="cpu").manual_seed(5)
-    clean = F.interpolate(torch.rand(N, 1, 16, 16, generator=g), size=(H, H), mode="bilinear",
+    clean = F.interpolate(torch.rand(N, C, 16, 16, generator=g), size=(H, H), mode="bilinear",
                           align_corners=False)
     tr = N2NTrainer(net, lr=3e-4, n_epoch=100, increase_ratio=2.0)
     state = None
@@ -595,12 +596,13 @@ def test_n2n_trajectory_vs_oracle(prec):
         rd = torch.randint(0, 8, (N * (H // 2) * (H // 2),), generator=g, dtype=torch.int64)
         l_gpu = tr.train_step(noisy.to(DEV), epoch=1, rd_idx=rd.to(DEV).to(torch.uint8),
                               noisy=noisy.to(DEV)).cpu().numpy()
-        r = unet_ref.n2n_step(flat, noisy, rd.numpy().astype(np.uint8), 0.02, adam_state=state)
+        r = unet_ref.n2n_step(flat, noisy, rd.numpy().astype(np.uint8), 0.02, adam_state=state,
+                             in_nc=C, out_nc=C)
         flat, state = r["params"], r["adam_state"]
         assert abs(l_gpu[0] - r["loss1"]) <= FP32_TOL * r["loss1"], (s, l_gpu, r["loss1"])
         assert abs(l_gpu[2] - r["loss"]) <= FP32_TOL * r["loss"], (s, l_gpu, r["loss"])
     x = (clean + (25.0 / 255.0) * torch.randn(clean.shape, generator=g)).float()
     with torch.no_grad():
         y = net(x.to(DEV)).cpu()
-    y_ref = unet_ref.forward(flat, x, 1, 1)
+    y_ref = unet_ref.forward(flat, x, C, C)
     assert rel_err(y.numpy(), y_ref.numpy()) < FP32_TOL
