@@ -6,6 +6,7 @@
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 import sys
@@ -24,20 +25,33 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
             "-Wno-unused-function", "-Wno-unused-variable"]
 
 
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) over the library's sources, headers and C-ABI header, in a
+    fixed order.  Compiled into dn_version() so a test can tie a loaded .so to the tree."""
+    h = hashlib.sha256()
+    paths = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    paths.append(os.path.join(ROOT, "include", "denoise_hip.h"))
+    for p in paths:
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def _newest_header() -> float:
     paths = [os.path.join(CSRC, h) for h in HEADERS]
     paths.append(os.path.join(ROOT, "include", "denoise_hip.h"))
     return max(os.path.getmtime(p) for p in paths)
 
 
-def _compile(src: str, force: bool) -> str:
+def _compile(src: str, force: bool, src_hash: str) -> str:
     s = os.path.join(CSRC, src)
     o = os.path.join(BUILD, src + ".o")
     if not force and os.path.exists(o):
         if os.path.getmtime(o) >= max(os.path.getmtime(s), _newest_header()):
             return o
     cmd = [HIPCC, *CXXFLAGS, "-x", "hip", "-c", s, "-o", o, f"-I{CSRC}",
-           f"-I{os.path.join(ROOT, 'include')}"]
+           f"-I{os.path.join(ROOT, 'include')}", f'-DDN_SRC_HASH="{src_hash}"']
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
@@ -48,13 +62,21 @@ def _compile(src: str, force: bool) -> str:
 
 def build(force: bool = False, jobs: int = 4) -> str:
     os.makedirs(BUILD, exist_ok=True)
+    # the mtime checks below are only a shortcut: a tree whose sources hash differently from
+    # the last build (a checkout, a copied tree) rebuilds everything
+    src_hash = source_hash()
+    stamp = os.path.join(BUILD, "src_hash")
+    if not os.path.exists(stamp) or open(stamp).read().strip() != src_hash:
+        force = True
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
+        objs = list(ex.map(lambda s: _compile(s, force, src_hash), SOURCES))
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(map(os.path.getmtime, objs)):
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    with open(stamp, "w") as f:
+        f.write(src_hash)
     return LIB
 
 

@@ -34,14 +34,14 @@ SIGNATURES = {
                                        POINTER(c_size_t)]),
     "dn_unet_forward": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
                                 c_size_t, c_void_p]),
-    "dn_unet_backward": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
+    "dn_unet_backward": (c_int, [POINTER(DnCfg), _F, _F, _F, _F, c_int, c_int, c_int, c_void_p,
                                  c_size_t, c_void_p]),
     "dn_unet_forward_bf16": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
                                      c_size_t, c_void_p]),
     "dn_unet_forward_prec": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
                                      c_size_t, c_int, c_void_p]),
-    "dn_unet_backward_prec": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
-                                      c_size_t, c_int, c_void_p]),
+    "dn_unet_backward_prec": (c_int, [POINTER(DnCfg), _F, _F, _F, _F, c_int, c_int, c_int,
+                                      c_void_p, c_size_t, c_int, c_void_p]),
     "dn_unet_debug_buffers": (c_int, [POINTER(DnCfg), c_int, c_int, c_int, c_int,
                                       POINTER(c_int64), c_int, POINTER(c_int)]),
     "dn_n2n_subsample": (c_int, [_F, c_int, c_int, c_int, c_int, _U8, c_uint64, c_uint64, c_uint64,

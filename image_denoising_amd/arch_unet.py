@@ -3,7 +3,8 @@
 Same constructor signature, same `state_dict` keys/shapes (so reference checkpoints load with
 `load_state_dict`), same `forward(x[N,C,H,W]) -> [N,out_nc,H,W]`.  Internally all parameters are
 views into ONE flat fp32 buffer in state_dict order (the layout the C-ABI consumes), and the
-forward/backward run through dn_unet_forward / dn_unet_backward.  The blind-spot variant
+forward/backward run through dn_unet_forward / dn_unet_backward (parameter gradients and, when the
+input requires grad, dL/dx).  The blind-spot variant
 (arch_unet.py:65-97) is out of scope and raises.
 """
 from __future__ import annotations
@@ -139,10 +140,14 @@ class _UNetFunction(torch.autograd.Function):
         N, H, W = ctx.shape
         dy = dy.contiguous()
         dflat = torch.empty_like(net._flat)
-        net._run_backward(dy, dflat, ctx.ws, N, H, W)
+        dx = None
+        if ctx.needs_input_grad[0]:  # dL/dx from the same backward pass (dn_unet_backward dx)
+            dx = torch.empty((N, net.in_nc, H, W), dtype=torch.float32, device=dy.device)
+        net._run_backward(dy, dflat, ctx.ws, N, H, W, dx=dx)
         ctx.ws = None
-        grads = [dflat[o:o + p.numel()].view_as(p) for (o, p) in net._param_views()]
-        return (None, None, *grads)
+        grads = [dflat[o:o + p.numel()].view_as(p) if need else None
+                 for (o, p), need in zip(net._param_views(), ctx.needs_input_grad[2:])]
+        return (dx, None, *grads)
 
 
 class UNet(nn.Module):
@@ -261,10 +266,11 @@ class UNet(nn.Module):
         _lib.call("dn_unet_forward_bf16", ctypes.byref(self._cfg), _lib.ptr(self._flat),
                   _lib.ptr(x), _lib.ptr(y), N, H, W, ws.data_ptr(), ws.numel(), _lib.stream_of(x))
 
-    def _run_backward(self, dy, dflat, ws, N, H, W):
+    def _run_backward(self, dy, dflat, ws, N, H, W, dx=None):
+        """dflat = dL/dparams (and dx = dL/dx when given) for dy = dL/dy"""
         _lib.call("dn_unet_backward_prec", ctypes.byref(self._cfg), _lib.ptr(self._flat),
-                  _lib.ptr(dy), _lib.ptr(dflat), N, H, W, ws.data_ptr(), ws.numel(), self._prec(),
-                  _lib.stream_of(dy))
+                  _lib.ptr(dy), _lib.ptr(dflat), _lib.ptr(dx), N, H, W, ws.data_ptr(), ws.numel(),
+                  self._prec(), _lib.stream_of(dy))
 
     # ---- nn.Module API ----------------------------------------------------------------
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -273,9 +279,9 @@ class UNet(nn.Module):
         N, _, H, W = x.shape
         if H % 32 or W % 32:
             raise ValueError("H and W must be multiples of 32 (arch_unet.py: 5 pooling levels)")
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            if x.requires_grad:
-                raise NotImplementedError("gradient w.r.t. the network input is not computed")
+        if torch.is_grad_enabled() and (x.requires_grad or
+                                        any(p.requires_grad for p in self.parameters())):
+            # autograd: parameter gradients and/or dL/dx, as the reference module gives
             return _UNetFunction.apply(x, self, *[p for _, p in self._param_views()])
         y = torch.empty((N, self.out_nc, H, W), dtype=torch.float32, device=x.device)
         self._run_forward_inference(x, y, self._workspace(N, H, W, with_backward=False))

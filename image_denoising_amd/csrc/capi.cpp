@@ -31,7 +31,11 @@ dn_status hip_status(hipError_t e, const char* what) {
 
 extern "C" {
 
-const char* dn_version(void) { return "denoise_hip 0.1.0 gfx950"; }
+#ifndef DN_SRC_HASH
+#define DN_SRC_HASH "unknown"
+#endif
+// src= the sha256 prefix of the sources this library was compiled from (_build.source_hash)
+const char* dn_version(void) { return "denoise_hip 0.2.0 gfx950 src=" DN_SRC_HASH; }
 
 int dn_last_error(char* buf, size_t len) {
   const std::string& s = g_last_error;
@@ -126,15 +130,15 @@ dn_status dn_unet_forward_bf16(const dn_unet_cfg* cfg, const float* params, cons
 }
 
 dn_status dn_unet_backward(const dn_unet_cfg* cfg, const float* params, const float* dy,
-                           float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
-                           void* stream) {
-  return dn_unet_backward_prec(cfg, params, dy, dparams, N, H, W, ws, ws_bytes, DN_PREC_FP32,
+                           float* dparams, float* dx, int N, int H, int W, void* ws,
+                           size_t ws_bytes, void* stream) {
+  return dn_unet_backward_prec(cfg, params, dy, dparams, dx, N, H, W, ws, ws_bytes, DN_PREC_FP32,
                                stream);
 }
 
 dn_status dn_unet_backward_prec(const dn_unet_cfg* cfg, const float* params, const float* dy,
-                                float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
-                                int precision, void* stream) {
+                                float* dparams, float* dx, int N, int H, int W, void* ws,
+                                size_t ws_bytes, int precision, void* stream) {
   DN_GUARD_BEGIN
   if (precision != DN_PREC_FP32 && precision != DN_PREC_FP32_X6)
     return fail(DN_ERR_ARG, "backward precision must be DN_PREC_FP32 or DN_PREC_FP32_X6");
@@ -145,7 +149,7 @@ dn_status dn_unet_backward_prec(const dn_unet_cfg* cfg, const float* params, con
   if (ws_bytes < (size_t)p.total_floats * sizeof(float))
     return fail(DN_ERR_WORKSPACE,
                 "workspace smaller than dn_unet_workspace_size(with_backward=1)");
-  return unet_backward(p, params, dy, dparams, static_cast<float*>(ws), (hipStream_t)stream,
+  return unet_backward(p, params, dy, dparams, dx, static_cast<float*>(ws), (hipStream_t)stream,
                        precision);
   DN_GUARD_END
 }

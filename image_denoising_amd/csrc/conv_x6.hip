@@ -240,8 +240,14 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   // an out-of-range offset, for which the buffer unit returns zeros) and exactly PPW DMAs per
   // wave per stage (past the last stage: a harmless re-load into a retired ring slot), so the
   // vmcnt counts below are compile-time constants.
+  // The resource covers only this tile's input rows [ry0, ry1) (based at row ry0), so its
+  // 32-bit byte extent and offsets stay below 2^31 for any image height (launch_fwd_x6 checks
+  // IH * IWt * in_stride * 4 < 2^31); 0x7fffffff is then always out of range.
+  const int ry0 = iy0 > 0 ? iy0 : 0, ry1 = iy0 + C::IH < a.IHt ? iy0 + C::IH : a.IHt;
+  const long row_floats = (long)a.IWt * a.in_stride;
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(inb), (short)0, a.IHt * a.IWt * a.in_stride * 4, 0x00020000);
+      const_cast<float*>(inb + ry0 * row_floats), (short)0,
+      (int)((ry1 - ry0) * row_floats * 4), 0x00020000);
   f32x4 xr[C::XITEMS];
   auto load_x = [&](int k0) {
 #pragma unroll
@@ -251,7 +257,7 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
       const int iy = pix / C::IW, ix = pix - iy * C::IW;
       const int gy = iy0 + iy, gx = ix0 + ix, k = k0 + 4 * q;
       const bool ok = e < C::XQ && gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt && k < a.K;
-      const int off = ok ? ((gy * a.IWt + gx) * a.in_stride + k) * 4 : 0x7fffffff;
+      const int off = ok ? (((gy - ry0) * a.IWt + gx) * a.in_stride + k) * 4 : 0x7fffffff;
       xr[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
   };
@@ -517,7 +523,9 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
   const int nz = a.zc > 0 ? (a.NOUT + a.zc - 1) / a.zc : 1;
   // large grids: the pipelined 16-row kernel (one workgroup per CU, >= 2 rounds of tiles)
   static const bool no_pipe = getenv("DN_X6_NOPIPE") != nullptr;  // A/B probe
-  const bool aligned = ((a.in_stride | a.in_off | a.K) & 3) == 0;
+  // the pipelined kernel addresses one tile's 18 input rows through a 32-bit buffer resource
+  const bool aligned = ((a.in_stride | a.in_off | a.K) & 3) == 0 &&
+                       (long)PCfg<6>::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL;
   auto pipe = [&]() {
     return np == 32 ? run_x6p<2>(a, nz, s) : (np == 48 ? run_x6p<3>(a, nz, s) : run_x6p<6>(a, nz, s));
   };

@@ -121,6 +121,11 @@ hipError_t launch_enc0_fwd(const float* x, int N, int C, int H, int W, const flo
 int enc0_wgrad_splits(int N, int H, int W);
 hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int N, int C, int H,
                              int W, float* slab, int splits, float* dwb, hipStream_t s);
+// dL/dx (NCHW) of the network input from enc_conv0's (48 ch) and dec_conv1a's (96 ch, input
+// channels [c1_base, c1_base + C) of c1_total) pre-activation gradients
+hipError_t launch_dgrad_input(const float* g0, const float* w0, const float* g1, const float* w1,
+                              int c1_total, int c1_base, int N, int C, int H, int W, float* dx,
+                              hipStream_t s);
 constexpr int EVAL_PARTS = 1024;
 hipError_t launch_u8_to_unit(const uint8_t* x, long n, float* y, hipStream_t s);
 hipError_t launch_tile_extract(const uint8_t* img, int C, int H, int W, int ps, int stride,

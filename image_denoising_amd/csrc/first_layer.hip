@@ -231,6 +231,81 @@ hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int N
 }
 
 // ------------------------------------------------------------------------------------
+// dL/dx of the network input (the reference's autograd, arch_unet.py:196-248): x feeds
+// enc_conv0 (C -> 48) and, as pool0, the last C channels of dec_conv1a's input (97 -> 96 for
+// C = 1), so
+//   dx[n][c][y][x] = sum_{t, co} W0[co][c][t] g0[n][y+1-ky][x+1-kx][co]
+//                  + sum_{t, co} W1[co][c1 + c][t] g1[n][y+1-ky][x+1-kx][co]
+// with g0 / g1 the gradients of the two layers' pre-activations (NHWC, 48 / 96 channels),
+// out-of-image taps skipped.  One output pixel per thread, all C channels; the weights of the
+// C input channels live transposed in LDS ([c][t][co], broadcast float4 reads); the 144
+// gradient channels of the 9 neighbours come through L1/L2 as float4 rows.  Fixed summation
+// order (taps, then enc_conv0's channels, then dec_conv1a's): deterministic.
+template <int C>
+__global__ __launch_bounds__(256) void k_dgrad_input(const float* __restrict__ g0,
+                                                     const float* __restrict__ w0,
+                                                     const float* __restrict__ g1,
+                                                     const float* __restrict__ w1, int c1_total,
+                                                     int c1_base, int N, int H, int W,
+                                                     float* __restrict__ dx) {
+  constexpr int C0 = 48, C1 = 96;
+  __shared__ __attribute__((aligned(16))) float wl[C][9][C0 + C1];
+  for (int e = threadIdx.x; e < C * 9 * (C0 + C1); e += 256) {
+    const int co = e % (C0 + C1), r = e / (C0 + C1), t = r % 9, c = r / 9;
+    wl[c][t][co] = co < C0 ? w0[((long)co * C + c) * 9 + t]
+                           : w1[((long)(co - C0) * c1_total + c1_base + c) * 9 + t];
+  }
+  __syncthreads();
+  const long hw = (long)H * W, total = (long)N * hw;
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= total) return;
+  const long n = p / hw;
+  const int r = (int)(p - n * hw), y = r / W, x = r - y * W;
+  float acc[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) acc[c] = 0.f;
+#pragma unroll 1
+  for (int t = 0; t < 9; ++t) {
+    const int ky = t / 3, kx = t - 3 * ky, sy = y + 1 - ky, sx = x + 1 - kx;
+    if (sy < 0 || sy >= H || sx < 0 || sx >= W) continue;
+    const long q = n * hw + (long)sy * W + sx;
+    const float4* a0 = reinterpret_cast<const float4*>(g0 + q * C0);
+    const float4* a1 = reinterpret_cast<const float4*>(g1 + q * C1);
+#pragma unroll
+    for (int j = 0; j < (C0 + C1) / 4; ++j) {
+      const float4 gv = j < C0 / 4 ? a0[j] : a1[j - C0 / 4];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float4 wv = *reinterpret_cast<const float4*>(&wl[c][t][4 * j]);
+        acc[c] = fmaf(gv.x, wv.x, acc[c]);
+        acc[c] = fmaf(gv.y, wv.y, acc[c]);
+        acc[c] = fmaf(gv.z, wv.z, acc[c]);
+        acc[c] = fmaf(gv.w, wv.w, acc[c]);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) dx[(n * C + c) * hw + r] = acc[c];
+}
+
+hipError_t launch_dgrad_input(const float* g0, const float* w0, const float* g1, const float* w1,
+                              int c1_total, int c1_base, int N, int C, int H, int W, float* dx,
+                              hipStream_t s) {
+  const long total = (long)N * H * W;
+  const dim3 grid((unsigned)((total + 255) / 256));
+#define DN_DGI(CC)                                                                           \
+  hipLaunchKernelGGL(k_dgrad_input<CC>, grid, dim3(256), 0, s, g0, w0, g1, w1, c1_total,    \
+                     c1_base, N, H, W, dx)
+  if (C == 1) DN_DGI(1);
+  else if (C == 2) DN_DGI(2);
+  else if (C == 3) DN_DGI(3);
+  else if (C == 4) DN_DGI(4);
+  else return hipErrorInvalidValue;
+#undef DN_DGI
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
 // Weight gradient of a thin 1x1 conv with 96 input and few output channels (nin_c,
 // arch_unet.py:190): dW[co][ci] = sum_p g[p][co] x[p][ci], db[co] = sum_p g[p][co].
 // 240 threads = 10 pixel phases x 24 float4 channel quads; per block a contiguous pixel range;

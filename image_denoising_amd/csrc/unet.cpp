@@ -561,8 +561,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
 // LeakyReLU' into their epilogue (mask = the layer input, which is the previous layer's
 // post-activation output); skip gradients are accumulated into the concat-gradient buffers.
 // ------------------------------------------------------------------------------------
-dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* ws,
-                        hipStream_t s, int prec) {
+dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* dx,
+                        float* ws, hipStream_t s, int prec) {
   const bool x6 = prec == DN_PREC_FP32_X6;
   // bf16x6 3x3 weight gradients (k_wgrad3x6) only on request (DN_X6_WGRAD=1): measured slower
   // than the fp32 k_wgrad3 in the step (37.5 vs 33.2 ms)
@@ -735,6 +735,10 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                     V(p.g_a0, nf), s));
   DN_TRY(launch_enc0_wgrad(ws + p.g_a0, nf, ws + p.xin, N, C, H(0), Wd(0), slab,
                            p.splits[ENC0], G(ENC0), s));
+  // dL/dx: the network input feeds enc_conv0 and (as pool0) dec_conv1a's last C channels
+  if (dx)
+    DN_TRY(launch_dgrad_input(ws + p.g_a0, prm + p.P.L[ENC0].woff, ws + p.g_d1a,
+                              prm + p.P.L[D1A].woff, p.c1k, 2 * nf, N, C, H(0), Wd(0), dx, s));
   return DN_OK;
 }
 

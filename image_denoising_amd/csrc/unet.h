@@ -68,8 +68,9 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
 // by three-way operand splitting, fp32-accurate), DN_PREC_BF16 (forward only, bf16 operands)
 dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
                        hipStream_t s, int prec = DN_PREC_FP32);
-dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* ws,
-                        hipStream_t s, int prec = DN_PREC_FP32);
+// dx (nullable): dL/dx of the network input, NCHW [N, in_nc, H, W]
+dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* dx,
+                        float* ws, hipStream_t s, int prec = DN_PREC_FP32);
 // zc of the bf16x6 data gradient of a 3x3 layer producing nout channels (0: one block)
 int x6_dgrad_zc(int nout);
 

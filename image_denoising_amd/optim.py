@@ -55,7 +55,12 @@ def reference_milestones(n_epoch: int):
 
 
 def lr_at_epoch(epoch: int, base_lr: float, n_epoch: int, gamma: float = 0.5) -> float:
-    """lr in effect during 1-based `epoch` (MultiStepLR.last_epoch == epoch-1)."""
+    """lr in effect during 1-based `epoch` (MultiStepLR.last_epoch == epoch-1).
+
+    MultiStepLR multiplies by gamma**count(m) when last_epoch reaches milestone m (the
+    construction step sets last_epoch = 0, so a milestone 0 fires at once; repeated milestones
+    count with multiplicity).  last_epoch never equals a negative milestone, which
+    reference_milestones() yields for n_epoch < 5 (int(20r) = 0): those never fire."""
     last = epoch - 1
-    k = sum(1 for m in reference_milestones(n_epoch) if m <= last)
+    k = sum(1 for m in reference_milestones(n_epoch) if 0 <= m <= last)
     return base_lr * gamma ** k

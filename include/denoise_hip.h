@@ -56,6 +56,8 @@ typedef struct dn_unet_cfg {
 } dn_unet_cfg;
 
 /* ---- library / errors ---------------------------------------------------------- */
+/* "denoise_hip <version> gfx950 src=<16 hex>": the hash identifies the sources the library was
+   built from (image_denoising_amd/_build.py source_hash) */
 const char* dn_version(void);
 /* copies the last error message of this thread into buf (NUL-terminated); returns its length */
 int dn_last_error(char* buf, size_t len);
@@ -85,18 +87,21 @@ dn_status dn_unet_forward_bf16(const dn_unet_cfg* cfg, const float* params, cons
                                float* y, int N, int H, int W, void* ws, size_t ws_bytes,
                                void* stream);
 /* dparams = dL/dparams given dy = dL/dy, for the activations saved by the last
-   dn_unet_forward on the same ws (same N,H,W).  dparams is overwritten (not accumulated). */
+   dn_unet_forward on the same ws (same N,H,W).  dparams is overwritten (not accumulated).
+   dx (nullable) receives dL/dx of the network input, NCHW [N,in_nc,H,W] (overwritten): the
+   input gradient autograd gives the reference module (arch_unet.py:194-260; x feeds enc_conv0
+   and, as pool0, the last in_nc channels of dec_conv1a's input). */
 dn_status dn_unet_backward(const dn_unet_cfg* cfg, const float* params, const float* dy,
-                           float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
-                           void* stream);
+                           float* dparams, float* dx, int N, int H, int W, void* ws,
+                           size_t ws_bytes, void* stream);
 /* dn_unet_forward / dn_unet_backward with the 3x3 convolutions' arithmetic chosen by
    precision (DN_PREC_*; the backward takes DN_PREC_FP32 or DN_PREC_FP32_X6). */
 dn_status dn_unet_forward_prec(const dn_unet_cfg* cfg, const float* params, const float* x,
                                float* y, int N, int H, int W, void* ws, size_t ws_bytes,
                                int precision, void* stream);
 dn_status dn_unet_backward_prec(const dn_unet_cfg* cfg, const float* params, const float* dy,
-                                float* dparams, int N, int H, int W, void* ws, size_t ws_bytes,
-                                int precision, void* stream);
+                                float* dparams, float* dx, int N, int H, int W, void* ws,
+                                size_t ws_bytes, int precision, void* stream);
 
 /* Debug/introspection: (offset_floats, channel_stride, level) of every NHWC buffer of the
    workspace plan, in the order c1 a0 a1 c2..c5 a2..a5 p5 a6 d{2..5}a d{2..5}b d1a d1b nin_a nin_b

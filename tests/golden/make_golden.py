@@ -97,26 +97,7 @@ def main():
     fx["c_sub2"] = ns["generate_subimages"](img, m2).numpy()
     np.savez_compressed(os.path.join(OUT, "subsampler.npz"), **fx)
 
-    # ---- 2. UNet forward / backward ------------------------------------------------------
-    for C, N, path in ((1, 2, "unet_c1.npz"), (3, 1, "unet_c3.npz")):
-        torch.manual_seed(0)
-        net = arch_unet.UNet(in_nc=C, out_nc=C, n_feature=48)
-        flat = flat_params(net)
-        x = torch.rand(N, C, 64, 64, generator=torch.Generator().manual_seed(1))
-        y = net(x)
-        loss = (y ** 2).mean()
-        loss.backward()
-        grad = torch.cat([p.grad.reshape(-1) for p in net.parameters()]).numpy()
-        fx = dict(x=x.numpy(), y=y.detach().numpy(), loss=np.float32(loss.item()),
-                  params_sha=np.array(sha(flat)), params_sum=np.float64(flat.astype(np.float64).sum()),
-                  params_head=flat[:64])
-        if C == 1:
-            fx["grad"] = grad
-        else:
-            idx = np.random.default_rng(0).choice(grad.size, 8192, replace=False)
-            fx["grad_idx"], fx["grad_sample"] = idx, grad[idx]
-        fx["grad_norms"] = np.array([np.linalg.norm(p.grad.numpy()) for p in net.parameters()])
-        np.savez_compressed(os.path.join(OUT, path), **fx)
+    unet_main()
 
     # ---- 3. one N2N step (training_script.md:137-155) with torch.optim.Adam ---------------
     torch.manual_seed(0)
@@ -181,6 +162,39 @@ def main():
     psnr = np.array([nsp["calculate_psnr"](a[i], b[i]) for i in range(2)])
     np.savez_compressed(os.path.join(OUT, "eval_psnr.npz"), a=a, b=b, psnr=psnr)
     print("golden fixtures written to", OUT)
+
+
+def unet_main():
+    """arch_unet.UNet (imported): init, forward, dL/dx and parameter gradients of mean(y^2), and
+    the state_dict key names / shapes (the checkpoint contract, evaluation.py:52-53)."""
+    sys.path.insert(0, REF)
+    import arch_unet  # noqa: E402
+
+    for C, N, path in ((1, 2, "unet_c1.npz"), (3, 1, "unet_c3.npz")):
+        torch.manual_seed(0)
+        net = arch_unet.UNet(in_nc=C, out_nc=C, n_feature=48)
+        flat = flat_params(net)
+        x = torch.rand(N, C, 64, 64, generator=torch.Generator().manual_seed(1))
+        x.requires_grad_(True)
+        y = net(x)
+        loss = (y ** 2).mean()
+        loss.backward()
+        grad = torch.cat([p.grad.reshape(-1) for p in net.parameters()]).numpy()
+        fx = dict(x=x.detach().numpy(), y=y.detach().numpy(), loss=np.float32(loss.item()),
+                  dx=x.grad.numpy(),
+                  params_sha=np.array(sha(flat)), params_sum=np.float64(flat.astype(np.float64).sum()),
+                  params_head=flat[:64],
+                  keys=np.array(list(net.state_dict().keys())),
+                  key_shapes=np.array([list(v.shape) + [0] * (4 - v.dim())
+                                       for v in net.state_dict().values()], dtype=np.int64))
+        if C == 1:
+            fx["grad"] = grad
+        else:
+            idx = np.random.default_rng(0).choice(grad.size, 8192, replace=False)
+            fx["grad_idx"], fx["grad_sample"] = idx, grad[idx]
+        fx["grad_norms"] = np.array([np.linalg.norm(p.grad.numpy()) for p in net.parameters()])
+        np.savez_compressed(os.path.join(OUT, path), **fx)
+    print("UNet fixtures written to", OUT)
 
 
 def adapter_main():
@@ -267,7 +281,7 @@ def iunet_main():
 
 if __name__ == "__main__":
     if "--only" in sys.argv:
-        {"adapter": adapter_main, "iunet": iunet_main}[sys.argv[sys.argv.index("--only") + 1]]()
+        {"adapter": adapter_main, "iunet": iunet_main, "unet": unet_main}[sys.argv[sys.argv.index("--only") + 1]]()
     else:
         main()
         adapter_main()

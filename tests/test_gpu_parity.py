@@ -39,6 +39,14 @@ def L():
     return _lib
 
 
+def test_gpu_library_built_from_these_sources():
+    """the .so the GPU box loads is the one compiled from this tree's sources"""
+    from image_denoising_amd import _build
+
+    v = L().lib().dn_version().decode()
+    assert v.endswith("src=" + _build.source_hash()), (v, _build.source_hash())
+
+
 def S():
     return torch.cuda.current_stream().cuda_stream
 
@@ -326,6 +334,30 @@ def test_unet_forward_backward_vs_reference(golden, C, name, prec):
     assert rel_err(norms, g["grad_norms"]) < FP32_TOL
 
 
+@pytest.mark.parametrize("prec", PRECS)
+@pytest.mark.parametrize("C,name", [(1, "unet_c1.npz"), (3, "unet_c3.npz")])
+def test_unet_input_grad_vs_reference(golden, C, name, prec):
+    """dL/dx through the boundary (dn_unet_backward's dx) against the reference module's own
+    autograd (fixture dx, arch_unet.py:194-260), with trainable and with frozen parameters."""
+    g = golden(name)
+    net = _net(C, prec)
+    x = torch.from_numpy(g["x"]).to(DEV).requires_grad_(True)
+    y = net(x)
+    (y ** 2).mean().backward()
+    assert x.grad is not None and x.grad.shape == x.shape
+    assert rel_err(x.grad.cpu().numpy(), g["dx"]) < FP32_TOL
+    assert all(p.grad is not None for p in net.parameters())
+    # frozen parameters (the adapter-finetune base, finetune.py:255-262): only dx flows
+    for p in net.parameters():
+        p.requires_grad_(False)
+    x2 = torch.from_numpy(g["x"]).to(DEV).requires_grad_(True)
+    (net(x2) ** 2).mean().backward()
+    assert torch.equal(x2.grad, x.grad)
+    # and no input gradient requested: the inference path, no graph
+    with torch.no_grad():
+        assert not net(x2).requires_grad
+
+
 def _unit_gain(net, seed=0):
     """weights x10 (undoing the reference's x0.1 init) and random biases: every U-Net level
     then contributes O(1) to the output, so a fault in any level shows up in y and in every
@@ -359,8 +391,10 @@ def _device_activations(net, x, r):
     net._run_forward(x.to(DEV).contiguous(), y, ws)
     dy = r.to(DEV).contiguous()
     dflat = torch.empty_like(net.flat_params)
-    net._run_backward(dy, dflat, ws, N, H, W)
+    dx = torch.full((N, C, H, W), float("nan"), device=DEV)
+    net._run_backward(dy, dflat, ws, N, H, W, dx=dx)
     torch.cuda.synchronize()
+    _device_activations.dx = dx.cpu()
     wsf = ws.view(torch.float32)
     acts = {}
     for i, name in enumerate(FWD_BUFS):
@@ -386,11 +420,14 @@ def test_unet_unit_gain_fwd_bwd_vs_fp64(C, N, H, W, prec):
     r = torch.randn(N, C, H, W, generator=torch.Generator().manual_seed(2))
     y, gg, acts = _device_activations(net, x, r)
     flat = net.flat_params.detach().cpu()
+    dx = _device_activations.dx
     p64 = flat.double().requires_grad_(True)
-    y64 = forward(p64, x.double(), C, C, masks=acts)
+    x64 = x.double().requires_grad_(True)
+    y64 = forward(p64, x64, C, C, masks=acts)
     assert rel_err(y.numpy(), y64.detach().numpy()) < FP32_TOL
     (y64 * r.double()).sum().backward()
     g64 = p64.grad.numpy()
+    assert rel_err(dx.numpy(), x64.grad.numpy()) < 2e-5
     gg = gg.numpy()
     off = 0
     for name_, ws, bl, _ in layer_table(C, C):

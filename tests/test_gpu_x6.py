@@ -198,3 +198,64 @@ def test_x6_backward_weight_vs_fp64(cin, cout, N, H, W):
     assert e6 < X6_TOL, (e6, e32)
     assert e6 < 4 * e32 + 1e-7, (e6, e32)
     assert rel_err(o6[nw:], ref_b) < X6_TOL
+
+
+def test_x6_forward_single_image_past_2gib():
+    """k_c3x6p reads its input tile through a 32-bit buffer resource: one 96-channel image of
+    2400 x 2432 pixels is 2.24 GB, past 2^31 bytes, so the resource is based at the tile's own
+    rows (a whole-image resource overflowed there).  The x6 output must equal the
+    fp32 kernel's (which addresses with 64-bit offsets) everywhere, bottom rows included."""
+    _lib = L()
+    N, H, W, C = 1, 2400, 2432, 96
+    assert H * W * C * 4 > 2 ** 31
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn(N, H, W, C, device=DEV, generator=g)
+    w = (torch.randn(C, C, 3, 3, device=DEV, generator=g) * 0.05).contiguous()
+    b = torch.randn(C, device=DEV, generator=g) * 0.1
+    outs = []
+    for x6 in (True, False):
+        y = torch.full((N, H, W, C), float("nan"), device=DEV)
+        if x6:
+            pk = _lib.scratch(_lib.lib().dn_conv2d_x6_pack_size(C, C, 0), DEV)
+            _lib.call("dn_conv2d_forward_x6", x.data_ptr(), C, N, H, W, C, w.data_ptr(),
+                      b.data_ptr(), C, 0, y.data_ptr(), C, pk.data_ptr(), pk.numel(), S())
+        else:
+            pk = _lib.scratch(_lib.lib().dn_conv2d_pack_size(C, C, 3, 0), DEV)
+            _lib.call("dn_conv2d_forward", x.data_ptr(), C, N, H, W, C, w.data_ptr(),
+                      b.data_ptr(), C, 3, 0, y.data_ptr(), C, pk.data_ptr(), pk.numel(), S())
+        outs.append(y)
+    y6, y32 = outs
+    assert bool(torch.isfinite(y6).all())
+    scale = float(y32.abs().max())
+    # both are fp32-accurate (~1e-6 of max against fp64); a mis-addressed tile is O(1) off
+    for r0, r1 in ((0, 32), (H // 2 - 16, H // 2 + 16), (H - 48, H)):
+        d = float((y6[:, r0:r1] - y32[:, r0:r1]).abs().max())
+        assert d < 1e-5 * scale, (r0, d, scale)
+    assert float((y6 - y32).abs().max()) < 1e-5 * scale
+    # and against fp64 on the last rows, the part past 2 GiB
+    xs = x[:, H - 18:].permute(0, 3, 1, 2).double().cpu()
+    ref = F.conv2d(F.pad(xs, (1, 1, 0, 1)), w.double().cpu(), b.double().cpu())[:, :, -16:]
+    got = y6[:, H - 16:].permute(0, 3, 1, 2).cpu()
+    assert rel_err(got.numpy(), ref.numpy()) < X6_TOL
+
+
+@pytest.mark.parametrize("scale", [1e-20, 1e-30, 1e-34, 1e-36, 1e-38])
+def test_x6_tiny_magnitude_operands(scale):
+    """The exact split needs every piece to be a normal bf16: |v| >= 2^-110 keeps even the
+    third piece (>= 2^-16 |v|) normal.  Below that the third and then the second piece become
+    subnormal, and whatever the matrix core does with them, the result may keep only the pieces
+    that survive (2^-16, then 2^-8 relative per operand).  Activations scaled by `scale`
+    against O(0.1) weights: the result is compared with fp64 relative to its own max."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 96, 32, 32, generator=g) * scale
+    w = torch.randn(96, 96, 3, 3, generator=g) * 0.1
+    b = torch.zeros(96)
+    ref = F.conv2d(x.double(), w.double(), None, padding=1)
+    y6 = _forward(x, w, b, 0, True)
+    y32 = _forward(x, w, b, 0, False)
+    e6, e32 = rel_err(y6.numpy(), ref.numpy()), rel_err(y32.numpy(), ref.numpy())
+    print(f"scale {scale:g}: x6 {e6:.3e}  fp32 {e32:.3e}  max|ref| {float(ref.abs().max()):.3e}")
+    if scale >= 2.0 ** -100:  # every piece normal: the full fp32-class bound
+        assert e6 < X6_TOL, (e6, e32)
+    else:  # documented degradation: no worse than losing the subnormal pieces
+        assert e6 < 2.0 ** -7 or e6 < 4 * e32 + 1e-7, (e6, e32)

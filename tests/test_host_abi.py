@@ -28,6 +28,15 @@ def test_library_exports_every_header_symbol():
     assert L.dn_version().startswith(b"denoise_hip")
 
 
+def test_library_built_from_these_sources():
+    """dn_version() carries the hash of the sources the .so was compiled from: the loaded
+    library is the one this tree builds (not a stale or foreign binary)"""
+    from image_denoising_amd import _build, _lib
+
+    v = _lib.lib().dn_version().decode()
+    assert v.endswith("src=" + _build.source_hash()), (v, _build.source_hash())
+
+
 def test_library_is_gfx950_code_object():
     from image_denoising_amd import _lib
 
@@ -118,7 +127,9 @@ def test_cpu_tensor_is_rejected():
 def test_multistep_lr_matches_torch_scheduler():
     from image_denoising_amd.optim import lr_at_epoch, reference_milestones
 
-    for n_epoch in (100, 30, 7):
+    # 1..4: int(20r) - 1 = -1 milestones (never fire) and repeated 0 milestones (fire at
+    # construction with multiplicity)
+    for n_epoch in (100, 30, 7, 6, 5, 4, 3, 2, 1):
         p = torch.nn.Parameter(torch.zeros(1))
         opt = torch.optim.Adam([p], lr=3e-4)
         sch = torch.optim.lr_scheduler.MultiStepLR(opt, milestones=reference_milestones(n_epoch),

@@ -77,11 +77,12 @@ def test_oracle_unet_forward_backward(golden, C, name):
     g = golden(name)
     torch.manual_seed(0)
     flat = reference_init(C, C, 48)
-    x = torch.from_numpy(g["x"])
+    x = torch.from_numpy(g["x"]).requires_grad_(True)
     p = flat.clone().requires_grad_(True)
     y = unet_ref.forward(p, x, C, C)
     assert rel_err(y.detach().numpy(), g["y"]) < 1e-5
     (y ** 2).mean().backward()
+    assert rel_err(x.grad.numpy(), g["dx"]) < 1e-4  # dL/dx of the reference module
     grad = p.grad.numpy()
     if "grad" in g:
         assert rel_err(grad, g["grad"]) < 1e-4
