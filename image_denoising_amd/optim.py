@@ -32,11 +32,7 @@ class FlatAdam:
         if grad.shape != self.params.shape:
             raise ValueError("grad and params differ in shape")
         self.step_count += 1
-        b1, b2 = self.betas
-        _lib.call("dn_adam_step", _lib.ptr(self.params), _lib.ptr(grad.contiguous()),
-                  _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq), self.params.numel(),
-                  float(self.lr), float(b1), float(b2), float(self.eps), self.step_count,
-                  float(grad_scale), _lib.stream_of(self.params))
+        adam_launch(self, grad.contiguous(), float(grad_scale))
 
     def state_dict(self):
         return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
@@ -47,6 +43,14 @@ class FlatAdam:
         self.exp_avg.copy_(sd["exp_avg"])
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])
         self.lr, self.betas, self.eps = sd["lr"], tuple(sd["betas"]), sd["eps"]
+
+
+def adam_launch(opt: FlatAdam, grad: torch.Tensor, grad_scale: float) -> None:
+    """one dn_adam_step over the flat buffers (step count already incremented)"""
+    b1, b2 = opt.betas
+    _lib.call("dn_adam_step", _lib.ptr(opt.params), _lib.ptr(grad), _lib.ptr(opt.exp_avg),
+              _lib.ptr(opt.exp_avg_sq), opt.params.numel(), float(opt.lr), float(b1), float(b2),
+              float(opt.eps), opt.step_count, float(grad_scale), _lib.stream_of(opt.params))
 
 
 def reference_milestones(n_epoch: int):

@@ -119,3 +119,175 @@ def test_shard_bases_partition_the_global_streams():
         assert e0 == r * b * C * H * W
         cells.append(philox.rd_idx(5, 7, b * (H // 2) * (W // 2), cell_base=c0))
     assert np.array_equal(np.concatenate(cells), philox.rd_idx(5, 7, world * b * (H // 2) * (W // 2)))
+
+
+# ---------------------------------------------------------------------------------------------
+# The PRODUCT trainers' data-parallel wiring (image_denoising_amd.trainer: broadcast at init,
+# one all-reduce of the flat gradient, 1/world folded into Adam) run with world 2 on the CPU.
+# Only the device launches are replaced by CPU stand-ins built from the oracle (the UNet passes,
+# the sub-sampler, the losses and the fused Adam kernel); every line of the trainers' own step,
+# the sharding and the collectives is the product code.
+# ---------------------------------------------------------------------------------------------
+TB, TH, TW = 4, 64, 64  # global batch, patch size
+
+
+def _cpu_stand_ins(net, tr):
+    """Route the trainers' device launches to the CPU oracle (test infrastructure only; runs in
+    spawned processes, so the patched modules never leak into the pytest process)."""
+    import image_denoising_amd.optim as optim_mod
+    import image_denoising_amd.trainer as trainer_mod
+    from image_denoising_amd import _lib
+    from oracle import n2n_ref, unet_ref
+
+    _lib.stream_of = lambda t: None
+    saved = {}
+
+    def run_forward(x, y, ws):
+        saved[ws.data_ptr()] = x.detach().clone()
+        with torch.no_grad():
+            y.copy_(unet_ref.forward(net.flat_params, x, net.in_nc, net.out_nc))
+
+    def run_backward(dy, dflat, ws, N, H, W, dx=None):
+        _, g = unet_ref.forward_backward(net.flat_params, saved[ws.data_ptr()], dy, net.in_nc,
+                                         net.out_nc)
+        dflat.copy_(g)
+
+    net._run_forward, net._run_backward = run_forward, run_backward
+
+    def subsample(img, rd_idx=None, seed=0, offset=0, cell_base=0):
+        s1, s2 = n2n_ref.subimages_closed_form(img.numpy(), rd_idx.numpy())
+        return torch.from_numpy(s1), torch.from_numpy(s2), rd_idx
+
+    def loss(out, sub2, den, rd_idx, lam):
+        l1, l2, l, dout = n2n_ref.n2n_loss(out, sub2, den.numpy(), rd_idx.numpy(), lam)
+        return torch.tensor([l1, l2, l]), torch.from_numpy(dout)
+
+    def sloss(pred, pred2, target, a, b, g):
+        l, dp_, dp2, parts = n2n_ref.structure_loss(pred, pred2, target, a, b, g)
+        return torch.tensor(parts), torch.from_numpy(dp_), torch.from_numpy(dp2)
+
+    def adam(opt, grad, grad_scale):  # dn_adam_step's formula (torch _single_tensor_adam)
+        b1, b2 = opt.betas
+        g = grad * grad_scale
+        opt.exp_avg.mul_(b1).add_(g, alpha=1 - b1)
+        opt.exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
+        bc1, bc2 = 1 - b1 ** opt.step_count, 1 - b2 ** opt.step_count
+        denom = (opt.exp_avg_sq.sqrt() / bc2 ** 0.5).add_(opt.eps)
+        opt.params.addcdiv_(opt.exp_avg, denom, value=-opt.lr / bc1)
+
+    trainer_mod.n2n_subsample, trainer_mod.n2n_loss = subsample, loss
+    trainer_mod.structure_loss = sloss
+    by_ptr = {t.data_ptr(): t for t in (tr.grad, getattr(tr, "grad2", tr.grad))}
+
+    def call(name, *a):  # the one raw launch left in the trainers: StructureTrainer's sum
+        assert name == "dn_accumulate", name
+        by_ptr[a[0]].add_(by_ptr[a[1]])
+
+    trainer_mod._lib.call = call
+    optim_mod.adam_launch = adam
+
+
+def _trainer_inputs():
+    from oracle import philox
+
+    g = torch.Generator().manual_seed(4)
+    clean = torch.rand(TB, 1, TH, TW, generator=g)
+    noisy = (clean + 0.1 * torch.randn(TB, 1, TH, TW, generator=g)).contiguous()
+    rd = torch.from_numpy(philox.rd_idx(1, 1, TB * (TH // 2) * (TW // 2)))
+    return clean, noisy, rd
+
+
+def _run_trainer(kind, rank, world, steps=2):
+    """steps of N2NTrainer / StructureTrainer on this rank's shard; returns per-step losses,
+    the (all-reduced) gradient of the last step / world, and the final flat parameters"""
+    from image_denoising_amd import UNet
+    from image_denoising_amd.trainer import N2NTrainer, StructureTrainer
+
+    torch.manual_seed(0)
+    net = UNet(1, 1, 48)
+    if rank == 1:  # replicas differ before the trainer's broadcast
+        with torch.no_grad():
+            net.flat_params.add_(0.5)
+    dist_on = world > 1
+    tr = (N2NTrainer(net, distributed=dist_on) if kind == "n2n"
+          else StructureTrainer(net, distributed=dist_on))
+    _cpu_stand_ins(net, tr)
+    clean, noisy, rd = _trainer_inputs()
+    b = TB // world
+    sl = slice(rank * b, (rank + 1) * b)
+    cells = (TH // 2) * (TW // 2)
+    losses = []
+    for _ in range(steps):
+        if kind == "n2n":
+            l = tr.train_step(clean[sl], epoch=1, rd_idx=rd[rank * b * cells:(rank + 1) * b * cells],
+                              noisy=noisy[sl])
+        else:
+            l = tr.train_step(clean[sl], noisy[sl], epoch=1)
+        losses.append(l.clone())
+    return torch.stack(losses), tr.grad / world, net.flat_params.clone()
+
+
+def _trainer_worker(rank, world, port, kind, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from image_denoising_amd import dist as dp
+
+    dp.init_from_env("gloo")
+    losses, grad, flat = _run_trainer(kind, rank, world)
+    # the global-batch loss is the mean of the equal shards' means
+    dp.allreduce_mean_(losses)
+    gathered = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    if rank == 0:
+        out_q.put((losses.numpy(), grad.numpy(), [g.numpy() for g in gathered]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _single_worker(kind, out_q):
+    losses, grad, flat = _run_trainer(kind, 0, 1)
+    out_q.put((losses.numpy(), grad.numpy(), flat.numpy()))
+
+
+def _spawn(target, args, nproc):
+    """run target(rank?, *args, q) in fresh spawned processes; rank 0's one queue item"""
+    import queue as _queue
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=((r,) if nproc > 1 else ()) + args + (q,))
+             for r in range(nproc)]
+    for p_ in procs:
+        p_.start()
+    got = None
+    try:
+        while got is None:
+            try:
+                got = q.get(timeout=5)
+            except _queue.Empty:
+                if any(p_.exitcode not in (None, 0) for p_ in procs):
+                    break
+    finally:
+        for p_ in procs:
+            p_.join(timeout=120)
+            if p_.is_alive():
+                p_.kill()
+    assert all(p_.exitcode == 0 for p_ in procs) and got is not None
+    return got
+
+
+@pytest.mark.parametrize("kind", ["n2n", "structure"])
+def test_two_rank_product_trainer_equals_full_batch(kind):
+    """N2NTrainer / StructureTrainer(distributed=True) on 2 gloo ranks == the single-process
+    trainer on the concatenated batch: broadcast (rank 1 starts perturbed), gradient all-reduce
+    and the 1/world grad_scale into Adam, over two steps (Adam state carried)."""
+    losses_dp, grad_dp, flats = _spawn(_trainer_worker, (2, _free_port(), kind), 2)
+    assert np.array_equal(flats[0], flats[1])  # replicas identical after two updates
+    losses, g, flat = _spawn(_single_worker, (kind,), 1)
+    assert np.abs(losses_dp - losses).max() <= 1e-5 * np.abs(losses).max()
+    assert np.abs(grad_dp - g).max() <= 1e-4 * np.abs(g).max()
+    # Adam's first steps move each weight by ~lr*sign(g): a gradient within rounding of 0 may
+    # take the other sign in either summation order; everything else agrees to rounding
+    d = np.abs(flats[0] - flat)
+    assert (d > 1e-6).mean() < 2e-3, (d > 1e-6).mean()
+    assert d.max() <= 2 * 2 * 3e-4 + 1e-6
