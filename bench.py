@@ -170,34 +170,80 @@ def pmc_traffic(tag=""):
     return d.get("traffic_bytes"), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(seconds_budget=20.0):
-    """The oracle (torch-CPU restatement of the reference N2N step, validated against the
-    reference in tests/test_oracle_golden.py) on a bounded sample of config 1."""
+def host_cpu_info():
+    """the host the CPU baseline runs on: nproc, the cores this process may use (affinity mask
+    and cgroup CPU quota: on the GPU box os.cpu_count() is the whole machine, not our share),
+    the CPU model"""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = os.cpu_count()
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpus"] = quota
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    info["omp_num_threads"] = os.environ.get("OMP_NUM_THREADS")
+    return info
+
+
+def _time_oracle_step(bs, H, reps, budget_s):
+    """median wall time of the oracle N2N step (+ Adam) at bs x 1 x H x H: 1 warm-up, then
+    `reps` timed steps (fewer if they would overrun budget_s); returns (median_s, n)"""
     import numpy as np
 
     from image_denoising_amd.arch_unet import reference_init
     from oracle import philox, unet_ref
 
-    threads = min(os.cpu_count() or 1, 16)
-    torch.set_num_threads(threads)
-    bs, H = 4, 256
     torch.manual_seed(0)
     flat = reference_init(1, 1, 48)
     clean = synthetic_clean(bs, H, H, 0, "cpu")
     noisy = clean + (25.0 / 255.0) * torch.from_numpy(
         philox.normal(0, 0, np.arange(clean.numel(), dtype=np.uint64)).reshape(clean.shape)).float()
     rd = philox.rd_idx(1, 1, bs * (H // 2) * (H // 2))
+    t0 = time.perf_counter()
     unet_ref.n2n_step(flat, noisy, rd, 0.02)  # warm-up
+    t_end = time.perf_counter() + budget_s
     times = []
-    t_end = time.perf_counter() + seconds_budget
-    while len(times) < 3 and (not times or time.perf_counter() + times[-1] < t_end):
+    while len(times) < reps and (not times or time.perf_counter() + times[-1] < t_end):
         t0 = time.perf_counter()
         unet_ref.n2n_step(flat, noisy, rd, 0.02)
         times.append(time.perf_counter() - t0)
-    med = sorted(times)[len(times) // 2]
-    return {"value": round(bs / med, 3), "unit": "patches/s", "cores": threads, "kind": "port",
-            "sample": f"oracle N2N step (torch-CPU restatement of train.py/arch_unet.py), bs={bs}, "
-                      f"{H}x{H}x1, nf=48, Adam; median of {len(times)} steps after 1 warm-up"}
+    return sorted(times)[len(times) // 2], len(times)
+
+
+def cpu_baseline(budget_s=150.0):
+    """the oracle (torch-CPU restatement of the reference N2N step +
+    Adam, validated against the reference in tests/test_oracle_golden.py) on the host cores of
+    the GPU box, at config 0 (8 x 1 x 128^2) and at config 1's shape (64 x 1 x 256^2, the
+    workload of `value`); median of 5 after 1 warm-up (config 1: fewer if 5 would overrun the
+    budget; the count is reported).  Threads = the cores this process may use."""
+    info = host_cpu_info()
+    threads = info["affinity"] or 1
+    if info["cgroup_cpus"]:
+        threads = min(threads, info["cgroup_cpus"])
+    torch.set_num_threads(threads)
+    t0, n0 = _time_oracle_step(8, 128, 5, budget_s)
+    t1, n1 = _time_oracle_step(64, 256, 5, budget_s)
+    return {"value": round(64 / t1, 3), "unit": "patches/s", "cores": threads, "kind": "port",
+            "sample": f"oracle N2N step (torch-CPU restatement of train.py/arch_unet.py) + Adam at "
+                      f"config 1's shape, 64x1x256x256, nf=48; median of {n1} after 1 warm-up",
+            "configs": {"config0_8x1x128x128": {"patches_per_s": round(8 / t0, 3),
+                                                "s_per_step": round(t0, 4), "timed_steps": n0},
+                        "config1_64x1x256x256": {"patches_per_s": round(64 / t1, 3),
+                                                 "s_per_step": round(t1, 4), "timed_steps": n1}},
+            "host": info, "threads": threads}
 
 
 def eval_image(seed=11, size=512):
