@@ -18,7 +18,9 @@
 //   buffered, one barrier per stage.  LDS rows are 32 bf16 (64 B) with the 16-B quad index
 //   XOR-swizzled by (row >> 1) & 3, which makes the per-lane ds_read_b128 operand reads
 //   conflict-free for every tap offset.
+#include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "conv_epi.h"
 #include "x6_core.h"
@@ -207,7 +209,7 @@ __device__ __forceinline__ void x6_barrier() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-template <int NT>
+template <int NT, int TAIL, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   using C = PCfg<NT>;
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
@@ -226,8 +228,8 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp) + (long)blockIdx.z * a.wp_z;
   const int nch = (a.K + C::KC - 1) / C::KC;
   // last chunk packed by x6_tail_mode: 2 im2col stages (mode 1) or 5 tap-pair stages (mode 2)
-  const int tail = a.x6_tail;
-  const int tail_st = tail == 1 ? 2 : 5;
+  constexpr int tail = TAIL;
+  constexpr int tail_st = tail == 1 ? 2 : 5;
   const int nst = 9 * nch - (tail ? 9 - tail_st : 0);
 
   f32x4 acc[C::MT][NT];
@@ -310,90 +312,471 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   // chunk's x tile into LDS and loads the one after into registers) requests stage st+S-1 into
   // slot (st-1) % S, which every wave left at the previous barrier.  The compiler's own waits
   // for the x registers then only ever cover DMAs issued a stage or more earlier.
-  for (int c = 0; c < nch; ++c) {
+  // MODE 0: a full 32-channel chunk tap, with the operand reads of a stage in one basic block
+  // (the MFMAs then wait for them with counted lgkmcnt); MODE 3: the tail instantiations.
+  auto stage = [&](auto mode_tag, int c, int t) {
+    constexpr int MODE = decltype(mode_tag)::value;
     const bool more = c + 1 < nch;
-    const bool thin = tail && !more;
-#pragma unroll 1
-    for (int t = 0; t < (thin ? tail_st : 9); ++t) {
-      const int st = 9 * c + t;
-      const __bf16* lw = ring + (st % C::S) * C::WSTP;
-      bf16x8 av[3][C::MT], bv[3][NT];
-      if (thin && tail == 1) {
-        // im2col stage t: lane group lg holds k = 8lg..8lg+7 = channels 0..3 of taps
-        // 8t+2lg and 8t+2lg+1 (taps past 8 are zero), read as 8 B from quad 0 of the pixel
-        const int ta = 8 * t + 2 * lg, tb = ta + 1;
-        const int ca = ta < 9 ? ta : 8, cb = tb < 9 ? tb : 8;
-        const int da = (ca / 3) * C::IW + ca % 3, db = (cb / 3) * C::IW + cb % 3;
-        const bf16x4 z4 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+    const int st = 9 * c + t;
+    const __bf16* lw = ring + (st % C::S) * C::WSTP;
+    bf16x8 av[3][C::MT], bv[3][NT];
+    // MODE 3: the last chunk's mode decided at run time (tail instantiations: one A-read path
+    // with branches keeps them at <= 256 VGPRs; two peeled paths would spill)
+    const int mode = MODE == 3 ? ((tail && c + 1 == nch) ? tail : 0) : MODE;
+    if (mode == 1) {
+      // im2col stage t: lane group lg holds k = 8lg..8lg+7 = channels 0..3 of taps
+      // 8t+2lg and 8t+2lg+1 (taps past 8 are zero), read as 8 B from quad 0 of the pixel
+      const int ta = 8 * t + 2 * lg, tb = ta + 1;
+      const int ca = ta < 9 ? ta : 8, cb = tb < 9 ? tb : 8;
+      const int da = (ca / 3) * C::IW + ca % 3, db = (cb / 3) * C::IW + cb % 3;
+      const bf16x4 z4 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
 #pragma unroll
-        for (int m = 0; m < C::MT; ++m) {
-          const int p0 = (wave * C::MT + m) * C::IW + li;
-          const int pa = p0 + da, pb = p0 + db;
-          const int oa = pa * C::KC + x6_swz(pa, 0) * 8, ob = pb * C::KC + x6_swz(pb, 0) * 8;
+      for (int m = 0; m < C::MT; ++m) {
+        const int p0 = (wave * C::MT + m) * C::IW + li;
+        const int pa = p0 + da, pb = p0 + db;
+        const int oa = pa * C::KC + x6_swz(pa, 0) * 8, ob = pb * C::KC + x6_swz(pb, 0) * 8;
 #pragma unroll
-          for (int p = 0; p < 3; ++p) {
-            bf16x4 va = *reinterpret_cast<const bf16x4*>(lx + p * C::XPL + oa);
-            bf16x4 vb = *reinterpret_cast<const bf16x4*>(lx + p * C::XPL + ob);
-            if (ta > 8) va = z4;
-            if (tb > 8) vb = z4;
-            av[p][m] = __builtin_shufflevector(va, vb, 0, 1, 2, 3, 4, 5, 6, 7);
-          }
-        }
-      } else if (thin) {
-        // tap-pair stage t: lane groups 0,1 hold channels 0..15 of tap 2t, groups 2,3 those of
-        // tap 2t+1 (zero past tap 8): quad lg & 1 of the pixel at that tap
-        const int ta = 2 * t + (lg >> 1);
-        const int ca = ta < 9 ? ta : 8;
-        const int da = (ca / 3) * C::IW + ca % 3;
-        const bf16x8 z8 = {};
-#pragma unroll
-        for (int m = 0; m < C::MT; ++m) {
-          const int pa = (wave * C::MT + m) * C::IW + li + da;
-          const int oa = pa * C::KC + x6_swz(pa, lg & 1) * 8;
-#pragma unroll
-          for (int p = 0; p < 3; ++p) {
-            const bf16x8 v = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + oa);
-            av[p][m] = ta > 8 ? z8 : v;
-          }
-        }
-      } else {
-        const int ky = t / 3, kx = t - 3 * ky;
-#pragma unroll
-        for (int m = 0; m < C::MT; ++m) {
-          const int pix = (wave * C::MT + m + ky) * C::IW + li + kx;
-          const int off = pix * C::KC + x6_swz(pix, lg) * 8;
-#pragma unroll
-          for (int p = 0; p < 3; ++p)
-            av[p][m] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
+        for (int p = 0; p < 3; ++p) {
+          bf16x4 va = *reinterpret_cast<const bf16x4*>(lx + p * C::XPL + oa);
+          bf16x4 vb = *reinterpret_cast<const bf16x4*>(lx + p * C::XPL + ob);
+          if (ta > 8) va = z4;
+          if (tb > 8) vb = z4;
+          av[p][m] = __builtin_shufflevector(va, vb, 0, 1, 2, 3, 4, 5, 6, 7);
         }
       }
+    } else if (mode == 2) {
+      // tap-pair stage t: lane groups 0,1 hold channels 0..15 of tap 2t, groups 2,3 those of
+      // tap 2t+1 (zero past tap 8): quad lg & 1 of the pixel at that tap
+      const int ta = 2 * t + (lg >> 1);
+      const int ca = ta < 9 ? ta : 8;
+      const int da = (ca / 3) * C::IW + ca % 3;
+      const bf16x8 z8 = {};
 #pragma unroll
-      for (int q = 0; q < NT; ++q) {
+      for (int m = 0; m < C::MT; ++m) {
+        const int pa = (wave * C::MT + m) * C::IW + li + da;
+        const int oa = pa * C::KC + x6_swz(pa, lg & 1) * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + oa);
+          av[p][m] = ta > 8 ? z8 : v;
+        }
+      }
+    } else {
+      const int ky = t / 3, kx = t - 3 * ky;
+#pragma unroll
+      for (int m = 0; m < C::MT; ++m) {
+        const int pix = (wave * C::MT + m + ky) * C::IW + li + kx;
+        const int off = pix * C::KC + x6_swz(pix, lg) * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          av[p][m] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
+      }
+    }
+    // B fragment groups in the order x6_group consumes them, read LOOK groups ahead of the
+    // MFMAs: the reads of group g + LOOK are issued after group g's MFMAs (into its freed
+    // registers), so every MFMA finds its operands in flight long enough, and the stage's
+    // operands never all live at once (the kernel is at 2 waves per SIMD, 256 VGPRs)
+    constexpr int QG = x6_qg(C::MT, NT), NG = NT / QG, LOOK = NG < 2 ? NG : 2;
+    auto read_b = [&](int g) {
+#pragma unroll
+      for (int q = g * QG; q < (g + 1) * QG; ++q) {
         const int row = q * 16 + li;
         const int off = row * C::KC + x6_swz(row, lg) * 8;
 #pragma unroll
         for (int p = 0; p < 3; ++p)
           bv[p][q] = *reinterpret_cast<const bf16x8*>(lw + p * C::WPL + off);
       }
-      x6_block<C::MT, NT, x6_qg(C::MT, NT)>(acc, av, bv);
-      const bool xstep = t == 8 && more;
-      if (xstep) {
-        x6_barrier();  // every wave is done with this chunk's x tile
-        store_x();
-        load_x((c + 2 < nch ? c + 2 : nch - 1) * C::KC);  // uniform count: re-load at the end
-      }
-      load_w(st + C::S - 1 < nst ? st + C::S - 1 : nst - 1, (st + C::S - 1) % C::S);
-      // own DMAs of stage st+1 landed: issued after them are those of stages st+2, st+S-1 and,
-      // in a chunk's first stage, the x loads issued at the previous chunk's end
-      if (t == 0 && c > 0) X6_WAITCNT_VM(C::PPW * (C::S - 2) + C::XITEMS);
-      else X6_WAITCNT_VM(C::PPW * (C::S - 2));
-      if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
-      x6_barrier();
+    };
+#pragma unroll
+    for (int g = 0; g < LOOK; ++g) read_b(g);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if constexpr (ABL == 1)
+        x6_group_chained<C::MT, NT, QG>(acc, av, bv, g * QG);
+      else
+        x6_group<C::MT, NT, QG>(acc, av, bv, g * QG);
+      __builtin_amdgcn_sched_barrier(0);
+      if (g + LOOK < NG) read_b(g + LOOK);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const bool xstep = t == 8 && more;
+    if (xstep && ABL != 5) {
+      x6_barrier();  // every wave is done with this chunk's x tile
+      store_x();
+      load_x((c + 2 < nch ? c + 2 : nch - 1) * C::KC);  // uniform count: re-load at the end
+    }
+    load_w(st + C::S - 1 < nst ? st + C::S - 1 : nst - 1, (st + C::S - 1) % C::S);
+    // own DMAs of stage st+1 landed: issued after them are those of stages st+2, st+S-1 and the
+    // next-but-one chunk's x loads when issued in this stage (xstep) or the previous one (a
+    // chunk's first stage) -- the x loads are not waited for here
+    if (xstep || (t == 0 && c > 0)) X6_WAITCNT_VM(C::PPW * (C::S - 2) + C::XITEMS);
+    else X6_WAITCNT_VM(C::PPW * (C::S - 2));
+    if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
+    if (ABL != 2 || xstep) x6_barrier();
+  };
+  // TAIL: the instantiation's last-chunk packing (the host passes a.x6_tail == TAIL)
+  int rep = 0;
+  for (int c = 0; c < nch; ++c) {
+    if constexpr (TAIL == 0) {
+#pragma unroll 1
+      for (int t = 0; t < 9; ++t) stage(std::integral_constant<int, 0>{}, c, t);
+      if (ABL == 4 && c + 1 == nch && rep == 0) { c = -1; rep = 1; }  // probe: 2 tiles per WG
+    } else {
+      const int ns = c + 1 < nch ? 9 : tail_st;
+#pragma unroll 1
+      for (int t = 0; t < ns; ++t) stage(std::integral_constant<int, 3>{}, c, t);
     }
   }
   X6_WAITCNT_VM(0);  // the trailing re-load DMAs must land before the LDS is reused
   x6_barrier();
   fwd_epilogue<NT, C::MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
+}
+
+// ------------------------------------------------------------------------------------
+// Persistent variant of k_c3x6p for large grids (k_c3x6q): one workgroup per CU walks the tiles
+// blockIdx.x, blockIdx.x + gridDim.x, ... and its x-tile chunk pipeline and weight-stage DMA
+// ring run on across tile boundaries (the next tile's first chunk is simply the next chunk;
+// stage g of the walk is stage g % nst of tile g / nst), so a tile costs no prologue (HBM
+// latency of its first x tile and weight stages), no pipeline drain and no workgroup launch.
+// The MFMA operands are swapped (A = weights, B = pixels): a lane's accumulator then holds 4
+// consecutive output channels of one pixel, and the epilogue stores them as float4 straight
+// from registers through a buffer resource (out-of-tile pixels get an out-of-range offset), so
+// every wave issues the same number of stores per tile and the vmcnt counts stay constants.
+// The bias of all output channels sits in LDS.  Output: NHWC, float4-aligned views.
+// ------------------------------------------------------------------------------------
+__device__ unsigned long long dn_x6q_times[4096];  // PROBE: per-workgroup start / end clocks
+__device__ int dn_x6q_probe;
+
+template <int NT, int TAIL>
+__global__ __launch_bounds__(512, 1) void k_c3x6q(FwdArgs a) {
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  using C = PCfg<NT>;
+  constexpr int MT = C::MT;
+  // ONE LDS object (a second __shared__ array makes the compiler wait for every LDS DMA before
+  // each LDS read): the bias lives past the main loop's bytes
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[163840];
+  float* lbias = reinterpret_cast<float*>(lds_raw + C::LBYTES_MAIN);
+  __bf16* lx = reinterpret_cast<__bf16*>(lds_raw);
+  __bf16* ring = lx + 3 * C::XPL;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
+  const int li = lane & 15, lg = lane >> 4;
+  const int tiles_x = (a.OW + C::TW - 1) / C::TW, tiles_y = (a.OH + C::TH - 1) / C::TH;
+  const int per_img = tiles_x * tiles_y;
+  const int nz = a.zc ? (a.NOUT + a.zc - 1) / a.zc : 1;
+  const int ntiles = per_img * a.N * nz;
+  const int G = gridDim.x;
+  const int my_n = (ntiles - (int)blockIdx.x + G - 1) / G;  // >= 1: the grid is <= ntiles
+  const int nch = (a.K + C::KC - 1) / C::KC;
+  constexpr int tail = TAIL;
+  constexpr int tail_st = tail == 1 ? 2 : 5;
+  const int nst = 9 * nch - (tail ? 9 - tail_st : 0);
+  const bool has_bias = (a.epi == EPI_BIAS || a.epi == EPI_BIAS_ACT) && a.bias != nullptr;
+  if (has_bias)
+    for (int e = tid; e < a.NOUT; e += C::WAVES * 64) lbias[e] = a.bias[e];
+
+  // tile ordinal i of this workgroup -> (output-channel block z, image n, tile origin)
+  struct Tile { int z, n, ty0, tx0; };
+  auto tile = [&](int i) {
+    const int T = (int)blockIdx.x + i * G;
+    Tile r;
+    r.z = T / (a.N * per_img);
+    const int rem = T - r.z * a.N * per_img;
+    r.n = rem / per_img;
+    const int p = rem - r.n * per_img;
+    r.ty0 = (p / tiles_x) * C::TH;
+    r.tx0 = (p % tiles_x) * C::TW;
+    return r;
+  };
+
+  f32x4 acc[MT][NT], ph[MT], pl[MT];  // ph / pl: the last group's fresh sums, added later
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    ph[m] = pl[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NT; ++q) acc[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // x chunk j of the walk (tile j / nch, channels 32 * (j % nch)); past the end: a harmless
+  // re-load of the last chunk, so every thread issues exactly XITEMS buffer loads per call.
+  // The resource covers the tile's input rows only (32-bit extents, see k_c3x6p).
+  f32x4 xr[C::XITEMS];
+  // the walk's chunks and weight stages are requested strictly in order: incremental cursors
+  // (a tile's origin is decoded once per tile, not per request)
+  int xi = 0, xc = 0;
+  Tile xT = tile(0);
+  auto load_x = [&]() {  // the next chunk of the walk
+    const bool past = xi >= my_n;
+    const int k0 = (past ? nch - 1 : xc) * C::KC;
+    const Tile T = xT;
+    if (++xc == nch) {
+      xc = 0;
+      if (++xi < my_n) xT = tile(xi);
+    }
+    const int iy0 = T.ty0 - 1, ix0 = T.tx0 - 1;
+    const int ry0 = iy0 > 0 ? iy0 : 0, ry1 = iy0 + C::IH < a.IHt ? iy0 + C::IH : a.IHt;
+    const long row_floats = (long)a.IWt * a.in_stride;
+    const float* inb = a.in + (long)T.n * a.IHt * row_floats + a.in_off;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(inb + ry0 * row_floats), (short)0, (int)((ry1 - ry0) * row_floats * 4),
+        0x00020000);
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * C::WAVES * 64;
+      const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+      const int iy = pix / C::IW, ix = pix - iy * C::IW;
+      const int gy = iy0 + iy, gx = ix0 + ix, k = k0 + 4 * q;
+      const bool ok = e < C::XQ && gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt && k < a.K;
+      const int off = ok ? (((gy - ry0) * a.IWt + gx) * a.in_stride + k) * 4 : 0x7fffffff;
+      xr[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * C::WAVES * 64;
+      if (e < C::XQ) {
+        const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+        const float f[4] = {xr[it][0], xr[it][1], xr[it][2], xr[it][3]};
+        bf16x4 h, m, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          __bf16 hj, mj, lj;
+          split3(f[j], hj, mj, lj);
+          h[j] = hj; m[j] = mj; l[j] = lj;
+        }
+        const int off = pix * C::KC + x6_swz(pix, q >> 1) * 8 + (q & 1) * 4;
+        *reinterpret_cast<bf16x4*>(lx + off) = h;
+        *reinterpret_cast<bf16x4*>(lx + C::XPL + off) = m;
+        *reinterpret_cast<bf16x4*>(lx + 2 * C::XPL + off) = l;
+      }
+    }
+  };
+  // weights of the next walk stage into the next ring slot (past the end: re-loads of the last)
+  int wi = 0, wst = 0, wslot = 0;
+  const __bf16* wcur = reinterpret_cast<const __bf16*>(a.wp) + (long)tile(0).z * a.wp_z;
+  auto load_w = [&]() {
+    const unsigned char* src =
+        reinterpret_cast<const unsigned char*>(wcur + (long)(wi < my_n ? wst : nst - 1) * C::WSTP);
+    unsigned char* dst = reinterpret_cast<unsigned char*>(ring + wslot * C::WSTP);
+    wslot = (wslot + 1) % C::S;
+    if (++wst == nst) {
+      wst = 0;
+      if (++wi < my_n) wcur = reinterpret_cast<const __bf16*>(a.wp) + (long)tile(wi).z * a.wp_z;
+    }
+#pragma unroll
+    for (int j = 0; j < C::PPW; ++j) {
+      const int piece = wave * C::PPW + j;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(src + piece * 1024 + lane * 16),
+          (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16, 0, 0);
+    }
+  };
+  // tile i's outputs: acc[m][q] = channels 16q + 4lg .. +3 of pixel (row wave*MT + m, col li);
+  // MT*NT buffer stores per wave whatever the tile's extent
+  constexpr int NSTORE = MT * NT;
+  auto epilogue = [&](int i) {
+    const Tile T = tile(i);
+    const int cz = a.zc ? T.z * a.zc : 0;
+    const int nout = a.zc ? min(16 * NT, a.NOUT - cz) : a.NOUT;
+    const int r0 = T.ty0, r1 = T.ty0 + C::TH < a.OH ? T.ty0 + C::TH : a.OH;
+    const long orow = (long)a.OW * a.out_stride;
+    float* ob = a.out + ((long)T.n * a.OH + r0) * orow;
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+        ob, (short)0, (int)((r1 - r0) * orow * 4), 0x00020000);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int gy = T.ty0 + wave * MT + m, gx = T.tx0 + li;
+      const bool pix_ok = gy < a.OH && gx < a.OW;
+      const long pix = ((long)T.n * a.OH + gy) * a.OW + gx;
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        const int c = 16 * q + 4 * lg;
+        const bool ok = pix_ok && c < nout;
+        f32x4 v = acc[m][q];
+        if (has_bias) {
+          const f32x4 b = *reinterpret_cast<const f32x4*>(lbias + cz + c);
+          v += b;
+        }
+        if (a.epi == EPI_BIAS_ACT) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * 0.2f;
+        } else if (ok && (a.epi == EPI_MASK || a.epi == EPI_ACCUM)) {
+          const float* src = a.epi == EPI_MASK ? a.mask + pix * a.mask_stride + a.mask_off + cz + c
+                                               : a.out + pix * a.out_stride + a.out_off + cz + c;
+          const f32x4 r = *reinterpret_cast<const f32x4*>(src);
+          if (a.epi == EPI_MASK) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = r[k] > 0.f ? v[k] : v[k] * 0.2f;
+          } else {
+            v = r + v;
+          }
+        }
+        const int off = ok ? (int)((((gy - r0) * (long)a.OW + gx) * a.out_stride + a.out_off + cz + c) * 4)
+                           : 0x7fffffff;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), ors, off, 0, 0);
+        acc[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
+  // prologue: chunk 0's x tile split into LDS, chunk 1's in registers, weight stages 0..S-2
+  load_x();
+  store_x();
+  load_x();
+#pragma unroll
+  for (int j = 0; j < C::S - 1; ++j) load_w();
+  X6_WAITCNT_VM(C::PPW * (C::S - 2));  // own DMAs of stage 0 landed
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile and bias stores done
+  x6_barrier();
+
+  // walk stage g = i * nst + st (tile ordinal i, chunk c, tap t); see k_c3x6p for the ring
+  auto stage = [&](int i, int c, int t, int g) {
+    const __bf16* lw = ring + (g % C::S) * C::WSTP;
+    const bool last_chunk = c + 1 == nch;
+    const int mode = (tail && last_chunk) ? tail : 0;
+    bf16x8 av[3][MT], bv[3][NT];
+    if (mode == 1) {
+      const int ta = 8 * t + 2 * lg, tb = ta + 1;
+      const int ca = ta < 9 ? ta : 8, cb = tb < 9 ? tb : 8;
+      const int da = (ca / 3) * C::IW + ca % 3, db = (cb / 3) * C::IW + cb % 3;
+      const bf16x4 z4 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int p0 = (wave * MT + m) * C::IW + li;
+        const int pa = p0 + da, pb = p0 + db;
+        const int oa = pa * C::KC + x6_swz(pa, 0) * 8, ob = pb * C::KC + x6_swz(pb, 0) * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          bf16x4 va = *reinterpret_cast<const bf16x4*>(lx + p * C::XPL + oa);
+          bf16x4 vb = *reinterpret_cast<const bf16x4*>(lx + p * C::XPL + ob);
+          if (ta > 8) va = z4;
+          if (tb > 8) vb = z4;
+          av[p][m] = __builtin_shufflevector(va, vb, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      }
+    } else if (mode == 2) {
+      const int ta = 2 * t + (lg >> 1);
+      const int ca = ta < 9 ? ta : 8;
+      const int da = (ca / 3) * C::IW + ca % 3;
+      const bf16x8 z8 = {};
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int pa = (wave * MT + m) * C::IW + li + da;
+        const int oa = pa * C::KC + x6_swz(pa, lg & 1) * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + oa);
+          av[p][m] = ta > 8 ? z8 : v;
+        }
+      }
+    } else {
+      const int ky = t / 3, kx = t - 3 * ky;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int pix = (wave * MT + m + ky) * C::IW + li + kx;
+        const int off = pix * C::KC + x6_swz(pix, lg) * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          av[p][m] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
+      }
+    }
+    // One output-channel fragment q per group: its 2*MT-chain of six products (fresh hi / lo
+    // sums) interleaved with the VALU adds of the PREVIOUS group (pending in ph / pl, the last
+    // group of a stage into the next stage), so no add waits on the MFMA that feeds it; the
+    // weight fragments are read two groups ahead.
+    auto read_b = [&](int q) {
+      const int row = q * 16 + li;
+      const int off = row * C::KC + x6_swz(row, lg) * 8;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        bv[p][q] = *reinterpret_cast<const bf16x8*>(lw + p * C::WPL + off);
+    };
+    read_b(0);
+    if (NT > 1) read_b(1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      if (q + 2 < NT) read_b(q + 2);
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      constexpr int PA[4] = {1, 0, 1, 2}, PB[4] = {0, 2, 1, 0};
+      f32x4 h[MT], l[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) h[m] = mfma_bf16(bv[0][q], av[0][m], z);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) l[m] = mfma_bf16(bv[1][q], av[0][m], z);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) l[m] = mfma_bf16(bv[PB[jj]][q], av[PA[jj]][m], l[m]);
+      const int qp = q == 0 ? NT - 1 : q - 1;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        acc[m][qp] += ph[m] + pl[m];
+        ph[m] = h[m];
+        pl[m] = l[m];
+      }
+      // schedule: the 3 reads two groups ahead, then MFMAs with the pending adds between them
+      if (q + 2 < NT) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+#pragma unroll
+      for (int r = 0; r < 4 * MT / 2; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int ns = (tail && last_chunk) ? tail_st : 9;
+    const bool xstep = t == ns - 1;  // the walk always has a next chunk (re-loads past its end)
+    const bool tile_end = last_chunk && xstep;
+    if (xstep) {
+      x6_barrier();  // every wave is done with this chunk's x tile
+      store_x();     // (waits for its registers: issued a chunk ago)
+    }
+    // after the split, so the x-register wait never covers the epilogue's stores
+    if (tile_end) {  // the pending last group, then the outputs (registers and global memory)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        acc[m][NT - 1] += ph[m] + pl[m];
+        ph[m] = pl[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      epilogue(i);
+    }
+    if (xstep) load_x();  // chunk j + 2 of the walk
+    load_w();  // stage g + S - 1
+    // own DMAs of stage g+1 landed: younger are those of stages g+2, g+S-1, the x loads of an
+    // xstep in this or the previous stage, and the epilogue's stores of this or the previous
+    // stage (all issued after stage g+1's DMAs)
+    const int younger = C::PPW * (C::S - 2) + (xstep || (t == 0 && g > 0) ? C::XITEMS : 0) +
+                        (tile_end || (t == 0 && c == 0 && i > 0) ? NSTORE : 0);
+    if (younger == C::PPW * (C::S - 2)) X6_WAITCNT_VM(C::PPW * (C::S - 2));
+    else if (younger == C::PPW * (C::S - 2) + C::XITEMS) X6_WAITCNT_VM(C::PPW * (C::S - 2) + C::XITEMS);
+    else X6_WAITCNT_VM(C::PPW * (C::S - 2) + C::XITEMS + NSTORE);
+    if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
+    x6_barrier();
+  };
+  int g = 0;
+  for (int i = 0; i < my_n; ++i)
+    for (int c = 0; c < nch; ++c) {
+      const int ns = (tail && c + 1 == nch) ? tail_st : 9;
+#pragma unroll 1
+      for (int t = 0; t < ns; ++t, ++g) stage(i, c, t, g);
+    }
+  X6_WAITCNT_VM(0);  // trailing re-load DMAs and the last stores
+  if (dn_x6q_probe && (threadIdx.x & 511) == 0 && blockIdx.x < 2048) {
+    volatile unsigned long long* tp = dn_x6q_times + 2 * blockIdx.x + (threadIdx.x >> 9);
+    tp[0] = t_start;
+    tp[1] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // Pre-split weight image, one per output-channel block z: [chunk][tap][piece][n < NP][32 k],
@@ -506,7 +889,82 @@ template <int NT>
 static hipError_t run_x6p(const FwdArgs& a, int nz, hipStream_t s) {
   using C = PCfg<NT>;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
-  hipLaunchKernelGGL((k_c3x6p<NT>), dim3(tx * ty, a.N, nz), dim3(C::WAVES * 64), 0, s, a);
+  const dim3 grid(tx * ty, a.N, nz), block(C::WAVES * 64);
+  if (a.x6_tail == 1)
+    hipLaunchKernelGGL((k_c3x6p<NT, 1>), grid, block, 0, s, a);
+  else if (a.x6_tail == 2)
+    hipLaunchKernelGGL((k_c3x6p<NT, 2>), grid, block, 0, s, a);
+  else {
+    static const int abl = getenv("DN_X6_ABL") ? atoi(getenv("DN_X6_ABL")) : 0;  // timing probes
+    if (abl == 1)
+      hipLaunchKernelGGL((k_c3x6p<NT, 0, 1>), grid, block, 0, s, a);
+    else if (abl == 2)
+      hipLaunchKernelGGL((k_c3x6p<NT, 0, 2>), grid, block, 0, s, a);
+    else if (abl == 4)
+      hipLaunchKernelGGL((k_c3x6p<NT, 0, 4>), dim3(grid.x, grid.y / 2, grid.z), block, 0, s, a);
+    else if (abl == 5)
+      hipLaunchKernelGGL((k_c3x6p<NT, 0, 5>), grid, block, 0, s, a);
+    else
+      hipLaunchKernelGGL((k_c3x6p<NT, 0>), grid, block, 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+static int cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+// PROBE: DN_X6_TIMES=1 prints the spread of the persistent kernel's workgroup end times
+static void x6q_times_report(int grid) {
+  unsigned long long t[4096];
+  hipDeviceSynchronize();
+  if (hipMemcpyFromSymbol(t, HIP_SYMBOL(dn_x6q_times), sizeof(unsigned long long) * 2 * grid) !=
+      hipSuccess)
+    return;
+  unsigned long long t0 = ~0ull, e_min = ~0ull, e_max = 0;
+  double e_sum = 0;
+  for (int b = 0; b < grid; ++b) {
+    t0 = t[2 * b] < t0 ? t[2 * b] : t0;
+  }
+  for (int b = 0; b < grid; ++b) {
+    const unsigned long long e = t[2 * b + 1] - t0;
+    e_min = e < e_min ? e : e_min;
+    e_max = e > e_max ? e : e_max;
+    e_sum += (double)e;
+  }
+  fprintf(stderr, "x6q end times (us since first start): min %.1f mean %.1f max %.1f\n",
+          e_min / 100.0, e_sum / grid / 100.0, e_max / 100.0);
+}
+
+// the persistent kernel: one workgroup per CU (at most one per tile)
+template <int NT>
+static hipError_t run_x6q(const FwdArgs& a, int nz, hipStream_t s) {
+  using C = PCfg<NT>;
+  const long ntiles = (long)((a.OW + C::TW - 1) / C::TW) * ((a.OH + C::TH - 1) / C::TH) * a.N * nz;
+  const int grid = (int)(ntiles < cu_count() ? ntiles : cu_count());
+  if (a.x6_tail == 1)
+    hipLaunchKernelGGL((k_c3x6q<NT, 1>), dim3(grid), dim3(C::WAVES * 64), 0, s, a);
+  else if (a.x6_tail == 2)
+    hipLaunchKernelGGL((k_c3x6q<NT, 2>), dim3(grid), dim3(C::WAVES * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_c3x6q<NT, 0>), dim3(grid), dim3(C::WAVES * 64), 0, s, a);
+  static const bool probe = getenv("DN_X6_TIMES") != nullptr;
+  if (probe) {
+    static int n = 0;
+    if (n++ == 0) {
+      int one = 1;
+      hipMemcpyToSymbol(HIP_SYMBOL(dn_x6q_probe), &one, sizeof(int));
+    } else {
+      x6q_times_report(grid);
+    }
+  }
   return hipGetLastError();
 }
 
@@ -529,11 +987,26 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
   auto pipe = [&]() {
     return np == 32 ? run_x6p<2>(a, nz, s) : (np == 48 ? run_x6p<3>(a, nz, s) : run_x6p<6>(a, nz, s));
   };
-  if (a.x6_tail) {  // tail-packed last chunk: only the pipelined kernel reads it
+  // the persistent kernel: NHWC float4 outputs (its epilogue stores from registers), the bias
+  // in the LDS left over by the main loop, 32-bit extents of one tile's 16 output rows
+  // opt-in while it measures slower than the per-tile kernel
+  static const bool no_persist = !(getenv("DN_X6_PERSIST") && atoi(getenv("DN_X6_PERSIST")) != 0);
+  const bool aux = a.epi == EPI_MASK;
+  const bool persist =
+      !no_persist && a.out_layout == OUT_NHWC && a.epi != EPI_BIAS_ADD &&
+      ((a.out_stride | a.out_off | a.NOUT) & 3) == 0 &&
+      (!aux || ((a.mask_stride | a.mask_off) & 3) == 0) &&
+      (long)PCfg<6>::TH * a.OW * a.out_stride * 4 < 0x7fffffffL &&
+      a.NOUT * 4 <= 163840 - PCfg<6>::LBYTES_MAIN;
+  auto run = [&]() {
+    if (!persist) return pipe();
+    return np == 32 ? run_x6q<2>(a, nz, s) : (np == 48 ? run_x6q<3>(a, nz, s) : run_x6q<6>(a, nz, s));
+  };
+  if (a.x6_tail) {  // tail-packed last chunk: only the pipelined kernels read it
     if (!aligned || a.x6_tail != x6_tail_mode(a.K)) return hipErrorInvalidValue;
-    return pipe();
+    return run();
   }
-  if (!no_pipe && x6_pipelined(a.N, a.OH, a.OW, a.NOUT, a.zc) && aligned) return pipe();
+  if (!no_pipe && x6_pipelined(a.N, a.OH, a.OW, a.NOUT, a.zc) && aligned) return run();
   if (np == 32)
     return x6_pick_mt<2>(a, nz) == 2 ? run_x6<2, 2>(a, nz, s) : run_x6<2, 1>(a, nz, s);
   if (np == 48)
