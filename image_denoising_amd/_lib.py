@@ -38,6 +38,8 @@ SIGNATURES = {
                                  c_size_t, c_void_p]),
     "dn_unet_forward_bf16": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
                                      c_size_t, c_void_p]),
+    "dn_unet_forward_n2n": (c_int, [POINTER(DnCfg), _F, _F, _F, _U8, c_int, c_int, c_int,
+                                    c_void_p, c_size_t, c_int, c_void_p]),
     "dn_unet_forward_prec": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
                                      c_size_t, c_int, c_void_p]),
     "dn_unet_backward_prec": (c_int, [POINTER(DnCfg), _F, _F, _F, _F, c_int, c_int, c_int,

@@ -250,6 +250,14 @@ class UNet(nn.Module):
                   _lib.ptr(x), _lib.ptr(y), N, H, W, ws.data_ptr(), ws.numel(), self._prec(),
                   _lib.stream_of(x))
 
+    def _run_forward_n2n(self, x, den, ws, rd_idx):
+        """the N2N no-grad pass: den = UNet(x) at the pair pixels of rd_idx only
+        (dn_unet_forward_n2n; training_script.md:141-144 reads nothing else)"""
+        N, _, H, W = x.shape
+        _lib.call("dn_unet_forward_n2n", ctypes.byref(self._cfg), _lib.ptr(self._flat),
+                  _lib.ptr(x), _lib.ptr(den), _lib.ptr(rd_idx), N, H, W, ws.data_ptr(), ws.numel(),
+                  self._prec(), _lib.stream_of(x))
+
     def set_inference_precision(self, dtype: str) -> "UNet":
         """'fp32' (default, the parity path) or 'bf16': no-grad forwards then multiply
         bf16-rounded operands on the bf16 matrix cores (fp32 accumulation and storage) —

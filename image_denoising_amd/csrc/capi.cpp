@@ -113,6 +113,24 @@ dn_status dn_unet_forward_prec(const dn_unet_cfg* cfg, const float* params, cons
   DN_GUARD_END
 }
 
+dn_status dn_unet_forward_n2n(const dn_unet_cfg* cfg, const float* params, const float* x,
+                              float* den, const uint8_t* rd_idx, int N, int H, int W, void* ws,
+                              size_t ws_bytes, int precision, void* stream) {
+  DN_GUARD_BEGIN
+  if (precision != DN_PREC_FP32 && precision != DN_PREC_FP32_X6)
+    return fail(DN_ERR_ARG, "precision must be DN_PREC_FP32 or DN_PREC_FP32_X6");
+  if (!cfg || !params || !x || !den || !rd_idx || !ws) return fail(DN_ERR_ARG, "null argument");
+  Plan p;
+  std::string err;
+  if (!build_plan(*cfg, N, H, W, false, p, err)) return fail(DN_ERR_ARG, err);
+  if (ws_bytes < (size_t)p.total_floats * sizeof(float))
+    return fail(DN_ERR_WORKSPACE, "workspace smaller than dn_unet_workspace_size()");
+  p.with_bwd = false;  // no-grad pass: nothing is saved
+  return unet_forward(p, params, x, den, static_cast<float*>(ws), (hipStream_t)stream, precision,
+                      rd_idx);
+  DN_GUARD_END
+}
+
 dn_status dn_unet_forward_bf16(const dn_unet_cfg* cfg, const float* params, const float* x,
                                float* y, int N, int H, int W, void* ws, size_t ws_bytes,
                                void* stream) {

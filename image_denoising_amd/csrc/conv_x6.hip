@@ -209,9 +209,16 @@ __device__ __forceinline__ void x6_barrier() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-template <int NT, int TAIL, int ABL = 0>
+// SEL: a.sel_rd's N2N pair pixels only (launch_fwd_x6_sel): a wave's two tile rows are one row
+// of 2x2 cells, whose 16 selected pixels (2 per cell) form ONE M fragment (the lane of fragment
+// row 2j + s reads its A operand at the pixel pair[rd][s] of cell j): half the MFMAs, the same
+// staging, per-pixel arithmetic unchanged (bit-identical outputs); the epilogue writes the
+// fragment as row ty0/2 + wave of the [OH/2][OW] pair image.
+template <int NT, int TAIL, int ABL = 0, bool SEL = false>
 __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   using C = PCfg<NT>;
+  static_assert(!SEL || TAIL == 0, "selected pixels: full 32-channel chunks only");
+  constexpr int MTC = SEL ? 1 : C::MT;  // M fragments computed per wave
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
   __bf16* lx = reinterpret_cast<__bf16*>(lds_raw);
   __bf16* ring = lx + 3 * C::XPL;
@@ -232,11 +239,21 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   constexpr int tail_st = tail == 1 ? 2 : 5;
   const int nst = 9 * nch - (tail ? 9 - tail_st : 0);
 
-  f32x4 acc[C::MT][NT];
+  f32x4 acc[MTC][NT];
 #pragma unroll
-  for (int m = 0; m < C::MT; ++m)
+  for (int m = 0; m < MTC; ++m)
 #pragma unroll
     for (int q = 0; q < NT; ++q) acc[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // SEL: x-tile pixel of this lane's fragment row (cell j = li / 2, pair member s = li % 2)
+  int selpix = 0;
+  if constexpr (SEL) {
+    const int ci = ty0 / 2 + wave, cj = tx0 / 2 + (li >> 1);
+    const int r = (ci < a.OH / 2 && cj < a.OW / 2)
+                      ? a.sel_rd[((long)n * (a.OH / 2) + ci) * (a.OW / 2) + cj] & 7 : 0;
+    constexpr unsigned kPair = 0xB721ED84u;  // train.py:151-154, 4 bits (a | b << 2) per rd
+    const int k = (kPair >> (4 * r + 2 * (li & 1))) & 3;
+    selpix = (2 * wave + (k >> 1)) * C::IW + 2 * (li >> 1) + (k & 1);
+  }
 
   // Exactly XITEMS buffer loads per thread per chunk (items outside the tile or the image get
   // an out-of-range offset, for which the buffer unit returns zeros) and exactly PPW DMAs per
@@ -319,7 +336,7 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     const bool more = c + 1 < nch;
     const int st = 9 * c + t;
     const __bf16* lw = ring + (st % C::S) * C::WSTP;
-    bf16x8 av[3][C::MT], bv[3][NT];
+    bf16x8 av[3][MTC], bv[3][NT];
     // MODE 3: the last chunk's mode decided at run time (tail instantiations: one A-read path
     // with branches keeps them at <= 256 VGPRs; two peeled paths would spill)
     const int mode = MODE == 3 ? ((tail && c + 1 == nch) ? tail : 0) : MODE;
@@ -361,6 +378,12 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
           av[p][m] = ta > 8 ? z8 : v;
         }
       }
+    } else if constexpr (SEL) {
+      const int ky = t / 3, kx = t - 3 * ky;
+      const int pix = selpix + ky * C::IW + kx;
+      const int off = pix * C::KC + x6_swz(pix, lg) * 8;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) av[p][0] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
     } else {
       const int ky = t / 3, kx = t - 3 * ky;
 #pragma unroll
@@ -376,7 +399,7 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     // MFMAs: the reads of group g + LOOK are issued after group g's MFMAs (into its freed
     // registers), so every MFMA finds its operands in flight long enough, and the stage's
     // operands never all live at once (the kernel is at 2 waves per SIMD, 256 VGPRs)
-    constexpr int QG = x6_qg(C::MT, NT), NG = NT / QG, LOOK = NG < 2 ? NG : 2;
+    constexpr int QG = x6_qg(MTC, NT), NG = NT / QG, LOOK = NG < 2 ? NG : 2;
     auto read_b = [&](int g) {
 #pragma unroll
       for (int q = g * QG; q < (g + 1) * QG; ++q) {
@@ -393,9 +416,9 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       if constexpr (ABL == 1)
-        x6_group_chained<C::MT, NT, QG>(acc, av, bv, g * QG);
+        x6_group_chained<MTC, NT, QG>(acc, av, bv, g * QG);
       else
-        x6_group<C::MT, NT, QG>(acc, av, bv, g * QG);
+        x6_group<MTC, NT, QG>(acc, av, bv, g * QG);
       __builtin_amdgcn_sched_barrier(0);
       if (g + LOOK < NG) read_b(g + LOOK);
       __builtin_amdgcn_sched_barrier(0);
@@ -430,7 +453,13 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   }
   X6_WAITCNT_VM(0);  // the trailing re-load DMAs must land before the LDS is reused
   x6_barrier();
-  fwd_epilogue<NT, C::MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
+  if constexpr (SEL) {  // the pair image: OH/2 rows, row ty0/2 + wave, column tx0 + fragment row
+    FwdArgs ap = a;
+    ap.OH = a.OH / 2;
+    fwd_epilogue<NT, 1, C::PS, false>(ap, acc, reinterpret_cast<float*>(lds_raw), ty0 / 2, tx0, n);
+  } else {
+    fwd_epilogue<NT, C::MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -910,6 +939,17 @@ static hipError_t run_x6p(const FwdArgs& a, int nz, hipStream_t s) {
   return hipGetLastError();
 }
 
+hipError_t launch_fwd_x6_sel(const FwdArgs& a, hipStream_t s) {
+  using C = PCfg<6>;
+  if (x6_np(a.NOUT, a.zc) != 96 || a.zc || a.K % 32 || a.x6_tail || !a.sel_rd ||
+      a.out_layout != OUT_NHWC || a.epi != EPI_BIAS_ACT || (a.OH | a.OW) & 1 ||
+      ((a.in_stride | a.in_off) & 3) || (long)C::IH * a.IWt * a.in_stride * 4 >= 0x7fffffffL)
+    return hipErrorInvalidValue;
+  const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
+  hipLaunchKernelGGL((k_c3x6p<6, 0, 0, true>), dim3(tx * ty, a.N, 1), dim3(C::WAVES * 64), 0, s, a);
+  return hipGetLastError();
+}
+
 static int cu_count() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -1363,7 +1403,17 @@ __global__ __launch_bounds__(256, 2) void k_nin_head_x6(FwdArgs a, HeadArgs hd, 
       }
       t += __shfl_xor(t, 16);
       t += __shfl_xor(t, 32);
-      if (lg == 0 && ok) hd.y[(((long)n * hd.oc + o) * a.OH + gy) * a.OW + gx] = t + hd.bc[o];
+      if (lg == 0 && ok) {
+        if (hd.rd) {  // pair image pixel (gy, gx) -> pixel pair[rd][gx & 1] of cell (gy, gx / 2)
+          const int r = hd.rd[((long)n * a.OH + gy) * (a.OW / 2) + (gx >> 1)] & 7;
+          constexpr unsigned kPair = 0xB721ED84u;
+          const int k = (kPair >> (4 * r + 2 * (gx & 1))) & 3;
+          hd.y[(((long)n * hd.oc + o) * 2 * a.OH + 2 * gy + (k >> 1)) * a.OW + (gx & ~1) + (k & 1)] =
+              t + hd.bc[o];
+        } else {
+          hd.y[(((long)n * hd.oc + o) * a.OH + gy) * a.OW + gx] = t + hd.bc[o];
+        }
+      }
     }
   }
 }

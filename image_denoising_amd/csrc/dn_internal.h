@@ -56,6 +56,9 @@ struct FwdArgs {
   const float* mask; int mask_stride, mask_off;
   int zc;        // > 0: blockIdx.z selects output channels [z*zc, z*zc+zc) (wide layers)
   int x6_tail;   // split-bf16 kernels: packing of the last K chunk, x6_tail_mode(K) (0: plain)
+  // split-bf16 3x3 forward, "selected pixels" mode (launch_fwd_x6_sel): per 2x2 output cell the
+  // N2N pair choice rd (0..7, [N][OH/2][OW/2]); only the cell's two pair pixels are computed
+  const unsigned char* sel_rd;
 };
 
 // Fused output head (arch_unet.py:186-190, 253-257): the dec_conv1b kernel keeps its
@@ -67,6 +70,9 @@ struct HeadArgs {
   int oc;
   float* y;                           // [N, oc, H, W]
   float* d1b; float* na; float* nb;   // optional NHWC (stride 96) saves for the backward
+  // the input is a pair image (launch_fwd_x6_sel): output pixel (i, 2j + s) of the head goes to
+  // y's pixel pair[rd[n][i][j]][s] of cell (i, j), y itself [N, oc, 2 * OH, OW]
+  const unsigned char* rd;
 };
 // Backward of the head: g_nb = leaky'(nb) * (Wc^T dy), g_na = leaky'(na) * (Wb^T g_nb),
 // g_d1b = leaky'(d1b) * (Wa^T g_na) over npx pixels (all NHWC stride 96, dy stride dy_stride)
@@ -155,6 +161,10 @@ hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStr
 // bf16x6 nin head (conv_x6.hip): pre-split nin_a | nin_b images (2 x X6_HEAD_BF bf16)
 hipError_t launch_pack_head_x6(const float* wa, const float* wb, void* out, hipStream_t s);
 hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* wimg, hipStream_t s);
+// dec_conv1b-shaped 3x3 forward (K = NOUT = 96, EPI_BIAS_ACT) on the two N2N pair pixels of every
+// 2x2 cell only (a.sel_rd): output = the "pair image" [N][OH/2][OW][96] NHWC, column 2j + s = pixel
+// pair[rd][s] of cell j (s = 0, 1), i.e. exactly the pixels training_script.md:141-144 reads
+hipError_t launch_fwd_x6_sel(const FwdArgs& a, hipStream_t s);
 // bf16x6 ConvTranspose2d(96, 96, 2, 2) forward: four pre-split parity images (4 x X6_HEAD_BF bf16)
 bool deconv_x6_ok(const FwdArgs& a);
 hipError_t launch_pack_deconv_x6(const float* w, void* out, hipStream_t s);

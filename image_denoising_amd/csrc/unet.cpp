@@ -368,7 +368,7 @@ hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, 
 // forward: arch_unet.py:194-260 (non-blind-spot branch)
 // ------------------------------------------------------------------------------------
 dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
-                       hipStream_t s, int prec) {
+                       hipStream_t s, int prec, const uint8_t* sel_rd) {
   const bool bf16 = prec == DN_PREC_BF16, x6 = prec == DN_PREC_FP32_X6;
   // bf16x6 96-channel deconvs (k_deconv_x6); DN_X6_DECONV=0 keeps the fp32 kernel (A/B)
   static const bool x6_deconv = !getenv("DN_X6_DECONV") || atoi(getenv("DN_X6_DECONV")) != 0;
@@ -511,6 +511,28 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
                         V(p.nb, 96), OUT_NHWC, s));
     DN_TRY(dn::conv_forward(V(p.nb, 96), N, H(0), Wd(0), 96, Wt(NINC), Bs(NINC), p.OC, 1, 0,
                             View{y, p.OC, 0}, OUT_NCHW, s));
+    return DN_OK;
+  }
+  // N2N no-grad pass (training_script.md:141-144 reads den at the pair pixels only): dec_conv1b
+  // and the head on those pixels, through the [N, H/2, W, 96] pair image in d1b's storage
+  if (x6 && sel_rd && !p.with_bwd) {
+    FwdArgs a{};
+    a.in = ws + p.d1a; a.in_stride = 96; a.in_off = 0; a.IHt = H(0); a.IWt = Wd(0);
+    a.N = N; a.OH = H(0); a.OW = Wd(0); a.K = 96; a.NOUT = 96;
+    a.wp = ws + p.packX[D1B]; a.bias = Bs(D1B); a.epi = EPI_BIAS_ACT;
+    a.out = ws + p.d1b; a.out_stride = 96; a.out_off = 0; a.out_layout = OUT_NHWC;
+    a.sel_rd = sel_rd;
+    DN_TRY(launch_fwd_x6_sel(a, s));
+    DN_TRY(launch_pack_head_x6(prm + p.P.L[NINA].woff, prm + p.P.L[NINB].woff, ws + p.packH, s));
+    FwdArgs ah{};
+    ah.in = ws + p.d1b; ah.in_stride = 96; ah.in_off = 0; ah.IHt = H(0) / 2; ah.IWt = Wd(0);
+    ah.N = N; ah.OH = H(0) / 2; ah.OW = Wd(0); ah.K = 96; ah.NOUT = 96;
+    HeadArgs h{};
+    h.ba = Bs(NINA); h.bb = Bs(NINB);
+    h.wc = prm + p.P.L[NINC].woff; h.bc = Bs(NINC); h.oc = p.OC;
+    h.y = y;
+    h.rd = sel_rd;
+    DN_TRY(launch_nin_head_x6(ah, h, ws + p.packH, s));
     return DN_OK;
   }
   if (x6) {  // dec_conv1b on the bf16x6 kernel, then the fused nin_a -> nin_b -> nin_c head

@@ -66,8 +66,10 @@ bool build_params(const dn_unet_cfg& c, ParamLayout& P, std::string& err);
 bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, std::string& err);
 // prec: DN_PREC_FP32 (fp32 matrix cores), DN_PREC_FP32_X6 (3x3 layers on the bf16 matrix cores
 // by three-way operand splitting, fp32-accurate), DN_PREC_BF16 (forward only, bf16 operands)
+// sel_rd (nullable, DN_PREC_FP32_X6 and no backward only): dec_conv1b and the head run on the
+// two N2N pair pixels of every 2x2 cell only; y is written at those pixels and nowhere else
 dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
-                       hipStream_t s, int prec = DN_PREC_FP32);
+                       hipStream_t s, int prec = DN_PREC_FP32, const uint8_t* sel_rd = nullptr);
 // dx (nullable): dL/dx of the network input, NCHW [N, in_nc, H, W]
 dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* dx,
                         float* ws, hipStream_t s, int prec = DN_PREC_FP32);

@@ -86,8 +86,10 @@ class N2NTrainer:
             noisy = noisy.contiguous()
         sub1, sub2, rd = n2n_subsample(noisy, rd_idx, seed=self.seed + 1, offset=2 * step + 1,
                                        cell_base=cell_base)
-        # no-grad full-resolution pass (training_script.md:141-142)
-        self.net._run_forward(noisy, b["den"], b["ws_den"])
+        self.last_rd = rd  # the step's per-cell pair choices (den is defined at those pixels)
+        # no-grad full-resolution pass (training_script.md:141-142); the loss reads the denoised
+        # image at the rd pair pixels only, so only those are produced (dn_unet_forward_n2n)
+        self.net._run_forward_n2n(noisy, b["den"], b["ws_den"], rd)
         # gradient pass at half resolution (training_script.md:146)
         self.net._run_forward(sub1, b["out"], b["ws_grad"])
         loss3, dout = n2n_loss(b["out"], sub2, b["den"], rd, self.lambda_for(epoch))

@@ -79,6 +79,17 @@ dn_status dn_unet_workspace_size(const dn_unet_cfg* cfg, int N, int H, int W, in
    when ws was sized with with_backward=1. */
 dn_status dn_unet_forward(const dn_unet_cfg* cfg, const float* params, const float* x, float* y,
                           int N, int H, int W, void* ws, size_t ws_bytes, void* stream);
+/* The N2N step's no-grad pass (training_script.md:141-144): den = UNet(x) needed only at the
+   two pixels of every 2x2 cell that generate_subimages' mask1 / mask2 pick (train.py:141-190),
+   given by rd_idx (one byte per cell, [N][H/2][W/2], values 0..7 as for dn_n2n_subsample).  den
+   (NCHW [N,out_nc,H,W]) is written at exactly those pixels; the others are left untouched.  With
+   DN_PREC_FP32_X6 dec_conv1b and the head are evaluated on those pixels only (half their work;
+   per-pixel arithmetic unchanged, so den at the pair pixels is bit-identical to
+   dn_unet_forward_prec's); with DN_PREC_FP32 the whole image is computed.  Same workspace as
+   dn_unet_forward (with_backward = 0); saves nothing for a backward. */
+dn_status dn_unet_forward_n2n(const dn_unet_cfg* cfg, const float* params, const float* x,
+                              float* den, const uint8_t* rd_idx, int N, int H, int W, void* ws,
+                              size_t ws_bytes, int precision, void* stream);
 /* Mixed-precision inference forward (the frozen base of the adapter finetune, BASELINE
    configs[4]): every 3x3 layer multiplies bf16-rounded activations and weights on the bf16
    matrix cores with fp32 accumulation; bias, activations, 1x1 layers, deconvs and storage stay
