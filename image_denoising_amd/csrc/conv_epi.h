@@ -47,6 +47,19 @@ __device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, const f32x4 (&acc
   float* st = lds + wave * 16 * PS;
   const bool bias_epi = (a.epi == EPI_BIAS || a.epi == EPI_BIAS_ACT || a.epi == EPI_BIAS_ADD) &&
                         a.bias != nullptr;
+  // float4 path: every load of a row (staged tile, bias, mask / old output) is issued before its
+  // stores -- a load after a store would wait for that store's completion (in-order vmcnt), which
+  // serialised the epilogue on one L2 round trip per float4 (6 us per 16x16x96 tile)
+  constexpr int NIT = (16 * NP / 4 + 63) / 64;  // float4 items per lane per row
+  const int NQv = nout >> 2;
+  float4 bvec[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int e = lane + 64 * k;
+    bvec[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (vec_out && bias_epi && e < 16 * NQv)
+      bvec[k] = *reinterpret_cast<const float4*>(a.bias + cz + 4 * (e - (e / NQv) * NQv));
+  }
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
 #pragma unroll
@@ -57,42 +70,51 @@ __device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, const f32x4 (&acc
     // barrier (a __syncthreads here would also drain the previous row's global stores)
     const int gy = ty0 + wrow + m;
     if (gy < a.OH && vec_out) {
-      const int NQ = nout >> 2;
-      for (int e = lane; e < 16 * NQ; e += 64) {
+      const int NQ = NQv;
+      float4 vv[NIT], rr[NIT];
+      long oiv[NIT];
+      bool okv[NIT];
+#pragma unroll
+      for (int k = 0; k < NIT; ++k) {  // phase 1: loads
+        const int e = lane + 64 * k;
         const int p = e / NQ, c = 4 * (e - p * NQ);
         const int gx = tx0 + p;
-        if (gx >= a.OW) continue;
-        float4 v = *reinterpret_cast<const float4*>(st + p * PS + c);
+        okv[k] = e < 16 * NQ && gx < a.OW;
+        vv[k] = rr[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        oiv[k] = 0;
+        if (!okv[k]) continue;
+        vv[k] = *reinterpret_cast<const float4*>(st + p * PS + c);
         const long pix = ((long)n * a.OH + gy) * a.OW + gx;
+        if (a.out_layout == OUT_NHWC)
+          oiv[k] = pix * a.out_stride + a.out_off + cz + c;
+        else
+          oiv[k] = (((long)n * 2 * a.OH + 2 * gy + (ab >> 1)) * 2 * a.OW + 2 * gx + (ab & 1)) *
+                       a.out_stride + a.out_off + c;
+        if (aux)
+          rr[k] = *reinterpret_cast<const float4*>(a.mask + pix * a.mask_stride + a.mask_off + cz + c);
+        else if (a.epi == EPI_ACCUM)
+          rr[k] = *reinterpret_cast<const float4*>(a.out + oiv[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < NIT; ++k) {  // phase 2: arithmetic and stores
+        if (!okv[k]) continue;
+        float4 v = vv[k];
         if (bias_epi) {
-          const float4 b = *reinterpret_cast<const float4*>(a.bias + cz + c);
-          v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+          v.x += bvec[k].x; v.y += bvec[k].y; v.z += bvec[k].z; v.w += bvec[k].w;
         }
+        const float4 r = rr[k];
         if (a.epi == EPI_BIAS_ACT) {
           v.x = v.x > 0.f ? v.x : v.x * 0.2f; v.y = v.y > 0.f ? v.y : v.y * 0.2f;
           v.z = v.z > 0.f ? v.z : v.z * 0.2f; v.w = v.w > 0.f ? v.w : v.w * 0.2f;
-        } else if (aux) {
-          const float4 r =
-              *reinterpret_cast<const float4*>(a.mask + pix * a.mask_stride + a.mask_off + cz + c);
-          if (a.epi == EPI_BIAS_ADD) {
-            v.x = r.x + v.x; v.y = r.y + v.y; v.z = r.z + v.z; v.w = r.w + v.w;
-          } else {
-            v.x = r.x > 0.f ? v.x : v.x * 0.2f; v.y = r.y > 0.f ? v.y : v.y * 0.2f;
-            v.z = r.z > 0.f ? v.z : v.z * 0.2f; v.w = r.w > 0.f ? v.w : v.w * 0.2f;
-          }
+        } else if (a.epi == EPI_BIAS_ADD) {
+          v.x = r.x + v.x; v.y = r.y + v.y; v.z = r.z + v.z; v.w = r.w + v.w;
+        } else if (a.epi == EPI_MASK) {
+          v.x = r.x > 0.f ? v.x : v.x * 0.2f; v.y = r.y > 0.f ? v.y : v.y * 0.2f;
+          v.z = r.z > 0.f ? v.z : v.z * 0.2f; v.w = r.w > 0.f ? v.w : v.w * 0.2f;
+        } else if (a.epi == EPI_ACCUM) {
+          v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
         }
-        long oi;
-        if (a.out_layout == OUT_NHWC)
-          oi = pix * a.out_stride + a.out_off + cz + c;
-        else
-          oi = (((long)n * 2 * a.OH + 2 * gy + (ab >> 1)) * 2 * a.OW + 2 * gx + (ab & 1)) *
-                   a.out_stride + a.out_off + c;
-        float4* o = reinterpret_cast<float4*>(a.out + oi);
-        if (a.epi == EPI_ACCUM) {
-          const float4 old = *o;
-          v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
-        }
-        *o = v;
+        *reinterpret_cast<float4*>(a.out + oiv[k]) = v;
       }
     } else if (gy < a.OH) {
       for (int e = lane; e < 16 * nout; e += 64) {

@@ -214,7 +214,7 @@ __device__ __forceinline__ void x6_barrier() {
 // row 2j + s reads its A operand at the pixel pair[rd][s] of cell j): half the MFMAs, the same
 // staging, per-pixel arithmetic unchanged (bit-identical outputs); the epilogue writes the
 // fragment as row ty0/2 + wave of the [OH/2][OW] pair image.
-template <int NT, int TAIL, int ABL = 0, bool SEL = false>
+template <int NT, int TAIL, bool SEL = false>
 __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   using C = PCfg<NT>;
   static_assert(!SEL || TAIL == 0, "selected pixels: full 32-channel chunks only");
@@ -314,14 +314,15 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     }
   };
 
-  // prologue: x tile of chunk 0 split into LDS, chunk 1's x in registers, weight stages
-  // 0 .. S-2 in flight
+  // prologue: weight stages 0 .. S-2 requested first (L2-resident), then the x tile of chunk 0
+  // (HBM) split into LDS -- the two latencies overlap -- and chunk 1's x into registers, which
+  // is not waited for (the first two stages allow its loads in flight)
+#pragma unroll
+  for (int j = 0; j < C::S - 1; ++j) load_w(j < nst ? j : nst - 1, j);
   load_x(0);
   store_x();
   load_x((nch > 1 ? 1 : 0) * C::KC);
-#pragma unroll
-  for (int j = 0; j < C::S - 1; ++j) load_w(j < nst ? j : nst - 1, j);
-  X6_WAITCNT_VM(C::PPW * (C::S - 2));  // own DMAs of stage 0 landed
+  X6_WAITCNT_VM(C::XITEMS);            // own DMAs of stages 0 .. S-2 landed (older than x1)
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
   x6_barrier();
 
@@ -415,16 +416,13 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      if constexpr (ABL == 1)
-        x6_group_chained<MTC, NT, QG>(acc, av, bv, g * QG);
-      else
-        x6_group<MTC, NT, QG>(acc, av, bv, g * QG);
+      x6_group<MTC, NT, QG>(acc, av, bv, g * QG);
       __builtin_amdgcn_sched_barrier(0);
       if (g + LOOK < NG) read_b(g + LOOK);
       __builtin_amdgcn_sched_barrier(0);
     }
     const bool xstep = t == 8 && more;
-    if (xstep && ABL != 5) {
+    if (xstep) {
       x6_barrier();  // every wave is done with this chunk's x tile
       store_x();
       load_x((c + 2 < nch ? c + 2 : nch - 1) * C::KC);  // uniform count: re-load at the end
@@ -433,18 +431,19 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     // own DMAs of stage st+1 landed: issued after them are those of stages st+2, st+S-1 and the
     // next-but-one chunk's x loads when issued in this stage (xstep) or the previous one (a
     // chunk's first stage) -- the x loads are not waited for here
-    if (xstep || (t == 0 && c > 0)) X6_WAITCNT_VM(C::PPW * (C::S - 2) + C::XITEMS);
-    else X6_WAITCNT_VM(C::PPW * (C::S - 2));
+    // (stages 0 and 1: the prologue's chunk-1 x loads are younger than their DMAs)
+    if (xstep || (t == 0 && c > 0) || (c == 0 && t < 2))
+      X6_WAITCNT_VM(C::PPW * (C::S - 2) + C::XITEMS);
+    else
+      X6_WAITCNT_VM(C::PPW * (C::S - 2));
     if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
-    if (ABL != 2 || xstep) x6_barrier();
+    x6_barrier();
   };
   // TAIL: the instantiation's last-chunk packing (the host passes a.x6_tail == TAIL)
-  int rep = 0;
   for (int c = 0; c < nch; ++c) {
     if constexpr (TAIL == 0) {
 #pragma unroll 1
       for (int t = 0; t < 9; ++t) stage(std::integral_constant<int, 0>{}, c, t);
-      if (ABL == 4 && c + 1 == nch && rep == 0) { c = -1; rep = 1; }  // probe: 2 tiles per WG
     } else {
       const int ns = c + 1 < nch ? 9 : tail_st;
 #pragma unroll 1
@@ -463,94 +462,74 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
-// Persistent variant of k_c3x6p for large grids (k_c3x6q): one workgroup per CU walks the tiles
-// blockIdx.x, blockIdx.x + gridDim.x, ... and its x-tile chunk pipeline and weight-stage DMA
-// ring run on across tile boundaries (the next tile's first chunk is simply the next chunk;
-// stage g of the walk is stage g % nst of tile g / nst), so a tile costs no prologue (HBM
-// latency of its first x tile and weight stages), no pipeline drain and no workgroup launch.
-// The MFMA operands are swapped (A = weights, B = pixels): a lane's accumulator then holds 4
-// consecutive output channels of one pixel, and the epilogue stores them as float4 straight
-// from registers through a buffer resource (out-of-tile pixels get an out-of-range offset), so
-// every wave issues the same number of stores per tile and the vmcnt counts stay constants.
-// The bias of all output channels sits in LDS.  Output: NHWC, float4-aligned views.
+// Two-workgroups-per-CU variant for large grids (k_c3x6h): 4 waves on an 8 x 16 x 16*NT tile
+// (wave w: rows 2w, 2w+1), 70 KB of LDS (the x tile's three planes + a 2-slot ring of unpadded
+// 18 KiB weight stages), so two workgroups share a CU and one's prologue (x tile from HBM) and
+// epilogue overlap the other's main loop -- the per-tile cost the one-workgroup-per-CU kernel
+// pays in series (k_c3x6p: ~4 us prologue + ~3 us epilogue per 16-row tile).  Stage st+1's
+// weights are DMA'd at the start of stage st (5 x 1 KiB per wave; the 18 pieces of a stage are
+// spread over the 4 waves, the two short waves re-load one of theirs, so every wave waits on a
+// constant count); the next chunk's x tile is loaded into registers at the start of a chunk,
+// after that stage's DMA, and split into LDS at its end.  Stage reads and MFMAs as k_c3x6p.
 // ------------------------------------------------------------------------------------
-__device__ unsigned long long dn_x6q_times[4096];  // PROBE: per-workgroup start / end clocks
-__device__ int dn_x6q_probe;
+template <int NT>
+struct HCfg {
+  static constexpr int WAVES = 4, MT = 2, S = 2;
+  static constexpr int TW = 16, TH = WAVES * MT, IH = TH + 2, IW = TW + 2, KC = 32, NP = 16 * NT;
+  static constexpr int XPIX = IH * IW;
+  static constexpr int XPL = XPIX * KC;
+  static constexpr int WPL = NP * KC;
+  static constexpr int WST = 3 * WPL;                 // bf16 per stage (unpadded)
+  static constexpr int WSTP = x6_wst(NP);             // stage stride of the packed image
+  static constexpr int PIECES = WST * 2 / 1024;       // 1 KiB DMA pieces per stage
+  static constexpr int PPW = (PIECES + WAVES - 1) / WAVES;
+  static_assert(PIECES * 1024 == WST * 2, "stage = whole KiB pieces");
+  static constexpr int XQ = XPIX * (KC / 4);
+  static constexpr int XITEMS = (XQ + WAVES * 64 - 1) / (WAVES * 64);
+  static constexpr int PS = NP + 4;
+  static constexpr int LBYTES_MAIN = 2 * 3 * XPL + 2 * S * WST;
+  static constexpr int LEPI = 4 * WAVES * 16 * PS;
+  static constexpr int LBYTES = LBYTES_MAIN > LEPI ? LBYTES_MAIN : LEPI;
+  static_assert(2 * LBYTES <= 163840, "two workgroups per CU");
+};
 
 template <int NT, int TAIL>
-__global__ __launch_bounds__(512, 1) void k_c3x6q(FwdArgs a) {
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  using C = PCfg<NT>;
+__global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
+  using C = HCfg<NT>;
   constexpr int MT = C::MT;
-  // ONE LDS object (a second __shared__ array makes the compiler wait for every LDS DMA before
-  // each LDS read): the bias lives past the main loop's bytes
-  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[163840];
-  float* lbias = reinterpret_cast<float*>(lds_raw + C::LBYTES_MAIN);
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
   __bf16* lx = reinterpret_cast<__bf16*>(lds_raw);
   __bf16* ring = lx + 3 * C::XPL;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int li = lane & 15, lg = lane >> 4;
-  const int tiles_x = (a.OW + C::TW - 1) / C::TW, tiles_y = (a.OH + C::TH - 1) / C::TH;
-  const int per_img = tiles_x * tiles_y;
-  const int nz = a.zc ? (a.NOUT + a.zc - 1) / a.zc : 1;
-  const int ntiles = per_img * a.N * nz;
-  const int G = gridDim.x;
-  const int my_n = (ntiles - (int)blockIdx.x + G - 1) / G;  // >= 1: the grid is <= ntiles
+  const int tiles_x = (a.OW + C::TW - 1) / C::TW;
+  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
+  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
+  const int n = blockIdx.y;
+  const int iy0 = ty0 - 1, ix0 = tx0 - 1;
+  const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
+  const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp) + (long)blockIdx.z * a.wp_z;
   const int nch = (a.K + C::KC - 1) / C::KC;
   constexpr int tail = TAIL;
   constexpr int tail_st = tail == 1 ? 2 : 5;
   const int nst = 9 * nch - (tail ? 9 - tail_st : 0);
-  const bool has_bias = (a.epi == EPI_BIAS || a.epi == EPI_BIAS_ACT) && a.bias != nullptr;
-  if (has_bias)
-    for (int e = tid; e < a.NOUT; e += C::WAVES * 64) lbias[e] = a.bias[e];
 
-  // tile ordinal i of this workgroup -> (output-channel block z, image n, tile origin)
-  struct Tile { int z, n, ty0, tx0; };
-  auto tile = [&](int i) {
-    const int T = (int)blockIdx.x + i * G;
-    Tile r;
-    r.z = T / (a.N * per_img);
-    const int rem = T - r.z * a.N * per_img;
-    r.n = rem / per_img;
-    const int p = rem - r.n * per_img;
-    r.ty0 = (p / tiles_x) * C::TH;
-    r.tx0 = (p % tiles_x) * C::TW;
-    return r;
-  };
-
-  f32x4 acc[MT][NT], ph[MT], pl[MT];  // ph / pl: the last group's fresh sums, added later
+  f32x4 acc[MT][NT];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    ph[m] = pl[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int q = 0; q < NT; ++q) acc[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
 
-  // x chunk j of the walk (tile j / nch, channels 32 * (j % nch)); past the end: a harmless
-  // re-load of the last chunk, so every thread issues exactly XITEMS buffer loads per call.
-  // The resource covers the tile's input rows only (32-bit extents, see k_c3x6p).
+  // input rows of this tile through a 32-bit buffer resource (see k_c3x6p)
+  const int ry0 = iy0 > 0 ? iy0 : 0, ry1 = iy0 + C::IH < a.IHt ? iy0 + C::IH : a.IHt;
+  const long row_floats = (long)a.IWt * a.in_stride;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(inb + ry0 * row_floats), (short)0, (int)((ry1 - ry0) * row_floats * 4),
+      0x00020000);
   f32x4 xr[C::XITEMS];
-  // the walk's chunks and weight stages are requested strictly in order: incremental cursors
-  // (a tile's origin is decoded once per tile, not per request)
-  int xi = 0, xc = 0;
-  Tile xT = tile(0);
-  auto load_x = [&]() {  // the next chunk of the walk
-    const bool past = xi >= my_n;
-    const int k0 = (past ? nch - 1 : xc) * C::KC;
-    const Tile T = xT;
-    if (++xc == nch) {
-      xc = 0;
-      if (++xi < my_n) xT = tile(xi);
-    }
-    const int iy0 = T.ty0 - 1, ix0 = T.tx0 - 1;
-    const int ry0 = iy0 > 0 ? iy0 : 0, ry1 = iy0 + C::IH < a.IHt ? iy0 + C::IH : a.IHt;
-    const long row_floats = (long)a.IWt * a.in_stride;
-    const float* inb = a.in + (long)T.n * a.IHt * row_floats + a.in_off;
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(inb + ry0 * row_floats), (short)0, (int)((ry1 - ry0) * row_floats * 4),
-        0x00020000);
+  auto load_x = [&](int k0) {
 #pragma unroll
     for (int it = 0; it < C::XITEMS; ++it) {
       const int e = tid + it * C::WAVES * 64;
@@ -583,90 +562,38 @@ __global__ __launch_bounds__(512, 1) void k_c3x6q(FwdArgs a) {
       }
     }
   };
-  // weights of the next walk stage into the next ring slot (past the end: re-loads of the last)
-  int wi = 0, wst = 0, wslot = 0;
-  const __bf16* wcur = reinterpret_cast<const __bf16*>(a.wp) + (long)tile(0).z * a.wp_z;
-  auto load_w = [&]() {
-    const unsigned char* src =
-        reinterpret_cast<const unsigned char*>(wcur + (long)(wi < my_n ? wst : nst - 1) * C::WSTP);
-    unsigned char* dst = reinterpret_cast<unsigned char*>(ring + wslot * C::WSTP);
-    wslot = (wslot + 1) % C::S;
-    if (++wst == nst) {
-      wst = 0;
-      if (++wi < my_n) wcur = reinterpret_cast<const __bf16*>(a.wp) + (long)tile(wi).z * a.wp_z;
-    }
+  // stage src_st's 18 pieces into slot `slot`: wave w copies pieces w, w+4, ...; a wave with
+  // fewer than PPW repeats its last piece (same bytes, same place) so every wave issues PPW
+  auto load_w = [&](int src_st, int slot) {
+    const unsigned char* src = reinterpret_cast<const unsigned char*>(wimg + (long)src_st * C::WSTP);
+    unsigned char* dst = reinterpret_cast<unsigned char*>(ring + slot * C::WST);
 #pragma unroll
     for (int j = 0; j < C::PPW; ++j) {
-      const int piece = wave * C::PPW + j;
+      int piece = wave + j * C::WAVES;
+      if (piece >= C::PIECES) piece -= C::WAVES;
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(src + piece * 1024 + lane * 16),
           (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16, 0, 0);
     }
   };
-  // tile i's outputs: acc[m][q] = channels 16q + 4lg .. +3 of pixel (row wave*MT + m, col li);
-  // MT*NT buffer stores per wave whatever the tile's extent
-  constexpr int NSTORE = MT * NT;
-  auto epilogue = [&](int i) {
-    const Tile T = tile(i);
-    const int cz = a.zc ? T.z * a.zc : 0;
-    const int nout = a.zc ? min(16 * NT, a.NOUT - cz) : a.NOUT;
-    const int r0 = T.ty0, r1 = T.ty0 + C::TH < a.OH ? T.ty0 + C::TH : a.OH;
-    const long orow = (long)a.OW * a.out_stride;
-    float* ob = a.out + ((long)T.n * a.OH + r0) * orow;
-    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
-        ob, (short)0, (int)((r1 - r0) * orow * 4), 0x00020000);
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const int gy = T.ty0 + wave * MT + m, gx = T.tx0 + li;
-      const bool pix_ok = gy < a.OH && gx < a.OW;
-      const long pix = ((long)T.n * a.OH + gy) * a.OW + gx;
-#pragma unroll
-      for (int q = 0; q < NT; ++q) {
-        const int c = 16 * q + 4 * lg;
-        const bool ok = pix_ok && c < nout;
-        f32x4 v = acc[m][q];
-        if (has_bias) {
-          const f32x4 b = *reinterpret_cast<const f32x4*>(lbias + cz + c);
-          v += b;
-        }
-        if (a.epi == EPI_BIAS_ACT) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * 0.2f;
-        } else if (ok && (a.epi == EPI_MASK || a.epi == EPI_ACCUM)) {
-          const float* src = a.epi == EPI_MASK ? a.mask + pix * a.mask_stride + a.mask_off + cz + c
-                                               : a.out + pix * a.out_stride + a.out_off + cz + c;
-          const f32x4 r = *reinterpret_cast<const f32x4*>(src);
-          if (a.epi == EPI_MASK) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = r[k] > 0.f ? v[k] : v[k] * 0.2f;
-          } else {
-            v = r + v;
-          }
-        }
-        const int off = ok ? (int)((((gy - r0) * (long)a.OW + gx) * a.out_stride + a.out_off + cz + c) * 4)
-                           : 0x7fffffff;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), ors, off, 0, 0);
-        acc[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  };
 
-  // prologue: chunk 0's x tile split into LDS, chunk 1's in registers, weight stages 0..S-2
-  load_x();
-  store_x();
-  load_x();
-#pragma unroll
-  for (int j = 0; j < C::S - 1; ++j) load_w();
-  X6_WAITCNT_VM(C::PPW * (C::S - 2));  // own DMAs of stage 0 landed
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile and bias stores done
+  // prologue: stage 0's weights (L2) and chunk 0's x tile (HBM) in flight together
+  load_w(0, 0);
+  load_x(0);
+  store_x();                           // waits for the x loads (and the older DMA)
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
   x6_barrier();
 
-  // walk stage g = i * nst + st (tile ordinal i, chunk c, tap t); see k_c3x6p for the ring
-  auto stage = [&](int i, int c, int t, int g) {
-    const __bf16* lw = ring + (g % C::S) * C::WSTP;
-    const bool last_chunk = c + 1 == nch;
-    const int mode = (tail && last_chunk) ? tail : 0;
+  auto stage = [&](int c, int t) {
+    const bool more = c + 1 < nch;
+    const int st = 9 * c + t;
+    const __bf16* lw = ring + (st & 1) * C::WST;
+    // stage st+1's weights into the other slot (every wave left it at the last barrier); past
+    // the end a re-load of the last stage
+    load_w(st + 1 < nst ? st + 1 : nst - 1, (st + 1) & 1);
+    if (t == 0 && more) load_x((c + 1) * C::KC);  // the next chunk, after this stage's DMA
     bf16x8 av[3][MT], bv[3][NT];
+    const int mode = (tail && c + 1 == nch) ? tail : 0;
     if (mode == 1) {
       const int ta = 8 * t + 2 * lg, tb = ta + 1;
       const int ca = ta < 9 ? ta : 8, cb = tb < 9 ? tb : 8;
@@ -712,100 +639,59 @@ __global__ __launch_bounds__(512, 1) void k_c3x6q(FwdArgs a) {
           av[p][m] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
       }
     }
-    // One output-channel fragment q per group: its 2*MT-chain of six products (fresh hi / lo
-    // sums) interleaved with the VALU adds of the PREVIOUS group (pending in ph / pl, the last
-    // group of a stage into the next stage), so no add waits on the MFMA that feeds it; the
-    // weight fragments are read two groups ahead.
-    auto read_b = [&](int q) {
-      const int row = q * 16 + li;
-      const int off = row * C::KC + x6_swz(row, lg) * 8;
+    constexpr int QG = x6_qg(MT, NT), NG = NT / QG, LOOK = NG < 2 ? NG : 2;
+    auto read_b = [&](int g) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
-        bv[p][q] = *reinterpret_cast<const bf16x8*>(lw + p * C::WPL + off);
+      for (int q = g * QG; q < (g + 1) * QG; ++q) {
+        const int row = q * 16 + li;
+        const int off = row * C::KC + x6_swz(row, lg) * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bv[p][q] = *reinterpret_cast<const bf16x8*>(lw + p * C::WPL + off);
+      }
     };
-    read_b(0);
-    if (NT > 1) read_b(1);
+#pragma unroll
+    for (int g = 0; g < LOOK; ++g) read_b(g);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int q = 0; q < NT; ++q) {
-      if (q + 2 < NT) read_b(q + 2);
-      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      constexpr int PA[4] = {1, 0, 1, 2}, PB[4] = {0, 2, 1, 0};
-      f32x4 h[MT], l[MT];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) h[m] = mfma_bf16(bv[0][q], av[0][m], z);
-#pragma unroll
-      for (int m = 0; m < MT; ++m) l[m] = mfma_bf16(bv[1][q], av[0][m], z);
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-        for (int m = 0; m < MT; ++m) l[m] = mfma_bf16(bv[PB[jj]][q], av[PA[jj]][m], l[m]);
-      const int qp = q == 0 ? NT - 1 : q - 1;
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        acc[m][qp] += ph[m] + pl[m];
-        ph[m] = h[m];
-        pl[m] = l[m];
-      }
-      // schedule: the 3 reads two groups ahead, then MFMAs with the pending adds between them
-      if (q + 2 < NT) {
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-#pragma unroll
-      for (int r = 0; r < 4 * MT / 2; ++r) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+    for (int g = 0; g < NG; ++g) {
+      x6_group<MT, NT, QG>(acc, av, bv, g * QG);
+      __builtin_amdgcn_sched_barrier(0);
+      if (g + LOOK < NG) read_b(g + LOOK);
       __builtin_amdgcn_sched_barrier(0);
     }
-    const int ns = (tail && last_chunk) ? tail_st : 9;
-    const bool xstep = t == ns - 1;  // the walk always has a next chunk (re-loads past its end)
-    const bool tile_end = last_chunk && xstep;
+    const int ns = (tail && c + 1 == nch) ? tail_st : 9;
+    const bool xstep = t == ns - 1 && more;
     if (xstep) {
       x6_barrier();  // every wave is done with this chunk's x tile
-      store_x();     // (waits for its registers: issued a chunk ago)
+      store_x();
     }
-    // after the split, so the x-register wait never covers the epilogue's stores
-    if (tile_end) {  // the pending last group, then the outputs (registers and global memory)
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        acc[m][NT - 1] += ph[m] + pl[m];
-        ph[m] = pl[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      epilogue(i);
-    }
-    if (xstep) load_x();  // chunk j + 2 of the walk
-    load_w();  // stage g + S - 1
-    // own DMAs of stage g+1 landed: younger are those of stages g+2, g+S-1, the x loads of an
-    // xstep in this or the previous stage, and the epilogue's stores of this or the previous
-    // stage (all issued after stage g+1's DMAs)
-    const int younger = C::PPW * (C::S - 2) + (xstep || (t == 0 && g > 0) ? C::XITEMS : 0) +
-                        (tile_end || (t == 0 && c == 0 && i > 0) ? NSTORE : 0);
-    if (younger == C::PPW * (C::S - 2)) X6_WAITCNT_VM(C::PPW * (C::S - 2));
-    else if (younger == C::PPW * (C::S - 2) + C::XITEMS) X6_WAITCNT_VM(C::PPW * (C::S - 2) + C::XITEMS);
-    else X6_WAITCNT_VM(C::PPW * (C::S - 2) + C::XITEMS + NSTORE);
+    // own DMAs of stage st+1 landed; younger: this stage's x loads (chunk start)
+    if (t == 0 && more) X6_WAITCNT_VM(C::XITEMS);
+    else X6_WAITCNT_VM(0);
     if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
     x6_barrier();
   };
-  int g = 0;
-  for (int i = 0; i < my_n; ++i)
-    for (int c = 0; c < nch; ++c) {
-      const int ns = (tail && c + 1 == nch) ? tail_st : 9;
+  for (int c = 0; c < nch; ++c) {
+    const int ns = (tail && c + 1 == nch) ? tail_st : 9;
 #pragma unroll 1
-      for (int t = 0; t < ns; ++t, ++g) stage(i, c, t, g);
-    }
-  X6_WAITCNT_VM(0);  // trailing re-load DMAs and the last stores
-  if (dn_x6q_probe && (threadIdx.x & 511) == 0 && blockIdx.x < 2048) {
-    volatile unsigned long long* tp = dn_x6q_times + 2 * blockIdx.x + (threadIdx.x >> 9);
-    tp[0] = t_start;
-    tp[1] = __builtin_amdgcn_s_memrealtime();
+    for (int t = 0; t < ns; ++t) stage(c, t);
   }
+  fwd_epilogue<NT, MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
+}
+
+template <int NT>
+static hipError_t run_x6h(const FwdArgs& a, int nz, hipStream_t s) {
+  using C = HCfg<NT>;
+  const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
+  const dim3 grid(tx * ty, a.N, nz), block(C::WAVES * 64);
+  if (a.x6_tail == 1)
+    hipLaunchKernelGGL((k_c3x6h<NT, 1>), grid, block, 0, s, a);
+  else if (a.x6_tail == 2)
+    hipLaunchKernelGGL((k_c3x6h<NT, 2>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((k_c3x6h<NT, 0>), grid, block, 0, s, a);
+  return hipGetLastError();
 }
 
 // Pre-split weight image, one per output-channel block z: [chunk][tap][piece][n < NP][32 k],
@@ -923,19 +809,8 @@ static hipError_t run_x6p(const FwdArgs& a, int nz, hipStream_t s) {
     hipLaunchKernelGGL((k_c3x6p<NT, 1>), grid, block, 0, s, a);
   else if (a.x6_tail == 2)
     hipLaunchKernelGGL((k_c3x6p<NT, 2>), grid, block, 0, s, a);
-  else {
-    static const int abl = getenv("DN_X6_ABL") ? atoi(getenv("DN_X6_ABL")) : 0;  // timing probes
-    if (abl == 1)
-      hipLaunchKernelGGL((k_c3x6p<NT, 0, 1>), grid, block, 0, s, a);
-    else if (abl == 2)
-      hipLaunchKernelGGL((k_c3x6p<NT, 0, 2>), grid, block, 0, s, a);
-    else if (abl == 4)
-      hipLaunchKernelGGL((k_c3x6p<NT, 0, 4>), dim3(grid.x, grid.y / 2, grid.z), block, 0, s, a);
-    else if (abl == 5)
-      hipLaunchKernelGGL((k_c3x6p<NT, 0, 5>), grid, block, 0, s, a);
-    else
-      hipLaunchKernelGGL((k_c3x6p<NT, 0>), grid, block, 0, s, a);
-  }
+  else
+    hipLaunchKernelGGL((k_c3x6p<NT, 0>), grid, block, 0, s, a);
   return hipGetLastError();
 }
 
@@ -946,65 +821,7 @@ hipError_t launch_fwd_x6_sel(const FwdArgs& a, hipStream_t s) {
       ((a.in_stride | a.in_off) & 3) || (long)C::IH * a.IWt * a.in_stride * 4 >= 0x7fffffffL)
     return hipErrorInvalidValue;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
-  hipLaunchKernelGGL((k_c3x6p<6, 0, 0, true>), dim3(tx * ty, a.N, 1), dim3(C::WAVES * 64), 0, s, a);
-  return hipGetLastError();
-}
-
-static int cu_count() {
-  static int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1)
-      v = 256;
-    return v;
-  }();
-  return n;
-}
-
-// PROBE: DN_X6_TIMES=1 prints the spread of the persistent kernel's workgroup end times
-static void x6q_times_report(int grid) {
-  unsigned long long t[4096];
-  hipDeviceSynchronize();
-  if (hipMemcpyFromSymbol(t, HIP_SYMBOL(dn_x6q_times), sizeof(unsigned long long) * 2 * grid) !=
-      hipSuccess)
-    return;
-  unsigned long long t0 = ~0ull, e_min = ~0ull, e_max = 0;
-  double e_sum = 0;
-  for (int b = 0; b < grid; ++b) {
-    t0 = t[2 * b] < t0 ? t[2 * b] : t0;
-  }
-  for (int b = 0; b < grid; ++b) {
-    const unsigned long long e = t[2 * b + 1] - t0;
-    e_min = e < e_min ? e : e_min;
-    e_max = e > e_max ? e : e_max;
-    e_sum += (double)e;
-  }
-  fprintf(stderr, "x6q end times (us since first start): min %.1f mean %.1f max %.1f\n",
-          e_min / 100.0, e_sum / grid / 100.0, e_max / 100.0);
-}
-
-// the persistent kernel: one workgroup per CU (at most one per tile)
-template <int NT>
-static hipError_t run_x6q(const FwdArgs& a, int nz, hipStream_t s) {
-  using C = PCfg<NT>;
-  const long ntiles = (long)((a.OW + C::TW - 1) / C::TW) * ((a.OH + C::TH - 1) / C::TH) * a.N * nz;
-  const int grid = (int)(ntiles < cu_count() ? ntiles : cu_count());
-  if (a.x6_tail == 1)
-    hipLaunchKernelGGL((k_c3x6q<NT, 1>), dim3(grid), dim3(C::WAVES * 64), 0, s, a);
-  else if (a.x6_tail == 2)
-    hipLaunchKernelGGL((k_c3x6q<NT, 2>), dim3(grid), dim3(C::WAVES * 64), 0, s, a);
-  else
-    hipLaunchKernelGGL((k_c3x6q<NT, 0>), dim3(grid), dim3(C::WAVES * 64), 0, s, a);
-  static const bool probe = getenv("DN_X6_TIMES") != nullptr;
-  if (probe) {
-    static int n = 0;
-    if (n++ == 0) {
-      int one = 1;
-      hipMemcpyToSymbol(HIP_SYMBOL(dn_x6q_probe), &one, sizeof(int));
-    } else {
-      x6q_times_report(grid);
-    }
-  }
+  hipLaunchKernelGGL((k_c3x6p<6, 0, true>), dim3(tx * ty, a.N, 1), dim3(C::WAVES * 64), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1027,20 +844,16 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
   auto pipe = [&]() {
     return np == 32 ? run_x6p<2>(a, nz, s) : (np == 48 ? run_x6p<3>(a, nz, s) : run_x6p<6>(a, nz, s));
   };
-  // the persistent kernel: NHWC float4 outputs (its epilogue stores from registers), the bias
-  // in the LDS left over by the main loop, 32-bit extents of one tile's 16 output rows
-  // opt-in while it measures slower than the per-tile kernel
-  static const bool no_persist = !(getenv("DN_X6_PERSIST") && atoi(getenv("DN_X6_PERSIST")) != 0);
-  const bool aux = a.epi == EPI_MASK;
-  const bool persist =
-      !no_persist && a.out_layout == OUT_NHWC && a.epi != EPI_BIAS_ADD &&
-      ((a.out_stride | a.out_off | a.NOUT) & 3) == 0 &&
-      (!aux || ((a.mask_stride | a.mask_off) & 3) == 0) &&
-      (long)PCfg<6>::TH * a.OW * a.out_stride * 4 < 0x7fffffffL &&
-      a.NOUT * 4 <= 163840 - PCfg<6>::LBYTES_MAIN;
+  // large grids: the two-workgroups-per-CU kernel where it measured faster (48 / 32 output
+  // channels: -6..-11 %; a 4-channel tail chunk: -3.6 %), else the one-per-CU kernel (equal
+  // within noise on the 96-channel shapes; tools/x6_micro.py); DN_X6_HALF=0/1 forces either
+  static const int half_env = getenv("DN_X6_HALF") ? atoi(getenv("DN_X6_HALF")) : -1;
+  const bool half_fits = (long)HCfg<6>::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL;
+  const bool half = half_fits && (half_env >= 0 ? half_env != 0 : (np <= 48 || a.x6_tail == 1));
   auto run = [&]() {
-    if (!persist) return pipe();
-    return np == 32 ? run_x6q<2>(a, nz, s) : (np == 48 ? run_x6q<3>(a, nz, s) : run_x6q<6>(a, nz, s));
+    if (half)
+      return np == 32 ? run_x6h<2>(a, nz, s) : (np == 48 ? run_x6h<3>(a, nz, s) : run_x6h<6>(a, nz, s));
+    return pipe();
   };
   if (a.x6_tail) {  // tail-packed last chunk: only the pipelined kernels read it
     if (!aligned || a.x6_tail != x6_tail_mode(a.K)) return hipErrorInvalidValue;

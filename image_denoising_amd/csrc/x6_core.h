@@ -96,50 +96,6 @@ __device__ __forceinline__ void x6_group(f32x4 (&acc)[MT][NT], const bf16x8 (&av
     for (int g = 0; g < QG; ++g) acc[m][q0 + g] += hi[m][g] + lo[m][g];
 }
 
-// x6_group with the operands' roles swapped (A = bv, B = av): the accumulator is the transposed
-// tile, acc[m][q] lane (li, lg) = rows 4lg..4lg+3 of bv's fragment q by column li of av's m
-template <int MT, int NT, int QG>
-__device__ __forceinline__ void x6_group_t(f32x4 (&acc)[MT][NT], const bf16x8 (&av)[3][MT],
-                                           const bf16x8 (&bv)[3][NT], int q0) {
-  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-  constexpr int PA[4] = {1, 0, 1, 2}, PB[4] = {0, 2, 1, 0};
-  f32x4 hi[MT][QG], lo[MT][QG];
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int g = 0; g < QG; ++g) hi[m][g] = mfma_bf16(bv[0][q0 + g], av[0][m], z);
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int g = 0; g < QG; ++g) lo[m][g] = mfma_bf16(bv[1][q0 + g], av[0][m], z);
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int g = 0; g < QG; ++g)
-        lo[m][g] = mfma_bf16(bv[PB[j]][q0 + g], av[PA[j]][m], lo[m][g]);
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int g = 0; g < QG; ++g) acc[m][q0 + g] += hi[m][g] + lo[m][g];
-}
-
-// ABLATION PROBE (timing experiments only, not fp32-accurate): all six products chained
-// straight into acc (no fresh block sums, no VALU adds)
-template <int MT, int NT, int QG>
-__device__ __forceinline__ void x6_group_chained(f32x4 (&acc)[MT][NT], const bf16x8 (&av)[3][MT],
-                                                 const bf16x8 (&bv)[3][NT], int q0) {
-  constexpr int PA[6] = {0, 0, 1, 0, 1, 2}, PB[6] = {0, 1, 0, 2, 1, 0};
-#pragma unroll
-  for (int j = 0; j < 6; ++j)
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int g = 0; g < QG; ++g)
-        acc[m][q0 + g] = mfma_bf16(av[PA[j]][m], bv[PB[j]][q0 + g], acc[m][q0 + g]);
-}
-
 template <int MT, int NT, int QG>
 __device__ __forceinline__ void x6_block(f32x4 (&acc)[MT][NT], const bf16x8 (&av)[3][MT],
                                          const bf16x8 (&bv)[3][NT]) {

@@ -152,7 +152,11 @@ def _cpu_stand_ins(net, tr):
                                          net.out_nc)
         dflat.copy_(g)
 
+    def run_forward_n2n(x, den, ws, rd_idx):  # the full image (a superset of the pair pixels)
+        run_forward(x, den, ws)
+
     net._run_forward, net._run_backward = run_forward, run_backward
+    net._run_forward_n2n = run_forward_n2n
 
     def subsample(img, rd_idx=None, seed=0, offset=0, cell_base=0):
         s1, s2 = n2n_ref.subimages_closed_form(img.numpy(), rd_idx.numpy())
