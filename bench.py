@@ -398,8 +398,12 @@ def main():
             step_flops = bs * (fwd_flops(H, H, C) + 3 * 864.0 * C * H * H)
         else:  # two fwd/bwd at full resolution
             step_flops = bs * 2 * 3 * fwd_flops(H, H, C)
-        traffic, traffic_src = (pmc_traffic("x6" if x6 else "") if (bs, H, C, iu, bf) == (64, 256, 1, False, False)
-                                else (None, None))
+        if (bs, H, C, iu, bf) == (64, 256, 1, False, False):
+            traffic, traffic_src = pmc_traffic("x6" if x6 else "")
+        elif bf and (bs, H, C, iu) == (16, 512, 1, False):
+            traffic, traffic_src = pmc_traffic("bf16")
+        else:
+            traffic, traffic_src = None, None
         model = "ImprovedUNet(n_feature=48)" if iu else "UNet(n_feature=48)"
         if iu and not ft:
             workload = (f"{args.mode} step with arch_unet.ImprovedUNet(n_feature=48, depth=4, noise=True) "

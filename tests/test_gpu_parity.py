@@ -599,6 +599,33 @@ def test_config1_full_size_step_properties(prec):
     assert torch.isfinite(tr.grad).all()
 
 
+@pytest.mark.parametrize("prec", PRECS)
+def test_config3_full_size_rgb_step_properties(prec):
+    """BASELINE configs[3] at full size: 32 x 3 x 256^2 RGB patches, one N2N step.  Images are
+    independent: image 0's denoised output at the pair pixels (all the step reads) is checked
+    against the oracle at full resolution."""
+    from image_denoising_amd import N2NTrainer
+    from oracle import unet_ref
+
+    net = _net(3, prec)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    clean = F.interpolate(torch.rand(32, 3, 32, 32, generator=g), size=(256, 256),
+                          mode="bilinear", align_corners=False).to(DEV)
+    tr = N2NTrainer(net, seed=1)
+    flat0 = net.flat_params.detach().cpu().clone()
+    loss3 = tr.train_step(clean, epoch=1)
+    torch.cuda.synchronize()
+    l = loss3.cpu().numpy()
+    assert np.isfinite(l).all() and l[0] > 0
+    assert bool(torch.isfinite(tr.grad).all()) and float(tr.grad.abs().max()) > 0
+    b = tr._bufs[next(iter(tr._bufs))]
+    den0, noisy0 = b["den"][:1].cpu(), b["noisy"][:1].cpu()
+    with torch.no_grad():
+        ref = unet_ref.forward(flat0, noisy0, 3, 3)
+    sel = np.broadcast_to(_pair_mask(tr.last_rd[:128 * 128].cpu(), 1, 256, 256), (1, 3, 256, 256))
+    assert rel_err(den0.numpy()[sel], ref.numpy()[sel]) < FP32_TOL
+
+
 @pytest.mark.parametrize("C", [1, 3])
 def test_structure_step_vs_oracle(C):
     """train.py:355-368 (Structure_loss step: two grad forwards, one backward, Adam) through

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc/$c -o run \
+  timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc/$c -o run \
     -- python3 tools/dominant_kernel.py > gpurun_out/pmc/$c.log 2>&1 || { echo "pmc $c failed"; exit 1; }
 done
 find gpurun_out/pmc -name '*.csv' | head
