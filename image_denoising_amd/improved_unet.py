@@ -179,6 +179,11 @@ class ImprovedUNet(nn.Module):
                   _lib.ptr(x), _lib.ptr(y), N, H, W, ws.data_ptr(), ws.numel(), self._prec(),
                   _lib.stream_of(x))
 
+    def _run_forward_n2n(self, x, den, ws, rd_idx):
+        """the N2N no-grad pass (N2NTrainer): the whole image, a superset of the rd pair pixels
+        the loss reads (the pair-pixel fast path is built for the UNet's dec_conv1b / head)"""
+        self._run_forward(x, den, ws)
+
     def _run_backward(self, dy, dflat, ws, N, H, W):
         _lib.call("dn_iunet_backward_prec", ctypes.byref(self._cfg), _lib.ptr(self._flat),
                   _lib.ptr(dy), _lib.ptr(dflat), N, H, W, ws.data_ptr(), ws.numel(), self._prec(),
