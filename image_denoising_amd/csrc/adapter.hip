@@ -9,7 +9,7 @@
 // The backward produces only the adapter's parameter gradients (the base is frozen and run
 // under no_grad, finetune.py:255-262; the noisy input needs none): a workgroup walks a fixed
 // set of 16x16 tiles, keeps its share of the 449 (C=1) / 1315 (C=3) parameter sums in
-// registers, writes one slab row, and k_reduce adds the rows in a fixed order.
+// registers, writes one slab row, and the batched reduction adds the rows in a fixed order.
 //
 // The loss kernel fuses L1(pred, clean) + lambda * gradient_loss(pred, clean)
 // (finetune.py:153-162) with its gradient in gather form (no atomics).

@@ -10,7 +10,7 @@
 //           -> conv forward, conv data-gradient (flipped/transposed weight view),
 //              deconv forward (1x1 GEMM + scatter epilogue), deconv data-gradient.
 //   k_wgrad weight-gradient: partial dW over a slice of pixels, one slab per split,
-//           then k_reduce sums the slabs in a fixed order (deterministic, no atomics).
+//           then k_reduce_batch sums the slabs in a fixed order (deterministic, no atomics).
 //
 // Data layout: activations NHWC fp32 (channels contiguous), weights in the reference's
 // PyTorch layout read through a strided view (no repacking pass).
@@ -33,7 +33,7 @@ constexpr int cround(int v, int mod, int res) { return v + (((res - v % mod) % m
 //   Wave w owns tile rows [w*MT, w*MT+MT); fragment m = one row of 16 pixels (MFMA M),
 //   fragment n = 16 output channels (MFMA N).  K = taps x input channels, staged through
 //   LDS KC channels at a time:
-//     - weights come pre-packed (k_pack) as one LDS image per chunk, [tap][k][n] padded to
+//     - weights come pre-packed (k_pack_batch) as one LDS image per chunk, [tap][k][n] padded to
 //       WNS, and are copied by global_load_lds_dwordx4 into a double-buffered slab;
 //     - the input tile (with halo) is prefetched into registers (float4 along channels)
 //       while the previous chunk computes, then written channel-major [k][pixel].
@@ -504,33 +504,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_head_bwd(HeadBwdArgs h) {
   }
 }
 
-// Weight packing: the per-chunk LDS image [chunk][tap][k][n] (zero padded) of a strided
-// weight view, one image set per blockIdx.z value (deconv forward: one per (a,b)).
-__global__ __launch_bounds__(256) void k_pack(WView wv, int K, int NOUT, int KC, int TAPS, int WNS,
-                                              int LW, int nch, int nz, float* __restrict__ out,
-                                              int zc, int ntot) {
-  const long per_z = (long)nch * LW, total = per_z * nz;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    const int z = (int)(e / per_z);
-    const long r = e - (long)z * per_z;
-    const int c = (int)(r / LW), q = (int)(r % LW);
-    float v = 0.f;
-    if (q < TAPS * KC * WNS) {
-      const int t = q / (KC * WNS), kk = (q / WNS) % KC, nn = q % WNS, k = c * KC + kk;
-      if (k < K && nn < NOUT && (zc == 0 || z * zc + nn < ntot)) {
-        const int tm = wv.flip ? (wv.taps - 1 - t) : t;
-        v = wv.w[wv.off + (long)z * wv.sZ + (long)k * wv.sK + (long)nn * wv.sN + (long)tm * wv.sT];
-      }
-    }
-    out[e] = v;
-  }
-}
-
 // ------------------------------------------------------------------------------------
 // Weight gradient.  MFMA M = output channels (gradient operand G), N = input channels x
 // taps (input operand X), K = pixels.  One workgroup = all output channels x 16*CIF input
 // channels x all taps, accumulated over a contiguous range of pixel chunks (a "split");
-// it writes its partial dW/db into slab[split]; k_reduce sums the slabs in a fixed order.
+// it writes its partial dW/db into slab[split]; k_reduce_batch sums the slabs in a fixed order.
 //   LDS keeps both operands in their natural NHWC order: G chunk [pixel][GS] and the input
 //   chunk (with halo for 3x3) [pixel][XS]; the strides make the 16x16x4 fragment reads
 //   conflict-free.  The next chunk is prefetched into registers (float4 along channels)
@@ -985,31 +963,34 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad1(WgradArgs a0, int up
   }
 }
 
-// out[e] = sum_s slab[s][e] in a fixed order (bit-reproducible): a workgroup owns 64
-// consecutive elements; wave w sums splits w, w+4, w+8, ... in order, then the four wave
-// partials are added in wave order.
-// Element e of the reduced vector goes to out[(e / grp) * ostride + ooff + e % grp] (the
-// identity for grp = n, ooff = 0): a compact slab can fill a strided slice of a gradient.
-__global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ slab, long stride,
-                                                int splits, long n, float* __restrict__ out,
-                                                long grp, long ostride, long ooff) {
+// out[omap(e)] = sum_s slab[s][imap(e)] in a fixed order (bit-reproducible): a workgroup owns
+// 64 elements of one job, its four waves sum interleaved quarters of the rows (four loads in
+// flight per lane), then wave 0 adds the four partials.  blockIdx.x -> job by the jobs' first
+// workgroups (b0, increasing).
+__global__ __launch_bounds__(256) void k_reduce_batch(RedBatch b) {
   __shared__ float part[4][64];
+  int jj = 0;
+  for (int q = 1; q < b.n; ++q)
+    if ((int)blockIdx.x >= b.j[q].b0) jj = q;
+  const RedJob& j = b.j[jj];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long e = (long)blockIdx.x * 64 + lane;
+  const long e = (long)((int)blockIdx.x - j.b0) * 64 + lane;
   float s = 0.f;
-  if (e < n) {
+  if (e < j.n) {
+    const float* src = j.slab + (e / j.ig) * j.is1 + (e % j.ig) * j.is2;
+    const long stride = j.stride;
     int i = wave;
-    for (; i + 12 < splits; i += 16) {  // four loads in flight per lane
-      const float v0 = slab[(long)i * stride + e], v1 = slab[(long)(i + 4) * stride + e];
-      const float v2 = slab[(long)(i + 8) * stride + e], v3 = slab[(long)(i + 12) * stride + e];
+    for (; i + 12 < j.splits; i += 16) {  // four loads in flight per lane
+      const float v0 = src[(long)i * stride], v1 = src[(long)(i + 4) * stride];
+      const float v2 = src[(long)(i + 8) * stride], v3 = src[(long)(i + 12) * stride];
       s += v0; s += v1; s += v2; s += v3;
     }
-    for (; i < splits; i += 4) s += slab[(long)i * stride + e];
+    for (; i < j.splits; i += 4) s += src[(long)i * stride];
   }
   part[wave][lane] = s;
   __syncthreads();
-  if (wave == 0 && e < n)
-    out[(e / grp) * ostride + ooff + e % grp] =
+  if (wave == 0 && e < j.n)
+    j.out[(e / j.og) * j.os1 + j.ooff + e % j.og] =
         ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
 }
 
@@ -1059,15 +1040,6 @@ hipError_t launch_head_bwd(const HeadBwdArgs& h, hipStream_t s) {
   return hipGetLastError();
 }
 
-// nin_a / nin_b as two single-chunk images [k][n] with row stride HEAD_WS
-hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_pack, dim3((HEAD_LW + 255) / 256), dim3(256), 0, s, wa, 96, 96, 96, 1,
-                     HEAD_WS, HEAD_LW, 1, 1, out, 0, 0);
-  hipLaunchKernelGGL(k_pack, dim3((HEAD_LW + 255) / 256), dim3(256), 0, s, wb, 96, 96, 96, 1,
-                     HEAD_WS, HEAD_LW, 1, 1, out + HEAD_LW, 0, 0);
-  return hipGetLastError();
-}
-
 template <int GATHER, int NT, int MT>
 static void geom(FwdGeom& g) {
   using C = FwdCfg<GATHER, NT, MT>;
@@ -1111,17 +1083,49 @@ long pack_floats(int gather, int nout, int K, int nz) {
   return nch * g.LW * nz;
 }
 
+bool pack_job(int gather, const WView& wv, int K, int nout, int nz, float* out, int zc, int ntot,
+              PackJob& j) {
+  FwdGeom g;
+  const long lim = 1L << 31;
+  if (!fwd_geometry(gather, nout, g) || wv.sK >= lim || wv.sN >= lim || wv.sT >= lim ||
+      wv.sZ >= lim)
+    return false;
+  j = PackJob{};
+  j.kind = PK_F32; j.w = wv.w + wv.off; j.out = out;
+  j.sK = (int)wv.sK; j.sN = (int)wv.sN; j.sT = (int)wv.sT; j.sZ = (int)wv.sZ;
+  j.taps = wv.taps; j.flip = wv.flip;
+  j.K = K; j.NOUT = nout; j.nz = nz; j.zc = zc; j.ntot = ntot; j.nch = (K + g.KC - 1) / g.KC;
+  j.g0 = g.KC; j.g1 = g.TAPS; j.g2 = g.WNS; j.g3 = g.LW;
+  return true;
+}
+
 hipError_t launch_pack(int gather, const WView& wv, int K, int nout, int nz, float* out,
                        hipStream_t s, int zc, int ntot) {
-  FwdGeom g;
-  if (!fwd_geometry(gather, nout, g)) return hipErrorInvalidValue;
-  const int nch = (K + g.KC - 1) / g.KC;
-  const long total = (long)nch * g.LW * nz;
-  long blocks = (total + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(k_pack, dim3((unsigned)blocks), dim3(256), 0, s, wv, K, nout, g.KC, g.TAPS,
-                     g.WNS, g.LW, nch, nz, out, zc, ntot);
-  return hipGetLastError();
+  PackBatch b;
+  if (!pack_job(gather, wv, K, nout, nz, out, zc, ntot, b.j[0])) return hipErrorInvalidValue;
+  b.n = 1;
+  return pack_flush(b, s);
+}
+
+// nin_a / nin_b as two single-chunk images [k][n] with row stride HEAD_WS
+static PackJob head_job(const WView& w, float* out) {
+  PackJob j{};
+  j.kind = PK_F32; j.w = w.w + w.off; j.out = out;
+  j.sK = (int)w.sK; j.sN = (int)w.sN; j.sT = (int)w.sT; j.sZ = (int)w.sZ;
+  j.taps = w.taps; j.flip = w.flip;
+  j.K = 96; j.NOUT = 96; j.nz = 1; j.nch = 1;
+  j.g0 = 96; j.g1 = 1; j.g2 = HEAD_WS; j.g3 = HEAD_LW;
+  return j;
+}
+
+hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s,
+                            PackBatch* pb) {
+  PackBatch local;
+  PackBatch& b = pb ? *pb : local;
+  hipError_t e = pack_add(b, head_job(wa, out), s);
+  if (e == hipSuccess) e = pack_add(b, head_job(wb, out + HEAD_LW), s);
+  if (e != hipSuccess || pb) return e;
+  return pack_flush(b, s);
 }
 
 // Tile height for a G_C3 launch: 16/8/4 rows (MT = 4/2/1) -- the fewest rounds of resident
@@ -1295,7 +1299,7 @@ hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s,
 // ---- general weight gradient (any Cout via output-channel blocks) ----------------------
 // 3x3: k_wgrad3 in blocks of 96 / 48 / 32 output channels (Cin >= 16, float4-aligned views);
 // 1x1: k_wgrad<W_C1> in blocks of 96 / 48.  Every block of one layer uses the same split count,
-// so each slab row ends up holding the whole [W ; b] image and one k_reduce finishes it.
+// so each slab row ends up holding the whole [W ; b] image and one reduction job finishes it.
 static int gw_block(int mode, int cout) {
   if (mode == W_C3) return cout <= 32 ? 32 : (cout <= 48 ? 48 : 96);
   return cout <= 48 ? 48 : 96;
@@ -1403,7 +1407,8 @@ long wgrad_slab_floats(int mode, int N, int KH, int KW, int cin, int cout) {
 }
 
 // k_wgrad1 + its reductions straight into dwb (PyTorch layout, bias after the weight)
-hipError_t launch_wgrad1(int mode, const WgradArgs& a0, float* dwb, hipStream_t s) {
+hipError_t launch_wgrad1(int mode, const WgradArgs& a0, float* dwb, hipStream_t s,
+                         RedBatch* rb) {
   const bool up2 = mode == W_UP2;
   const int sp = wgrad1_splits(mode, a0.N, a0.KH, a0.KW), z = up2 ? 4 : 1;
   const long W = (long)a0.Cout * a0.Cin, row = W + a0.Cout;
@@ -1417,28 +1422,59 @@ hipError_t launch_wgrad1(int mode, const WgradArgs& a0, float* dwb, hipStream_t 
     hipLaunchKernelGGL((k_wgrad1<3, 3, 1, 3>), grid, dim3(192), 0, s, a, (int)up2);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (!up2) return launch_reduce(a.slab, row, sp, row, dwb, s);
-  for (int ab = 0; ab < 4; ++ab) {  // W[ci][co][a][b]
-    e = launch_reduce_scatter(a.slab + (long)ab * sp * row, row, sp, W, dwb, 1, 4, ab, s);
+  if (!up2) return launch_reduce(a.slab, row, sp, row, dwb, s, rb);
+  // W[ci][co][a][b] in output order: element e = 4 (ci*Cout + co) + ab lives in parity ab's
+  // block of sp rows
+  RedJob j = red_job(a.slab, row, sp, 4 * W, dwb);
+  j.ig = 4; j.is1 = 1; j.is2 = (int)(sp * row);
+  e = red_add(rb, j, s);
+  if (e != hipSuccess) return e;
+  return launch_reduce(a.slab + W, row, 4 * sp, a.Cout, dwb + 4 * W, s, rb);  // bias: all rows
+}
+
+RedJob red_job(const float* slab, long stride, int splits, long n, float* out) {
+  RedJob j{};
+  j.slab = slab; j.out = out;
+  j.stride = (int)stride; j.splits = splits; j.n = (int)n;
+  j.ig = (int)n; j.is1 = 0; j.is2 = 1;
+  j.og = (int)n; j.os1 = 0; j.ooff = 0;
+  return j;
+}
+
+hipError_t red_flush(RedBatch& b, hipStream_t s) {
+  if (b.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_reduce_batch, dim3((unsigned)b.blocks), dim3(256), 0, s, b);
+  b.n = 0;
+  b.blocks = 0;
+  return hipGetLastError();
+}
+
+hipError_t red_add(RedBatch* b, const RedJob& j, hipStream_t s) {
+  if (j.n <= 0) return hipSuccess;
+  RedBatch local;
+  RedBatch& r = b ? *b : local;
+  if (r.n == kRedJobs) {
+    hipError_t e = red_flush(r, s);
     if (e != hipSuccess) return e;
   }
-  return launch_reduce(a.slab + W, row, 4 * sp, a.Cout, dwb + 4 * W, s);  // bias: all rows
+  r.j[r.n] = j;
+  r.j[r.n].b0 = r.blocks;
+  r.blocks += (j.n + 63) / 64;
+  ++r.n;
+  return b ? hipSuccess : red_flush(r, s);
 }
 
 hipError_t launch_reduce(const float* slab, long slab_stride, int splits, long n, float* out,
-                         hipStream_t s) {
-  const long blocks = (n + 63) / 64;
-  hipLaunchKernelGGL(k_reduce, dim3((unsigned)blocks), dim3(256), 0, s, slab, slab_stride, splits,
-                     n, out, n, 0L, 0L);
-  return hipGetLastError();
+                         hipStream_t s, RedBatch* rb) {
+  return red_add(rb, red_job(slab, slab_stride, splits, n, out), s);
 }
 
 hipError_t launch_reduce_scatter(const float* slab, long slab_stride, int splits, long n,
-                                 float* out, long grp, long ostride, long ooff, hipStream_t s) {
-  const long blocks = (n + 63) / 64;
-  hipLaunchKernelGGL(k_reduce, dim3((unsigned)blocks), dim3(256), 0, s, slab, slab_stride, splits,
-                     n, out, grp, ostride, ooff);
-  return hipGetLastError();
+                                 float* out, long grp, long ostride, long ooff, hipStream_t s,
+                                 RedBatch* rb) {
+  RedJob j = red_job(slab, slab_stride, splits, n, out);
+  j.og = (int)grp; j.os1 = (int)ostride; j.ooff = (int)ooff;
+  return red_add(rb, j, s);
 }
 
 }  // namespace dn

@@ -18,6 +18,7 @@
 //   buffered, one barrier per stage.  LDS rows are 32 bf16 (64 B) with the 16-B quad index
 //   XOR-swizzled by (row >> 1) & 3, which makes the per-lane ds_read_b128 operand reads
 //   conflict-free for every tap offset.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <type_traits>
@@ -700,43 +701,143 @@ static hipError_t run_x6h(const FwdArgs& a, int nz, hipStream_t s) {
 // tail (x6_tail_mode, for k_c3x6p): the last chunk's channels packed over its first stages:
 // 1: (<= 4 channels) im2col, k = 4*tap + channel (stage 0: taps 0..7, stage 1: tap 8);
 // 2: (<= 16 channels) two taps per stage, k = 16*(tap - 2*stage) + channel (5 stages).
-__global__ __launch_bounds__(256) void k_pack_x6(WView wv, int K, int NOUT, int NP, int nch,
-                                                 int nz, int zc, int ntot, int tail,
-                                                 __bf16* __restrict__ out) {
-  const int wst = x6_wst(NP), pad = wst - 3 * NP * 32;
-  const long per_z = (long)nch * 9 * NP * 32, total = per_z * nz;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    const int z = (int)(e / per_z);
-    const long r = e - (long)z * per_z;
-    const int kk = (int)(r % 32), nn = (int)((r / 32) % NP);
-    const int ct = (int)(r / (32L * NP)), c = ct / 9;
-    int t = ct % 9, k = c * 32 + kk;
-    bool live = true;
-    if (tail == 1 && c == nch - 1) {
-      const int kg = 32 * t + kk;  // im2col index of the tail stage: 4 * tap + channel
-      live = t < 2 && kg < 36;
-      t = kg >> 2;
-      k = c * 32 + (kg & 3);
-    } else if (tail == 2 && c == nch - 1) {  // tap pair: 16 * (tap - 2t) + channel
-      const int tap = 2 * t + (kk >> 4);
-      live = t < 5 && tap < 9;
-      t = tap < 9 ? tap : 8;
-      k = c * 32 + (kk & 15);
-    }
-    float v = 0.f;
-    if (live && k < K && nn < NOUT && (zc == 0 || z * zc + nn < ntot)) {
-      const int tm = wv.flip ? wv.taps - 1 - t : t;
-      v = wv.w[wv.off + (long)z * wv.sZ + (long)k * wv.sK + (long)nn * wv.sN + (long)tm * wv.sT];
-    }
-    __bf16 h, m, l;
-    split3(v, h, m, l);
-    __bf16* st = out + ((long)z * nch * 9 + ct) * wst;
-    const int o = nn * 32 + x6_swz(nn, kk >> 3) * 8 + (kk & 7);
-    st[o] = h;
-    st[NP * 32 + o] = m;
-    st[2 * NP * 32 + o] = l;
-    if ((int)(r % (32L * NP)) < pad) st[3 * NP * 32 + (int)(r % (32L * NP))] = (__bf16)0.f;
+__device__ __forceinline__ void pk_x6(const PackJob& j, long e) {
+  const int NP = j.g0, nch = j.nch, wst = x6_wst(NP), pad = wst - 3 * NP * 32;
+  const long per_z = (long)nch * 9 * NP * 32;
+  const int z = (int)(e / per_z);
+  const long r = e - (long)z * per_z;
+  const int kk = (int)(r % 32), nn = (int)((r / 32) % NP);
+  const int ct = (int)(r / (32L * NP)), c = ct / 9;
+  int t = ct % 9, k = c * 32 + kk;
+  bool live = true;
+  if (j.tail == 1 && c == nch - 1) {
+    const int kg = 32 * t + kk;  // im2col index of the tail stage: 4 * tap + channel
+    live = t < 2 && kg < 36;
+    t = kg >> 2;
+    k = c * 32 + (kg & 3);
+  } else if (j.tail == 2 && c == nch - 1) {  // tap pair: 16 * (tap - 2t) + channel
+    const int tap = 2 * t + (kk >> 4);
+    live = t < 5 && tap < 9;
+    t = tap < 9 ? tap : 8;
+    k = c * 32 + (kk & 15);
   }
+  float v = 0.f;
+  if (live && k < j.K && nn < j.NOUT && (j.zc == 0 || z * j.zc + nn < j.ntot)) {
+    const int tm = j.flip ? j.taps - 1 - t : t;
+    v = j.w[(long)z * j.sZ + (long)k * j.sK + (long)nn * j.sN + (long)tm * j.sT];
+  }
+  __bf16 h, m, l;
+  split3(v, h, m, l);
+  __bf16* st = static_cast<__bf16*>(j.out) + ((long)z * nch * 9 + ct) * wst;
+  const int o = nn * 32 + x6_swz(nn, kk >> 3) * 8 + (kk & 7);
+  st[o] = h;
+  st[NP * 32 + o] = m;
+  st[2 * NP * 32 + o] = l;
+  if ((int)(r % (32L * NP)) < pad) st[3 * NP * 32 + (int)(r % (32L * NP))] = (__bf16)0.f;
+}
+
+// the forward-family kernel's per-chunk LDS image [chunk][tap][k][n] (zero padded), one image
+// set per z (deconv forward: one per (a,b))
+__device__ __forceinline__ void pk_f32(const PackJob& j, long e) {
+  const int KC = j.g0, TAPS = j.g1, WNS = j.g2, LW = j.g3;
+  const long per_z = (long)j.nch * LW;
+  const int z = (int)(e / per_z);
+  const long r = e - (long)z * per_z;
+  const int c = (int)(r / LW), q = (int)(r % LW);
+  float v = 0.f;
+  if (q < TAPS * KC * WNS) {
+    const int t = q / (KC * WNS), kk = (q / WNS) % KC, nn = q % WNS, k = c * KC + kk;
+    if (k < j.K && nn < j.NOUT && (j.zc == 0 || z * j.zc + nn < j.ntot)) {
+      const int tm = j.flip ? (j.taps - 1 - t) : t;
+      v = j.w[(long)z * j.sZ + (long)k * j.sK + (long)nn * j.sN + (long)tm * j.sT];
+    }
+  }
+  static_cast<float*>(j.out)[e] = v;
+}
+
+// nin_a / nin_b (OIHW 96x96x1x1) -> the two pre-split head images: [plane][b][out][32] in the
+// head kernel's permuted K order (see k_nin_head_x6)
+__device__ __forceinline__ void pk_head_x6(const PackJob& j, long e) {
+  const int layer = (int)(e / X6_HEAD_BF), r0 = (int)(e % X6_HEAD_BF);
+  const int p = r0 / (3 * 96 * 32), row = (r0 / 32) % (3 * 96), k = r0 % 32;  // row = b*96 + o
+  const int b = row / 96, o = row % 96, g = k >> 3, jj = k & 7;
+  const int ch = 32 * b + (jj < 4 ? 4 * g + jj : 16 + 4 * g + (jj - 4));
+  __bf16 h, m, l;
+  split3((layer ? j.w2 : j.w)[o * 96 + ch], h, m, l);
+  static_cast<__bf16*>(j.out)[layer * X6_HEAD_BF + (p * 3 * 96 + row) * 32 + x6_swz(row, g) * 8 + jj] =
+      p == 0 ? h : (p == 1 ? m : l);
+}
+
+// raw deconv weight W[ci][co][a][b] (96, 96, 2, 2) -> four pre-split parity images
+__device__ __forceinline__ void pk_deconv_x6(const PackJob& j, long e) {
+  const int par = (int)(e / X6_HEAD_BF), r0 = (int)(e % X6_HEAD_BF);
+  const int p = r0 / (3 * 96 * 32), row = (r0 / 32) % (3 * 96), k = r0 % 32;  // row = b*96 + co
+  const int b = row / 96, co = row % 96;
+  __bf16 h, m, l;
+  split3(j.w[((32 * b + k) * 96 + co) * 4 + par], h, m, l);  // par = 2a + b
+  static_cast<__bf16*>(j.out)[par * X6_HEAD_BF + (p * 3 * 96 + row) * 32 + x6_swz(row, k >> 3) * 8 + (k & 7)] =
+      p == 0 ? h : (p == 1 ? m : l);
+}
+
+__global__ __launch_bounds__(256) void k_pack_batch(PackBatch b) {
+  const PackJob& j = b.j[blockIdx.y];
+  const long total = pack_job_elems(j);
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    switch (j.kind) {
+      case PK_F32: pk_f32(j, e); break;
+      case PK_X6: pk_x6(j, e); break;
+      case PK_DECONV_X6: pk_deconv_x6(j, e); break;
+      case PK_HEAD_X6: pk_head_x6(j, e); break;
+      default: static_cast<float*>(j.out)[e] = 0.f; break;
+    }
+  }
+}
+
+hipError_t pack_flush(PackBatch& b, hipStream_t s) {
+  if (b.n == 0) return hipSuccess;
+  long blocks = 1;
+  for (int i = 0; i < b.n; ++i) blocks = std::max(blocks, (pack_job_elems(b.j[i]) + 255) / 256);
+  hipLaunchKernelGGL(k_pack_batch, dim3((unsigned)std::min(blocks, 128L), (unsigned)b.n), dim3(256),
+                     0, s, b);
+  b.n = 0;
+  return hipGetLastError();
+}
+
+hipError_t pack_add(PackBatch& b, const PackJob& j, hipStream_t s) {
+  if (b.n == kPackJobs) {
+    hipError_t e = pack_flush(b, s);
+    if (e != hipSuccess) return e;
+  }
+  b.j[b.n++] = j;
+  return hipSuccess;
+}
+
+// a WView's element strides as the job's ints (false when one does not fit)
+static bool pack_view(const WView& wv, PackJob& j) {
+  const long lim = 1L << 31;
+  if (wv.sK >= lim || wv.sN >= lim || wv.sT >= lim || wv.sZ >= lim) return false;
+  j.w = wv.w + wv.off;
+  j.sK = (int)wv.sK; j.sN = (int)wv.sN; j.sT = (int)wv.sT; j.sZ = (int)wv.sZ;
+  j.taps = wv.taps; j.flip = wv.flip;
+  return true;
+}
+
+PackJob pack_job_head_x6(const float* wa, const float* wb, void* out) {
+  PackJob j{};
+  j.kind = PK_HEAD_X6; j.w = wa; j.w2 = wb; j.out = out;
+  return j;
+}
+
+PackJob pack_job_deconv_x6(const float* w, void* out) {
+  PackJob j{};
+  j.kind = PK_DECONV_X6; j.w = w; j.out = out;
+  return j;
+}
+
+PackJob pack_job_zero(float* out, int n) {
+  PackJob j{};
+  j.kind = PK_ZERO; j.out = out; j.g0 = n;
+  return j;
 }
 
 template <int NT, int MT>
@@ -765,21 +866,26 @@ int x6_tail_mode(int K) {
   return r == 0 ? 0 : (r <= 4 ? 1 : (r <= 16 ? 2 : 0));
 }
 
-hipError_t launch_pack_x6(const WView& wv, int K, int nout, int zc, void* out, hipStream_t s,
-                          int tail) {
+bool pack_job_x6(const WView& wv, int K, int nout, int zc, void* out, int tail, PackJob& j) {
   const long total = x6_pack_elems(K, nout, zc);
-  if (total < 0 || wv.taps != 9 || (tail && tail != x6_tail_mode(K)))
-    return hipErrorInvalidValue;
-  const int np = x6_np(nout, zc);
-  const int nz = zc > 0 ? (nout + zc - 1) / zc : 1;
+  if (total < 0 || wv.taps != 9 || (tail && tail != x6_tail_mode(K))) return false;
   WView v = wv;
   if (zc > 0) v.sZ = (long)zc * wv.sN;  // block z = output channels [z*zc, z*zc + zc)
-  long blocks = ((long)nz * ((K + 31) / 32) * 9 * np * 32 + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(k_pack_x6, dim3((unsigned)blocks), dim3(256), 0, s, v, K,
-                     zc > 0 ? zc : nout, np, (K + 31) / 32, nz, zc, nout, tail,
-                     static_cast<__bf16*>(out));
-  return hipGetLastError();
+  j = PackJob{};
+  if (!pack_view(v, j)) return false;
+  j.kind = PK_X6; j.out = out;
+  j.K = K; j.NOUT = zc > 0 ? zc : nout; j.g0 = x6_np(nout, zc); j.nch = (K + 31) / 32;
+  j.nz = zc > 0 ? (nout + zc - 1) / zc : 1; j.zc = zc; j.ntot = nout; j.tail = tail;
+  return true;
+}
+
+hipError_t launch_pack_x6(const WView& wv, int K, int nout, int zc, void* out, hipStream_t s,
+                          int tail) {
+  PackBatch b;
+  PackJob j;
+  if (!pack_job_x6(wv, K, nout, zc, out, tail, j)) return hipErrorInvalidValue;
+  b.j[b.n++] = j;
+  return pack_flush(b, s);
 }
 
 // Tile height 8/4 rows: the fewest rounds of resident workgroups, each weighed by its length
@@ -1101,23 +1207,9 @@ hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s) {
 // directly the B operand of the next GEMM: for K block b (32 channels) lane group g supplies
 // channels {32b + 4g + r, 32b + 16 + 4g + r} (r < 4) = registers 2b and 2b+1 of its tile
 // fragment, split into three bf16x8 planes in registers.  The weight images are pre-split
-// in the same permuted K order (k_pack_head_x6: [plane][b][out][32], 64-B rows, quads
+// in the same permuted K order (pk_head_x6: [plane][b][out][32], 64-B rows, quads
 // swizzled) and DMA'd into one 54 KiB LDS slot per layer.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pack_head_x6(const float* __restrict__ wa,
-                                                      const float* __restrict__ wb,
-                                                      __bf16* __restrict__ out) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= 2 * X6_HEAD_BF) return;
-  const int layer = e / X6_HEAD_BF, r0 = e % X6_HEAD_BF;
-  const int p = r0 / (3 * 96 * 32), row = (r0 / 32) % (3 * 96), k = r0 % 32;  // row = b*96 + o
-  const int b = row / 96, o = row % 96, g = k >> 3, j = k & 7;
-  const int ch = 32 * b + (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4));
-  __bf16 h, m, l;
-  split3((layer ? wb : wa)[o * 96 + ch], h, m, l);
-  out[layer * X6_HEAD_BF + (p * 3 * 96 + row) * 32 + x6_swz(row, g) * 8 + j] = p == 0 ? h : (p == 1 ? m : l);
-}
-
 template <int MT>
 __global__ __launch_bounds__(256, 2) void k_nin_head_x6(FwdArgs a, HeadArgs hd, const __bf16* wimg) {
   __shared__ __attribute__((aligned(16))) __bf16 lw[X6_HEAD_BF];
@@ -1233,9 +1325,9 @@ __global__ __launch_bounds__(256, 2) void k_nin_head_x6(FwdArgs a, HeadArgs hd, 
 
 // nin_a / nin_b weights (OIHW 96x96x1x1, contiguous) -> the two pre-split head images
 hipError_t launch_pack_head_x6(const float* wa, const float* wb, void* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_pack_head_x6, dim3((2 * X6_HEAD_BF + 255) / 256), dim3(256), 0, s, wa, wb,
-                     static_cast<__bf16*>(out));
-  return hipGetLastError();
+  PackBatch b;
+  b.j[b.n++] = pack_job_head_x6(wa, wb, out);
+  return pack_flush(b, s);
 }
 
 hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* wimg, hipStream_t s) {
@@ -1260,19 +1352,6 @@ hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* w
 // four parity workgroups of a tile are 8 block indices apart, i.e. on one XCD, so three of
 // the four input reads hit that XCD's L2.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pack_deconv_x6(const float* __restrict__ w,
-                                                        __bf16* __restrict__ out) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= 4 * X6_HEAD_BF) return;
-  const int par = e / X6_HEAD_BF, r0 = e % X6_HEAD_BF;
-  const int p = r0 / (3 * 96 * 32), row = (r0 / 32) % (3 * 96), k = r0 % 32;  // row = b*96 + co
-  const int b = row / 96, co = row % 96;
-  __bf16 h, m, l;
-  split3(w[((32 * b + k) * 96 + co) * 4 + par], h, m, l);  // W[ci][co][a][b], par = 2a + b
-  out[par * X6_HEAD_BF + (p * 3 * 96 + row) * 32 + x6_swz(row, k >> 3) * 8 + (k & 7)] =
-      p == 0 ? h : (p == 1 ? m : l);
-}
-
 template <int MT>
 __global__ __launch_bounds__(256, 2) void k_deconv_x6(FwdArgs a, const __bf16* wimg, int ntiles) {
   __shared__ __attribute__((aligned(16))) __bf16 lw[X6_HEAD_BF];
@@ -1337,9 +1416,9 @@ bool deconv_x6_ok(const FwdArgs& a) {
 
 // raw deconv weight (96, 96, 2, 2) -> four pre-split parity images (4 x X6_HEAD_BF bf16)
 hipError_t launch_pack_deconv_x6(const float* w, void* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_pack_deconv_x6, dim3((4 * X6_HEAD_BF + 255) / 256), dim3(256), 0, s, w,
-                     static_cast<__bf16*>(out));
-  return hipGetLastError();
+  PackBatch b;
+  b.j[b.n++] = pack_job_deconv_x6(w, out);
+  return pack_flush(b, s);
 }
 
 // a: in = x (IHt = OH = h, IWt = OW = w), out = the 2h x 2w view, bias; K = NOUT = 96

@@ -49,7 +49,7 @@ struct FwdArgs {
   const float* in; int in_stride, in_off; int IHt, IWt;  // NHWC input, spatial dims
   int N, OH, OW;                                         // output domain (deconv: input res)
   int K, NOUT;                                           // reduction channels, output channels
-  const float* wp; long wp_z;                            // packed weights (k_pack), z stride
+  const float* wp; long wp_z;                            // packed weights (k_pack_batch), z stride
   const float* bias;
   int epi;
   float* out; int out_stride, out_off; int out_layout;
@@ -112,9 +112,69 @@ struct View {
 // geometry of the packed per-chunk weight image of the forward-family kernel
 struct FwdGeom { int KC, TAPS, WNS, LW; };
 
+// ---- batched weight packing (conv_x6.hip) ----
+// Every weight image a pass needs is written by ONE launch: blockIdx.y = job, each job a
+// grid-stride loop over its image.  The kinds: the fp32 per-chunk image of the forward-family
+// kernel ([chunk][tap][k][n]), the pre-split bf16x6 image of a 3x3 layer, the four bf16x6 parity
+// images of a 96-channel deconv, the two bf16x6 head images, and a zero fill (the weight
+// gradients' 64-float DMA padding).  Strides of the weight view are element strides (< 2^31).
+enum PackKind { PK_F32 = 0, PK_X6 = 1, PK_DECONV_X6 = 2, PK_HEAD_X6 = 3, PK_ZERO = 4 };
+struct PackJob {
+  const float* w;   // view origin (WView.w + off); PK_HEAD_X6: nin_a, PK_DECONV_X6: raw weight
+  const float* w2;  // PK_HEAD_X6: nin_b
+  void* out;
+  int sK, sN, sT, sZ, taps, flip;
+  int kind, K, NOUT, nz, zc, ntot, nch, tail;
+  int g0, g1, g2, g3;  // PK_F32: KC, TAPS, WNS, LW; PK_X6: NP; PK_ZERO: floats
+};
+constexpr int kPackJobs = 24;  // 24 x 104 B of kernel arguments
+struct PackBatch {
+  PackJob j[kPackJobs];
+  int n = 0;
+};
+static_assert(sizeof(PackBatch) <= 3072, "pack batch exceeds the kernel-argument budget");
+// elements (= threads of work) of one job
+__host__ __device__ inline long pack_job_elems(const PackJob& j) {
+  switch (j.kind) {
+    case PK_F32: return (long)j.nch * j.g3 * j.nz;
+    case PK_X6: return (long)j.nz * j.nch * 9 * j.g0 * 32;
+    case PK_DECONV_X6: return 4L * 3 * 3 * 96 * 32;
+    case PK_HEAD_X6: return 2L * 3 * 3 * 96 * 32;
+    default: return j.g0;
+  }
+}
+hipError_t pack_flush(PackBatch& b, hipStream_t s);  // one launch; empties b
+hipError_t pack_add(PackBatch& b, const PackJob& j, hipStream_t s);  // flushes a full batch first
+bool pack_job_x6(const WView& wv, int K, int nout, int zc, void* out, int tail, PackJob& j);
+PackJob pack_job_head_x6(const float* wa, const float* wb, void* out);
+PackJob pack_job_deconv_x6(const float* w, void* out);
+PackJob pack_job_zero(float* out, int n);
+
+// ---- batched fixed-order reduction of weight-gradient slabs (conv.hip) ----
+// out[omap(e)] = sum_s slab[s * stride + imap(e)], e < n, rows summed in a fixed order
+// (bit-reproducible); imap(e) = (e / ig) * is1 + (e % ig) * is2, omap(e) = (e / og) * os1 +
+// e % og + ooff.  A backward queues every layer's reduction (each layer owns its slab) and
+// launches them together.
+struct RedJob {
+  const float* slab;
+  float* out;
+  int stride, splits, n, ig, is1, is2, og, os1, ooff, b0;  // b0: first workgroup of the job
+};
+constexpr int kRedJobs = 40;
+struct RedBatch {
+  RedJob j[kRedJobs];
+  int n = 0, blocks = 0;
+};
+static_assert(sizeof(RedBatch) <= 3072, "reduction batch exceeds the kernel-argument budget");
+RedJob red_job(const float* slab, long stride, int splits, long n, float* out);  // identity maps
+hipError_t red_add(RedBatch* b, const RedJob& j, hipStream_t s);  // b == nullptr: launched alone
+hipError_t red_flush(RedBatch& b, hipStream_t s);                 // one launch; empties b
+
 // ---- launchers (conv.hip) ----
 bool fwd_geometry(int gather, int nout, FwdGeom& g);
 long pack_floats(int gather, int nout, int K, int nz);  // floats of a packed weight set
+bool pack_job(int gather, const WView& wv, int K, int nout, int nz, float* out, int zc, int ntot,
+              PackJob& j);
 hipError_t launch_pack(int gather, const WView& wv, int K, int nout, int nz, float* out,
                        hipStream_t s, int zc = 0, int ntot = 0);
 // forward-family launch with explicit tile width NT (16*NT output channels per z-block) and
@@ -126,7 +186,8 @@ hipError_t launch_enc0_fwd(const float* x, int N, int C, int H, int W, const flo
                            int cat_zero_to, float* xcopy, hipStream_t s);
 int enc0_wgrad_splits(int N, int H, int W);
 hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int N, int C, int H,
-                             int W, float* slab, int splits, float* dwb, hipStream_t s);
+                             int W, float* slab, int splits, float* dwb, hipStream_t s,
+                             RedBatch* rb = nullptr);
 // dL/dx (NCHW) of the network input from enc_conv0's (48 ch) and dec_conv1a's (96 ch, input
 // channels [c1_base, c1_base + C) of c1_total) pre-activation gradients
 hipError_t launch_dgrad_input(const float* g0, const float* w0, const float* g1, const float* w1,
@@ -152,12 +213,14 @@ hipError_t launch_wgrad_c3_thin(const float* g, int cout, const float* x, int N,
                                 int W, float* slab, long slab_stride, int cin_total, int ci_base,
                                 int with_bias, int splits, hipStream_t s);
 hipError_t launch_wgrad_thin(const float* g, int g_stride, int cout, const float* x, long npx,
-                             float* slab, int splits, float* dwb, hipStream_t s);
+                             float* slab, int splits, float* dwb, hipStream_t s,
+                             RedBatch* rb = nullptr);
 hipError_t launch_accumulate(float* dst, const float* src, long n, hipStream_t s);
 hipError_t launch_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);
 // nin_a -> nin_b -> nin_c on an activated dec_conv1b output (a.in, a.K = 96); h.d1b unused
 hipError_t launch_nin_head(const FwdArgs& a, const HeadArgs& h, hipStream_t s);
-hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s);
+hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStream_t s,
+                            PackBatch* pb = nullptr);  // pb: queued, not launched
 // bf16x6 nin head (conv_x6.hip): pre-split nin_a | nin_b images (2 x X6_HEAD_BF bf16)
 hipError_t launch_pack_head_x6(const float* wa, const float* wb, void* out, hipStream_t s);
 hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* wimg, hipStream_t s);
@@ -177,11 +240,13 @@ int wgrad_splits_x6(const WgradArgs& a, int splits);  // split count when the x6
 hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s);
 bool wgrad1_ok(int mode, const WgradArgs& a);
 long wgrad_slab_floats(int mode, int N, int KH, int KW, int cin, int cout);
-hipError_t launch_wgrad1(int mode, const WgradArgs& a, float* dwb, hipStream_t s);
+hipError_t launch_wgrad1(int mode, const WgradArgs& a, float* dwb, hipStream_t s,
+                         RedBatch* rb = nullptr);
 hipError_t launch_reduce_scatter(const float* slab, long slab_stride, int splits, long n,
-                                 float* out, long grp, long ostride, long ooff, hipStream_t s);
+                                 float* out, long grp, long ostride, long ooff, hipStream_t s,
+                                 RedBatch* rb = nullptr);
 hipError_t launch_reduce(const float* slab, long slab_stride, int splits, long n, float* out,
-                         hipStream_t s);
+                         hipStream_t s, RedBatch* rb = nullptr);
 bool fwd_supported(int gather, int nout);
 int gwgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
 bool gwgrad_ok(int mode, int Cin, int Cout, const View& g, const View& x);

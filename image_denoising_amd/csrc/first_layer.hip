@@ -11,7 +11,7 @@
 //                 buffer (the "pool0" skip of arch_unet.py:197, 247-248), zero-padding it to a
 //                 float4 boundary.
 //   k_enc0_wgrad  dW[co][ci][t] and db[co] as partial sums over a pixel range per block
-//                 (fixed order), one slab row per block; k_reduce adds the rows in order.
+//                 (fixed order), one slab row per block; the batched reduction adds the rows in order.
 #include "dn_internal.h"
 
 namespace dn {
@@ -222,12 +222,13 @@ hipError_t launch_wgrad_c3_thin(const float* g, int cout, const float* x, int N,
 }
 
 hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int N, int C, int H,
-                             int W, float* slab, int splits, float* dwb, hipStream_t s) {
+                             int W, float* slab, int splits, float* dwb, hipStream_t s,
+                             RedBatch* rb) {
   if (g_stride != E0_CO) return hipErrorInvalidValue;
   const long n_el = (long)E0_CO * 9 * C + E0_CO;
   hipError_t e = launch_wgrad_c3_thin(g, E0_CO, x, N, C, H, W, slab, n_el, C, 0, 1, splits, s);
   if (e != hipSuccess) return e;
-  return launch_reduce(slab, n_el, splits, n_el, dwb, s);
+  return launch_reduce(slab, n_el, splits, n_el, dwb, s, rb);
 }
 
 // ------------------------------------------------------------------------------------
@@ -310,7 +311,7 @@ hipError_t launch_dgrad_input(const float* g0, const float* w0, const float* g1,
 // arch_unet.py:190): dW[co][ci] = sum_p g[p][co] x[p][ci], db[co] = sum_p g[p][co].
 // 240 threads = 10 pixel phases x 24 float4 channel quads; per block a contiguous pixel range;
 // the phases are summed in a fixed order into one slab row in PyTorch layout (W[co][ci] then
-// b[co]); k_reduce sums the rows in order.
+// b[co]); the batched reduction sums the rows in order.
 template <int CO>
 __global__ __launch_bounds__(256) void k_wgrad_thin(const float* __restrict__ g, int g_stride,
                                                     const float* __restrict__ x, long npx, long per,
@@ -361,7 +362,7 @@ int wgrad_thin_splits(long npx) {
 }
 
 hipError_t launch_wgrad_thin(const float* g, int g_stride, int cout, const float* x, long npx,
-                             float* slab, int splits, float* dwb, hipStream_t s) {
+                             float* slab, int splits, float* dwb, hipStream_t s, RedBatch* rb) {
   const long per = (npx + splits - 1) / splits;
   if (cout == 1)
     hipLaunchKernelGGL(k_wgrad_thin<1>, dim3(splits), dim3(256), 0, s, g, g_stride, x, npx, per, slab);
@@ -376,7 +377,7 @@ hipError_t launch_wgrad_thin(const float* g, int g_stride, int cout, const float
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const long n_el = (long)cout * 96 + cout;
-  return launch_reduce(slab, n_el, splits, n_el, dwb, s);
+  return launch_reduce(slab, n_el, splits, n_el, dwb, s, rb);
 }
 
 }  // namespace dn

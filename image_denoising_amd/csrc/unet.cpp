@@ -127,7 +127,10 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
     p.packF[i] = alloc_f(n);
   }
   p.packH = alloc_f(2 * HEAD_LW > X6_HEAD_BF ? 2 * HEAD_LW : X6_HEAD_BF);  // fp32 | bf16x6 head images
-  p.packUX = alloc_f(2 * X6_HEAD_BF);  // 4 x X6_HEAD_BF bf16
+  for (int i = 0; i < NL; ++i) {  // 4 x X6_HEAD_BF bf16 per 96-channel deconv
+    const Layer& L = p.P.L[i];
+    p.packUX[i] = (L.deconv && L.cin == 96 && L.cout == 96) ? alloc_f(2 * X6_HEAD_BF) : -1;
+  }
   for (int i = 0; i < NL; ++i) {  // bf16 images (2 bytes each) of the 3x3 layers
     const Layer& L = p.P.L[i];
     p.packBF[i] = -1;
@@ -193,8 +196,10 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
       }
       p.packXB[i] = alloc_f((e + 1) / 2);
     }
-    // slab: max over layers of splits * (W + b)
-    long slab = 0;
+    // weight-gradient slabs, one per layer (the backward queues every layer's reduction and
+    // launches them together at its end): splits * (W + b) after 64 floats
+    p.zeros = alloc_f(64);
+    p.slab_floats = 0;
     for (int i = 0; i < NL; ++i) {
       const Layer& L = p.P.L[i];
       int lvl = layer_level(i);
@@ -209,11 +214,9 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
                       ? (long)sp * (L.wcount + L.cout)
                       : wgrad_slab_floats(mode, N, KH, KW, L.cin, L.cout);
       if (i == D1A) need += (long)enc0_wgrad_splits(N, KH, KW) * 96 * p.C * 9;  // input slice
-      slab = std::max(slab, need);
+      p.slab[i] = alloc_f(64 + need);
+      p.slab_floats += 64 + need;
     }
-    p.slab = alloc(0, 0);
-    off = p.slab + 64 + (slab + 63) / 64 * 64;  // 64 zero floats in front (wgrad DMA padding)
-    p.slab_floats = slab;
   }
   p.total_floats = off;
   p.with_bwd = bwd;
@@ -343,25 +346,28 @@ hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const flo
 }
 
 hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, int cout, int cin,
-                 float* dwb, float* slab, int splits, hipStream_t s, bool x6) {
+                 float* dwb, float* slab, int splits, hipStream_t s, bool x6, const float* zeros,
+                 RedBatch* rb) {
   WgradArgs a{};
   a.g = g.p; a.g_stride = g.stride; a.g_off = g.off;
   a.x = x.p; a.x_stride = x.stride; a.x_off = x.off;
   a.N = N; a.KH = KH; a.KW = KW; a.Cout = cout; a.Cin = cin;
   const int taps = mode == W_C3 ? 9 : (mode == W_UP2 ? 4 : 1);
   const long n = (long)cout * cin * taps + cout;
-  // slab scratch layout: [64 zero floats | splits x (W + b)]
-  a.zeros = slab;
+  // slab scratch layout: [64 floats | splits x (W + b)]
+  a.zeros = zeros ? zeros : slab;
   a.slab = slab + 64; a.slab_stride = n;
   a.wlayout = mode == W_UP2 ? 1 : 0;
   a.cin_total = cin; a.ci_base = 0; a.bias = 1;
-  hipError_t e = hipMemsetAsync(slab, 0, 64 * sizeof(float), s);
-  if (e != hipSuccess) return e;
-  if (wgrad1_ok(mode, a)) return launch_wgrad1(mode, a, dwb, s);  // 1x1 / deconv, own splits
+  if (!zeros) {
+    hipError_t e = hipMemsetAsync(slab, 0, 64 * sizeof(float), s);
+    if (e != hipSuccess) return e;
+  }
+  if (wgrad1_ok(mode, a)) return launch_wgrad1(mode, a, dwb, s, rb);  // 1x1 / deconv, own splits
   if (x6 && mode == W_C3) splits = wgrad_splits_x6(a, splits);
-  e = launch_wgrad(mode, a, splits, s, x6);
+  hipError_t e = launch_wgrad(mode, a, splits, s, x6);
   if (e != hipSuccess) return e;
-  return launch_reduce(slab + 64, n, splits, n, dwb, s);
+  return launch_reduce(slab + 64, n, splits, n, dwb, s, rb);
 }
 
 // ------------------------------------------------------------------------------------
@@ -415,21 +421,23 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     return launch_fwd_bf16(a, st, ksize);
   };
 
+  // DN_X6_HEAD=0: the fp32 nin head (A/B); the pair-pixel pass always takes the bf16x6 head
+  static const bool head_x6_env = !getenv("DN_X6_HEAD") || atoi(getenv("DN_X6_HEAD")) != 0;
+  const bool sel = x6 && sel_rd && !p.with_bwd;
+  const bool head_x6 = x6 && (head_x6_env || sel);
+  auto deconv_x6_layer = [&](int i) { return x6 && x6_deconv && p.packUX[i] >= 0; };
   // ConvTranspose2d(2,2): fp32 kernel, or the bf16 1x1 kernel per output parity
   auto deconv_forward = [&](const View& xin, int Nn, int h, int w, int cin, const float* wp,
                             const float* b, int cout, const View& out, hipStream_t st) -> hipError_t {
     int i = ENC1;
     while (i < NL && Wt(i) != wp) ++i;
-    if (x6 && x6_deconv && i < NL && cin == 96 && cout == 96) {
-      // bf16x6 parity GEMMs; the pre-split image is rebuilt per layer (stream-ordered reuse)
+    if (i < NL && deconv_x6_layer(i)) {  // bf16x6 parity GEMMs on the layer's pre-split images
       FwdArgs a{};
       a.in = xin.p; a.in_stride = xin.stride; a.in_off = xin.off; a.IHt = h; a.IWt = w;
       a.N = Nn; a.OH = h; a.OW = w; a.K = cin; a.NOUT = cout; a.bias = b;
       a.out = out.p; a.out_stride = out.stride; a.out_off = out.off;
-      if (deconv_x6_ok(a)) {
-        hipError_t e = launch_pack_deconv_x6(prm + p.P.L[i].woff, ws + p.packUX, st);
-        return e != hipSuccess ? e : launch_deconv_x6(a, ws + p.packUX, st);
-      }
+      if (!deconv_x6_ok(a)) return hipErrorInvalidValue;
+      return launch_deconv_x6(a, ws + p.packUX[i], st);
     }
     if (!bf16 || i == NL || p.packBF[i] < 0)
       return dn::deconv_forward(xin, Nn, h, w, cin, wp, b, cout, out, st);
@@ -442,17 +450,38 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     return launch_fwd_bf16(a, st, 1);
   };
 
-  for (int i = ENC1; i < NINA; ++i) {  // pack the weights into the kernels' per-chunk LDS images
+  // every weight image of the pass in one launch (the bf16 images on their own kernel)
+  PackBatch pb;
+  auto add = [&](bool ok, const PackJob& j) { return ok ? pack_add(pb, j, s) : hipErrorInvalidValue; };
+  for (int i = ENC1; i < NINA; ++i) {
     const Layer& L = p.P.L[i];
     const float* w = prm + L.woff;
+    PackJob j;
     if (L.deconv && bf16) DN_TRY(launch_pack_bf16_deconv(w, L.cin, L.cout, ws + p.packBF[i], s));
-    else if (L.deconv) DN_TRY(pack_deconv_fwd(w, L.cin, L.cout, ws + p.packF[i], s));
+    else if (L.deconv && deconv_x6_layer(i)) DN_TRY(add(true, pack_job_deconv_x6(w, ws + p.packUX[i])));
+    else if (L.deconv) DN_TRY(add(pack_job(G_UP, deconv_fwd_view(w, L.cout), L.cin, L.cout, 4,
+                                            ws + p.packF[i], 0, 0, j), j));
     else if (bf16) DN_TRY(launch_pack_bf16(conv_fwd_view(w, L.cin, 3), L.cin, L.cout,
                                            ws + p.packBF[i], s));
-    else if (x6) DN_TRY(launch_pack_x6(conv_fwd_view(w, L.cin, 3), L.cin, L.cout, 0,
-                                       ws + p.packX[i], s, x6_tail_f(i)));
-    else DN_TRY(pack_conv_fwd(w, L.cin, L.cout, L.k, ws + p.packF[i], s));
+    else if (x6) DN_TRY(add(pack_job_x6(conv_fwd_view(w, L.cin, 3), L.cin, L.cout, 0,
+                                        ws + p.packX[i], x6_tail_f(i), j), j));
+    else DN_TRY(add(pack_job(L.k == 3 ? G_C3 : G_C1, conv_fwd_view(w, L.cin, L.k), L.cin, L.cout, 1,
+                             ws + p.packF[i], 0, 0, j), j));
   }
+  if (bf16) {  // nin_a, nin_b on the bf16 kernel, nin_c (96 -> out_nc) on the fp32 one
+    for (int i = NINA; i <= NINB; ++i)
+      DN_TRY(launch_pack_bf16(conv_fwd_view(prm + p.P.L[i].woff, 96, 1), 96, 96,
+                              ws + p.packBF[i], s, 1));
+    PackJob j;
+    DN_TRY(add(pack_job(G_C1, conv_fwd_view(prm + p.P.L[NINC].woff, 96, 1), 96, p.OC, 1,
+                        ws + p.packF[NINC], 0, 0, j), j));
+  } else if (head_x6) {
+    DN_TRY(add(true, pack_job_head_x6(prm + p.P.L[NINA].woff, prm + p.P.L[NINB].woff, ws + p.packH)));
+  } else {
+    DN_TRY(launch_pack_head(conv_fwd_view(prm + p.P.L[NINA].woff, 96, 1),
+                            conv_fwd_view(prm + p.P.L[NINB].woff, 96, 1), ws + p.packH, s, &pb));
+  }
+  DN_TRY(pack_flush(pb, s));
   // enc_conv0, fused with pool0 = x -> channels [2nf, 2nf+C) of the up1 concat buffer
   DN_TRY(launch_enc0_fwd(x, N, C, p.H, p.W, prm + p.P.L[ENC0].woff, Bs(ENC0), ws + p.a0,
                          ws + p.c1, p.c1s, 2 * nf, p.c1s, p.with_bwd ? ws + p.xin : nullptr, s));
@@ -501,10 +530,6 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   if (bf16) {  // dec_conv1b, nin_a, nin_b on the bf16 kernel, then nin_c (96 -> out_nc, fp32)
     DN_TRY(conv_forward(V(p.d1a, 96), N, H(0), Wd(0), 96, Wt(D1B), Bs(D1B), 96, 3, 1,
                         V(p.d1b, 96), OUT_NHWC, s));
-    for (int i = NINA; i <= NINB; ++i)
-      DN_TRY(launch_pack_bf16(conv_fwd_view(prm + p.P.L[i].woff, 96, 1), 96, 96,
-                              ws + p.packBF[i], s, 1));
-    DN_TRY(pack_conv_fwd(prm + p.P.L[NINC].woff, 96, p.OC, 1, ws + p.packF[NINC], s));
     DN_TRY(conv_forward(V(p.d1b, 96), N, H(0), Wd(0), 96, Wt(NINA), Bs(NINA), 96, 1, 1,
                         V(p.na, 96), OUT_NHWC, s));
     DN_TRY(conv_forward(V(p.na, 96), N, H(0), Wd(0), 96, Wt(NINB), Bs(NINB), 96, 1, 1,
@@ -515,7 +540,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   }
   // N2N no-grad pass (training_script.md:141-144 reads den at the pair pixels only): dec_conv1b
   // and the head on those pixels, through the [N, H/2, W, 96] pair image in d1b's storage
-  if (x6 && sel_rd && !p.with_bwd) {
+  if (sel) {
     FwdArgs a{};
     a.in = ws + p.d1a; a.in_stride = 96; a.in_off = 0; a.IHt = H(0); a.IWt = Wd(0);
     a.N = N; a.OH = H(0); a.OW = Wd(0); a.K = 96; a.NOUT = 96;
@@ -523,7 +548,6 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     a.out = ws + p.d1b; a.out_stride = 96; a.out_off = 0; a.out_layout = OUT_NHWC;
     a.sel_rd = sel_rd;
     DN_TRY(launch_fwd_x6_sel(a, s));
-    DN_TRY(launch_pack_head_x6(prm + p.P.L[NINA].woff, prm + p.P.L[NINB].woff, ws + p.packH, s));
     FwdArgs ah{};
     ah.in = ws + p.d1b; ah.in_stride = 96; ah.in_off = 0; ah.IHt = H(0) / 2; ah.IWt = Wd(0);
     ah.N = N; ah.OH = H(0) / 2; ah.OW = Wd(0); ah.K = 96; ah.NOUT = 96;
@@ -538,13 +562,6 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   if (x6) {  // dec_conv1b on the bf16x6 kernel, then the fused nin_a -> nin_b -> nin_c head
     DN_TRY(conv_forward(V(p.d1a, 96), N, H(0), Wd(0), 96, Wt(D1B), Bs(D1B), 96, 3, 1,
                         V(p.d1b, 96), OUT_NHWC, s));
-    // DN_X6_HEAD=0: the fp32 nin head (A/B)
-    static const bool head_x6 = !getenv("DN_X6_HEAD") || atoi(getenv("DN_X6_HEAD")) != 0;
-    if (head_x6)
-      DN_TRY(launch_pack_head_x6(prm + p.P.L[NINA].woff, prm + p.P.L[NINB].woff, ws + p.packH, s));
-    else
-      DN_TRY(launch_pack_head(conv_fwd_view(prm + p.P.L[NINA].woff, 96, 1),
-                              conv_fwd_view(prm + p.P.L[NINB].woff, 96, 1), ws + p.packH, s));
     FwdArgs a{};
     a.in = ws + p.d1b; a.in_stride = 96; a.in_off = 0; a.IHt = H(0); a.IWt = Wd(0);
     a.N = N; a.OH = H(0); a.OW = Wd(0); a.K = 96; a.NOUT = 96;
@@ -559,8 +576,6 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   }
   // dec_conv1b + nin_a + nin_b + nin_c in one kernel (arch_unet.py:251-257); the
   // intermediate activations are written only when a backward will read them
-  DN_TRY(launch_pack_head(conv_fwd_view(prm + p.P.L[NINA].woff, 96, 1),
-                          conv_fwd_view(prm + p.P.L[NINB].woff, 96, 1), ws + p.packH, s));
   {
     FwdArgs a{};
     a.in = ws + p.d1a; a.in_stride = 96; a.in_off = 0; a.IHt = H(0); a.IWt = Wd(0);
@@ -596,25 +611,40 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   auto Wt = [&](int i) { return ws + p.packB[i]; };  // packed data-gradient weights
   auto G = [&](int i) { return dprm + p.P.L[i].woff; };
   auto V = [&](long off, int stride, int coff = 0) { return View{ws + off, stride, coff}; };
-  float* slab = ws + p.slab;
   auto x6_tail_b = [&](int i) -> int {  // as x6_tail_f in the forward, for the data gradients
     const int l = layer_level(i), nout = dgrad_nout(p, i);
     return x6_pipelined(N, H(l), Wd(l), nout, x6_dgrad_zc(nout)) ? x6_tail_mode(p.P.L[i].cout)
                                                                   : 0;
   };
-  for (int i = ENC1; i < NINA; ++i) {  // flipped/transposed weight images for the data gradients
-    const Layer& L = p.P.L[i];
-    const float* w = prm + L.woff;
-    if (L.deconv) {
-      DN_TRY(pack_deconv_dgrad(w, L.cout, L.cin, ws + p.packB[i], s));
-    } else if (x6 && p.packXB[i] >= 0) {
-      const int nout = dgrad_nout(p, i);
-      DN_TRY(launch_pack_x6(conv_dgrad_view(w, L.cin, 3), L.cout, nout, x6_dgrad_zc(nout),
-                            ws + p.packXB[i], s, x6_tail_b(i)));
-    } else {
-      DN_TRY(pack_conv_dgrad(w, L.cin, dgrad_nout(p, i), L.cout, L.k, ws + p.packB[i], s));
+  // flipped/transposed weight images for the data gradients, the head's images and the
+  // weight gradients' zero padding: one launch
+  {
+    PackBatch pb;
+    auto add = [&](bool ok, const PackJob& j) { return ok ? pack_add(pb, j, s) : hipErrorInvalidValue; };
+    for (int i = ENC1; i < NINA; ++i) {
+      const Layer& L = p.P.L[i];
+      const float* w = prm + L.woff;
+      PackJob j;
+      if (L.deconv) {
+        DN_TRY(add(pack_job(G_DN2, deconv_dgrad_view(w, L.cout), L.cout, L.cin, 1, ws + p.packB[i],
+                            0, 0, j), j));
+      } else if (x6 && p.packXB[i] >= 0) {
+        const int nout = dgrad_nout(p, i);
+        DN_TRY(add(pack_job_x6(conv_dgrad_view(w, L.cin, 3), L.cout, nout, x6_dgrad_zc(nout),
+                               ws + p.packXB[i], x6_tail_b(i), j), j));
+      } else {
+        DN_TRY(add(pack_job(L.k == 3 ? G_C3 : G_C1, conv_dgrad_view(w, L.cin, L.k), L.cout,
+                            dgrad_nout(p, i), 1, ws + p.packB[i], 0, 0, j), j));
+      }
     }
+    DN_TRY(launch_pack_head(conv_dgrad_view(prm + p.P.L[NINB].woff, 96, 1),
+                            conv_dgrad_view(prm + p.P.L[NINA].woff, 96, 1), ws + p.packHB, s, &pb));
+    DN_TRY(add(true, pack_job_zero(ws + p.zeros, 64)));
+    DN_TRY(pack_flush(pb, s));
   }
+  RedBatch rb;  // every weight gradient's reduction, launched together at the end
+  const float* Z = ws + p.zeros;
+  auto SL = [&](int i) { return ws + p.slab[i]; };
   // 3x3 data gradients: the fp32 kernel or the bf16x6 one
   auto conv_dgrad = [&](const View& dz, int Nn, int h, int w, int cout, const float* wp, int nout,
                         int ksize, int epi, const View& mask, const View& dx,
@@ -647,8 +677,6 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   }
   // nin_c -> nin_b -> nin_a data gradients in one kernel (g_nb, g_na, g_d1b), then the three
   // 1x1 weight gradients from them
-  DN_TRY(launch_pack_head(conv_dgrad_view(prm + p.P.L[NINB].woff, 96, 1),
-                          conv_dgrad_view(prm + p.P.L[NINA].woff, 96, 1), ws + p.packHB, s));
   {
     HeadBwdArgs h{};
     h.wp = ws + p.packHB;
@@ -660,40 +688,46 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     DN_TRY(launch_head_bwd(h, s));
   }
   if (OC <= 4)
-    DN_TRY(launch_wgrad_thin(dyv.p, dyv.stride, OC, ws + p.nb, (long)N * H(0) * Wd(0), slab,
-                             p.splits[NINC], G(NINC), s));
+    DN_TRY(launch_wgrad_thin(dyv.p, dyv.stride, OC, ws + p.nb, (long)N * H(0) * Wd(0),
+                             SL(NINC) + 64, p.splits[NINC], G(NINC), s, &rb));
   else
-    DN_TRY(wgrad(W_C1, dyv, V(p.nb, 96), N, H(0), Wd(0), OC, 96, G(NINC), slab, p.splits[NINC], s));
-  DN_TRY(wgrad(W_C1, V(p.g_nb, 96), V(p.na, 96), N, H(0), Wd(0), 96, 96, G(NINB), slab,
-               p.splits[NINB], s));
-  DN_TRY(wgrad(W_C1, V(p.g_na, 96), V(p.d1b, 96), N, H(0), Wd(0), 96, 96, G(NINA), slab,
-               p.splits[NINA], s));
-  DN_TRY(wgrad(W_C3, V(p.g_d1b, 96), V(p.d1a, 96), N, H(0), Wd(0), 96, 96, G(D1B), slab,
-               p.splits[D1B], s, x6w));
+    DN_TRY(wgrad(W_C1, dyv, V(p.nb, 96), N, H(0), Wd(0), OC, 96, G(NINC), SL(NINC), p.splits[NINC], s, false, Z, &rb));
+  DN_TRY(wgrad(W_C1, V(p.g_nb, 96), V(p.na, 96), N, H(0), Wd(0), 96, 96, G(NINB), SL(NINB),
+               p.splits[NINB], s, false, Z, &rb));
+  DN_TRY(wgrad(W_C1, V(p.g_na, 96), V(p.d1b, 96), N, H(0), Wd(0), 96, 96, G(NINA), SL(NINA),
+               p.splits[NINA], s, false, Z, &rb));
+  DN_TRY(wgrad(W_C3, V(p.g_d1b, 96), V(p.d1a, 96), N, H(0), Wd(0), 96, 96, G(D1B), SL(D1B),
+               p.splits[D1B], s, x6w, Z, &rb));
   DN_TRY(conv_dgrad(V(p.g_d1b, 96), N, H(0), Wd(0), 96, Wt(D1B), 96, 3, EPI_MASK,
                     V(p.d1a, 96), V(p.g_d1a, 96), s));
   // dec_conv1a weight gradient: the MFMA kernel over the up1 channels [0, 2nf) and the thin
-  // kernel over the network-input channels [2nf, 2nf + C), into the same slab rows
+  // kernel over the network-input channels [2nf, 2nf + C), each into its own slab rows and
+  // reduced into its own columns of W[co][c1k][9]
   {
     const long n = (long)96 * p.c1k * 9 + 96;
+    float* slab = SL(D1A) + 64;
     WgradArgs a{};
     a.g = ws + p.g_d1a; a.g_stride = 96; a.g_off = 0;
     a.x = ws + p.c1; a.x_stride = p.c1s; a.x_off = 0;
     a.N = N; a.KH = H(0); a.KW = Wd(0); a.Cout = 96; a.Cin = 2 * nf;
-    a.zeros = slab; a.slab = slab + 64; a.slab_stride = n;
+    a.zeros = Z; a.slab = slab; a.slab_stride = n;
     a.wlayout = 0; a.cin_total = p.c1k; a.ci_base = 0; a.bias = 1;
-    DN_TRY(hipMemsetAsync(slab, 0, 64 * sizeof(float), s));
     const int sp = x6w ? wgrad_splits_x6(a, p.splits[D1A]) : p.splits[D1A];
     DN_TRY(launch_wgrad(W_C3, a, sp, s, x6w));
-    DN_TRY(launch_reduce(slab + 64, n, sp, n, G(D1A), s));
-    // input-channel slice: own (compact [co][C][9]) slab after the MFMA kernel's rows, own
-    // split count, then scattered into W[co][2nf + ci][t] (overwrites the unreduced columns)
-    float* thin = slab + 64 + (long)p.splits[D1A] * n;
+    RedJob j = red_job(slab, n, sp, 96L * 2 * nf * 9, G(D1A));  // W[co][ci < 2nf][t]
+    j.ig = j.og = 2 * nf * 9;
+    j.is1 = j.os1 = p.c1k * 9;
+    DN_TRY(red_add(&rb, j, s));
+    DN_TRY(red_add(&rb, red_job(slab + 96L * p.c1k * 9, n, sp, 96, G(D1A) + 96L * p.c1k * 9), s));
+    // input-channel slice: compact [co][C][9] rows after the MFMA kernel's, own split count,
+    // scattered into W[co][2nf + ci][t]
+    float* thin = slab + (long)p.splits[D1A] * n;
     const long nt = 96L * C * 9;
     const int st = enc0_wgrad_splits(N, H(0), Wd(0));
     DN_TRY(launch_wgrad_c3_thin(ws + p.g_d1a, 96, ws + p.xin, N, C, H(0), Wd(0), thin, nt, C, 0,
                                 0, st, s));
-    DN_TRY(launch_reduce_scatter(thin, nt, st, nt, G(D1A), 9L * C, 9L * p.c1k, 9L * 2 * nf, s));
+    DN_TRY(launch_reduce_scatter(thin, nt, st, nt, G(D1A), 9L * C, 9L * p.c1k, 9L * 2 * nf, s,
+                                 &rb));
   }
   // only the up1 part of the concat needs a gradient (pool0 is the network input)
   DN_TRY(conv_dgrad(V(p.g_d1a, 96), N, H(0), Wd(0), 96, Wt(D1A), 2 * nf, 3, EPI_PLAIN, none,
@@ -706,29 +740,29 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   for (int l = 1; l <= 4; ++l) {
     const int iu = up_idx[l - 1];  // deconv producing level l-1 from level l
     // deconv wgrad: x = d_l b (level l), dU at level l-1
-    DN_TRY(wgrad(W_UP2, dU, V(p.db[l], 2 * nf), N, H(l), Wd(l), 2 * nf, 2 * nf, G(iu), slab,
-                 p.splits[iu], s));
+    DN_TRY(wgrad(W_UP2, dU, V(p.db[l], 2 * nf), N, H(l), Wd(l), 2 * nf, 2 * nf, G(iu), SL(iu),
+                 p.splits[iu], s, false, Z, &rb));
     DN_TRY(deconv_dgrad(dU, N, H(l), Wd(l), 2 * nf, Wt(iu), 2 * nf, V(p.db[l], 2 * nf), EPI_MASK,
                         V(p.g_db[l], 2 * nf), s));
     const int ia = da_idx[l], ib = ia + 1;
     DN_TRY(wgrad(W_C3, V(p.g_db[l], 2 * nf), V(p.da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, 2 * nf,
-                 G(ib), slab, p.splits[ib], s, x6w));
+                 G(ib), SL(ib), p.splits[ib], s, x6w, Z, &rb));
     DN_TRY(conv_dgrad(V(p.g_db[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ib), 2 * nf, 3,
                       EPI_MASK, V(p.da[l], 2 * nf), V(p.g_da[l], 2 * nf), s));
     DN_TRY(wgrad(W_C3, V(p.g_da[l], 2 * nf), V(p.c[l], p.cs[l]), N, H(l), Wd(l), 2 * nf, p.cs[l],
-                 G(ia), slab, p.splits[ia], s, x6w));
+                 G(ia), SL(ia), p.splits[ia], s, x6w, Z, &rb));
     DN_TRY(conv_dgrad(V(p.g_da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ia), p.cs[l], 3,
                       EPI_PLAIN, none, V(p.g_c[l], p.cs[l]), s));
     dU = V(p.g_c[l], p.cs[l], 0);  // [u_{l+1} grad | skip grad]
   }
   // up5: x = a6 (level 5), dU = g_c5[0:nf]
-  DN_TRY(wgrad(W_UP2, V(p.g_c[4], p.cs[4], 0), V(p.a6, nf), N, H(5), Wd(5), nf, nf, G(UP5), slab,
-               p.splits[UP5], s));
+  DN_TRY(wgrad(W_UP2, V(p.g_c[4], p.cs[4], 0), V(p.a6, nf), N, H(5), Wd(5), nf, nf, G(UP5), SL(UP5),
+               p.splits[UP5], s, false, Z, &rb));
   DN_TRY(deconv_dgrad(V(p.g_c[4], p.cs[4], 0), N, H(5), Wd(5), nf, Wt(UP5), nf, V(p.a6, nf),
                       EPI_MASK, V(p.g_a6, nf), s));
   // enc_conv6 (input p5, level 5)
-  DN_TRY(wgrad(W_C3, V(p.g_a6, nf), V(p.p5, nf), N, H(5), Wd(5), nf, nf, G(ENC6), slab,
-               p.splits[ENC6], s, x6w));
+  DN_TRY(wgrad(W_C3, V(p.g_a6, nf), V(p.p5, nf), N, H(5), Wd(5), nf, nf, G(ENC6), SL(ENC6),
+               p.splits[ENC6], s, x6w, Z, &rb));
   DN_TRY(conv_dgrad(V(p.g_a6, nf), N, H(5), Wd(5), nf, Wt(ENC6), nf, 3, EPI_PLAIN, none,
                     V(p.g_p5, nf), s));
   // pool5 backward -> g_a5 (level 4)
@@ -738,7 +772,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     const int li = ENC2 + (l - 1);
     const int skip = (l == 4) ? nf : 2 * nf;
     DN_TRY(wgrad(W_C3, V(p.g_a[l], nf), V(p.c[l], p.cs[l], skip), N, H(l), Wd(l), nf, nf, G(li),
-                 slab, p.splits[li], s, x6w));
+                 SL(li), p.splits[li], s, x6w, Z, &rb));
     DN_TRY(conv_dgrad(V(p.g_a[l], nf), N, H(l), Wd(l), nf, Wt(li), nf, 3, EPI_ACCUM, none,
                       V(p.g_c[l], p.cs[l], skip), s));
     // pool_l backward: d p_l (skip slice) -> gradient of the level l-1 activation
@@ -751,12 +785,13 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     }
   }
   // enc_conv1 (input a0), enc_conv0 (input x = c1 slice; no data gradient needed)
-  DN_TRY(wgrad(W_C3, V(p.g_a1, nf), V(p.a0, nf), N, H(0), Wd(0), nf, nf, G(ENC1), slab,
-               p.splits[ENC1], s, x6w));
+  DN_TRY(wgrad(W_C3, V(p.g_a1, nf), V(p.a0, nf), N, H(0), Wd(0), nf, nf, G(ENC1), SL(ENC1),
+               p.splits[ENC1], s, x6w, Z, &rb));
   DN_TRY(conv_dgrad(V(p.g_a1, nf), N, H(0), Wd(0), nf, Wt(ENC1), nf, 3, EPI_MASK, V(p.a0, nf),
                     V(p.g_a0, nf), s));
-  DN_TRY(launch_enc0_wgrad(ws + p.g_a0, nf, ws + p.xin, N, C, H(0), Wd(0), slab,
-                           p.splits[ENC0], G(ENC0), s));
+  DN_TRY(launch_enc0_wgrad(ws + p.g_a0, nf, ws + p.xin, N, C, H(0), Wd(0), SL(ENC0) + 64,
+                           p.splits[ENC0], G(ENC0), s, &rb));
+  DN_TRY(red_flush(rb, s));
   // dL/dx: the network input feeds enc_conv0 and (as pool0) dec_conv1a's last C channels
   if (dx)
     DN_TRY(launch_dgrad_input(ws + p.g_a0, prm + p.P.L[ENC0].woff, ws + p.g_d1a,

@@ -40,7 +40,7 @@ struct Plan {
   long d1a, d1b, na, nb;
   long packF[NL];               // packed forward weight images
   long packH;                   // fused head: nin_a | nin_b images (2 x HEAD_LW)
-  long packUX;                  // bf16x6 deconv parity images (one layer at a time)
+  long packUX[NL];              // bf16x6 parity images of the 96-channel deconvs (-1: none)
   long packBF[NL];              // bf16 images of the 3x3 layers (mixed-precision forward)
   long packX[NL];               // pre-split bf16x6 images of the 3x3 layers (forward)
   long fwd_floats;
@@ -52,7 +52,9 @@ struct Plan {
   long packB[NL];               // packed data-gradient weight images
   long packXB[NL];              // pre-split bf16x6 data-gradient images of the 3x3 layers
   long packHB;                  // fused head backward: nin_b^T | nin_a^T images
-  long slab, slab_floats;
+  long zeros;                   // 64 zero floats (weight-gradient DMA padding)
+  long slab[NL];                // per-layer weight-gradient slabs: [64 | splits x (W + b)]
+  long slab_floats;             // all slabs
   int splits[NL];
   long total_floats;
 };
@@ -98,7 +100,10 @@ hipError_t deconv_forward(const View& x, int N, int h, int w, int cin, const flo
                           const float* b, int cout, const View& out, hipStream_t s);
 hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const float* wp, int cin,
                         const View& mask, int epi, const View& dx, hipStream_t s);
+// slab: [64 floats | splits x (W + b)]; zeros == nullptr: the 64 floats are zeroed here and
+// serve as the DMA padding; rb: the reduction is queued, not launched
 hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, int cout, int cin,
-                 float* dwb, float* slab, int splits, hipStream_t s, bool x6 = false);
+                 float* dwb, float* slab, int splits, hipStream_t s, bool x6 = false,
+                 const float* zeros = nullptr, RedBatch* rb = nullptr);
 
 }  // namespace dn

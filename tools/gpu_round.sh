@@ -12,5 +12,10 @@ rc=$?; echo "bench rc=$rc"; grep '^{' gpurun_out/bench_default.log | cut -c1-600
 [ $rc -ne 0 ] && { tail -5 gpurun_out/bench_default.log; exit $rc; }
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_default -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 4 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof_default.log 2>&1
-echo "rocprof rc=$?"
-cd $GRAFT_REPO_ROOT && KERNEL=x6 bash tools/pmc.sh && python3 tools/pmc_summary.py r1 x6
+rc=$?; echo "rocprof rc=$rc"
+cd $GRAFT_REPO_ROOT
+db=$(find gpurun_out/prof_default -name '*.db' | head -1)
+[ -n "$db" ] && python3 tools/kstats.py "$db" --csv gpurun_out/prof_default_kernel_stats.csv --top 40
+[ $rc -ne 0 ] && exit $rc
+[ "${SKIP_PMC:-0}" = "1" ] && exit 0
+KERNEL=x6 bash tools/pmc.sh && python3 tools/pmc_summary.py ${TAG:-r2} x6
