@@ -565,6 +565,26 @@ dn_status dn_deconv2x2_forward(const float* x, int N, int H, int W, int Cin, con
   return hip_status(e, "dn_deconv2x2_forward");
 }
 
+size_t dn_deconv2x2_x6_pack_size(void) { return 4 * sizeof(uint16_t) * (size_t)X6_HEAD_BF; }
+
+dn_status dn_deconv2x2_forward_x6(const float* x, int N, int H, int W, const float* w,
+                                  const float* b, float* y, int y_stride, int y_off, void* pack_ws,
+                                  size_t pack_bytes, void* stream) {
+  if (!x || !w || !b || !y) return fail(DN_ERR_ARG, "null argument");
+  if (N < 1 || H < 1 || W < 1 || y_stride < y_off + 96 || ((y_stride | y_off) & 3))
+    return fail(DN_ERR_ARG, "bad shape");
+  if (dn_status st = need_pack(pack_ws, pack_bytes, dn_deconv2x2_x6_pack_size())) return st;
+  hipStream_t s = (hipStream_t)stream;
+  FwdArgs a{};
+  a.in = x; a.in_stride = 96; a.in_off = 0; a.IHt = H; a.IWt = W;
+  a.N = N; a.OH = H; a.OW = W; a.K = 96; a.NOUT = 96; a.bias = b;
+  a.out = y; a.out_stride = y_stride; a.out_off = y_off;
+  if (!deconv_x6_ok(a)) return fail(DN_ERR_ARG, "shape outside the bf16x6 deconv kernel");
+  hipError_t e = launch_pack_deconv_x6(w, pack_ws, s);
+  if (e == hipSuccess) e = launch_deconv_x6(a, pack_ws, s);
+  return hip_status(e, "dn_deconv2x2_forward_x6");
+}
+
 dn_status dn_deconv2x2_backward_data(const float* dy, int dy_stride, int N, int H, int W, int Cout,
                                      const float* w, int Cin, const float* mask, float* dx,
                                      void* pack_ws, size_t pack_bytes, void* stream) {

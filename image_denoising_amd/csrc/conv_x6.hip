@@ -1208,45 +1208,67 @@ hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s) {
 // channels {32b + 4g + r, 32b + 16 + 4g + r} (r < 4) = registers 2b and 2b+1 of its tile
 // fragment, split into three bf16x8 planes in registers.  The weight images are pre-split
 // in the same permuted K order (pk_head_x6: [plane][b][out][32], 64-B rows, quads
-// swizzled) and DMA'd into one 54 KiB LDS slot per layer.
+// swizzled) and DMA'd into LDS once per workgroup (54 KiB per layer).
 // ------------------------------------------------------------------------------------
-template <int MT>
-__global__ __launch_bounds__(256, 2) void k_nin_head_x6(FwdArgs a, HeadArgs hd, const __bf16* wimg) {
-  __shared__ __attribute__((aligned(16))) __bf16 lw[X6_HEAD_BF];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// Persistent: one 8-wave workgroup per CU keeps both images (108 KiB) and the biases / nin_c
+// weights in LDS for the whole launch; wave-tiles are single 16-pixel rows, taken in a wave-
+// strided loop, the next row's input loaded into registers while the current one computes
+// (the images are read from L2 once per CU, not once per tile).
+// SAVE: na / nb written for the backward; PAIR: the input is a pair image (hd.rd)
+template <bool SAVE, bool PAIR>
+__global__ __launch_bounds__(512, 1) void k_nin_head_x6(FwdArgs a, HeadArgs hd, const __bf16* wimg,
+                                                      int nwt) {
+  __shared__ __attribute__((aligned(16))) __bf16 lw[2 * X6_HEAD_BF];
+  __shared__ __attribute__((aligned(16))) float lb[2 * 96 + X6_HEAD_OCMAX * 97];  // ba|bb|wc|bc
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 15, lg = lane >> 4;
-  const int tiles_x = (a.OW + 15) / 16;
-  const int ty0 = (blockIdx.x / tiles_x) * 4 * MT, tx0 = (blockIdx.x % tiles_x) * 16;
-  const int n = blockIdx.y, gx = tx0 + li;
-  auto dma = [&](const __bf16* src) {  // 54 KiB = 54 x (4 waves ... ) 1 KiB wave copies
-    for (int q = wave; q < X6_HEAD_BF * 2 / 1024; q += 4)
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(src + q * 512 + lane * 8),
-          (__attribute__((address_space(3))) void*)(lw + q * 512), 16, 0, 0);
-  };
-  dma(wimg);
-  f32x4 acc[MT][6];
-#pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    const int gy = ty0 + wave * MT + m;
-    const bool ok = gy < a.OH && gx < a.OW;
-    const float* p = a.in + (((long)n * a.IHt + gy) * a.IWt + gx) * a.in_stride + a.in_off + 4 * lg;
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const float4 v = ok ? *reinterpret_cast<const float4*>(p + q * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
-      acc[m][q] = f32x4{v.x, v.y, v.z, v.w};
-    }
+  for (int q = wave; q < 2 * X6_HEAD_BF * 2 / 1024; q += 8)
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(wimg + q * 512 + lane * 8),
+        (__attribute__((address_space(3))) void*)(lw + q * 512), 16, 0, 0);
+  for (int e = threadIdx.x; e < 2 * 96 + hd.oc * 97; e += 512) {
+    float v;
+    if (e < 96) v = hd.ba[e];
+    else if (e < 192) v = hd.bb[e - 96];
+    else if (e < 192 + hd.oc * 96) v = hd.wc[e - 192];
+    else v = hd.bc[e - 192 - hd.oc * 96];
+    lb[e] = v;
   }
+  const float* lbc = lb + 192 + hd.oc * 96;
+  const int tiles_x = (a.OW + 15) / 16;
+  const int wstride = gridDim.x * 8;
+  // per-row buffer resources, out-of-range offsets instead of branches (see k_deconv_x6)
+  const long in_row = (long)a.IWt * a.in_stride;
+  auto load = [&](int wt, f32x4 (&v)[6], int& rd) {
+    const int n = wt / (a.OH * tiles_x), r = wt - n * a.OH * tiles_x;
+    const int gy = r / tiles_x, gx = (r - gy * tiles_x) * 16 + li;
+    const bool ok = wt < nwt && gx < a.OW;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.in + ((long)n * a.IHt + gy) * in_row + a.in_off), (short)0,
+        (int)(in_row * 4), 0x00020000);
+    const int off = ok ? (gx * a.in_stride + 4 * lg) * 4 : 0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+      v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 64 * q, 0, 0));
+    if constexpr (PAIR) {  // the cell's pair choice, loaded with the row (no wait of its own later)
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<unsigned char*>(hd.rd + ((long)n * a.OH + gy) * (a.OW / 2)), (short)0,
+          a.OW / 2, 0x00020000);
+      rd = __builtin_amdgcn_raw_buffer_load_b8(rr, ok ? gx >> 1 : 0x7fffffff, 0, 0);
+    }
+  };
   auto bias_act = [](f32x4& v, float4 b) {
     v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * 0.2f;
   };
-  auto save = [&](float* dst, long pix, int q, const f32x4& v) {
-    *reinterpret_cast<float4*>(dst + pix * 96 + q * 16 + 4 * lg) = make_float4(v[0], v[1], v[2], v[3]);
+  auto save = [&](float* dst, long row, int off, const f32x4& v, int q) {  // 16 px x 96 ch
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst + row * a.OW * 96, (short)0,
+                                                                        a.OW * 96 * 4, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rs, off + 64 * q, 0, 0);
   };
-  // out = W (LDS image) x in, three 32-channel K blocks of six split products each
-  auto gemm96 = [&](const f32x4 (&in)[6], f32x4 (&out)[6][1]) {
+  // out = W (LDS image at `img`) x in, three 32-channel K blocks of six split products each
+  auto gemm96 = [&](const __bf16* img, const f32x4 (&in)[6], f32x4 (&out)[6][1]) {
 #pragma unroll
     for (int f = 0; f < 6; ++f) out[f][0] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1261,67 +1283,81 @@ __global__ __launch_bounds__(256, 2) void k_nin_head_x6(FwdArgs a, HeadArgs hd, 
         const int row = b * 96 + f * 16 + li;
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
-          wv[pl][f] = *reinterpret_cast<const bf16x8*>(lw + (pl * 3 * 96 + row) * 32 + x6_swz(row, lg) * 8);
+          wv[pl][f] = *reinterpret_cast<const bf16x8*>(img + (pl * 3 * 96 + row) * 32 + x6_swz(row, lg) * 8);
       }
       x6_block<6, 1, 1>(out, wv, xv);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  __syncthreads();  // nin_a image landed (the DMA's vmcnt is drained by the barrier)
-#pragma unroll
-  for (int m = 0; m < MT; ++m) {  // phase 1: acc[m] <- na
-    const int gy = ty0 + wave * MT + m;
-    f32x4 u[6][1];
-    gemm96(acc[m], u);
-#pragma unroll
-    for (int f = 0; f < 6; ++f) {
-      bias_act(u[f][0], *reinterpret_cast<const float4*>(hd.ba + f * 16 + 4 * lg));
-      acc[m][f] = u[f][0];
-    }
-    if (hd.na && gy < a.OH && gx < a.OW)
-#pragma unroll
-      for (int f = 0; f < 6; ++f) save(hd.na, ((long)n * a.OH + gy) * a.OW + gx, f, acc[m][f]);
-  }
-  __syncthreads();  // everyone done with nin_a
-  dma(wimg + X6_HEAD_BF);
-  __syncthreads();  // nin_b image landed
-#pragma unroll
-  for (int m = 0; m < MT; ++m) {  // phase 2: nb, then nin_c
-    const int gy = ty0 + wave * MT + m;
-    const bool ok = gy < a.OH && gx < a.OW;
-    const long pix = ((long)n * a.OH + gy) * a.OW + gx;
-    f32x4 v[6][1];
-    gemm96(acc[m], v);
+  // one wave-tile; two register sets (xa, xb) alternate so that the next tile's loads are in
+  // flight while this one computes and no copy forces a wait for them (or for the stores)
+  auto tile = [&](int wt, const f32x4 (&xin)[6], int rd) {
+    const int n = wt / (a.OH * tiles_x), r = wt - n * a.OH * tiles_x;
+    const int gy = r / tiles_x, gx = (r - gy * tiles_x) * 16 + li;
+    const bool ok = gx < a.OW;
+    const long row = (long)n * a.OH + gy;
+    const int soff = ok ? (gx * 96 + 4 * lg) * 4 : 0x7fffffff;
+    f32x4 u[6][1], h[6];
+    gemm96(lw, xin, u);  // nin_a
 #pragma unroll
     for (int f = 0; f < 6; ++f) {
-      bias_act(v[f][0], *reinterpret_cast<const float4*>(hd.bb + f * 16 + 4 * lg));
-      if (hd.nb && ok) save(hd.nb, pix, f, v[f][0]);
+      bias_act(u[f][0], *reinterpret_cast<const float4*>(lb + f * 16 + 4 * lg));
+      h[f] = u[f][0];
     }
-    // nin_c (fp32 VALU): per-lane partial over its 24 channels, then across the lane groups
+    if constexpr (SAVE)
+#pragma unroll
+      for (int f = 0; f < 6; ++f) save(hd.na, row, soff, h[f], f);
+    gemm96(lw + X6_HEAD_BF, h, u);  // nin_b
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+      bias_act(u[f][0], *reinterpret_cast<const float4*>(lb + 96 + f * 16 + 4 * lg));
+      if constexpr (SAVE) save(hd.nb, row, soff, u[f][0], f);
+    }
+    // nin_c (fp32 VALU): per-lane partial over its 24 channels, then across the lane groups;
+    // lane group 0 stores (the others get an out-of-range offset)
+    // PAIR: pair image pixel (gy, gx) -> pixel pair[rd][gx & 1] of cell (gy, gx / 2), i.e. y's
+    // rows 2gy, 2gy + 1
+    int yoff = 0x7fffffff;
+    if (lg == 0 && ok) {
+      if constexpr (PAIR) {
+        constexpr unsigned kPair = 0xB721ED84u;
+        const int k = (kPair >> (4 * (rd & 7) + 2 * (gx & 1))) & 3;
+        yoff = ((k >> 1) * a.OW + (gx & ~1) + (k & 1)) * 4;
+      } else {
+        yoff = gx * 4;
+      }
+    }
+    constexpr int YR = PAIR ? 2 : 1;  // y rows per wave-tile
     for (int o = 0; o < hd.oc; ++o) {
       float t = 0.f;
 #pragma unroll
       for (int f = 0; f < 6; ++f) {
-        const float4 w = *reinterpret_cast<const float4*>(hd.wc + o * 96 + f * 16 + 4 * lg);
-        t = fmaf(w.x, v[f][0][0], t); t = fmaf(w.y, v[f][0][1], t);
-        t = fmaf(w.z, v[f][0][2], t); t = fmaf(w.w, v[f][0][3], t);
+        const float4 w = *reinterpret_cast<const float4*>(lb + 192 + o * 96 + f * 16 + 4 * lg);
+        t = fmaf(w.x, u[f][0][0], t); t = fmaf(w.y, u[f][0][1], t);
+        t = fmaf(w.z, u[f][0][2], t); t = fmaf(w.w, u[f][0][3], t);
       }
       t += __shfl_xor(t, 16);
       t += __shfl_xor(t, 32);
-      if (lg == 0 && ok) {
-        if (hd.rd) {  // pair image pixel (gy, gx) -> pixel pair[rd][gx & 1] of cell (gy, gx / 2)
-          const int r = hd.rd[((long)n * a.OH + gy) * (a.OW / 2) + (gx >> 1)] & 7;
-          constexpr unsigned kPair = 0xB721ED84u;
-          const int k = (kPair >> (4 * r + 2 * (gx & 1))) & 3;
-          hd.y[(((long)n * hd.oc + o) * 2 * a.OH + 2 * gy + (k >> 1)) * a.OW + (gx & ~1) + (k & 1)] =
-              t + hd.bc[o];
-        } else {
-          hd.y[(((long)n * hd.oc + o) * a.OH + gy) * a.OW + gx] = t + hd.bc[o];
-        }
-      }
+      const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+          hd.y + (((long)n * hd.oc + o) * YR * a.OH + YR * gy) * a.OW, (short)0, YR * a.OW * 4,
+          0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, t + lbc[o]), ry, yoff, 0, 0);
     }
+  };
+  int wt = blockIdx.x * 8 + wave;
+  f32x4 xa[6], xb[6];
+  int ra = 0, rb = 0;
+  load(wt, xa, ra);
+  __syncthreads();  // images, biases and nin_c weights landed
+  for (; wt < nwt; wt += 2 * wstride) {
+    load(wt + wstride, xb, rb);
+    tile(wt, xa, ra);
+    if (wt + wstride >= nwt) break;
+    load(wt + 2 * wstride, xa, ra);
+    tile(wt + wstride, xb, rb);
   }
 }
+
 
 // nin_a / nin_b weights (OIHW 96x96x1x1, contiguous) -> the two pre-split head images
 hipError_t launch_pack_head_x6(const float* wa, const float* wb, void* out, hipStream_t s) {
@@ -1331,60 +1367,86 @@ hipError_t launch_pack_head_x6(const float* wa, const float* wb, void* out, hipS
 }
 
 hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* wimg, hipStream_t s) {
-  if (a.K != 96 || h.oc < 1 || ((a.in_stride | a.in_off) & 3)) return hipErrorInvalidValue;
-  const long tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16);
-  const int mt = tiles < 1024 ? 1 : 2;
-  const dim3 grid(((a.OW + 15) / 16) * ((a.OH + 4 * mt - 1) / (4 * mt)), a.N, 1);
+  if (a.K != 96 || h.oc < 1 || h.oc > X6_HEAD_OCMAX || ((a.in_stride | a.in_off) & 3) ||
+      (long)a.IWt * a.in_stride * 4 >= 0x7fffffffL || (long)a.OW * 96 * 4 * 2 >= 0x7fffffffL)
+    return hipErrorInvalidValue;
+  const long nwt = (long)a.N * a.OH * ((a.OW + 15) / 16);  // one 16-pixel row per wave-tile
+  if (nwt >= (1L << 31) - (1L << 20)) return hipErrorInvalidValue;
+  long blocks = (nwt + 7) / 8;
+  if (blocks > 256) blocks = 256;  // one workgroup per CU
   const __bf16* w = static_cast<const __bf16*>(wimg);
-  if (mt == 1) hipLaunchKernelGGL((k_nin_head_x6<1>), grid, dim3(256), 0, s, a, h, w);
-  else hipLaunchKernelGGL((k_nin_head_x6<2>), grid, dim3(256), 0, s, a, h, w);
+  const dim3 grid((unsigned)blocks), block(512);
+  const bool save = h.na && h.nb;
+  if (save && h.rd) return hipErrorInvalidValue;  // the pair pass saves nothing
+  if (h.rd) hipLaunchKernelGGL((k_nin_head_x6<false, true>), grid, block, 0, s, a, h, w, (int)nwt);
+  else if (save) hipLaunchKernelGGL((k_nin_head_x6<true, false>), grid, block, 0, s, a, h, w, (int)nwt);
+  else hipLaunchKernelGGL((k_nin_head_x6<false, false>), grid, block, 0, s, a, h, w, (int)nwt);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------
 // ConvTranspose2d(96, 96, 2, 2) forward (UpsampleCat's deconv, arch_unet.py:51-62) in the
 // bf16x6 arithmetic: out(2y+a, 2x+b, co) = bias[co] + sum_ci x(y, x, ci) W[ci][co][a][b].
-// Workgroup = one output parity (a, b) x 4 waves x MT low-res rows of 16 pixels; the parity's
-// 96x96 weight matrix is pre-split ([plane][K block][co][32 ci], 64-B rows, swizzled quads;
-// 54 KiB) and DMA'd into LDS.  A lane's B operand is 8 consecutive input channels of its
-// pixel (two float4 loads, split in registers); the 16x16 C/D tile (rows = output channels,
-// columns = pixels) is stored as float4 channel quads at the scattered output pixel.  The
-// four parity workgroups of a tile are 8 block indices apart, i.e. on one XCD, so three of
-// the four input reads hit that XCD's L2.
+// Each parity's 96x96 weight matrix is pre-split ([plane][K block][co][32 ci], 64-B rows,
+// swizzled quads; 54 KiB) and DMA'd into LDS.  A lane's B operand is 8 consecutive input
+// channels of its pixel (two float4 loads, split in registers); the 16x16 C/D tile (rows =
+// output channels, columns = pixels) is stored as float4 channel quads at the scattered
+// output pixel.
 // ------------------------------------------------------------------------------------
-template <int MT>
-__global__ __launch_bounds__(256, 2) void k_deconv_x6(FwdArgs a, const __bf16* wimg, int ntiles) {
-  __shared__ __attribute__((aligned(16))) __bf16 lw[X6_HEAD_BF];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// Persistent: one 8-wave workgroup per CU holds two parity images, (a, 0) and (a, 1), waves 0-3 /
+// 4-7 computing those parities; the two workgroups of a group (blockIdx.x bit 3 = a, the other
+// bits = group; same XCD) cover the four parities of the same wave-tiles -- one low-res row of
+// 16 pixels -- so three of the four reads of an input row hit that XCD's L2.  The next row's
+// input is loaded into registers while the current one computes; the images are read from L2
+// once per workgroup.
+__global__ __launch_bounds__(512, 1) void k_deconv_x6(FwdArgs a, const __bf16* wimg, int nwt) {
+  __shared__ __attribute__((aligned(16))) __bf16 lw[2 * X6_HEAD_BF];
+  __shared__ __attribute__((aligned(16))) float lbias[96];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 15, lg = lane >> 4;
-  const int bx = blockIdx.x;
-  const int par = (bx >> 3) & 3, tile = ((bx >> 5) << 3) | (bx & 7);
-  if (tile >= ntiles) return;
-  const int tiles_x = (a.OW + 15) / 16, tiles_y = (a.OH + 4 * MT - 1) / (4 * MT);
-  const int n = tile / (tiles_x * tiles_y), rt = tile % (tiles_x * tiles_y);
-  const int ty0 = (rt / tiles_x) * 4 * MT, tx0 = (rt % tiles_x) * 16, gx = tx0 + li;
-  const int pa = par >> 1, pb = par & 1;
-  const __bf16* src = wimg + par * X6_HEAD_BF;
-  for (int q = wave; q < X6_HEAD_BF * 2 / 1024; q += 4)
+  const int pa = (blockIdx.x >> 3) & 1, pb = wave >> 2, wq = wave & 3;
+  const int grp = ((blockIdx.x >> 4) << 3) | (blockIdx.x & 7), ngrp = gridDim.x >> 1;
+  const __bf16* src = wimg + 2 * pa * X6_HEAD_BF;  // parities 2a, 2a + 1
+  for (int q = wave; q < 2 * X6_HEAD_BF * 2 / 1024; q += 8)
     __builtin_amdgcn_global_load_lds(
         (const __attribute__((address_space(1))) void*)(src + q * 512 + lane * 8),
         (__attribute__((address_space(3))) void*)(lw + q * 512), 16, 0, 0);
-  __syncthreads();  // weight image landed
+  if (threadIdx.x < 96) lbias[threadIdx.x] = a.bias[threadIdx.x];
+  const __bf16* img = lw + pb * X6_HEAD_BF;
+  const int tiles_x = (a.OW + 15) / 16;
+  const int wstride = ngrp * 4;
+  // loads and stores through per-row buffer resources: out-of-range lanes (past the row or the
+  // last wave-tile) get an out-of-range offset instead of a branch, so every wave-tile issues the
+  // same 6 loads and 6 stores and the compiler's counted waits cover exactly the loads they need.
+  // Constant offsets go into the vector offset (folded into the instruction's offset field), never
+  // into soffset: a 16-byte buffer store with an SGPR soffset whose data registers were rewritten
+  // by the very next instruction (an LDS read) stored a corrupted last dword on some lanes.
+  const long in_row = (long)a.IWt * a.in_stride, out_row = 2L * a.OW * a.out_stride;
+  auto load = [&](int wt, float4 (&v)[6]) {
+    const int n = wt / (a.OH * tiles_x), r = wt - n * a.OH * tiles_x;
+    const int gy = r / tiles_x, gx = (r - gy * tiles_x) * 16 + li;
+    const bool ok = wt < nwt && gx < a.OW;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.in + ((long)n * a.IHt + gy) * in_row + a.in_off), (short)0,
+        (int)(in_row * 4), 0x00020000);
+    const int off = ok ? (gx * a.in_stride + 8 * lg) * 4 : 0x7fffffff;
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    const int gy = ty0 + wave * MT + m;
-    const bool ok = gy < a.OH && gx < a.OW;
-    const float* xp = a.in + (((long)n * a.IHt + gy) * a.IWt + gx) * a.in_stride + a.in_off + 8 * lg;
+    for (int b = 0; b < 3; ++b) {
+      v[2 * b] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 128 * b, 0, 0));
+      v[2 * b + 1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 128 * b + 16, 0, 0));
+    }
+  };
+  // one wave-tile; two register sets alternate (see k_nin_head_x6)
+  auto tile = [&](int wt, const float4 (&xin)[6]) {
+    const int n = wt / (a.OH * tiles_x), r = wt - n * a.OH * tiles_x;
+    const int gy = r / tiles_x, gx = (r - gy * tiles_x) * 16 + li;
     f32x4 out[6][1];
 #pragma unroll
     for (int f = 0; f < 6; ++f) out[f][0] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int b = 0; b < 3; ++b) {
-      float v8[8];
-      const float4 u0 = ok ? *reinterpret_cast<const float4*>(xp + 32 * b) : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4 u1 = ok ? *reinterpret_cast<const float4*>(xp + 32 * b + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-      v8[0] = u0.x; v8[1] = u0.y; v8[2] = u0.z; v8[3] = u0.w;
-      v8[4] = u1.x; v8[5] = u1.y; v8[6] = u1.z; v8[7] = u1.w;
+      const float4 u0 = xin[2 * b], u1 = xin[2 * b + 1];
+      const float v8[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
       bf16x8 xv[3][1];
       split3x8(v8, xv[0][0], xv[1][0], xv[2][0]);
       bf16x8 wv[3][6];
@@ -1393,25 +1455,39 @@ __global__ __launch_bounds__(256, 2) void k_deconv_x6(FwdArgs a, const __bf16* w
         const int row = b * 96 + f * 16 + li;
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
-          wv[pl][f] = *reinterpret_cast<const bf16x8*>(lw + (pl * 3 * 96 + row) * 32 + x6_swz(row, lg) * 8);
+          wv[pl][f] = *reinterpret_cast<const bf16x8*>(img + (pl * 3 * 96 + row) * 32 + x6_swz(row, lg) * 8);
       }
       x6_block<6, 1, 1>(out, wv, xv);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (ok) {
-      float* op = a.out + (((long)n * 2 * a.OH + 2 * gy + pa) * 2 * a.OW + 2 * gx + pb) * a.out_stride + a.out_off;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + ((long)n * 2 * a.OH + 2 * gy + pa) * out_row + a.out_off, (short)0,
+        (int)(out_row * 4), 0x00020000);
+    const int off = gx < a.OW ? ((2 * gx + pb) * a.out_stride + 4 * lg) * 4 : 0x7fffffff;
 #pragma unroll
-      for (int f = 0; f < 6; ++f) {
-        const float4 bb = *reinterpret_cast<const float4*>(a.bias + f * 16 + 4 * lg);
-        *reinterpret_cast<float4*>(op + f * 16 + 4 * lg) =
-            make_float4(out[f][0][0] + bb.x, out[f][0][1] + bb.y, out[f][0][2] + bb.z, out[f][0][3] + bb.w);
-      }
+    for (int f = 0; f < 6; ++f) {
+      const float4 bb = *reinterpret_cast<const float4*>(lbias + f * 16 + 4 * lg);
+      const float4 o = make_float4(out[f][0][0] + bb.x, out[f][0][1] + bb.y, out[f][0][2] + bb.z,
+                                   out[f][0][3] + bb.w);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rs, off + 64 * f, 0, 0);
     }
+  };
+  int wt = grp * 4 + wq;
+  float4 xa[6], xb[6];
+  load(wt, xa);
+  __syncthreads();  // parity images and bias landed
+  for (; wt < nwt; wt += 2 * wstride) {
+    load(wt + wstride, xb);
+    tile(wt, xa);
+    if (wt + wstride >= nwt) break;
+    load(wt + 2 * wstride, xa);
+    tile(wt + wstride, xb);
   }
 }
 
-bool deconv_x6_ok(const FwdArgs& a) {
-  return a.K == 96 && a.NOUT == 96 && !((a.in_stride | a.in_off | a.out_stride | a.out_off) & 3);
+bool deconv_x6_ok(const FwdArgs& a) {  // float4 views; per-row buffer extents below 2^31 bytes
+  return a.K == 96 && a.NOUT == 96 && !((a.in_stride | a.in_off | a.out_stride | a.out_off) & 3) &&
+         (long)a.IWt * a.in_stride * 4 < 0x7fffffffL && 2L * a.OW * a.out_stride * 4 < 0x7fffffffL;
 }
 
 // raw deconv weight (96, 96, 2, 2) -> four pre-split parity images (4 x X6_HEAD_BF bf16)
@@ -1424,13 +1500,14 @@ hipError_t launch_pack_deconv_x6(const float* w, void* out, hipStream_t s) {
 // a: in = x (IHt = OH = h, IWt = OW = w), out = the 2h x 2w view, bias; K = NOUT = 96
 hipError_t launch_deconv_x6(const FwdArgs& a, const void* wimg, hipStream_t s) {
   if (!deconv_x6_ok(a)) return hipErrorInvalidValue;
-  const long tiles1 = (long)a.N * ((a.OH + 3) / 4) * ((a.OW + 15) / 16);
-  const int mt = tiles1 < 2048 ? 1 : 2;
-  const long nt = (long)a.N * ((a.OH + 4 * mt - 1) / (4 * mt)) * ((a.OW + 15) / 16);
-  const dim3 grid((unsigned)((nt + 7) / 8 * 32));
-  const __bf16* w = static_cast<const __bf16*>(wimg);
-  if (mt == 1) hipLaunchKernelGGL((k_deconv_x6<1>), grid, dim3(256), 0, s, a, w, (int)nt);
-  else hipLaunchKernelGGL((k_deconv_x6<2>), grid, dim3(256), 0, s, a, w, (int)nt);
+  const long nwt = (long)a.N * a.OH * ((a.OW + 15) / 16);  // one low-res 16-pixel row per wave-tile
+  if (nwt >= (1L << 31) - (1L << 20)) return hipErrorInvalidValue;
+  // groups of two workgroups (one per parity row a), a multiple of 8 groups (one per XCD)
+  long groups = (nwt + 3) / 4;
+  if (groups > 128) groups = 128;
+  groups = (groups + 7) / 8 * 8;
+  hipLaunchKernelGGL(k_deconv_x6, dim3((unsigned)(2 * groups)), dim3(512), 0, s, a,
+                     static_cast<const __bf16*>(wimg), (int)nwt);
   return hipGetLastError();
 }
 

@@ -87,6 +87,7 @@ struct HeadBwdArgs {
 constexpr int HEAD_WS = 100;   // k-row stride of a head weight image (conflict-free A reads)
 constexpr int HEAD_LW = 9728;  // 96 * HEAD_WS rounded up to 256 floats
 constexpr int X6_HEAD_BF = 3 * 3 * 96 * 32;  // bf16 per layer of the bf16x6 head image (54 KiB)
+constexpr int X6_HEAD_OCMAX = 16;  // most nin_c outputs of the bf16x6 head (kept in its LDS)
 
 struct WgradArgs {
   const float* g; int g_stride, g_off;  // gradient operand (rows = co), NHWC

@@ -423,8 +423,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
 
   // DN_X6_HEAD=0: the fp32 nin head (A/B); the pair-pixel pass always takes the bf16x6 head
   static const bool head_x6_env = !getenv("DN_X6_HEAD") || atoi(getenv("DN_X6_HEAD")) != 0;
-  const bool sel = x6 && sel_rd && !p.with_bwd;
-  const bool head_x6 = x6 && (head_x6_env || sel);
+  const bool sel = x6 && sel_rd && !p.with_bwd && p.OC <= X6_HEAD_OCMAX;
+  const bool head_x6 = x6 && (head_x6_env || sel) && p.OC <= X6_HEAD_OCMAX;
   auto deconv_x6_layer = [&](int i) { return x6 && x6_deconv && p.packUX[i] >= 0; };
   // ConvTranspose2d(2,2): fp32 kernel, or the bf16 1x1 kernel per output parity
   auto deconv_forward = [&](const View& xin, int Nn, int h, int w, int cin, const float* wp,

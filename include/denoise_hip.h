@@ -228,6 +228,12 @@ dn_status dn_conv2d_backward_weight_x6(const float* dz, const float* x, int x_st
 dn_status dn_deconv2x2_forward(const float* x, int N, int H, int W, int Cin, const float* w,
                                const float* b, int Cout, float* y, int y_stride, int y_off,
                                void* pack_ws, size_t pack_bytes, void* stream);
+/* The same ConvTranspose2d(96, 96, 2, 2) at fp32 accuracy on the bf16 matrix cores
+   (DN_PREC_FP32_X6); pack_bytes >= dn_deconv2x2_x6_pack_size().  x channel stride 96. */
+size_t dn_deconv2x2_x6_pack_size(void);
+dn_status dn_deconv2x2_forward_x6(const float* x, int N, int H, int W, const float* w,
+                                  const float* b, float* y, int y_stride, int y_off, void* pack_ws,
+                                  size_t pack_bytes, void* stream);
 dn_status dn_deconv2x2_backward_data(const float* dy, int dy_stride, int N, int H, int W, int Cout,
                                      const float* w, int Cin, const float* mask, float* dx,
                                      void* pack_ws, size_t pack_bytes, void* stream);

@@ -259,3 +259,32 @@ def test_x6_tiny_magnitude_operands(scale):
         assert e6 < X6_TOL, (e6, e32)
     else:  # documented degradation: no worse than losing the subnormal pieces
         assert e6 < 2.0 ** -7 or e6 < 4 * e32 + 1e-7, (e6, e32)
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 8, 8), (3, 13, 37), (4, 64, 64)])
+def test_x6_deconv_forward_vs_fp64_and_deterministic(N, H, W):
+    """ConvTranspose2d(96, 96, 2, 2) on the bf16 matrix cores (k_deconv_x6, persistent, per-row
+    buffer loads / stores): fp32 accuracy against fp64, written into a strided concat buffer
+    without touching the other channels, and bit-identical across repeated launches."""
+    _lib = L()
+    torch.manual_seed(N * 100 + H)
+    x = torch.randn(N, 96, H, W, dtype=torch.float64)
+    w = torch.randn(96, 96, 2, 2, dtype=torch.float64) * 0.1
+    b = torch.randn(96, dtype=torch.float64) * 0.1
+    ref = F.conv_transpose2d(x, w, b, stride=2)
+    stride, off = 104, 4  # output at channels [4, 100) of a 104-channel concat buffer
+    xg = nhwc(x.float()).to(DEV)
+    wg, bg = w.float().to(DEV), b.float().to(DEV)
+    pk = _lib.scratch(_lib.lib().dn_deconv2x2_x6_pack_size(), DEV)
+    outs = []
+    for _ in range(3):
+        yg = torch.full((N, 2 * H, 2 * W, stride), 7.0, device=DEV)
+        _lib.call("dn_deconv2x2_forward_x6", xg.data_ptr(), N, H, W, wg.data_ptr(), bg.data_ptr(),
+                  yg.data_ptr(), stride, off, pk.data_ptr(), pk.numel(), S())
+        outs.append(yg)
+    torch.cuda.synchronize()
+    y = outs[0]
+    assert rel_err(y[..., off:off + 96].permute(0, 3, 1, 2).cpu().numpy(), ref.numpy()) < X6_TOL
+    assert bool((y[..., :off] == 7.0).all()) and bool((y[..., off + 96:] == 7.0).all())
+    for o in outs[1:]:
+        assert torch.equal(o, y)
