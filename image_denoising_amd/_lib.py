@@ -83,6 +83,8 @@ SIGNATURES = {
     "dn_deconv2x2_x6_pack_size": (c_size_t, []),
     "dn_deconv2x2_forward_x6": (c_int, [_F, c_int, c_int, c_int, _F, _F, _F, c_int, c_int, c_void_p,
                                         c_size_t, c_void_p]),
+    "dn_deconv2x2_backward_data_x6": (c_int, [_F, c_int, c_int, c_int, c_int, _F, _F, _F, c_void_p,
+                                              c_size_t, c_void_p]),
     "dn_deconv2x2_backward_data": (c_int, [_F, c_int, c_int, c_int, c_int, c_int, _F, c_int, _F,
                                            _F, c_void_p, c_size_t, c_void_p]),
     "dn_deconv2x2_wgrad_slab_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),

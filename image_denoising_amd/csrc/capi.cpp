@@ -585,6 +585,26 @@ dn_status dn_deconv2x2_forward_x6(const float* x, int N, int H, int W, const flo
   return hip_status(e, "dn_deconv2x2_forward_x6");
 }
 
+dn_status dn_deconv2x2_backward_data_x6(const float* dy, int dy_stride, int N, int H, int W,
+                                        const float* w, const float* mask, float* dx,
+                                        void* pack_ws, size_t pack_bytes, void* stream) {
+  if (!dy || !w || !dx) return fail(DN_ERR_ARG, "null argument");
+  if (N < 1 || H < 1 || W < 1 || dy_stride < 96 || (dy_stride & 3)) return fail(DN_ERR_ARG, "bad shape");
+  if (dn_status st = need_pack(pack_ws, pack_bytes, dn_deconv2x2_x6_pack_size())) return st;
+  hipStream_t s = (hipStream_t)stream;
+  FwdArgs a{};
+  a.in = dy; a.in_stride = dy_stride; a.in_off = 0; a.IHt = 2 * H; a.IWt = 2 * W;
+  a.N = N; a.OH = H; a.OW = W; a.K = 96; a.NOUT = 96;
+  a.epi = mask ? EPI_MASK : EPI_PLAIN; a.mask = mask; a.mask_stride = 96; a.mask_off = 0;
+  a.out = dx; a.out_stride = 96; a.out_off = 0;
+  if (!deconv_dgrad_x6_ok(a)) return fail(DN_ERR_ARG, "shape outside the bf16x6 deconv kernel");
+  PackBatch b;
+  b.j[b.n++] = pack_job_deconv_dgrad_x6(w, pack_ws);
+  hipError_t e = pack_flush(b, s);
+  if (e == hipSuccess) e = launch_deconv_dgrad_x6(a, pack_ws, s);
+  return hip_status(e, "dn_deconv2x2_backward_data_x6");
+}
+
 dn_status dn_deconv2x2_backward_data(const float* dy, int dy_stride, int N, int H, int W, int Cout,
                                      const float* w, int Cin, const float* mask, float* dx,
                                      void* pack_ws, size_t pack_bytes, void* stream) {

@@ -779,6 +779,19 @@ __device__ __forceinline__ void pk_deconv_x6(const PackJob& j, long e) {
       p == 0 ? h : (p == 1 ? m : l);
 }
 
+// raw deconv weight W[ci][co][a][b] (96, 96, 2, 2) -> the data gradient's pre-split images: per
+// input-channel half h and parity, [plane][K block (32 co)][row = ci - 48h][32 co] (X6_DG_BF each)
+constexpr int X6_DG_BF = 3 * 3 * 48 * 32;
+__device__ __forceinline__ void pk_deconv_dgrad_x6(const PackJob& j, long e) {
+  const int h = (int)(e / (4 * X6_DG_BF)), par = (int)(e / X6_DG_BF) % 4, r0 = (int)(e % X6_DG_BF);
+  const int p = r0 / (3 * 48 * 32), row = (r0 / 32) % (3 * 48), k = r0 % 32;  // row = kb*48 + ci'
+  const int kb = row / 48, ci = 48 * h + row % 48, co = 32 * kb + k;
+  __bf16 hh, m, l;
+  split3(j.w[((long)ci * 96 + co) * 4 + par], hh, m, l);
+  static_cast<__bf16*>(j.out)[(long)(h * 4 + par) * X6_DG_BF + (p * 3 * 48 + row) * 32 +
+                              x6_swz(row, k >> 3) * 8 + (k & 7)] = p == 0 ? hh : (p == 1 ? m : l);
+}
+
 __global__ __launch_bounds__(256) void k_pack_batch(PackBatch b) {
   const PackJob& j = b.j[blockIdx.y];
   const long total = pack_job_elems(j);
@@ -788,6 +801,7 @@ __global__ __launch_bounds__(256) void k_pack_batch(PackBatch b) {
       case PK_X6: pk_x6(j, e); break;
       case PK_DECONV_X6: pk_deconv_x6(j, e); break;
       case PK_HEAD_X6: pk_head_x6(j, e); break;
+      case PK_DECONV_DGRAD_X6: pk_deconv_dgrad_x6(j, e); break;
       default: static_cast<float*>(j.out)[e] = 0.f; break;
     }
   }
@@ -831,6 +845,12 @@ PackJob pack_job_head_x6(const float* wa, const float* wb, void* out) {
 PackJob pack_job_deconv_x6(const float* w, void* out) {
   PackJob j{};
   j.kind = PK_DECONV_X6; j.w = w; j.out = out;
+  return j;
+}
+
+PackJob pack_job_deconv_dgrad_x6(const float* w, void* out) {
+  PackJob j{};
+  j.kind = PK_DECONV_DGRAD_X6; j.w = w; j.out = out;
   return j;
 }
 
@@ -1508,6 +1528,144 @@ hipError_t launch_deconv_x6(const FwdArgs& a, const void* wimg, hipStream_t s) {
   groups = (groups + 7) / 8 * 8;
   hipLaunchKernelGGL(k_deconv_x6, dim3((unsigned)(2 * groups)), dim3(512), 0, s, a,
                      static_cast<const __bf16*>(wimg), (int)nwt);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// Data gradient of the 96-channel ConvTranspose2d(2, 2) (arch_unet.py:51-62) in the bf16x6
+// arithmetic: dx(y, x, ci) = sum_{a,b} sum_co dy(2y+a, 2x+b, co) W[ci][co][a][b] (x leaky'(mask)),
+// a GEMM with K = 4 parities x 96.  Persistent, one 8-wave workgroup per CU holding the images of
+// one input-channel half h for all four parities (4 x 27 KiB; the two halves' workgroups of a
+// group share an XCD and the same wave-tiles, so the second read of dy hits L2); a wave-tile is
+// one row of 16 output pixels x 48 channels, computed in four parity steps whose dy rows are
+// loaded one step ahead (two alternating register sets), the mask with the last step.
+// ------------------------------------------------------------------------------------
+template <bool MASKED>
+__global__ __launch_bounds__(512, 1) void k_deconv_dgrad_x6(FwdArgs a, const __bf16* wimg, int nwt) {
+  __shared__ __attribute__((aligned(16))) __bf16 lw[4 * X6_DG_BF];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, lg = lane >> 4;
+  const int h = (blockIdx.x >> 3) & 1;
+  const int grp = ((blockIdx.x >> 4) << 3) | (blockIdx.x & 7), ngrp = gridDim.x >> 1;
+  const __bf16* src = wimg + (long)h * 4 * X6_DG_BF;
+  for (int q = wave; q < 4 * X6_DG_BF * 2 / 1024; q += 8)
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(src + q * 512 + lane * 8),
+        (__attribute__((address_space(3))) void*)(lw + q * 512), 16, 0, 0);
+  const int tiles_x = (a.OW + 15) / 16;
+  const int wstride = ngrp * 8;
+  // per-row buffer resources, constant offsets in the vector offset (see k_deconv_x6)
+  const long in_row = (long)a.IWt * a.in_stride;
+  auto load = [&](int wt, int par, float4 (&v)[6]) {  // dy row 2gy + a, pixels 2gx + b
+    const int n = wt / (a.OH * tiles_x), r = wt - n * a.OH * tiles_x;
+    const int gy = r / tiles_x, gx = (r - gy * tiles_x) * 16 + li;
+    const bool ok = wt < nwt && gx < a.OW;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.in + ((long)n * a.IHt + 2 * gy + (par >> 1)) * in_row + a.in_off),
+        (short)0, (int)(in_row * 4), 0x00020000);
+    const int off = ok ? ((2 * gx + (par & 1)) * a.in_stride + 8 * lg) * 4 : 0x7fffffff;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      v[2 * b] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 128 * b, 0, 0));
+      v[2 * b + 1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 128 * b + 16, 0, 0));
+    }
+  };
+  auto row_rsrc = [&](const float* base, int stride, int wt) {  // output-resolution row of wt
+    const int n = wt / (a.OH * tiles_x), r = wt - n * a.OH * tiles_x;
+    const int gy = r / tiles_x;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(base + ((long)n * a.OH + gy) * a.OW * stride), (short)0,
+        a.OW * stride * 4, 0x00020000);
+  };
+  auto pix_off = [&](int wt, int stride, int coff) {  // this lane's channel quad, or out of range
+    const int r = wt % (a.OH * tiles_x), gx = (r % tiles_x) * 16 + li;
+    return wt < nwt && gx < a.OW ? (gx * stride + coff + 48 * h + 4 * lg) * 4 : 0x7fffffff;
+  };
+  auto mload = [&](int wt, float4 (&m)[3]) {
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(a.mask, a.mask_stride, wt);
+    const int off = pix_off(wt, a.mask_stride, a.mask_off);
+#pragma unroll
+    for (int f = 0; f < 3; ++f)
+      m[f] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 64 * f, 0, 0));
+  };
+  auto step = [&](int par, const float4 (&xin)[6], f32x4 (&acc)[3][1]) {
+    const __bf16* img = lw + par * X6_DG_BF;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const float4 u0 = xin[2 * b], u1 = xin[2 * b + 1];
+      const float v8[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+      bf16x8 xv[3][1];
+      split3x8(v8, xv[0][0], xv[1][0], xv[2][0]);
+      bf16x8 wv[3][3];
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        const int row = b * 48 + f * 16 + li;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          wv[pl][f] = *reinterpret_cast<const bf16x8*>(img + (pl * 3 * 48 + row) * 32 + x6_swz(row, lg) * 8);
+      }
+      x6_block<3, 1, 1>(acc, wv, xv);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the running sums materialised here: otherwise the compiler defers the fp32 adds of the
+    // block sums to the epilogue and keeps every step's MFMA results live (it spills)
+#pragma unroll
+    for (int f = 0; f < 3; ++f) asm volatile("" : "+v"(acc[f][0]));
+  };
+  auto epilogue = [&](int wt, const f32x4 (&acc)[3][1], const float4 (&m)[3]) {
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(a.out, a.out_stride, wt);
+    const int off = pix_off(wt, a.out_stride, a.out_off);
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      float4 o = make_float4(acc[f][0][0], acc[f][0][1], acc[f][0][2], acc[f][0][3]);
+      if constexpr (MASKED) {
+        o.x *= m[f].x > 0.f ? 1.f : 0.2f; o.y *= m[f].y > 0.f ? 1.f : 0.2f;
+        o.z *= m[f].z > 0.f ? 1.f : 0.2f; o.w *= m[f].w > 0.f ? 1.f : 0.2f;
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rs, off + 64 * f, 0, 0);
+    }
+  };
+  int wt = grp * 8 + wave;
+  float4 xa[6], xb[6], m[3] = {};
+  load(wt, 0, xa);
+  __syncthreads();  // images landed
+  for (; wt < nwt; wt += wstride) {
+    f32x4 acc[3][1];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) acc[f][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    load(wt, 1, xb);
+    step(0, xa, acc);
+    load(wt, 2, xa);
+    step(1, xb, acc);
+    load(wt, 3, xb);
+    if constexpr (MASKED) mload(wt, m);
+    step(2, xa, acc);
+    load(wt + wstride, 0, xa);
+    step(3, xb, acc);
+    epilogue(wt, acc, m);
+  }
+}
+
+bool deconv_dgrad_x6_ok(const FwdArgs& a) {  // float4 views; per-row buffer extents below 2^31
+  return a.K == 96 && a.NOUT == 96 && a.IHt == 2 * a.OH && a.IWt == 2 * a.OW &&
+         !((a.in_stride | a.in_off | a.out_stride | a.out_off) & 3) &&
+         (a.epi == EPI_PLAIN || (a.epi == EPI_MASK && a.mask && !((a.mask_stride | a.mask_off) & 3))) &&
+         (long)a.IWt * a.in_stride * 4 < 0x7fffffffL && (long)a.OW * a.out_stride * 4 < 0x7fffffffL &&
+         (a.epi != EPI_MASK || (long)a.OW * a.mask_stride * 4 < 0x7fffffffL);
+}
+
+hipError_t launch_deconv_dgrad_x6(const FwdArgs& a, const void* wimg, hipStream_t s) {
+  if (!deconv_dgrad_x6_ok(a)) return hipErrorInvalidValue;
+  const long nwt = (long)a.N * a.OH * ((a.OW + 15) / 16);  // one 16-pixel output row per wave-tile
+  if (nwt >= (1L << 31) - (1L << 20)) return hipErrorInvalidValue;
+  // groups of two workgroups (one per input-channel half), a multiple of 8 groups (one per XCD)
+  long groups = (nwt + 7) / 8;
+  if (groups > 128) groups = 128;
+  groups = (groups + 7) / 8 * 8;
+  const dim3 grid((unsigned)(2 * groups)), block(512);
+  const __bf16* w = static_cast<const __bf16*>(wimg);
+  if (a.epi == EPI_MASK) hipLaunchKernelGGL(k_deconv_dgrad_x6<true>, grid, block, 0, s, a, w, (int)nwt);
+  else hipLaunchKernelGGL(k_deconv_dgrad_x6<false>, grid, block, 0, s, a, w, (int)nwt);
   return hipGetLastError();
 }
 

@@ -119,7 +119,8 @@ struct FwdGeom { int KC, TAPS, WNS, LW; };
 // kernel ([chunk][tap][k][n]), the pre-split bf16x6 image of a 3x3 layer, the four bf16x6 parity
 // images of a 96-channel deconv, the two bf16x6 head images, and a zero fill (the weight
 // gradients' 64-float DMA padding).  Strides of the weight view are element strides (< 2^31).
-enum PackKind { PK_F32 = 0, PK_X6 = 1, PK_DECONV_X6 = 2, PK_HEAD_X6 = 3, PK_ZERO = 4 };
+enum PackKind { PK_F32 = 0, PK_X6 = 1, PK_DECONV_X6 = 2, PK_HEAD_X6 = 3, PK_ZERO = 4,
+                PK_DECONV_DGRAD_X6 = 5 };
 struct PackJob {
   const float* w;   // view origin (WView.w + off); PK_HEAD_X6: nin_a, PK_DECONV_X6: raw weight
   const float* w2;  // PK_HEAD_X6: nin_b
@@ -141,6 +142,7 @@ __host__ __device__ inline long pack_job_elems(const PackJob& j) {
     case PK_X6: return (long)j.nz * j.nch * 9 * j.g0 * 32;
     case PK_DECONV_X6: return 4L * 3 * 3 * 96 * 32;
     case PK_HEAD_X6: return 2L * 3 * 3 * 96 * 32;
+    case PK_DECONV_DGRAD_X6: return 4L * 3 * 3 * 96 * 32;
     default: return j.g0;
   }
 }
@@ -149,6 +151,7 @@ hipError_t pack_add(PackBatch& b, const PackJob& j, hipStream_t s);  // flushes 
 bool pack_job_x6(const WView& wv, int K, int nout, int zc, void* out, int tail, PackJob& j);
 PackJob pack_job_head_x6(const float* wa, const float* wb, void* out);
 PackJob pack_job_deconv_x6(const float* w, void* out);
+PackJob pack_job_deconv_dgrad_x6(const float* w, void* out);
 PackJob pack_job_zero(float* out, int n);
 
 // ---- batched fixed-order reduction of weight-gradient slabs (conv.hip) ----
@@ -233,6 +236,11 @@ hipError_t launch_fwd_x6_sel(const FwdArgs& a, hipStream_t s);
 bool deconv_x6_ok(const FwdArgs& a);
 hipError_t launch_pack_deconv_x6(const float* w, void* out, hipStream_t s);
 hipError_t launch_deconv_x6(const FwdArgs& a, const void* wimg, hipStream_t s);
+// its data gradient: a.in = dy (IHt x IWt = 2 OH x 2 OW, stride in_stride), a.out = dx (OH x OW,
+// stride out_stride), a.mask (EPI_MASK) / EPI_PLAIN; K = NOUT = 96; wimg = the pre-split images
+// (pack_job_deconv_dgrad_x6, 4 x X6_HEAD_BF bf16)
+bool deconv_dgrad_x6_ok(const FwdArgs& a);
+hipError_t launch_deconv_dgrad_x6(const FwdArgs& a, const void* wimg, hipStream_t s);
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
 hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s, bool x6 = false);
 // bf16x6 3x3 weight gradient (conv_x6.hip): 96 outputs, Cin >= 32, rows >= 8 wide

@@ -184,6 +184,8 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
       p.packB[i] = alloc_f(n);
     }
     p.packHB = alloc_f(2 * HEAD_LW);
+    for (int i = 0; i < NL; ++i)  // 4 x X6_HEAD_BF bf16 per 96-channel deconv
+      p.packUXB[i] = p.packUX[i] >= 0 ? alloc_f(2 * X6_HEAD_BF) : -1;
     for (int i = 0; i < NL; ++i) {  // bf16x6 data-gradient images of the 3x3 layers
       const Layer& L = p.P.L[i];
       p.packXB[i] = -1;
@@ -616,6 +618,20 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     return x6_pipelined(N, H(l), Wd(l), nout, x6_dgrad_zc(nout)) ? x6_tail_mode(p.P.L[i].cout)
                                                                   : 0;
   };
+  // bf16x6 data gradients of the 96-channel deconvs (DN_X6_DECONV=0: the fp32 kernel, A/B)
+  static const bool x6_deconv = !getenv("DN_X6_DECONV") || atoi(getenv("DN_X6_DECONV")) != 0;
+  auto x6_dgrad_deconv = [&](int i) { return x6 && x6_deconv && p.packUXB[i] >= 0; };
+  auto deconv_dgrad = [&](const View& dy, int Nn, int h, int w, int cout, int i, int cin,
+                          const View& mask, int epi, const View& dx, hipStream_t st) -> hipError_t {
+    if (!x6_dgrad_deconv(i))
+      return dn::deconv_dgrad(dy, Nn, h, w, cout, Wt(i), cin, mask, epi, dx, st);
+    FwdArgs a{};
+    a.in = dy.p; a.in_stride = dy.stride; a.in_off = dy.off; a.IHt = 2 * h; a.IWt = 2 * w;
+    a.N = Nn; a.OH = h; a.OW = w; a.K = cout; a.NOUT = cin;
+    a.epi = epi; a.mask = mask.p; a.mask_stride = mask.stride; a.mask_off = mask.off;
+    a.out = dx.p; a.out_stride = dx.stride; a.out_off = dx.off;
+    return launch_deconv_dgrad_x6(a, ws + p.packUXB[i], st);
+  };
   // flipped/transposed weight images for the data gradients, the head's images and the
   // weight gradients' zero padding: one launch
   {
@@ -625,7 +641,9 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
       const Layer& L = p.P.L[i];
       const float* w = prm + L.woff;
       PackJob j;
-      if (L.deconv) {
+      if (L.deconv && x6_dgrad_deconv(i)) {
+        DN_TRY(add(true, pack_job_deconv_dgrad_x6(w, ws + p.packUXB[i])));
+      } else if (L.deconv) {
         DN_TRY(add(pack_job(G_DN2, deconv_dgrad_view(w, L.cout), L.cout, L.cin, 1, ws + p.packB[i],
                             0, 0, j), j));
       } else if (x6 && p.packXB[i] >= 0) {
@@ -742,7 +760,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     // deconv wgrad: x = d_l b (level l), dU at level l-1
     DN_TRY(wgrad(W_UP2, dU, V(p.db[l], 2 * nf), N, H(l), Wd(l), 2 * nf, 2 * nf, G(iu), SL(iu),
                  p.splits[iu], s, false, Z, &rb));
-    DN_TRY(deconv_dgrad(dU, N, H(l), Wd(l), 2 * nf, Wt(iu), 2 * nf, V(p.db[l], 2 * nf), EPI_MASK,
+    DN_TRY(deconv_dgrad(dU, N, H(l), Wd(l), 2 * nf, iu, 2 * nf, V(p.db[l], 2 * nf), EPI_MASK,
                         V(p.g_db[l], 2 * nf), s));
     const int ia = da_idx[l], ib = ia + 1;
     DN_TRY(wgrad(W_C3, V(p.g_db[l], 2 * nf), V(p.da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, 2 * nf,
@@ -758,7 +776,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   // up5: x = a6 (level 5), dU = g_c5[0:nf]
   DN_TRY(wgrad(W_UP2, V(p.g_c[4], p.cs[4], 0), V(p.a6, nf), N, H(5), Wd(5), nf, nf, G(UP5), SL(UP5),
                p.splits[UP5], s, false, Z, &rb));
-  DN_TRY(deconv_dgrad(V(p.g_c[4], p.cs[4], 0), N, H(5), Wd(5), nf, Wt(UP5), nf, V(p.a6, nf),
+  DN_TRY(deconv_dgrad(V(p.g_c[4], p.cs[4], 0), N, H(5), Wd(5), nf, UP5, nf, V(p.a6, nf),
                       EPI_MASK, V(p.g_a6, nf), s));
   // enc_conv6 (input p5, level 5)
   DN_TRY(wgrad(W_C3, V(p.g_a6, nf), V(p.p5, nf), N, H(5), Wd(5), nf, nf, G(ENC6), SL(ENC6),

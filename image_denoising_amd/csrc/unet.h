@@ -52,6 +52,7 @@ struct Plan {
   long packB[NL];               // packed data-gradient weight images
   long packXB[NL];              // pre-split bf16x6 data-gradient images of the 3x3 layers
   long packHB;                  // fused head backward: nin_b^T | nin_a^T images
+  long packUXB[NL];             // bf16x6 data-gradient images of the 96-channel deconvs (-1: none)
   long zeros;                   // 64 zero floats (weight-gradient DMA padding)
   long slab[NL];                // per-layer weight-gradient slabs: [64 | splits x (W + b)]
   long slab_floats;             // all slabs

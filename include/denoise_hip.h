@@ -234,6 +234,11 @@ size_t dn_deconv2x2_x6_pack_size(void);
 dn_status dn_deconv2x2_forward_x6(const float* x, int N, int H, int W, const float* w,
                                   const float* b, float* y, int y_stride, int y_off, void* pack_ws,
                                   size_t pack_bytes, void* stream);
+/* Its data gradient (same pack size): dx [N,H,W,96] (contiguous) from dy [N,2H,2W,*] (channel
+   stride dy_stride), times LeakyReLU'(mask) when mask [N,H,W,96] is not null. */
+dn_status dn_deconv2x2_backward_data_x6(const float* dy, int dy_stride, int N, int H, int W,
+                                        const float* w, const float* mask, float* dx,
+                                        void* pack_ws, size_t pack_bytes, void* stream);
 dn_status dn_deconv2x2_backward_data(const float* dy, int dy_stride, int N, int H, int W, int Cout,
                                      const float* w, int Cin, const float* mask, float* dx,
                                      void* pack_ws, size_t pack_bytes, void* stream);

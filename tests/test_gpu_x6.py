@@ -288,3 +288,35 @@ def test_x6_deconv_forward_vs_fp64_and_deterministic(N, H, W):
     assert bool((y[..., :off] == 7.0).all()) and bool((y[..., off + 96:] == 7.0).all())
     for o in outs[1:]:
         assert torch.equal(o, y)
+
+
+@pytest.mark.parametrize("N,H,W,dy_stride,masked", [(2, 8, 8, 96, True), (3, 13, 37, 144, True),
+                                                    (2, 16, 40, 100, False)])
+def test_x6_deconv_backward_data_vs_fp64(N, H, W, dy_stride, masked):
+    """Data gradient of ConvTranspose2d(96, 96, 2, 2) on the bf16 matrix cores
+    (k_deconv_dgrad_x6): fp32 accuracy against fp64 with and without the LeakyReLU' mask, from a
+    strided concat-buffer gradient, bit-identical across repeated launches."""
+    _lib = L()
+    torch.manual_seed(N * 10 + W)
+    x = torch.randn(N, 96, H, W, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(96, 96, 2, 2, dtype=torch.float64) * 0.1
+    y = F.conv_transpose2d(x, w, None, stride=2)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    mask = torch.randn(N, 96, H, W, dtype=torch.float64)
+    ref = torch.where(mask > 0, x.grad, x.grad * 0.2) if masked else x.grad
+    dyg = torch.zeros(N, 2 * H, 2 * W, dy_stride, device=DEV)
+    dyg[..., :96] = nhwc(dy.float()).to(DEV)
+    mg = nhwc(mask.float()).to(DEV)
+    wg = w.float().to(DEV)
+    pk = _lib.scratch(_lib.lib().dn_deconv2x2_x6_pack_size(), DEV)
+    outs = []
+    for _ in range(3):
+        dx = torch.full((N, H, W, 96), 7.0, device=DEV)
+        _lib.call("dn_deconv2x2_backward_data_x6", dyg.data_ptr(), dy_stride, N, H, W, wg.data_ptr(),
+                  mg.data_ptr() if masked else None, dx.data_ptr(), pk.data_ptr(), pk.numel(), S())
+        outs.append(dx)
+    torch.cuda.synchronize()
+    assert rel_err(outs[0].permute(0, 3, 1, 2).cpu().numpy(), ref.detach().numpy()) < X6_TOL
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
