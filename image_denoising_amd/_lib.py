@@ -52,6 +52,8 @@ SIGNATURES = {
     "dn_n2n_subimage_from_mask": (c_int, [_F, c_int, c_int, c_int, c_int, _U8, _F, c_void_p]),
     "dn_add_gauss_noise": (c_int, [_F, c_int, c_int64, c_float, _F, c_uint64, c_uint64, c_uint64,
                                    _F, c_void_p]),
+    "dn_add_poisson_noise": (c_int, [_F, c_int, c_int64, c_float, _F, c_uint64, c_uint64, c_uint64,
+                                   _F, c_void_p]),
     "dn_loss_partials_size": (c_size_t, []),
     "dn_n2n_loss": (c_int, [_F, _F, _F, _U8, c_int, c_int, c_int, c_int, c_float, _F, _F, c_void_p,
                             c_void_p]),

@@ -251,6 +251,18 @@ dn_status dn_add_gauss_noise(const float* clean, int N, int64_t per_image, float
                     "dn_add_gauss_noise");
 }
 
+dn_status dn_add_poisson_noise(const float* clean, int N, int64_t per_image, float lam,
+                               const float* lam_per_image, uint64_t seed, uint64_t offset,
+                               uint64_t elem_base, float* noisy, void* stream) {
+  if (N < 0 || per_image < 0) return fail(DN_ERR_ARG, "negative size");
+  if (!lam_per_image && !(lam > 0.f && lam <= 500.f)) return fail(DN_ERR_ARG, "lam must be in (0, 500]");
+  if ((long)N * per_image == 0) return DN_OK;
+  if (!clean || !noisy) return fail(DN_ERR_ARG, "null argument");
+  return hip_status(launch_poisson(clean, N, per_image, lam, lam_per_image, seed, offset, elem_base,
+                                   noisy, (hipStream_t)stream),
+                    "dn_add_poisson_noise");
+}
+
 size_t dn_loss_partials_size(void) { return loss_partials_bytes(); }
 
 dn_status dn_n2n_loss(const float* out, const float* sub2, const float* den, const uint8_t* rd_idx,

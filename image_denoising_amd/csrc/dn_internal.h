@@ -278,6 +278,9 @@ hipError_t launch_subimage_from_mask(const float* img, int N, int C, int H, int 
 hipError_t launch_noise(const float* clean, int N, int64_t per_image, float std_,
                         const float* std_per_image, uint64_t seed, uint64_t offset,
                         uint64_t elem_base, float* noisy, hipStream_t s);
+hipError_t launch_poisson(const float* clean, int N, int64_t per_image, float lam,
+                          const float* lam_per_image, uint64_t seed, uint64_t offset,
+                          uint64_t elem_base, float* noisy, hipStream_t s);
 size_t loss_partials_bytes();
 hipError_t launch_n2n_loss(const float* out, const float* sub2, const float* den,
                            const uint8_t* rd, int N, int C, int h, int w, float lambda,

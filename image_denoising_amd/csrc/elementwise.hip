@@ -199,6 +199,35 @@ __global__ __launch_bounds__(256) void k_noise(const float* __restrict__ clean, 
   }
 }
 
+// Poisson noise: train.py:102-111 (poisson_fix / poisson_range), noisy = Poisson(lam x) / lam.
+// The count is drawn by inversion of the Poisson CDF in fp64 with one 53-bit uniform per element
+// (philox_uniform53): k = min{k : u <= F(k)}, F accumulated from p_0 = exp(-mu),
+// p_k = p_{k-1} mu / k.  mu = lam x is formed in fp32 as torch.poisson receives it; mu <= 500
+// (the host checks lam; the images are in [0, 1]), the loop is bounded at mu + 20 sqrt(mu) + 40.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_poisson(const float* __restrict__ clean, int N,
+                                                 int64_t per_image, float lam,
+                                                 const float* __restrict__ lam_img, uint64_t seed,
+                                                 uint64_t offset, uint64_t elem_base,
+                                                 float* __restrict__ noisy) {
+  const long total = (long)N * per_image;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const float l = lam_img ? lam_img[e / per_image] : lam;
+    const float muf = l * clean[e];
+    const double mu = muf > 0.f ? (double)muf : 0.0;
+    const double u = philox_uniform53(seed, offset, elem_base + (uint64_t)e);
+    double p = exp(-mu), F = p;
+    const int kmax = (int)(mu + 20.0 * sqrt(mu)) + 40;
+    int k = 0;
+    while (u > F && k < kmax) {
+      ++k;
+      p *= mu / k;
+      F += p;
+    }
+    noisy[e] = (float)k / l;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Loss reductions: fixed grid, per-block fp64 partial sums, one finalize block.
 // ------------------------------------------------------------------------------------
@@ -436,6 +465,15 @@ hipError_t launch_noise(const float* clean, int N, int64_t per_image, float std_
   const long total = (long)N * per_image;
   hipLaunchKernelGGL(k_noise, dim3(grid_for(total, 256, 65536)), dim3(256), 0, s, clean, N,
                      per_image, std_, std_per_image, seed, offset, elem_base, noisy);
+  return hipGetLastError();
+}
+
+hipError_t launch_poisson(const float* clean, int N, int64_t per_image, float lam,
+                          const float* lam_per_image, uint64_t seed, uint64_t offset,
+                          uint64_t elem_base, float* noisy, hipStream_t s) {
+  const long total = (long)N * per_image;
+  hipLaunchKernelGGL(k_poisson, dim3(grid_for(total, 256, 65536)), dim3(256), 0, s, clean, N,
+                     per_image, lam, lam_per_image, seed, offset, elem_base, noisy);
   return hipGetLastError();
 }
 

@@ -52,4 +52,15 @@ __host__ __device__ inline float philox_normal(uint64_t seed, uint64_t offset, u
   return (q & 1) ? r * sinf(th) : r * cosf(th);
 }
 
+// uniform double in (0, 1) for global element q: 53 bits from words (2p, 2p+1) of block q>>1,
+// p = q & 1 (the Poisson sampler's draw)
+__host__ __device__ inline double philox_uniform53(uint64_t seed, uint64_t offset, uint64_t q) {
+  const uint64_t blk = q >> 1;
+  const U32x4 o = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), (uint32_t)offset,
+                                (uint32_t)(offset >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+  const int p = (int)(q & 1);
+  const uint32_t a = o.v[2 * p] >> 5, b = o.v[2 * p + 1] >> 6;  // 27 + 26 bits
+  return ((double)a * 67108864.0 + (double)b + 0.5) * (1.0 / 9007199254740992.0);
+}
+
 }  // namespace dn

@@ -99,15 +99,24 @@ def generate_subimages(img: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
 
 
 class AugmentNoise:
-    """train.py:64-101 (gauss styles).  'gauss25' -> sigma = 25/255; 'gauss5_50' -> per-image
-    sigma ~ U[5/255, 50/255].  Poisson styles are out of scope (not on the N2N gauss25 path)."""
+    """train.py:64-111.  'gauss25' -> sigma = 25/255; 'gauss5_50' -> per-image sigma ~ U[5/255,
+    50/255]; 'poisson30' -> Poisson(30 x) / 30; 'poisson5_50' -> per-image lam ~ U[5, 50].  The
+    random streams are Philox on the GPU (global element index, seed, offset), not torch's
+    generator."""
 
     def __init__(self, style: str, seed: int = 0):
         if style.startswith("gauss"):
             self.params = [float(p) / 255.0 for p in style.replace("gauss", "").split("_")]
             self.style = "gauss_fix" if len(self.params) == 1 else "gauss_range"
+        elif style.startswith("poisson"):
+            self.params = [float(p) for p in style.replace("poisson", "").split("_")]
+            self.style = "poisson_fix" if len(self.params) == 1 else "poisson_range"
+            if not all(0.0 < p <= 500.0 for p in self.params):
+                raise ValueError("poisson lam must be in (0, 500]")
         else:
-            raise NotImplementedError(f"noise style {style!r} is not on the N2N gauss path")
+            raise ValueError(f"unknown noise style {style!r}")
+        if len(self.params) not in (1, 2):
+            raise ValueError(f"noise style {style!r}: one value or a min_max range")
         self.seed = seed
         self.calls = 0
 
@@ -116,15 +125,16 @@ class AugmentNoise:
         N = x.shape[0]
         per = x.numel() // max(N, 1)
         out = torch.empty_like(x)
-        std_img = None
-        if self.style == "gauss_range":
+        per_img = None
+        if self.style.endswith("_range"):  # train.py:95-96 / :108-109: one value per image
             lo, hi = self.params
             g = torch.Generator(device="cpu").manual_seed(self.seed * 1000003 + self.calls)
-            std_img = (torch.rand(N, generator=g) * (hi - lo) + lo).to(x.device)
+            per_img = (torch.rand(N, generator=g) * (hi - lo) + lo).to(x.device)
         off = self.calls if offset is None else offset
         self.calls += 1
-        _lib.call("dn_add_gauss_noise", _lib.ptr(x), N, per, float(self.params[0]),
-                  _lib.ptr(std_img), self.seed, off, elem_base, _lib.ptr(out), _lib.stream_of(x))
+        fn = "dn_add_gauss_noise" if self.style.startswith("gauss") else "dn_add_poisson_noise"
+        _lib.call(fn, _lib.ptr(x), N, per, float(self.params[0]), _lib.ptr(per_img), self.seed, off,
+                  elem_base, _lib.ptr(out), _lib.stream_of(x))
         return out
 
 

@@ -145,6 +145,14 @@ dn_status dn_n2n_subimage_from_mask(const float* img, int N, int C, int H, int W
 dn_status dn_add_gauss_noise(const float* clean, int N, int64_t per_image, float std_,
                              const float* std_per_image, uint64_t seed, uint64_t offset,
                              uint64_t elem_base, float* noisy, void* stream);
+/* Poisson noise, train.py:102-111 (AugmentNoise poisson_fix / poisson_range; replaces
+   torch.poisson(lam * x, generator) / lam): noisy = Poisson(lam * clean) / lam, lam per image
+   from lam_per_image when not null.  Counts by fp64 CDF inversion of one 53-bit Philox uniform
+   per element (same global-index stream convention as the Gaussian).  0 < lam <= 500 and clean
+   in [0, 1] (lam * clean <= 500). */
+dn_status dn_add_poisson_noise(const float* clean, int N, int64_t per_image, float lam,
+                               const float* lam_per_image, uint64_t seed, uint64_t offset,
+                               uint64_t elem_base, float* noisy, void* stream);
 
 /* ---- losses ------------------------------------------------------------------------ */
 /* N2N regularised loss, training_script.md:141-153.  out, sub2: [N,C,h,w]; den: [N,C,2h,2w]

@@ -121,6 +121,29 @@ def test_gauss_noise_matches_philox_oracle():
     assert np.abs(noisy.cpu().numpy() - ref).max() < 2e-6
 
 
+@pytest.mark.parametrize("per_image", [False, True])
+def test_poisson_noise_matches_philox_oracle(per_image):
+    """dn_add_poisson_noise (train.py:102-111) bit-exact against the oracle's sampler (same
+    Philox draws, same fp64 inversion), with one lam or one per image; and AugmentNoise's
+    poisson styles route to it."""
+    from image_denoising_amd import _lib
+    from image_denoising_amd.n2n import AugmentNoise
+    from oracle import philox
+
+    torch.manual_seed(1)
+    clean = torch.rand(3, 1, 40, 24, device=DEV)
+    lam_img = torch.tensor([5.0, 30.0, 50.0], device=DEV) if per_image else None
+    out = torch.empty_like(clean)
+    _lib.call("dn_add_poisson_noise", clean.data_ptr(), 3, clean[0].numel(), 30.0,
+              lam_img.data_ptr() if per_image else None, 21, 3, 0, out.data_ptr(),
+              torch.cuda.current_stream().cuda_stream)
+    ref = philox.poisson_noise(clean.cpu().numpy(), lam_img.cpu().numpy() if per_image else 30.0,
+                               seed=21, offset=3)
+    assert np.array_equal(out.cpu().numpy(), ref)
+    aug = AugmentNoise("poisson30", seed=21)
+    assert torch.equal(aug.add_train_noise(clean, offset=3), out) if not per_image else True
+
+
 # ---------------------------------------------------------------------------------------
 # op-level convolution kernels vs torch fp32 on the CPU
 # ---------------------------------------------------------------------------------------
