@@ -1,7 +1,8 @@
 """The N2N training step (training_script.md:128-155 with train.py's sub-sampler), fused on
 the HIP path with no host synchronisation:
 
-    noisy  = clean + sigma*N(0,1)                     dn_add_gauss_noise   (train.py:84-94)
+    noisy  = clean + sigma*N(0,1)                     dn_add_gauss_noise   (train.py:84-101)
+             (or Poisson(lam clean) / lam             dn_add_poisson_noise (train.py:102-111))
     sub1, sub2, rd = neighbour sub-sample(noisy)      dn_n2n_subsample     (train.py:141-190)
     den    = UNet(noisy)            [no grad]         dn_unet_forward      (arch_unet.py:194)
     out    = UNet(sub1)             [saved]           dn_unet_forward
@@ -21,7 +22,7 @@ import torch
 from . import _lib
 from . import dist as dp
 from .arch_unet import UNet
-from .n2n import n2n_loss, n2n_subsample
+from .n2n import AugmentNoise, n2n_loss, n2n_subsample
 from .optim import FlatAdam, lr_at_epoch
 from .util import structure_loss
 
@@ -29,13 +30,18 @@ from .util import structure_loss
 class N2NTrainer:
     def __init__(self, net: UNet, lr: float = 3e-4, n_epoch: int = 100,
                  increase_ratio: float = 2.0, gamma: float = 0.5, noise_std: float = 25.0 / 255.0,
-                 seed: int = 0, distributed: bool | None = None):
+                 seed: int = 0, distributed: bool | None = None, noise_style: str | None = None):
+        """noise_style: a train.py --noisetype ('gauss25', 'gauss5_50', 'poisson30',
+        'poisson5_50'); None = Gaussian of std noise_std.  Range styles draw one value per image
+        of the GLOBAL batch (seeded by the step), so a rank's shard sees the same values as the
+        single-process run."""
         self.net = net
         self.base_lr = lr
         self.n_epoch = n_epoch
         self.increase_ratio = increase_ratio
         self.gamma = gamma
         self.noise_std = noise_std
+        self.noise = AugmentNoise(noise_style) if noise_style else None
         self.seed = seed
         self.distributed = dp.is_distributed() if distributed is None else distributed
         self.world, self.rank = dp.world_and_rank() if self.distributed else (1, 0)
@@ -80,8 +86,18 @@ class N2NTrainer:
         elem_base, cell_base = dp.shard_bases(self.rank, N, C, H, W)
         if noisy is None:
             noisy = b["noisy"]
-            _lib.call("dn_add_gauss_noise", _lib.ptr(clean), N, C * H * W, float(self.noise_std),
-                      None, self.seed, 2 * step, elem_base, _lib.ptr(noisy), stream)
+            fn, val, per_img = "dn_add_gauss_noise", float(self.noise_std), None
+            if self.noise is not None:
+                if not self.noise.style.startswith("gauss"):
+                    fn = "dn_add_poisson_noise"
+                val = float(self.noise.params[0])
+                if self.noise.style.endswith("_range"):
+                    lo, hi = self.noise.params
+                    g = torch.Generator(device="cpu").manual_seed(self.seed * 1000003 + step)
+                    allv = torch.rand(N * self.world, generator=g) * (hi - lo) + lo
+                    per_img = allv[self.rank * N:(self.rank + 1) * N].to(clean.device)
+            _lib.call(fn, _lib.ptr(clean), N, C * H * W, val, _lib.ptr(per_img), self.seed, 2 * step,
+                      elem_base, _lib.ptr(noisy), stream)
         else:
             noisy = noisy.contiguous()
         sub1, sub2, rd = n2n_subsample(noisy, rd_idx, seed=self.seed + 1, offset=2 * step + 1,

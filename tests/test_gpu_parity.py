@@ -596,6 +596,34 @@ def test_n2n_step_deterministic(prec):
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("style", ["gauss25", "poisson30", "poisson5_50", "gauss5_50"])
+def test_n2n_step_noise_styles(style):
+    """N2NTrainer(noise_style=...) synthesises the step's noisy batch with the chosen train.py
+    --noisetype (gauss25 equal to the default noise_std path) and steps on it."""
+    from image_denoising_amd import N2NTrainer
+    from oracle import philox
+
+    clean = torch.rand(4, 1, 64, 64, device=DEV)
+    tr = N2NTrainer(_net(1, "fp32_x6"), seed=5, noise_style=style)
+    loss3 = tr.train_step(clean, epoch=1)
+    noisy = tr._bufs[next(iter(tr._bufs))]["noisy"].cpu()
+    assert np.isfinite(loss3.cpu().numpy()).all()
+    if style == "gauss25":
+        tr0 = N2NTrainer(_net(1, "fp32_x6"), seed=5)
+        tr0.train_step(clean, epoch=1)
+        assert torch.equal(tr0._bufs[next(iter(tr0._bufs))]["noisy"].cpu(), noisy)
+    elif style == "poisson30":
+        ref = philox.poisson_noise(clean.cpu().numpy(), 30.0, seed=5, offset=0)
+        assert np.array_equal(noisy.numpy(), ref)
+    elif style == "poisson5_50":  # one lam per image of the global batch, seeded by the step
+        g = torch.Generator(device="cpu").manual_seed(5 * 1000003 + 0)
+        lam = (torch.rand(4, generator=g) * (50.0 - 5.0) + 5.0).numpy()
+        ref = philox.poisson_noise(clean.cpu().numpy(), lam, seed=5, offset=0)
+        assert np.array_equal(noisy.numpy(), ref)
+    else:
+        assert float((noisy - clean.cpu()).std()) > 0.0
+
+
 @pytest.mark.parametrize("prec", PRECS)
 def test_config1_full_size_step_properties(prec):
     """BASELINE config 1 (bs=64, 256x256x1): one full N2N step; per-image independence lets a
