@@ -995,229 +995,190 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
 
 
 // ------------------------------------------------------------------------------------
-// 3x3 weight gradient at fp32 accuracy on the bf16 matrix cores (96 output channels).
-// GEMM M = 96 output channels, N = 32 input channels x 9 taps, K = pixels; workgroup = 3 x 2
-// waves, wave (wm, wn) owns output fragments {2wm, 2wm+1} x input channels [16wn, 16wn+16)
-// x 9 taps.  One K stage = 32 pixels (a 32-wide row segment, or 2 / 4 rows of 16 / 8 pixels)
-// = ONE v_mfma_f32_16x16x32_bf16 K block: lane group g holds stage pixels 8g..8g+7.
-// Operands are loaded into registers (float4 along channels) one stage ahead, then split once
-// into three bf16 planes and transposed into LDS with the pixel index contiguous:
-//   G  [plane][co][k]                          (64-B rows, 16-B quads XOR-swizzled)
-//   X  [dx][plane][row][ci][col]  col = k - dx  (one copy per horizontal tap, so every
-//                                                operand read is one aligned ds_read_b128)
-// and each (fragment, tap) runs the six piece products of x6_block, summed from zero and
-// added to the fp32 accumulators (no long-sum rounding bias; see x6_block).
+// 3x3 weight gradient at fp32 accuracy on the bf16 matrix cores (k_wgrad3s: 96 or 48 output
+// channels).  GEMM M = output channels, N = input channels x 9 taps, K = pixels.  The staging
+// is the fp32 k_wgrad3's (conv.hip): each 32-pixel K stage of the gradient G [px][Cout] and of
+// the input X [(sh+2) rows][sw+2][CIB] (halo included) is copied by per-lane global_load_lds
+// into double-buffered LDS, one barrier per stage -- no staging registers.  The split happens
+// at the operand read: a lane's 8 K values (stage pixels 4j + lg, j < 8: any K order serves
+// when A and B use the same one, and this one keeps the ds_read_b32 conflict-free and the
+// addresses immediate offsets of one per-lane base) are read as fp32, split into three bf16
+// pieces in registers, and each (output fragment, tap) runs the six piece products of x6_block
+// from zero, added to the fp32 accumulators.  Wave (wm, wn): MFW output-channel fragments x 16
+// input channels x 9 taps; the bias gradient is the G pieces against a ones fragment.
 // ------------------------------------------------------------------------------------
-template <int SWL>
-struct Wx6Cfg {
-  static constexpr int SW = 1 << SWL, SH = 32 >> SWL, RH = SH + 2, XW = SW + 2;
-  static constexpr int COUT = 96, CIB = 32, MFW = 2, WM = 3, WN = 2, NTHR = 64 * WM * WN;
-  static constexpr int GPL = COUT * 32;                  // bf16 per G plane
-  static constexpr int XPL = RH * CIB * SW;              // bf16 per X plane (one dx copy)
-  static constexpr int XITEMS = (CIB / 4) * RH * (XW / 2);  // (ci quad, row, column pair)
-  static constexpr int XI = (XITEMS + NTHR - 1) / NTHR;
-  static constexpr int LBYTES = 2 * (3 * GPL + 9 * XPL);
-  static_assert(16 * (COUT / 4) == NTHR, "one G item (channel quad, pixel pair) per thread");
+template <int CO_FR, int WM, int WN>
+struct Ws3Cfg {
+  static constexpr int COUT = 16 * CO_FR, MFW = CO_FR / WM, CIB = 16 * WN;
+  static constexpr int NW = WM * WN, NTHR = 64 * NW;
+  static constexpr int PC = 32, XW = PC + 2, XH = 3;
+  static constexpr int LGF = PC * COUT;                          // G floats per stage
+  static constexpr int LXF = (XH * XW * CIB + 255) / 256 * 256;  // X floats per stage
+  static constexpr int LGP = LGF / 256, LXP = LXF / 256;         // 1 KiB DMA pieces
+  static constexpr int LBUF = LGF + LXF;
+  static_assert(LGF % 256 == 0, "G stage must be whole 1 KiB pieces");
 };
 
-template <int SWL>
-__global__ __launch_bounds__(384, 3) void k_wgrad3x6(WgradArgs a0) {
-  using C = Wx6Cfg<SWL>;
+template <int CO_FR, int WM, int WN, int SWL>
+__global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
+  using C = Ws3Cfg<CO_FR, WM, WN>;
+  constexpr int MFW = C::MFW;
   const WgradArgs a = wg_block(a0);
-  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
-  __bf16* lg = reinterpret_cast<__bf16*>(lds_raw);
-  __bf16* lx = lg + 3 * C::GPL;
+  __shared__ __attribute__((aligned(16))) float lds[2 * C::LBUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / C::WN, wn = wave % C::WN;
-  const int li = lane & 15, lgp = lane >> 4;
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 15, lg = lane >> 4;
   const int ci0 = blockIdx.y * C::CIB;
-  constexpr int sw = C::SW, sh = C::SH;
+  // K stage = 32 pixels: one row segment of 32, or 32/sw whole rows of sw pixels (narrow levels)
+  constexpr int sw = 1 << SWL, sh = C::PC >> SWL, xw = sw + 2;
+  static_assert(sw >= 4, "a lane's pixels 4j + lg stay in one stage row per j");
   const int ux = (a.KW + sw - 1) / sw, uy = (a.KH + sh - 1) / sh;
   const long U = (long)a.N * uy * ux;
   const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
   const bool do_bias = a.bias && blockIdx.y == 0 && wn == 0;
 
-  f32x4 acc[9][C::MFW][1];
-  f32x4 accb[C::MFW];
+  f32x4 acc[9][MFW][1];
+  f32x4 accb[MFW][1];
 #pragma unroll
-  for (int i = 0; i < C::MFW; ++i) {
-    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < MFW; ++i) {
+    accb[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[t][i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-
-  // this thread's G item: output-channel quad gq, stage pixel pair (2gk, 2gk+1)
-  const int gq = tid % (C::COUT / 4), gk = tid / (C::COUT / 4);
-  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  f32x4 rg[2], rx[C::XI][2];
-
-  auto load = [&](long u) {
+  auto glds = [](const float* g, float* l) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+  };
+  auto issue = [&](long u, float* buf) {
     const int n = (int)(u / ((long)uy * ux));
     const int rem = (int)(u - (long)n * uy * ux);
     const int py0 = (rem / ux) * sh, px0 = (rem % ux) * sw;
-    const float* gb = a.g + (long)n * a.KH * a.KW * a.g_stride + a.g_off + 4 * gq;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int k = 2 * gk + j;
-      const int gy = py0 + (k >> SWL), gx = px0 + (k & (sw - 1));
-      rg[j] = (gy < a.KH && gx < a.KW)
-                  ? *reinterpret_cast<const f32x4*>(gb + ((long)gy * a.KW + gx) * a.g_stride)
-                  : z4;
+    const float* gb = a.g + (long)n * a.KH * a.KW * a.g_stride + a.g_off;
+    for (int p = wave; p < C::LGP; p += C::NW) {
+      const int idx = p * 256 + lane * 4;
+      const int px = idx / C::COUT, co = idx - px * C::COUT;
+      const int gy = py0 + (px >> SWL), gx = px0 + (px & (sw - 1));
+      const float* src = (gy < a.KH && gx < a.KW && co < a.Cout)
+                             ? gb + ((long)gy * a.KW + gx) * a.g_stride + co : a.zeros;
+      glds(src, buf + p * 256);
     }
     const float* xb = a.x + (long)n * a.KH * a.KW * a.x_stride + a.x_off;
-#pragma unroll
-    for (int q = 0; q < C::XI; ++q) {
-      const int it = tid + q * C::NTHR;
-      const int cq = it % (C::CIB / 4), rest = it / (C::CIB / 4);
-      const int r = rest / (C::XW / 2), cp = rest % (C::XW / 2);
-      const int gy = py0 - 1 + r, ci = ci0 + 4 * cq;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int gx = px0 - 1 + 2 * cp + j;
-        const bool ok = it < C::XITEMS && gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW &&
-                        ci < a.Cin;
-        rx[q][j] = ok ? *reinterpret_cast<const f32x4*>(xb + ((long)gy * a.KW + gx) * a.x_stride + ci)
-                      : z4;
-      }
+    const int xpix = (sh + 2) * xw;
+    for (int p = wave; p < C::LXP; p += C::NW) {
+      const int idx = p * 256 + lane * 4;
+      const int px = idx / C::CIB, q = idx - px * C::CIB;
+      const int yy = px / xw, xx = px - yy * xw;
+      const int gy = py0 - 1 + yy, gx = px0 - 1 + xx, ci = ci0 + q;
+      const bool ok = px < xpix && gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW && ci < a.Cin;
+      const float* src = ok ? xb + ((long)gy * a.KW + gx) * a.x_stride + ci : a.zeros;
+      glds(src, buf + C::LGF + p * 256);
     }
   };
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
 
-  auto store = [&]() {
-    unsigned* lgw = reinterpret_cast<unsigned*>(lg);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {  // G: [plane][co][k], pair (2gk, 2gk+1) = one 32-bit word
-      const int co = 4 * gq + c, k = 2 * gk;
-      unsigned w[3];
-      split3x2(rg[0][c], rg[1][c], w[0], w[1], w[2]);
-      const int off = co * 32 + x6_swz(co, k >> 3) * 8 + (k & 7);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) lgw[(p * C::GPL + off) >> 1] = w[p];
-    }
-#pragma unroll
-    for (int q = 0; q < C::XI; ++q) {
-      const int it = tid + q * C::NTHR;
-      if (it >= C::XITEMS) continue;
-      const int cq = it % (C::CIB / 4), rest = it / (C::CIB / 4);
-      const int r = rest / (C::XW / 2), cp = rest % (C::XW / 2);
-      const int c0 = 2 * cp;  // halo columns c0, c0 + 1 -> k = c - dx in copy dx
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int row = r * C::CIB + 4 * cq + c;
-        unsigned w[3];
-        split3x2(rx[q][0][c], rx[q][1][c], w[0], w[1], w[2]);
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx) {
-#pragma unroll
-          for (int p = 0; p < 3; ++p) {
-            __bf16* dst = lx + (dx * 3 + p) * C::XPL;
-            const int k0 = c0 - dx;  // even for dx = 0, 2
-            auto at = [&](int k) {
-              return SWL == 5 ? row * 32 + x6_swz(row, k >> 3) * 8 + (k & 7) : row * sw + k;
-            };
-            if (dx != 1) {
-              if (k0 >= 0 && k0 + 1 < sw) reinterpret_cast<unsigned*>(dst)[at(k0) >> 1] = w[p];
-            } else {
-              const unsigned short lo = (unsigned short)(w[p] & 0xffffu);
-              const unsigned short hi = (unsigned short)(w[p] >> 16);
-              if (k0 >= 0) reinterpret_cast<unsigned short*>(dst)[at(k0)] = lo;
-              if (k0 + 1 < sw) reinterpret_cast<unsigned short*>(dst)[at(k0 + 1)] = hi;
-            }
-          }
-        }
-      }
-    }
-  };
-
-  if (u_beg < u_end) load(u_beg);
+  if (u_beg < u_end) issue(u_beg, lds);
+  __syncthreads();
   for (long u = u_beg; u < u_end; ++u) {
-    __syncthreads();  // everyone done reading the previous stage
-    store();
-    __syncthreads();
-    bf16x8 av[3][C::MFW];
+    const int cb = (int)((u - u_beg) & 1);
+    const float* lgs = lds + cb * C::LBUF;
+    const float* lxs = lgs + C::LGF;
+    if (u + 1 < u_end) issue(u + 1, lds + (cb ^ 1) * C::LBUF);
+    // A: the wave's MFW gradient fragments, K value j = stage pixel 4j + lg
+    bf16x8 av[3][MFW];
 #pragma unroll
-    for (int i = 0; i < C::MFW; ++i) {
-      const int co = (wm * C::MFW + i) * 16 + li;
+    for (int i = 0; i < MFW; ++i) {
+      float v[8];
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
-        av[p][i] = *reinterpret_cast<const bf16x8*>(lg + p * C::GPL + co * 32 + x6_swz(co, lgp) * 8);
+      for (int j = 0; j < 8; ++j) v[j] = lgs[(4 * j + lg) * C::COUT + (wm * MFW + i) * 16 + li];
+      split3x8(v, av[0][i], av[1][i], av[2][i]);
     }
-    if (do_bias) {  // sum over pixels: the G pieces against ones (exact in bf16)
-      bf16x8 one;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) one[e] = (__bf16)1.0f;
-#pragma unroll
-      for (int i = 0; i < C::MFW; ++i) {
-        const f32x4 hi = mfma_bf16(av[0][i], one, z4);
-        f32x4 lo = mfma_bf16(av[1][i], one, z4);
-        lo = mfma_bf16(av[2][i], one, lo);
-        accb[i] += hi + lo;
-      }
-    }
-    // lane group lgp holds stage pixels 8lgp..8lgp+7: row r0, columns c0.. (within one row)
-    const int k0 = 8 * lgp, r0 = k0 >> SWL, c0 = k0 & (sw - 1);
-    const int ci = wn * 16 + li;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      const int row = (r0 + t / 3) * C::CIB + ci;
-      const int off = SWL == 5 ? row * 32 + x6_swz(row, lgp) * 8 : row * sw + c0;
-      bf16x8 bv[3][1];
+      const int ky = t / 3, kx = t - 3 * ky;
+      float v[8];
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
-        bv[p][0] = *reinterpret_cast<const bf16x8*>(lx + ((t % 3) * 3 + p) * C::XPL + off);
-      x6_block<C::MFW, 1, 1>(acc[t], av, bv);
-      // keep the scheduler from interleaving taps: each tap's fresh hi / lo sums would stay
-      // live across the others and spill (two lo chains per tap are enough in flight)
-      __builtin_amdgcn_sched_barrier(0);
+      for (int j = 0; j < 8; ++j) {
+        // (4j + lg) >> SWL == (4j) >> SWL and (4j + lg) & (sw - 1) == ((4j) & (sw - 1)) + lg
+        const int pr = (4 * j) >> SWL, pcc = ((4 * j) & (sw - 1)) + lg;
+        v[j] = lxs[((pr + ky) * xw + pcc + kx) * C::CIB + wn * 16 + li];
+      }
+      bf16x8 bv[3][1];
+      split3x8(v, bv[0][0], bv[1][0], bv[2][0]);
+      x6_block<MFW, 1, 1>(acc[t], av, bv);
+      // the tap's running sums materialised here (a deferred add keeps its MFMA results live)
+#pragma unroll
+      for (int i = 0; i < MFW; ++i) asm volatile("" : "+v"(acc[t][i][0]));
     }
-    if (u + 1 < u_end) load(u + 1);  // in flight while the other workgroup computes
+    if (do_bias) {
+#pragma unroll
+      for (int i = 0; i < MFW; ++i) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 hi = mfma_bf16(av[0][i], ones, z);
+        f32x4 lo = mfma_bf16(av[1][i], ones, z);
+        lo = mfma_bf16(av[2][i], ones, lo);
+        accb[i][0] += hi + lo;
+      }
+    }
+    __syncthreads();  // next stage landed (vmcnt(0)); everyone done with this buffer
   }
 
   float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
-  const int cio = ci0 + wn * 16 + li;
+  const int ci = ci0 + wn * 16 + li;
   const int cot = a.cout_total ? a.cout_total : a.Cout;
 #pragma unroll
-  for (int i = 0; i < C::MFW; ++i)
+  for (int i = 0; i < MFW; ++i)
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = (wm * C::MFW + i) * 16 + 4 * lgp + r;
-        if (cio < a.Cin)
-          slab[((long)(a.co_base + co) * a.cin_total + a.ci_base + cio) * 9 + t] = acc[t][i][0][r];
+        const int co = (wm * MFW + i) * 16 + 4 * lg + r;
+        if (co < a.Cout && ci < a.Cin)
+          slab[((long)(a.co_base + co) * a.cin_total + a.ci_base + ci) * 9 + t] = acc[t][i][0][r];
       }
   if (do_bias && li == 0) {
 #pragma unroll
-    for (int i = 0; i < C::MFW; ++i)
+    for (int i = 0; i < MFW; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = (wm * C::MFW + i) * 16 + 4 * lgp + r;
-        slab[(long)cot * a.cin_total * 9 + a.co_base + co] = accb[i][r];
+        const int co = (wm * MFW + i) * 16 + 4 * lg + r;
+        if (co < a.Cout) slab[(long)cot * a.cin_total * 9 + a.co_base + co] = accb[i][0][r];
       }
   }
 }
 
-// 96 output channels, 16-byte aligned NHWC views whose channel quads stay inside each pixel,
-// rows at least 8 wide (a lane's 8 K values must lie in one row)
+// 96 or 48 output channels, Cin >= 32, 16-byte aligned NHWC views whose channel quads stay
+// inside each pixel (the staging of k_wgrad3)
 bool wgrad3_x6_ok(const WgradArgs& a) {
-  if (a.Cout != 96 || a.Cin < 32 || a.KW < 8 || !a.zeros) return false;
+  if ((a.Cout != 96 && a.Cout != 48) || a.Cin < 32 || !a.zeros || a.zc > 0) return false;
   if ((a.g_stride | a.g_off | a.x_stride | a.x_off) & 3) return false;
-  return a.x_off + ((a.Cin + 3) & ~3) <= a.x_stride && a.g_off + 96 <= a.g_stride;
+  return a.x_off + ((a.Cin + 3) & ~3) <= a.x_stride;
 }
 
 // two workgroups per CU: splits x input-channel blocks fill one round of 512
 int wgrad_splits_x6(const WgradArgs& a, int splits) {
   if (!wgrad3_x6_ok(a)) return splits;
-  const int cap = 512 / ((a.Cin + 31) / 32);
+  const int cib = a.Cout == 96 ? 32 : 48;
+  const int cap = 512 / ((a.Cin + cib - 1) / cib);
   return splits < cap ? splits : (cap < 1 ? 1 : cap);
 }
 
-hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s) {
-  const dim3 grid(splits, (a.Cin + 31) / 32, 1);
-  if (a.KW >= 32) hipLaunchKernelGGL(k_wgrad3x6<5>, grid, dim3(384), 0, s, a);
-  else if (a.KW >= 16) hipLaunchKernelGGL(k_wgrad3x6<4>, grid, dim3(384), 0, s, a);
-  else hipLaunchKernelGGL(k_wgrad3x6<3>, grid, dim3(384), 0, s, a);
+template <int CO_FR, int WM, int WN>
+static hipError_t run_wgrad3s(const WgradArgs& a, int splits, hipStream_t s) {
+  using C = Ws3Cfg<CO_FR, WM, WN>;
+  const dim3 grid(splits, (a.Cin + C::CIB - 1) / C::CIB, 1), block(C::NTHR);
+  if (a.KW >= 32) hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 5>), grid, block, 0, s, a);
+  else if (a.KW >= 16) hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 4>), grid, block, 0, s, a);
+  else if (a.KW >= 8) hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 3>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 2>), grid, block, 0, s, a);
   return hipGetLastError();
+}
+
+hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s) {
+  if (!wgrad3_x6_ok(a)) return hipErrorInvalidValue;
+  return a.Cout == 96 ? run_wgrad3s<6, 2, 2>(a, splits, s) : run_wgrad3s<3, 1, 3>(a, splits, s);
 }
 
 // ------------------------------------------------------------------------------------

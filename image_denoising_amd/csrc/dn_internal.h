@@ -243,7 +243,7 @@ bool deconv_dgrad_x6_ok(const FwdArgs& a);
 hipError_t launch_deconv_dgrad_x6(const FwdArgs& a, const void* wimg, hipStream_t s);
 int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
 hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s, bool x6 = false);
-// bf16x6 3x3 weight gradient (conv_x6.hip): 96 outputs, Cin >= 32, rows >= 8 wide
+// bf16x6 3x3 weight gradient (conv_x6.hip, k_wgrad3s): 96 or 48 outputs, Cin >= 32
 bool wgrad3_x6_ok(const WgradArgs& a);
 int wgrad_splits_x6(const WgradArgs& a, int splits);  // split count when the x6 kernel is taken
 hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s);

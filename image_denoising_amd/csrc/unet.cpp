@@ -603,9 +603,9 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
 dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* dx,
                         float* ws, hipStream_t s, int prec) {
   const bool x6 = prec == DN_PREC_FP32_X6;
-  // bf16x6 3x3 weight gradients (k_wgrad3x6) only on request (DN_X6_WGRAD=1): measured slower
-  // than the fp32 k_wgrad3 in the step (37.5 vs 33.2 ms)
-  static const bool x6w_env = getenv("DN_X6_WGRAD") && atoi(getenv("DN_X6_WGRAD")) != 0;
+  // bf16x6 3x3 weight gradients (k_wgrad3s, split at the operand read); DN_X6_WGRAD=0 keeps the
+  // fp32 k_wgrad3 (A/B: 26.7 vs 27.9 ms per step)
+  static const bool x6w_env = !getenv("DN_X6_WGRAD") || atoi(getenv("DN_X6_WGRAD")) != 0;
   const bool x6w = x6 && x6w_env;
   const int N = p.N, nf = p.nf, C = p.C;
   auto H = [&](int l) { return p.H >> l; };

@@ -176,12 +176,13 @@ def _wgrad(dz, x, x6):
     return dwb.cpu().numpy()
 
 
-# k_wgrad3<6, 3, 2, *, X6>: 96 outputs; 32-wide rows and the 16/8/4-wide multi-row K stages;
+# k_wgrad3s (split at the operand read): 96 / 48 outputs; 32-wide rows and the 16/8/4-wide
+# multi-row K stages;
 # Cin 96 / 144 (concat) / 48 / 97 (a partial 32-channel block); long pixel sums (64 x 128^2)
 @pytest.mark.parametrize("cin,cout,N,H,W", [
     (96, 96, 2, 32, 32), (144, 96, 2, 16, 32), (48, 96, 2, 64, 64), (97, 96, 1, 32, 32),
     (96, 96, 4, 16, 16), (96, 96, 8, 8, 8), (96, 96, 16, 4, 4), (96, 96, 64, 128, 128),
-    (48, 48, 2, 32, 32),  # 48 outputs: the fp32 kernel behind the same entry point
+    (48, 48, 2, 32, 32), (144, 48, 4, 16, 16), (48, 48, 64, 128, 128),  # 48 outputs
 ])
 def test_x6_backward_weight_vs_fp64(cin, cout, N, H, W):
     g = torch.Generator().manual_seed(7)
