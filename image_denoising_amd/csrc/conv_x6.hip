@@ -996,27 +996,28 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
 
 // ------------------------------------------------------------------------------------
 // 3x3 weight gradient at fp32 accuracy on the bf16 matrix cores (k_wgrad3s: 96 or 48 output
-// channels).  GEMM M = output channels, N = input channels x 9 taps, K = pixels.  The staging
-// is the fp32 k_wgrad3's (conv.hip): each 32-pixel K stage of the gradient G [px][Cout] and of
-// the input X [(sh+2) rows][sw+2][CIB] (halo included) is copied by per-lane global_load_lds
-// into double-buffered LDS, one barrier per stage -- no staging registers.  The split happens
-// at the operand read: a lane's 8 K values (stage pixels 4j + lg, j < 8: any K order serves
-// when A and B use the same one, and this one keeps the ds_read_b32 conflict-free and the
-// addresses immediate offsets of one per-lane base) are read as fp32, split into three bf16
-// pieces in registers, and each (output fragment, tap) runs the six piece products of x6_block
-// from zero, added to the fp32 accumulators.  Wave (wm, wn): MFW output-channel fragments x 16
-// input channels x 9 taps; the bias gradient is the G pieces against a ones fragment.
+// channels).  GEMM M = output channels, N = input channels x 9 taps, K = pixels.  Each 32-pixel
+// K stage of the gradient G [px][GS] and of the input X [(sh+2) rows][sw+2][XS] (halo included;
+// GS / XS = channels + 4, so lane groups 8 pixels apart fall on opposite bank halves) is copied
+// by per-lane global_load_lds into double-buffered LDS (padding slots load zeros), one barrier
+// per stage -- no staging registers.  The split happens at the operand read: lane group lg's 8 K
+// values are the stage pixels 8lg .. 8lg+7, read as fp32 and split into three bf16 pieces in
+// registers.  For X that makes the three horizontal taps of a kernel row sliding windows of ONE
+// 10-pixel read: kx = 0 and 2 are whole-register offsets of its split pieces, kx = 1 a 16-bit
+// funnel shift.  Each (output fragment, tap) runs the six piece products of x6_block from zero,
+// added to the fp32 accumulators.  Wave (wm, wn): MFW output-channel fragments x 16 input
+// channels x 9 taps; the bias gradient is the G pieces against a ones fragment.
 // ------------------------------------------------------------------------------------
 template <int CO_FR, int WM, int WN>
 struct Ws3Cfg {
   static constexpr int COUT = 16 * CO_FR, MFW = CO_FR / WM, CIB = 16 * WN;
   static constexpr int NW = WM * WN, NTHR = 64 * NW;
-  static constexpr int PC = 32, XW = PC + 2, XH = 3;
-  static constexpr int LGF = PC * COUT;                          // G floats per stage
-  static constexpr int LXF = (XH * XW * CIB + 255) / 256 * 256;  // X floats per stage
-  static constexpr int LGP = LGF / 256, LXP = LXF / 256;         // 1 KiB DMA pieces
+  static constexpr int PC = 32, GS = COUT + 4, XS = CIB + 4;
+  static constexpr int XPIX = 3 * 34;                              // widest stage: 3 rows x 34
+  static constexpr int LGF = (PC * GS + 255) / 256 * 256;          // G floats per stage
+  static constexpr int LXF = (XPIX * XS + 255) / 256 * 256;        // X floats per stage
+  static constexpr int LGP = LGF / 256, LXP = LXF / 256;           // 1 KiB DMA pieces
   static constexpr int LBUF = LGF + LXF;
-  static_assert(LGF % 256 == 0, "G stage must be whole 1 KiB pieces");
 };
 
 template <int CO_FR, int WM, int WN, int SWL>
@@ -1030,9 +1031,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
   const int wm = wave / WN, wn = wave % WN;
   const int li = lane & 15, lg = lane >> 4;
   const int ci0 = blockIdx.y * C::CIB;
-  // K stage = 32 pixels: one row segment of 32, or 32/sw whole rows of sw pixels (narrow levels)
+  // K stage = 32 pixels: one row segment of 32, or 32/sw whole rows of sw >= 8 pixels
   constexpr int sw = 1 << SWL, sh = C::PC >> SWL, xw = sw + 2;
-  static_assert(sw >= 4, "a lane's pixels 4j + lg stay in one stage row per j");
+  static_assert(sw >= 8, "a lane group's 8 K pixels lie in one stage row");
   const int ux = (a.KW + sw - 1) / sw, uy = (a.KH + sh - 1) / sh;
   const long U = (long)a.N * uy * ux;
   const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
@@ -1057,9 +1058,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
     const float* gb = a.g + (long)n * a.KH * a.KW * a.g_stride + a.g_off;
     for (int p = wave; p < C::LGP; p += C::NW) {
       const int idx = p * 256 + lane * 4;
-      const int px = idx / C::COUT, co = idx - px * C::COUT;
+      const int px = idx / C::GS, co = idx - px * C::GS;
       const int gy = py0 + (px >> SWL), gx = px0 + (px & (sw - 1));
-      const float* src = (gy < a.KH && gx < a.KW && co < a.Cout)
+      const float* src = (px < C::PC && co < a.Cout && gy < a.KH && gx < a.KW)
                              ? gb + ((long)gy * a.KW + gx) * a.g_stride + co : a.zeros;
       glds(src, buf + p * 256);
     }
@@ -1067,10 +1068,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
     const int xpix = (sh + 2) * xw;
     for (int p = wave; p < C::LXP; p += C::NW) {
       const int idx = p * 256 + lane * 4;
-      const int px = idx / C::CIB, q = idx - px * C::CIB;
+      const int px = idx / C::XS, q = idx - px * C::XS;
       const int yy = px / xw, xx = px - yy * xw;
       const int gy = py0 - 1 + yy, gx = px0 - 1 + xx, ci = ci0 + q;
-      const bool ok = px < xpix && gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW && ci < a.Cin;
+      const bool ok = px < xpix && q < C::CIB && gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW &&
+                      ci < a.Cin;
       const float* src = ok ? xb + ((long)gy * a.KW + gx) * a.x_stride + ci : a.zeros;
       glds(src, buf + C::LGF + p * 256);
     }
@@ -1078,6 +1080,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
   bf16x8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+  // this lane group's 8 K pixels: stage row pr0, columns pc0 .. pc0 + 7
+  const int pr0 = (8 * lg) >> SWL, pc0 = (8 * lg) & (sw - 1);
 
   if (u_beg < u_end) issue(u_beg, lds);
   __syncthreads();
@@ -1086,31 +1090,45 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
     const float* lgs = lds + cb * C::LBUF;
     const float* lxs = lgs + C::LGF;
     if (u + 1 < u_end) issue(u + 1, lds + (cb ^ 1) * C::LBUF);
-    // A: the wave's MFW gradient fragments, K value j = stage pixel 4j + lg
+    // A: the wave's MFW gradient fragments
     bf16x8 av[3][MFW];
 #pragma unroll
     for (int i = 0; i < MFW; ++i) {
       float v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = lgs[(4 * j + lg) * C::COUT + (wm * MFW + i) * 16 + li];
+      for (int j = 0; j < 8; ++j) v[j] = lgs[(8 * lg + j) * C::GS + (wm * MFW + i) * 16 + li];
       split3x8(v, av[0][i], av[1][i], av[2][i]);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(av[p][i]));  // kept, not re-split per tap
     }
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int ky = t / 3, kx = t - 3 * ky;
-      float v[8];
+    for (int ky = 0; ky < 3; ++ky) {
+      // the kernel row's 10-pixel window, split once: P[plane][d] = pieces of pixels 2d, 2d+1
+      const float* xr = lxs + ((pr0 + ky) * xw + pc0) * C::XS + wn * 16 + li;
+      float w[10];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        // (4j + lg) >> SWL == (4j) >> SWL and (4j + lg) & (sw - 1) == ((4j) & (sw - 1)) + lg
-        const int pr = (4 * j) >> SWL, pcc = ((4 * j) & (sw - 1)) + lg;
-        v[j] = lxs[((pr + ky) * xw + pcc + kx) * C::CIB + wn * 16 + li];
+      for (int m = 0; m < 10; ++m) w[m] = xr[m * C::XS];
+      unsigned P[3][5];
+#pragma unroll
+      for (int d = 0; d < 5; ++d) split3x2(w[2 * d], w[2 * d + 1], P[0][d], P[1][d], P[2][d]);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        bf16x8 bv[3][1];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          u32x4_t q;
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+            q[d] = kx == 0 ? P[pl][d]
+                           : (kx == 2 ? P[pl][d + 1] : __builtin_amdgcn_alignbit(P[pl][d + 1], P[pl][d], 16));
+          bv[pl][0] = __builtin_bit_cast(bf16x8, q);
+        }
+        const int t = 3 * ky + kx;
+        x6_block<MFW, 1, 1>(acc[t], av, bv);
+        // the tap's running sums materialised here (a deferred add keeps its MFMA results live)
+#pragma unroll
+        for (int i = 0; i < MFW; ++i) asm volatile("" : "+v"(acc[t][i][0]));
       }
-      bf16x8 bv[3][1];
-      split3x8(v, bv[0][0], bv[1][0], bv[2][0]);
-      x6_block<MFW, 1, 1>(acc[t], av, bv);
-      // the tap's running sums materialised here (a deferred add keeps its MFMA results live)
-#pragma unroll
-      for (int i = 0; i < MFW; ++i) asm volatile("" : "+v"(acc[t][i][0]));
     }
     if (do_bias) {
 #pragma unroll
@@ -1149,10 +1167,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
   }
 }
 
-// 96 or 48 output channels, Cin >= 32, 16-byte aligned NHWC views whose channel quads stay
-// inside each pixel (the staging of k_wgrad3)
+// 96 or 48 output channels, Cin >= 32, rows >= 8 wide, 16-byte aligned NHWC views whose
+// channel quads stay inside each pixel (the staging of k_wgrad3)
 bool wgrad3_x6_ok(const WgradArgs& a) {
-  if ((a.Cout != 96 && a.Cout != 48) || a.Cin < 32 || !a.zeros || a.zc > 0) return false;
+  if ((a.Cout != 96 && a.Cout != 48) || a.Cin < 32 || a.KW < 8 || !a.zeros || a.zc > 0) return false;
   if ((a.g_stride | a.g_off | a.x_stride | a.x_off) & 3) return false;
   return a.x_off + ((a.Cin + 3) & ~3) <= a.x_stride;
 }
@@ -1171,8 +1189,7 @@ static hipError_t run_wgrad3s(const WgradArgs& a, int splits, hipStream_t s) {
   const dim3 grid(splits, (a.Cin + C::CIB - 1) / C::CIB, 1), block(C::NTHR);
   if (a.KW >= 32) hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 5>), grid, block, 0, s, a);
   else if (a.KW >= 16) hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 4>), grid, block, 0, s, a);
-  else if (a.KW >= 8) hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 3>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 2>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 3>), grid, block, 0, s, a);
   return hipGetLastError();
 }
 

@@ -45,6 +45,20 @@ def dgrad(cin, cout, H, x6):  # dx [N,H,H,cin] from dz [N,H,H,cout]
     return timeit(f)
 
 
+def wgrad(cin, cout, H, x6):  # dW, db from dz [N,H,H,cout] and x [N,H,H,cin] (+ the reduction)
+    dz = torch.randn(N, H, H, cout, device="cuda")
+    x = torch.randn(N, H, H, cin, device="cuda")
+    dwb = torch.empty(cout * cin * 9 + cout, device="cuda")
+    slab = _lib.scratch(_lib.lib().dn_conv2d_wgrad_slab_size(N, H, H, cin, cout, 3), "cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    head = (dz.data_ptr(), x.data_ptr(), cin, N, H, H, cin, cout)
+    if x6:
+        f = lambda: _lib.call("dn_conv2d_backward_weight_x6", *head, dwb.data_ptr(), slab.data_ptr(), st)
+    else:
+        f = lambda: _lib.call("dn_conv2d_backward_weight", *head, 3, dwb.data_ptr(), slab.data_ptr(), st)
+    return timeit(f)
+
+
 if __name__ == "__main__":
     shapes = [("fwd", 48, 48, H) for H in (256, 128, 64, 32, 16, 8)] + \
              [("fwd", 96, 96, H) for H in (256, 128, 64, 32, 16)] + \
