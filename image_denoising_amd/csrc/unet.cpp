@@ -8,6 +8,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 namespace dn {
 
@@ -600,6 +602,35 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
 // LeakyReLU' into their epilogue (mask = the layer input, which is the previous layer's
 // post-activation output); skip gradients are accumulated into the concat-gradient buffers.
 // ------------------------------------------------------------------------------------
+// The weight gradients of the backward run on a second stream (DN_BWD_STREAMS=0: one stream):
+// they only read gradients and forward activations that nothing later in the backward rewrites
+// (the accumulations into a concat gradient's skip slice touch channels no weight gradient
+// reads) and write their own slabs, so they overlap the data-gradient chain; each is forked
+// from the main stream after the kernel that produced its gradient, and the branch is joined
+// before the batched reduction.
+struct SideStream {
+  hipStream_t st = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+static SideStream* side_stream() {
+  static std::mutex mu;
+  static std::map<int, SideStream> per_device;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  SideStream& ss = per_device[dev];
+  if (!ss.st) {
+    if (hipStreamCreateWithFlags(&ss.st, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess) {
+      ss = SideStream{};
+      return nullptr;
+    }
+  }
+  return &ss;
+}
+
 dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* dx,
                         float* ws, hipStream_t s, int prec) {
   const bool x6 = prec == DN_PREC_FP32_X6;
@@ -662,6 +693,14 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   }
   RedBatch rb;  // every weight gradient's reduction, launched together at the end
   const float* Z = ws + p.zeros;
+  static const bool two_env = !getenv("DN_BWD_STREAMS") || atoi(getenv("DN_BWD_STREAMS")) != 0;
+  SideStream* side = two_env ? side_stream() : nullptr;
+  hipStream_t s2 = side ? side->st : s;
+  auto fork = [&]() -> hipError_t {  // the side stream continues after main's work so far
+    if (!side) return hipSuccess;
+    hipError_t e = hipEventRecord(side->fork, s);
+    return e != hipSuccess ? e : hipStreamWaitEvent(side->st, side->fork, 0);
+  };
   auto SL = [&](int i) { return ws + p.slab[i]; };
   // 3x3 data gradients: the fp32 kernel or the bf16x6 one
   auto conv_dgrad = [&](const View& dz, int Nn, int h, int w, int cout, const float* wp, int nout,
@@ -705,17 +744,22 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     h.npx = (long)N * H(0) * Wd(0);
     DN_TRY(launch_head_bwd(h, s));
   }
+  DN_TRY(fork());
   if (OC <= 4)
     DN_TRY(launch_wgrad_thin(dyv.p, dyv.stride, OC, ws + p.nb, (long)N * H(0) * Wd(0),
-                             SL(NINC) + 64, p.splits[NINC], G(NINC), s, &rb));
+                             SL(NINC) + 64, p.splits[NINC], G(NINC), s2, &rb));
   else
-    DN_TRY(wgrad(W_C1, dyv, V(p.nb, 96), N, H(0), Wd(0), OC, 96, G(NINC), SL(NINC), p.splits[NINC], s, false, Z, &rb));
+    DN_TRY(wgrad(W_C1, dyv, V(p.nb, 96), N, H(0), Wd(0), OC, 96, G(NINC), SL(NINC),
+                 p.splits[NINC], s2, false, Z, &rb));
+  DN_TRY(fork());
   DN_TRY(wgrad(W_C1, V(p.g_nb, 96), V(p.na, 96), N, H(0), Wd(0), 96, 96, G(NINB), SL(NINB),
-               p.splits[NINB], s, false, Z, &rb));
+               p.splits[NINB], s2, false, Z, &rb));
+  DN_TRY(fork());
   DN_TRY(wgrad(W_C1, V(p.g_na, 96), V(p.d1b, 96), N, H(0), Wd(0), 96, 96, G(NINA), SL(NINA),
-               p.splits[NINA], s, false, Z, &rb));
+               p.splits[NINA], s2, false, Z, &rb));
+  DN_TRY(fork());
   DN_TRY(wgrad(W_C3, V(p.g_d1b, 96), V(p.d1a, 96), N, H(0), Wd(0), 96, 96, G(D1B), SL(D1B),
-               p.splits[D1B], s, x6w, Z, &rb));
+               p.splits[D1B], s2, x6w, Z, &rb));
   DN_TRY(conv_dgrad(V(p.g_d1b, 96), N, H(0), Wd(0), 96, Wt(D1B), 96, 3, EPI_MASK,
                     V(p.d1a, 96), V(p.g_d1a, 96), s));
   // dec_conv1a weight gradient: the MFMA kernel over the up1 channels [0, 2nf) and the thin
@@ -731,7 +775,8 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     a.zeros = Z; a.slab = slab; a.slab_stride = n;
     a.wlayout = 0; a.cin_total = p.c1k; a.ci_base = 0; a.bias = 1;
     const int sp = x6w ? wgrad_splits_x6(a, p.splits[D1A]) : p.splits[D1A];
-    DN_TRY(launch_wgrad(W_C3, a, sp, s, x6w));
+    DN_TRY(fork());
+    DN_TRY(launch_wgrad(W_C3, a, sp, s2, x6w));
     RedJob j = red_job(slab, n, sp, 96L * 2 * nf * 9, G(D1A));  // W[co][ci < 2nf][t]
     j.ig = j.og = 2 * nf * 9;
     j.is1 = j.os1 = p.c1k * 9;
@@ -743,7 +788,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     const long nt = 96L * C * 9;
     const int st = enc0_wgrad_splits(N, H(0), Wd(0));
     DN_TRY(launch_wgrad_c3_thin(ws + p.g_d1a, 96, ws + p.xin, N, C, H(0), Wd(0), thin, nt, C, 0,
-                                0, st, s));
+                                0, st, s2));
     DN_TRY(launch_reduce_scatter(thin, nt, st, nt, G(D1A), 9L * C, 9L * p.c1k, 9L * 2 * nf, s,
                                  &rb));
   }
@@ -758,29 +803,34 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   for (int l = 1; l <= 4; ++l) {
     const int iu = up_idx[l - 1];  // deconv producing level l-1 from level l
     // deconv wgrad: x = d_l b (level l), dU at level l-1
+    DN_TRY(fork());
     DN_TRY(wgrad(W_UP2, dU, V(p.db[l], 2 * nf), N, H(l), Wd(l), 2 * nf, 2 * nf, G(iu), SL(iu),
-                 p.splits[iu], s, false, Z, &rb));
+                 p.splits[iu], s2, false, Z, &rb));
     DN_TRY(deconv_dgrad(dU, N, H(l), Wd(l), 2 * nf, iu, 2 * nf, V(p.db[l], 2 * nf), EPI_MASK,
                         V(p.g_db[l], 2 * nf), s));
     const int ia = da_idx[l], ib = ia + 1;
+    DN_TRY(fork());
     DN_TRY(wgrad(W_C3, V(p.g_db[l], 2 * nf), V(p.da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, 2 * nf,
-                 G(ib), SL(ib), p.splits[ib], s, x6w, Z, &rb));
+                 G(ib), SL(ib), p.splits[ib], s2, x6w, Z, &rb));
     DN_TRY(conv_dgrad(V(p.g_db[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ib), 2 * nf, 3,
                       EPI_MASK, V(p.da[l], 2 * nf), V(p.g_da[l], 2 * nf), s));
+    DN_TRY(fork());
     DN_TRY(wgrad(W_C3, V(p.g_da[l], 2 * nf), V(p.c[l], p.cs[l]), N, H(l), Wd(l), 2 * nf, p.cs[l],
-                 G(ia), SL(ia), p.splits[ia], s, x6w, Z, &rb));
+                 G(ia), SL(ia), p.splits[ia], s2, x6w, Z, &rb));
     DN_TRY(conv_dgrad(V(p.g_da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ia), p.cs[l], 3,
                       EPI_PLAIN, none, V(p.g_c[l], p.cs[l]), s));
     dU = V(p.g_c[l], p.cs[l], 0);  // [u_{l+1} grad | skip grad]
   }
   // up5: x = a6 (level 5), dU = g_c5[0:nf]
+  DN_TRY(fork());
   DN_TRY(wgrad(W_UP2, V(p.g_c[4], p.cs[4], 0), V(p.a6, nf), N, H(5), Wd(5), nf, nf, G(UP5), SL(UP5),
-               p.splits[UP5], s, false, Z, &rb));
+               p.splits[UP5], s2, false, Z, &rb));
   DN_TRY(deconv_dgrad(V(p.g_c[4], p.cs[4], 0), N, H(5), Wd(5), nf, UP5, nf, V(p.a6, nf),
                       EPI_MASK, V(p.g_a6, nf), s));
   // enc_conv6 (input p5, level 5)
+  DN_TRY(fork());
   DN_TRY(wgrad(W_C3, V(p.g_a6, nf), V(p.p5, nf), N, H(5), Wd(5), nf, nf, G(ENC6), SL(ENC6),
-               p.splits[ENC6], s, x6w, Z, &rb));
+               p.splits[ENC6], s2, x6w, Z, &rb));
   DN_TRY(conv_dgrad(V(p.g_a6, nf), N, H(5), Wd(5), nf, Wt(ENC6), nf, 3, EPI_PLAIN, none,
                     V(p.g_p5, nf), s));
   // pool5 backward -> g_a5 (level 4)
@@ -789,8 +839,9 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   for (int l = 4; l >= 1; --l) {
     const int li = ENC2 + (l - 1);
     const int skip = (l == 4) ? nf : 2 * nf;
+    DN_TRY(fork());
     DN_TRY(wgrad(W_C3, V(p.g_a[l], nf), V(p.c[l], p.cs[l], skip), N, H(l), Wd(l), nf, nf, G(li),
-                 SL(li), p.splits[li], s, x6w, Z, &rb));
+                 SL(li), p.splits[li], s2, x6w, Z, &rb));
     DN_TRY(conv_dgrad(V(p.g_a[l], nf), N, H(l), Wd(l), nf, Wt(li), nf, 3, EPI_ACCUM, none,
                       V(p.g_c[l], p.cs[l], skip), s));
     // pool_l backward: d p_l (skip slice) -> gradient of the level l-1 activation
@@ -803,12 +854,18 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     }
   }
   // enc_conv1 (input a0), enc_conv0 (input x = c1 slice; no data gradient needed)
+  DN_TRY(fork());
   DN_TRY(wgrad(W_C3, V(p.g_a1, nf), V(p.a0, nf), N, H(0), Wd(0), nf, nf, G(ENC1), SL(ENC1),
-               p.splits[ENC1], s, x6w, Z, &rb));
+               p.splits[ENC1], s2, x6w, Z, &rb));
   DN_TRY(conv_dgrad(V(p.g_a1, nf), N, H(0), Wd(0), nf, Wt(ENC1), nf, 3, EPI_MASK, V(p.a0, nf),
                     V(p.g_a0, nf), s));
+  DN_TRY(fork());
   DN_TRY(launch_enc0_wgrad(ws + p.g_a0, nf, ws + p.xin, N, C, H(0), Wd(0), SL(ENC0) + 64,
-                           p.splits[ENC0], G(ENC0), s, &rb));
+                           p.splits[ENC0], G(ENC0), s2, &rb));
+  if (side) {  // join the weight-gradient branch before the reduction reads the slabs
+    DN_TRY(hipEventRecord(side->join, s2));
+    DN_TRY(hipStreamWaitEvent(s, side->join, 0));
+  }
   DN_TRY(red_flush(rb, s));
   // dL/dx: the network input feeds enc_conv0 and (as pool0) dec_conv1a's last C channels
   if (dx)

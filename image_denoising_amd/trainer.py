@@ -17,6 +17,8 @@ noise and the mask pair of a patch do not depend on the world size.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -51,6 +53,17 @@ class N2NTrainer:
         self.grad = torch.zeros_like(net.flat_params)
         self.global_step = 0
         self._bufs = {}
+
+    _side = {}
+
+    @classmethod
+    def _side_stream(cls, device):
+        if os.environ.get("DN_STEP_STREAMS", "1") == "0" or torch.device(device).type != "cuda":
+            return None
+        st = cls._side.get(device)
+        if st is None:
+            st = cls._side[device] = torch.cuda.Stream(device=device)
+        return st
 
     def lambda_for(self, epoch: int) -> float:
         # training_script.md:148 Lambda = epoch / n_epoch * ratio
@@ -105,9 +118,20 @@ class N2NTrainer:
         self.last_rd = rd  # the step's per-cell pair choices (den is defined at those pixels)
         # no-grad full-resolution pass (training_script.md:141-142); the loss reads the denoised
         # image at the rd pair pixels only, so only those are produced (dn_unet_forward_n2n)
-        self.net._run_forward_n2n(noisy, b["den"], b["ws_den"], rd)
+        # It runs on a second stream beside the gradient pass's forward (separate workspaces,
+        # both only read the parameters); the loss waits for both.  DN_STEP_STREAMS=0: one stream.
+        side = self._side_stream(clean.device)
+        main = torch.cuda.current_stream(clean.device) if side is not None else None
+        if side is not None:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self.net._run_forward_n2n(noisy, b["den"], b["ws_den"], rd)
+        else:
+            self.net._run_forward_n2n(noisy, b["den"], b["ws_den"], rd)
         # gradient pass at half resolution (training_script.md:146)
         self.net._run_forward(sub1, b["out"], b["ws_grad"])
+        if side is not None:
+            main.wait_stream(side)
         loss3, dout = n2n_loss(b["out"], sub2, b["den"], rd, self.lambda_for(epoch))
         self.net._run_backward(dout, self.grad, b["ws_grad"], N, H // 2, W // 2)
         # RCCL all-reduce(sum) over xGMI, one per step; 1/world folded into Adam
