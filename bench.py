@@ -440,7 +440,7 @@ def main():
             "step_tflops": round(step_flops / (ms_step * 1e-3) / 1e12, 2),
             "step_frac_of_fp32_peak": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
             "roofline": {"bound": "mfma",
-                         "kernel": ("k_fwd_bf16<NT=6,MT=4> (96->96 3x3, bf16 MFMA)" if bf else
+                         "kernel": ("k_fwd_bf16p<NT=6,MT=4> (96->96 3x3, bf16 MFMA)" if bf else
                                     "k_c3x6p<NT=6> (dec_conv1b 96->96 3x3 @256^2, fp32 as 6 "
                                     "split-bf16 products; peak = bf16 dense / 6)" if x6 else
                                     "k_fwd<G_C3,NT=6,MT=4> (dec_conv1b 96->96 3x3 @256^2)"),

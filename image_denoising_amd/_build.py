@@ -14,15 +14,22 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
-BUILD = os.path.join(PKG, "_objs")
-LIB = os.path.join(PKG, "libdenoise_hip.so")
+# DN_BUILD_TAG=t + DN_EXTRA_CXXFLAGS: a variant library libdenoise_hip_t.so (objects in _objs_t)
+# for same-box A/B runs (DN_LIB_PATH selects it at load time); the default build has no tag
+TAG = os.environ.get("DN_BUILD_TAG", "")
+BUILD = os.path.join(PKG, "_objs" + (f"_{TAG}" if TAG else ""))
+LIB = os.path.join(PKG, "libdenoise_hip" + (f"_{TAG}" if TAG else "") + ".so")
 SOURCES = ["conv.hip", "conv_bf16.hip", "conv_x6.hip", "elementwise.hip", "first_layer.hip", "eval.hip", "adapter.hip", "iunet_ops.hip", "unet.cpp",
            "iunet.cpp", "capi.cpp"]
 HEADERS = ["dn_internal.h", "conv_epi.h", "x6_core.h", "philox.h", "unet.h", "iunet.h", "iunet_ops.h"]
 ARCH = os.environ.get("DN_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
-            "-Wno-unused-function", "-Wno-unused-variable"]
+            "-Wno-unused-function", "-Wno-unused-variable",
+            *os.environ.get("DN_EXTRA_CXXFLAGS", "").split()]
+# the bf16x6 kernels keep their fp32 adds scalar: the SLP vectorizer would pair them into
+# v_pk_add_f32, which costs more issue cycles beside MFMAs than the two adds (x6_core.h)
+FILE_FLAGS = {"conv_x6.hip": ["-fno-slp-vectorize"]}
 
 
 def source_hash() -> str:
@@ -50,7 +57,7 @@ def _compile(src: str, force: bool, src_hash: str) -> str:
     if not force and os.path.exists(o):
         if os.path.getmtime(o) >= max(os.path.getmtime(s), _newest_header()):
             return o
-    cmd = [HIPCC, *CXXFLAGS, "-x", "hip", "-c", s, "-o", o, f"-I{CSRC}",
+    cmd = [HIPCC, *CXXFLAGS, *FILE_FLAGS.get(src, []), "-x", "hip", "-c", s, "-o", o, f"-I{CSRC}",
            f"-I{os.path.join(ROOT, 'include')}", f'-DDN_SRC_HASH="{src_hash}"']
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

@@ -18,6 +18,8 @@
 namespace dn {
 
 constexpr int AD_T = 16;    // output tile edge
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 constexpr int AD_HID = 16;  // hidden channels (adapter.py:13 default, finetune.py --adapter_hidden)
 
 template <int C>
@@ -109,29 +111,46 @@ __global__ __launch_bounds__(256) void k_adapter_fwd(const float* __restrict__ p
   }
 }
 
+// Parameter-gradient tasks of a tile, each a kernel row of one sum (its three horizontal taps
+// share the row reads): dW1 (h, i, ky), dW2 (c, h, ky), then db1 (h) and db2 (c).  A task reads
+// 16-float rows as float4 / float2 vectors and sums in the pixel order q = 16 r + col.
 template <int C>
-__global__ __launch_bounds__(256) void k_adapter_bwd(const float* __restrict__ prm,
+struct AdTasks {
+  static constexpr int T1 = AD_HID * 2 * C * 3, T2 = C * AD_HID * 3, TB1 = AD_HID, TB2 = C;
+  static constexpr int NT = T1 + T2 + TB1 + TB2;
+  static constexpr int TPT = (NT + 255) / 256;  // tasks per thread
+};
+
+template <int C>
+__global__ __launch_bounds__(256, 3) void k_adapter_bwd(const float* __restrict__ prm,
                                                      const float* __restrict__ noisy,
                                                      const float* __restrict__ base,
                                                      const float* __restrict__ dout, int N, int H,
                                                      int W, float* __restrict__ slab) {
   using A = AdCfg<C>;
+  using T = AdTasks<C>;
   constexpr int XA = A::XE * A::XE, HA = A::HE * A::HE, TA = AD_T * AD_T;
-  __shared__ float sx[A::CI * XA];
-  __shared__ float sh[AD_HID * HA];
-  __shared__ float sdo[C * HA];
-  __shared__ float sdp[AD_HID * TA];
+  __shared__ __attribute__((aligned(16))) float sx[A::CI * XA];
+  __shared__ __attribute__((aligned(16))) float sh[AD_HID * HA];
+  __shared__ __attribute__((aligned(16))) float sdo[C * HA];
+  __shared__ __attribute__((aligned(16))) float sdp[AD_HID * TA];
   const int tid = threadIdx.x;
   const int tiles_x = (W + AD_T - 1) / AD_T, tiles_y = (H + AD_T - 1) / AD_T;
   const long ntiles = (long)N * tiles_x * tiles_y;
-  float acc[A::PPT];
+  float acc[T::TPT][3];
 #pragma unroll
-  for (int j = 0; j < A::PPT; ++j) acc[j] = 0.f;
+  for (int j = 0; j < T::TPT; ++j) acc[j][0] = acc[j][1] = acc[j][2] = 0.f;
 
   for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int n = (int)(tile / ((long)tiles_x * tiles_y));
     const int r = (int)(tile - (long)n * tiles_x * tiles_y);
     const int ty0 = (r / tiles_x) * AD_T, tx0 = (r % tiles_x) * AD_T;
+    // the weights re-read per tile (scalar loads): an opaque copy of the pointer keeps the
+    // compiler from hoisting all of them out of the tile loop into vector registers
+    const float* pw = prm;
+    asm volatile("" : "+s"(pw));
+    int tt = tid;  // likewise for the per-thread LDS addresses (hoisted, they spill for C = 3)
+    asm volatile("" : "+v"(tt));
     load_cat_tile<C>(noisy, base, n, H, W, ty0 - 2, tx0 - 2, sx);
     for (int e = tid; e < C * HA; e += 256) {  // dout with a 1-pixel halo, 0 outside the image
       const int c = e / HA, q = e - c * HA;
@@ -140,10 +159,10 @@ __global__ __launch_bounds__(256) void k_adapter_bwd(const float* __restrict__ p
                    ? dout[(((long)n * C + c) * H + gy) * W + gx] : 0.f;
     }
     __syncthreads();
-    hidden_tile<C>(prm, sx, H, W, ty0 - 1, tx0 - 1, sh);
+    hidden_tile<C>(pw, sx, H, W, ty0 - 1, tx0 - 1, sh);
     __syncthreads();
     {  // d pre-activation of the hidden layer at the tile's own pixels
-      const int qy = tid / AD_T, qx = tid % AD_T;
+      const int qy = tt / AD_T, qx = tt % AD_T;
 #pragma unroll 2
       for (int h = 0; h < AD_HID; ++h) {
         float g = 0.f;
@@ -151,48 +170,92 @@ __global__ __launch_bounds__(256) void k_adapter_bwd(const float* __restrict__ p
         for (int c = 0; c < C; ++c)
 #pragma unroll
           for (int t = 0; t < 9; ++t)  // hidden q feeds out p = q - (dy-1, dx-1)
-            g = fmaf(prm[A::W2 + (c * AD_HID + h) * 9 + t],
+            g = fmaf(pw[A::W2 + (c * AD_HID + h) * 9 + t],
                      sdo[c * HA + (qy + 2 - t / 3) * A::HE + qx + 2 - t % 3], g);
         const bool on = sh[h * HA + (qy + 1) * A::HE + qx + 1] > 0.f;  // relu'
-        sdp[h * TA + tid] = on ? g : 0.f;
+        sdp[h * TA + tt] = on ? g : 0.f;
       }
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < A::PPT; ++j) {
-      const int p = tid + 256 * j;
-      if (p >= A::NP) continue;
-      float s = acc[j];
-      if (p < A::B1) {  // dW1[h][i][dy][dx] = sum_q dpre[h][q] * x[i][q + (dy-1, dx-1)]
-        const int h = p / (A::CI * 9), i = (p / 9) % A::CI, t = p % 9;
-        const float* xs = sx + i * XA + (t / 3 + 1) * A::XE + t % 3 + 1;
+    for (int j = 0; j < T::TPT; ++j) {
+      const int k = tt + 256 * j;
+      if (k >= T::NT) continue;
+      float a0 = acc[j][0], a1 = acc[j][1], a2 = acc[j][2];
+      if (k < T::T1) {  // dW1[h][i][ky][kx] = sum_q dpre[h][q] * x[i][q + (ky-1, kx-1)]
+        const int h = k / (A::CI * 3), i = (k / 3) % A::CI, ky = k % 3;
+        const float* xs = sx + i * XA + (ky + 1) * A::XE;  // input row r+ky+1 (halo 2), cols 0..19
         const float* ds = sdp + h * TA;
-        for (int q = 0; q < TA; ++q) s = fmaf(ds[q], xs[(q / AD_T) * A::XE + q % AD_T], s);
-      } else if (p < A::W2) {  // db1
-        const float* ds = sdp + (p - A::B1) * TA;
-        for (int q = 0; q < TA; ++q) s += ds[q];
-      } else if (p < A::B2) {  // dW2[c][h][dy][dx] = sum_p dout[c][p] * hid[h][p + (dy-1, dx-1)]
-        const int pp = p - A::W2;
-        const int c = pp / (AD_HID * 9), h = (pp / 9) % AD_HID, t = pp % 9;
-        const float* hs = sh + h * HA + (t / 3) * A::HE + t % 3;
-        const float* os = sdo + c * HA + A::HE + 1;
-        for (int q = 0; q < TA; ++q) {
-          const int o = (q / AD_T) * A::HE + q % AD_T;
-          s = fmaf(os[o], hs[o], s);
+#pragma unroll 1
+        for (int rr = 0; rr < AD_T; ++rr) {
+          f4 d[4], x[5];
+#pragma unroll
+          for (int v = 0; v < 4; ++v) d[v] = *reinterpret_cast<const f4*>(ds + rr * AD_T + 4 * v);
+#pragma unroll
+          for (int v = 0; v < 5; ++v) x[v] = *reinterpret_cast<const f4*>(xs + rr * A::XE + 4 * v);
+#pragma unroll
+          for (int c = 0; c < AD_T; ++c) {
+            const float dc = d[c >> 2][c & 3];
+            a0 = fmaf(dc, x[(c + 1) >> 2][(c + 1) & 3], a0);
+            a1 = fmaf(dc, x[(c + 2) >> 2][(c + 2) & 3], a1);
+            a2 = fmaf(dc, x[(c + 3) >> 2][(c + 3) & 3], a2);
+          }
+        }
+      } else if (k < T::T1 + T::T2) {  // dW2[c][h][ky][kx] = sum_p dout[c][p] * hid[h][p + (ky-1, kx-1)]
+        const int kk = k - T::T1;
+        const int c = kk / (AD_HID * 3), h = (kk / 3) % AD_HID, ky = kk % 3;
+        const float* hs = sh + h * HA + ky * A::HE;  // hidden row r+ky (halo 1), cols 0..17
+        const float* os = sdo + c * HA + A::HE;      // dout row r+1, cols 0..17 (1..16 used)
+#pragma unroll 1
+        for (int rr = 0; rr < AD_T; ++rr) {
+          f2 o[9], hv[9];
+#pragma unroll
+          for (int v = 0; v < 9; ++v) {
+            o[v] = *reinterpret_cast<const f2*>(os + rr * A::HE + 2 * v);
+            hv[v] = *reinterpret_cast<const f2*>(hs + rr * A::HE + 2 * v);
+          }
+#pragma unroll
+          for (int cc = 0; cc < AD_T; ++cc) {
+            const float oc = o[(cc + 1) >> 1][(cc + 1) & 1];
+            a0 = fmaf(oc, hv[cc >> 1][cc & 1], a0);
+            a1 = fmaf(oc, hv[(cc + 1) >> 1][(cc + 1) & 1], a1);
+            a2 = fmaf(oc, hv[(cc + 2) >> 1][(cc + 2) & 1], a2);
+          }
+        }
+      } else if (k < T::T1 + T::T2 + T::TB1) {  // db1
+        const float* ds = sdp + (k - T::T1 - T::T2) * TA;
+        for (int q = 0; q < TA; q += 4) {
+          const f4 v = *reinterpret_cast<const f4*>(ds + q);
+          a0 += v[0]; a0 += v[1]; a0 += v[2]; a0 += v[3];
         }
       } else {  // db2
-        const float* os = sdo + (p - A::B2) * HA + A::HE + 1;
-        for (int q = 0; q < TA; ++q) s += os[(q / AD_T) * A::HE + q % AD_T];
+        const float* os = sdo + (k - T::T1 - T::T2 - T::TB1) * HA + A::HE;
+        for (int rr = 0; rr < AD_T; ++rr)
+#pragma unroll
+          for (int cc = 1; cc <= AD_T; ++cc) a0 += os[rr * A::HE + cc];
       }
-      acc[j] = s;
+      acc[j][0] = a0; acc[j][1] = a1; acc[j][2] = a2;
     }
     __syncthreads();
   }
+  // the slab row in state_dict order (AdCfg offsets)
   float* row = slab + (long)blockIdx.x * A::NP;
 #pragma unroll
-  for (int j = 0; j < A::PPT; ++j) {
-    const int p = tid + 256 * j;
-    if (p < A::NP) row[p] = acc[j];
+  for (int j = 0; j < T::TPT; ++j) {
+    const int k = tid + 256 * j;
+    if (k >= T::NT) continue;
+    if (k < T::T1) {
+      const int h = k / (A::CI * 3), i = (k / 3) % A::CI, ky = k % 3;
+      for (int kx = 0; kx < 3; ++kx) row[(h * A::CI + i) * 9 + ky * 3 + kx] = acc[j][kx];
+    } else if (k < T::T1 + T::T2) {
+      const int kk = k - T::T1;
+      const int c = kk / (AD_HID * 3), h = (kk / 3) % AD_HID, ky = kk % 3;
+      for (int kx = 0; kx < 3; ++kx) row[A::W2 + (c * AD_HID + h) * 9 + ky * 3 + kx] = acc[j][kx];
+    } else if (k < T::T1 + T::T2 + T::TB1) {
+      row[A::B1 + k - T::T1 - T::T2] = acc[j][0];
+    } else {
+      row[A::B2 + k - T::T1 - T::T2 - T::TB1] = acc[j][0];
+    }
   }
 }
 

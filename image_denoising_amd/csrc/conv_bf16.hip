@@ -13,6 +13,8 @@
 //   double-buffered by global_load_lds.  Per stage a wave issues 3*MT*NT MFMAs of 16x16x32.
 //   LDS rows are 40 bf16 (80 B: 32 + 8 pad) per pixel / per (tap, output channel): a lane's
 //   8-element operand (k = 8*(lane>>4) .. +7) is one ds_read_b128.
+#include <cstdlib>
+
 #include "dn_internal.h"
 
 namespace dn {
@@ -42,6 +44,50 @@ struct BCfg {
 __device__ __forceinline__ void glds16b(const void* g, void* l) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+// epilogue: stage each 16-pixel row through LDS, write whole pixels as float4 (NHWC; OUT_UP2:
+// the deconv parity scatter of blockIdx.z)
+template <int NT, int MT, int PS>
+__device__ __forceinline__ void bf_epilogue(const FwdArgs& a, const f32x4b (&acc)[MT][NT],
+                                            unsigned char* lds_raw, int ty0, int tx0, int n,
+                                            int wave, int lane) {
+  const int li = lane & 15, lg = lane >> 4;
+  float* stg = reinterpret_cast<float*>(lds_raw) + wave * 16 * PS;
+  const int NQ = a.NOUT >> 2;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) stg[(4 * lg + r) * PS + q * 16 + li] = acc[m][q][r];
+    __syncthreads();
+    const int gy = ty0 + wave * MT + m;
+    if (gy < a.OH) {
+      for (int e = lane; e < 16 * NQ; e += 64) {
+        const int p = e / NQ, cc = 4 * (e - p * NQ);
+        const int gx = tx0 + p;
+        if (gx >= a.OW) continue;
+        float4 v = *reinterpret_cast<const float4*>(stg + p * PS + cc);
+        const float4 b = *reinterpret_cast<const float4*>(a.bias + cc);
+        v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+        if (a.epi == EPI_BIAS_ACT) {
+          v.x = v.x > 0.f ? v.x : v.x * 0.2f; v.y = v.y > 0.f ? v.y : v.y * 0.2f;
+          v.z = v.z > 0.f ? v.z : v.z * 0.2f; v.w = v.w > 0.f ? v.w : v.w * 0.2f;
+        }
+        long oi;
+        if (a.out_layout == OUT_UP2) {  // ConvTranspose2d(2,2) scatter: pixel (2y+a, 2x+b)
+          const int ab = (int)blockIdx.z;
+          oi = (((long)n * 2 * a.OH + 2 * gy + (ab >> 1)) * 2 * a.OW + 2 * gx + (ab & 1)) *
+                   a.out_stride + a.out_off + cc;
+        } else {
+          oi = (((long)n * a.OH + gy) * a.OW + gx) * a.out_stride + a.out_off + cc;
+        }
+        *reinterpret_cast<float4*>(a.out + oi) = v;
+      }
+    }
+    __syncthreads();
+  }
 }
 
 template <int NT, int MT, bool K3>
@@ -148,42 +194,144 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16(FwdArgs a) {
     __syncthreads();  // next stage's weights landed (vmcnt(0)), next x tile written
   }
 
-  // epilogue: stage each 16-pixel row through LDS, write whole pixels as float4 (NHWC)
-  float* stg = reinterpret_cast<float*>(lds_raw) + wave * 16 * C::PS;
-  const int NQ = a.NOUT >> 2;
+  bf_epilogue<NT, MT, C::PS>(a, acc, lds_raw, ty0, tx0, n, wave, lane);
+}
+
+// ------------------------------------------------------------------------------------
+// Pipelined 3x3 variant (float4-aligned input views, K % 4 == 0): the tile and LDS layout of
+// k_fwd_bf16, but ONE barrier per weight stage and the waits counted per wave.  Stage st+1's
+// weights are DMA'd into the other ring slot at the start of stage st (every wave issues the
+// same PPW pieces; short waves re-load their last one); the next chunk's x tile is requested
+// into registers at its first stage (buffer loads with out-of-range offsets for the halo and
+// the image border, so the count is fixed) and rounded into LDS at its last.  The wait before
+// a stage's barrier is vmcnt(XITEMS) at a chunk's first stage (the x loads younger than the
+// weight DMAs stay in flight across the chunk), vmcnt(0) otherwise: the x tile's HBM latency
+// is hidden behind two weight stages instead of stalling the stage it was issued in (k_fwd_bf16
+// waits for it at that stage's barrier).
+// ------------------------------------------------------------------------------------
+#define BF_WAITCNT_VM(n) \
+  __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
+
+__device__ __forceinline__ void bf_barrier() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no compiler motion of LDS accesses across it
+  __builtin_amdgcn_s_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+template <int NT, int MT>
+__global__ __launch_bounds__(256, 2) void k_fwd_bf16p(FwdArgs a) {
+  using C = BCfg<NT, MT, true>;
+  constexpr int PIECES = C::WST / 512, PPW = (PIECES + 3) / 4;
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
+  __bf16* lx = reinterpret_cast<__bf16*>(lds_raw);
+  __bf16* ring = lx + C::LXB;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lg = lane >> 4;
+  const int tiles_x = (a.OW + C::TW - 1) / C::TW;
+  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
+  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
+  const int n = blockIdx.y;
+  const int iy0 = ty0 - 1, ix0 = tx0 - 1;
+  const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
+  const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp);
+  const int nch = (a.K + C::KC - 1) / C::KC;
+  const int nst = 3 * nch;
+
+  f32x4b acc[MT][NT];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
+  for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int q = 0; q < NT; ++q)
+    for (int q = 0; q < NT; ++q) acc[m][q] = f32x4b{0.f, 0.f, 0.f, 0.f};
+
+  // this tile's input rows through a 32-bit buffer resource (host: < 2 GiB per tile's rows)
+  const int ry0 = iy0 > 0 ? iy0 : 0, ry1 = iy0 + C::IH < a.IHt ? iy0 + C::IH : a.IHt;
+  const long row_floats = (long)a.IWt * a.in_stride;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(inb + ry0 * row_floats), (short)0, (int)((ry1 - ry0) * row_floats * 4),
+      0x00020000);
+  f32x4b xr[C::XITEMS];
+  auto load_x = [&](int k0) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) stg[(4 * lg + r) * C::PS + q * 16 + li] = acc[m][q][r];
-    __syncthreads();
-    const int gy = ty0 + wave * MT + m;
-    if (gy < a.OH) {
-      for (int e = lane; e < 16 * NQ; e += 64) {
-        const int p = e / NQ, cc = 4 * (e - p * NQ);
-        const int gx = tx0 + p;
-        if (gx >= a.OW) continue;
-        float4 v = *reinterpret_cast<const float4*>(stg + p * C::PS + cc);
-        const float4 b = *reinterpret_cast<const float4*>(a.bias + cc);
-        v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
-        if (a.epi == EPI_BIAS_ACT) {
-          v.x = v.x > 0.f ? v.x : v.x * 0.2f; v.y = v.y > 0.f ? v.y : v.y * 0.2f;
-          v.z = v.z > 0.f ? v.z : v.z * 0.2f; v.w = v.w > 0.f ? v.w : v.w * 0.2f;
-        }
-        long oi;
-        if (a.out_layout == OUT_UP2) {  // ConvTranspose2d(2,2) scatter: pixel (2y+a, 2x+b)
-          const int ab = (int)blockIdx.z;
-          oi = (((long)n * 2 * a.OH + 2 * gy + (ab >> 1)) * 2 * a.OW + 2 * gx + (ab & 1)) *
-                   a.out_stride + a.out_off + cc;
-        } else {
-          oi = (((long)n * a.OH + gy) * a.OW + gx) * a.out_stride + a.out_off + cc;
-        }
-        *reinterpret_cast<float4*>(a.out + oi) = v;
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * 256;
+      const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+      const int iy = pix / C::IW, ix = pix - iy * C::IW;
+      const int gy = iy0 + iy, gx = ix0 + ix, k = k0 + 4 * q;
+      const bool ok = e < C::XQ && gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt && k < a.K;
+      const int off = ok ? (((gy - ry0) * a.IWt + gx) * a.in_stride + k) * 4 : 0x7fffffff;
+      xr[it] = __builtin_bit_cast(f32x4b, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * 256;
+      if (e < C::XQ) {
+        const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        bf16x4 h;
+        h[0] = (__bf16)xr[it][0]; h[1] = (__bf16)xr[it][1];
+        h[2] = (__bf16)xr[it][2]; h[3] = (__bf16)xr[it][3];
+        *reinterpret_cast<bf16x4*>(lx + pix * C::XS + 4 * q) = h;
       }
     }
-    __syncthreads();
+  };
+  auto load_w = [&](int st, int slot) {  // stage st = chunk * 3 + ky: PPW 1 KiB pieces per wave
+    const __bf16* src = wimg + (long)st * C::WST;
+    __bf16* dst = ring + slot * C::WST;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      int p = wave + 4 * j;
+      if (p >= PIECES) p -= 4;
+      glds16b(src + p * 512 + lane * 8, dst + p * 512);
+    }
+  };
+
+  load_w(0, 0);
+  load_x(0);
+  store_x();                           // waits for the x loads (and the older DMAs)
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
+  bf_barrier();
+
+#pragma unroll 1
+  for (int st = 0; st < nst; ++st) {
+    const int c = st / 3, ky = st - 3 * c;
+    const bool more = c + 1 < nch;
+    const __bf16* lw = ring + (st & 1) * C::WST;
+    load_w(st + 1 < nst ? st + 1 : nst - 1, (st + 1) & 1);  // past the end: a re-load
+    if (ky == 0 && more) load_x((c + 1) * C::KC);
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      bf16x8 av[MT], bv[NT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int r = wave * MT + m;
+        av[m] = *reinterpret_cast<const bf16x8*>(lx + ((r + ky) * C::IW + li + kx) * C::XS + 8 * lg);
+      }
+#pragma unroll
+      for (int q = 0; q < NT; ++q)
+        bv[q] = *reinterpret_cast<const bf16x8*>(lw + (kx * C::NP + q * 16 + li) * C::WS + 8 * lg);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int q = 0; q < NT; ++q)
+          acc[m][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], bv[q], acc[m][q], 0, 0, 0);
+    }
+    const bool xstep = ky == 2 && more;
+    if (xstep) {
+      bf_barrier();  // every wave is done with this chunk's x tile
+      store_x();
+    }
+    // own DMAs of stage st+1 landed; younger: the next chunk's x loads (issued at ky == 0)
+    if (ky == 0 && more) BF_WAITCNT_VM(C::XITEMS);
+    else BF_WAITCNT_VM(0);
+    if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
+    bf_barrier();
   }
+  __syncthreads();
+  bf_epilogue<NT, MT, C::PS>(a, acc, lds_raw, ty0, tx0, n, wave, lane);
 }
 
 // bf16 weight image: [chunk][ky][kx][n][WS] (k = chunk*32 + kk for kk < 32; zero padded), each
@@ -223,6 +371,11 @@ static int bf16_nt(int nout) { return nout <= 48 ? 3 : (nout <= 96 ? 6 : 0); }
 static long bf16_stage(int nt, int ksize) {
   if (ksize == 3) return nt == 3 ? BCfg<3, 4, true>::WST : BCfg<6, 4, true>::WST;
   return nt == 3 ? BCfg<3, 4, false>::WST : BCfg<6, 4, false>::WST;
+}
+
+long bf16_stage_elems(int nout, int ksize) {
+  const int nt = bf16_nt(nout);
+  return nt == 0 || (ksize != 1 && ksize != 3) ? -1 : bf16_stage(nt, ksize);
 }
 
 // bf16 elements of the packed image of a 3x3 (ksize 3) or 1x1 layer (K inputs, nout <= 96)
@@ -273,6 +426,19 @@ hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize) {
   if (ksize == 1) {
     if (nt == 3) return small ? run_bf16<3, 1, false>(a, s) : run_bf16<3, 4, false>(a, s);
     return small ? run_bf16<6, 1, false>(a, s) : run_bf16<6, 4, false>(a, s);
+  }
+  // pipelined kernel: aligned views, whole channel quads, < 2 GiB of input rows per tile
+  static const bool pipe_env = !getenv("DN_BF16_PIPE") || atoi(getenv("DN_BF16_PIPE")) != 0;
+  const bool pipe = pipe_env && !small && a.out_layout == OUT_NHWC && a.K % 4 == 0 &&
+                    ((a.in_stride | a.in_off) & 3) == 0 &&
+                    (long)BCfg<6, 4, true>::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL;
+  if (pipe) {
+    const int tx = (a.OW + 15) / 16, ty = (a.OH + 15) / 16;
+    if (nt == 3)
+      hipLaunchKernelGGL((k_fwd_bf16p<3, 4>), dim3(tx * ty, a.N, 1), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_fwd_bf16p<6, 4>), dim3(tx * ty, a.N, 1), dim3(256), 0, s, a);
+    return hipGetLastError();
   }
   if (nt == 3) return small ? run_bf16<3, 1, true>(a, s) : run_bf16<3, 4, true>(a, s);
   return small ? run_bf16<6, 1, true>(a, s) : run_bf16<6, 4, true>(a, s);

@@ -473,9 +473,9 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
 // constant count); the next chunk's x tile is loaded into registers at the start of a chunk,
 // after that stage's DMA, and split into LDS at its end.  Stage reads and MFMAs as k_c3x6p.
 // ------------------------------------------------------------------------------------
-template <int NT>
+template <int NT, int MT_ = 2>
 struct HCfg {
-  static constexpr int WAVES = 4, MT = 2, S = 2;
+  static constexpr int WAVES = 4, MT = MT_, S = 2;
   static constexpr int TW = 16, TH = WAVES * MT, IH = TH + 2, IW = TW + 2, KC = 32, NP = 16 * NT;
   static constexpr int XPIX = IH * IW;
   static constexpr int XPL = XPIX * KC;
@@ -494,9 +494,9 @@ struct HCfg {
   static_assert(2 * LBYTES <= 163840, "two workgroups per CU");
 };
 
-template <int NT, int TAIL>
+template <int NT, int TAIL, int MT_ = 2>
 __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
-  using C = HCfg<NT>;
+  using C = HCfg<NT, MT_>;
   constexpr int MT = C::MT;
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
   __bf16* lx = reinterpret_cast<__bf16*>(lds_raw);
@@ -593,54 +593,11 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
     // the end a re-load of the last stage
     load_w(st + 1 < nst ? st + 1 : nst - 1, (st + 1) & 1);
     if (t == 0 && more) load_x((c + 1) * C::KC);  // the next chunk, after this stage's DMA
-    bf16x8 av[3][MT], bv[3][NT];
     const int mode = (tail && c + 1 == nch) ? tail : 0;
-    if (mode == 1) {
-      const int ta = 8 * t + 2 * lg, tb = ta + 1;
-      const int ca = ta < 9 ? ta : 8, cb = tb < 9 ? tb : 8;
-      const int da = (ca / 3) * C::IW + ca % 3, db = (cb / 3) * C::IW + cb % 3;
-      const bf16x4 z4 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int p0 = (wave * MT + m) * C::IW + li;
-        const int pa = p0 + da, pb = p0 + db;
-        const int oa = pa * C::KC + x6_swz(pa, 0) * 8, ob = pb * C::KC + x6_swz(pb, 0) * 8;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          bf16x4 va = *reinterpret_cast<const bf16x4*>(lx + p * C::XPL + oa);
-          bf16x4 vb = *reinterpret_cast<const bf16x4*>(lx + p * C::XPL + ob);
-          if (ta > 8) va = z4;
-          if (tb > 8) vb = z4;
-          av[p][m] = __builtin_shufflevector(va, vb, 0, 1, 2, 3, 4, 5, 6, 7);
-        }
-      }
-    } else if (mode == 2) {
-      const int ta = 2 * t + (lg >> 1);
-      const int ca = ta < 9 ? ta : 8;
-      const int da = (ca / 3) * C::IW + ca % 3;
-      const bf16x8 z8 = {};
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int pa = (wave * MT + m) * C::IW + li + da;
-        const int oa = pa * C::KC + x6_swz(pa, lg & 1) * 8;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const bf16x8 v = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + oa);
-          av[p][m] = ta > 8 ? z8 : v;
-        }
-      }
-    } else {
-      const int ky = t / 3, kx = t - 3 * ky;
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int pix = (wave * MT + m + ky) * C::IW + li + kx;
-        const int off = pix * C::KC + x6_swz(pix, lg) * 8;
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          av[p][m] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
-      }
-    }
-    constexpr int QG = x6_qg(MT, NT), NG = NT / QG, LOOK = NG < 2 ? NG : 2;
+    // MT = 4: the A pieces of two rows at a time (registers), the B fragments read once for all
+    constexpr int MH = MT >= 4 ? 2 : MT;
+    constexpr int QG = MT >= 4 ? 1 : x6_qg(MT, NT), NG = NT / QG, LOOK = NG < 2 ? NG : 2;
+    bf16x8 bv[3][NT];
     auto read_b = [&](int g) {
 #pragma unroll
       for (int q = g * QG; q < (g + 1) * QG; ++q) {
@@ -652,14 +609,72 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
       }
     };
 #pragma unroll
-    for (int g = 0; g < LOOK; ++g) read_b(g);
-    __builtin_amdgcn_sched_barrier(0);
+    for (int mh = 0; mh < MT / MH; ++mh) {
+      bf16x8 av[3][MH];
+      if (mode == 1) {
+        const int ta = 8 * t + 2 * lg, tb = ta + 1;
+        const int ca = ta < 9 ? ta : 8, cb = tb < 9 ? tb : 8;
+        const int da = (ca / 3) * C::IW + ca % 3, db = (cb / 3) * C::IW + cb % 3;
+        const bf16x4 z4 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      x6_group<MT, NT, QG>(acc, av, bv, g * QG);
+        for (int i = 0; i < MH; ++i) {
+          const int p0 = (wave * MT + mh * MH + i) * C::IW + li;
+          const int pa = p0 + da, pb = p0 + db;
+          const int oa = pa * C::KC + x6_swz(pa, 0) * 8, ob = pb * C::KC + x6_swz(pb, 0) * 8;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            bf16x4 va = *reinterpret_cast<const bf16x4*>(lx + p * C::XPL + oa);
+            bf16x4 vb = *reinterpret_cast<const bf16x4*>(lx + p * C::XPL + ob);
+            if (ta > 8) va = z4;
+            if (tb > 8) vb = z4;
+            av[p][i] = __builtin_shufflevector(va, vb, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+        }
+      } else if (mode == 2) {
+        const int ta = 2 * t + (lg >> 1);
+        const int ca = ta < 9 ? ta : 8;
+        const int da = (ca / 3) * C::IW + ca % 3;
+        const bf16x8 z8 = {};
+#pragma unroll
+        for (int i = 0; i < MH; ++i) {
+          const int pa = (wave * MT + mh * MH + i) * C::IW + li + da;
+          const int oa = pa * C::KC + x6_swz(pa, lg & 1) * 8;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const bf16x8 v = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + oa);
+            av[p][i] = ta > 8 ? z8 : v;
+          }
+        }
+      } else {
+        const int ky = t / 3, kx = t - 3 * ky;
+#pragma unroll
+        for (int i = 0; i < MH; ++i) {
+          const int pix = (wave * MT + mh * MH + i + ky) * C::IW + li + kx;
+          const int off = pix * C::KC + x6_swz(pix, lg) * 8;
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            av[p][i] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
+        }
+      }
+      if (mh == 0) {
+#pragma unroll
+        for (int g = 0; g < LOOK; ++g) read_b(g);
+      }
       __builtin_amdgcn_sched_barrier(0);
-      if (g + LOOK < NG) read_b(g + LOOK);
-      __builtin_amdgcn_sched_barrier(0);
+      f32x4(&acch)[MH][NT] = *reinterpret_cast<f32x4(*)[MH][NT]>(&acc[mh * MH]);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        x6_group<MH, NT, QG>(acch, av, bv, g * QG);
+        if constexpr (MT >= 4) {  // the block sums' adds here, not deferred (live MFMA results)
+#pragma unroll
+          for (int i = 0; i < MH; ++i)
+#pragma unroll
+            for (int q = g * QG; q < (g + 1) * QG; ++q) asm volatile("" : "+v"(acch[i][q]));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (mh == 0 && g + LOOK < NG) read_b(g + LOOK);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     const int ns = (tail && c + 1 == nch) ? tail_st : 9;
     const bool xstep = t == ns - 1 && more;
@@ -681,17 +696,17 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
   fwd_epilogue<NT, MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
 }
 
-template <int NT>
+template <int NT, int MT = 2>
 static hipError_t run_x6h(const FwdArgs& a, int nz, hipStream_t s) {
-  using C = HCfg<NT>;
+  using C = HCfg<NT, MT>;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
   const dim3 grid(tx * ty, a.N, nz), block(C::WAVES * 64);
   if (a.x6_tail == 1)
-    hipLaunchKernelGGL((k_c3x6h<NT, 1>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_c3x6h<NT, 1, MT>), grid, block, 0, s, a);
   else if (a.x6_tail == 2)
-    hipLaunchKernelGGL((k_c3x6h<NT, 2>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_c3x6h<NT, 2, MT>), grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL((k_c3x6h<NT, 0>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_c3x6h<NT, 0, MT>), grid, block, 0, s, a);
   return hipGetLastError();
 }
 
@@ -792,6 +807,25 @@ __device__ __forceinline__ void pk_deconv_dgrad_x6(const PackJob& j, long e) {
                               x6_swz(row, k >> 3) * 8 + (k & 7)] = p == 0 ? hh : (p == 1 ? m : l);
 }
 
+// launch_pack_bf16's image (k_pack_bf16, conv_bf16.hip): [chunk][ky][kx][n][40], zero padded
+__device__ __forceinline__ void pk_bf16(const PackJob& j, long e) {
+  const int NP = j.g0, WST = j.g1, spc = j.g2 ? 3 : 1;
+  const long st = e / WST;
+  const int r = (int)(e - st * WST);
+  const int c = (int)(st / spc), ky = (int)(st % spc);
+  float v = 0.f;
+  if (r < spc * NP * 40) {
+    const int kx = r / (NP * 40), nn = (r / 40) % NP, kk = r % 40;
+    const int k = c * 32 + kk;
+    if (kk < 32 && k < j.K && nn < j.NOUT) {
+      const int t = j.g2 ? ky * 3 + kx : 0;
+      const int tm = j.flip ? j.taps - 1 - t : t;
+      v = j.w[(long)k * j.sK + (long)nn * j.sN + (long)tm * j.sT];
+    }
+  }
+  static_cast<__bf16*>(j.out)[e] = (__bf16)v;
+}
+
 __global__ __launch_bounds__(256) void k_pack_batch(PackBatch b) {
   const PackJob& j = b.j[blockIdx.y];
   const long total = pack_job_elems(j);
@@ -802,6 +836,7 @@ __global__ __launch_bounds__(256) void k_pack_batch(PackBatch b) {
       case PK_DECONV_X6: pk_deconv_x6(j, e); break;
       case PK_HEAD_X6: pk_head_x6(j, e); break;
       case PK_DECONV_DGRAD_X6: pk_deconv_dgrad_x6(j, e); break;
+      case PK_BF16: pk_bf16(j, e); break;
       default: static_cast<float*>(j.out)[e] = 0.f; break;
     }
   }
@@ -852,6 +887,15 @@ PackJob pack_job_deconv_dgrad_x6(const float* w, void* out) {
   PackJob j{};
   j.kind = PK_DECONV_DGRAD_X6; j.w = w; j.out = out;
   return j;
+}
+
+bool pack_job_bf16(const WView& wv, int K, int nout, int ksize, void* out, PackJob& j) {
+  j = PackJob{};
+  const long st = bf16_stage_elems(nout, ksize), tot = bf16_pack_elems(K, nout, ksize);
+  if (st < 0 || tot < 0 || tot >= (1L << 31) || !pack_view(wv, j)) return false;
+  j.kind = PK_BF16; j.out = out; j.K = K; j.NOUT = nout;
+  j.g0 = nout <= 48 ? 48 : 96; j.g1 = (int)st; j.g2 = ksize == 3; j.g3 = (int)tot;
+  return true;
 }
 
 PackJob pack_job_zero(float* out, int n) {
@@ -976,7 +1020,14 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
   static const int half_env = getenv("DN_X6_HALF") ? atoi(getenv("DN_X6_HALF")) : -1;
   const bool half_fits = (long)HCfg<6>::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL;
   const bool half = half_fits && (half_env >= 0 ? half_env != 0 : (np <= 48 || a.x6_tail == 1));
+  // 48 / 32 output channels: 16-row tiles (4 rows per wave, twice the MFMAs per operand read
+  // and per stage barrier) when they fill two rounds of resident workgroups; DN_X6_H4=0 keeps 8
+  static const bool h4_env = !getenv("DN_X6_H4") || atoi(getenv("DN_X6_H4")) != 0;
+  const long tiles16 = (long)a.N * nz * ((a.OH + 15) / 16) * ((a.OW + 15) / 16);
+  const bool h4 = h4_env && np <= 48 && tiles16 >= 1024 &&
+                  (long)HCfg<3, 4>::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL;
   auto run = [&]() {
+    if (half && h4) return np == 32 ? run_x6h<2, 4>(a, nz, s) : run_x6h<3, 4>(a, nz, s);
     if (half)
       return np == 32 ? run_x6h<2>(a, nz, s) : (np == 48 ? run_x6h<3>(a, nz, s) : run_x6h<6>(a, nz, s));
     return pipe();
@@ -1137,7 +1188,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
         const f32x4 hi = mfma_bf16(av[0][i], ones, z);
         f32x4 lo = mfma_bf16(av[1][i], ones, z);
         lo = mfma_bf16(av[2][i], ones, lo);
-        accb[i][0] += hi + lo;
+        x6_acc_add(accb[i][0], hi, lo);
       }
     }
     __syncthreads();  // next stage landed (vmcnt(0)); everyone done with this buffer

@@ -120,14 +120,15 @@ struct FwdGeom { int KC, TAPS, WNS, LW; };
 // images of a 96-channel deconv, the two bf16x6 head images, and a zero fill (the weight
 // gradients' 64-float DMA padding).  Strides of the weight view are element strides (< 2^31).
 enum PackKind { PK_F32 = 0, PK_X6 = 1, PK_DECONV_X6 = 2, PK_HEAD_X6 = 3, PK_ZERO = 4,
-                PK_DECONV_DGRAD_X6 = 5 };
+                PK_DECONV_DGRAD_X6 = 5, PK_BF16 = 6 };
 struct PackJob {
   const float* w;   // view origin (WView.w + off); PK_HEAD_X6: nin_a, PK_DECONV_X6: raw weight
   const float* w2;  // PK_HEAD_X6: nin_b
   void* out;
   int sK, sN, sT, sZ, taps, flip;
   int kind, K, NOUT, nz, zc, ntot, nch, tail;
-  int g0, g1, g2, g3;  // PK_F32: KC, TAPS, WNS, LW; PK_X6: NP; PK_ZERO: floats
+  int g0, g1, g2, g3;  // PK_F32: KC, TAPS, WNS, LW; PK_X6: NP; PK_ZERO: floats;
+                       // PK_BF16: NP, stage elements, 3x3?, image elements
 };
 constexpr int kPackJobs = 24;  // 24 x 104 B of kernel arguments
 struct PackBatch {
@@ -143,6 +144,7 @@ __host__ __device__ inline long pack_job_elems(const PackJob& j) {
     case PK_DECONV_X6: return 4L * 3 * 3 * 96 * 32;
     case PK_HEAD_X6: return 2L * 3 * 3 * 96 * 32;
     case PK_DECONV_DGRAD_X6: return 4L * 3 * 3 * 96 * 32;
+    case PK_BF16: return j.g3;
     default: return j.g0;
   }
 }
@@ -153,6 +155,8 @@ PackJob pack_job_head_x6(const float* wa, const float* wb, void* out);
 PackJob pack_job_deconv_x6(const float* w, void* out);
 PackJob pack_job_deconv_dgrad_x6(const float* w, void* out);
 PackJob pack_job_zero(float* out, int n);
+// the bf16 image of launch_pack_bf16 (conv_bf16.hip) as a job of the pass's pack launch
+bool pack_job_bf16(const WView& wv, int K, int nout, int ksize, void* out, PackJob& j);
 
 // ---- batched fixed-order reduction of weight-gradient slabs (conv.hip) ----
 // out[omap(e)] = sum_s slab[s * stride + imap(e)], e < n, rows summed in a fixed order
@@ -295,6 +299,7 @@ hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, 
 
 // ---- mixed-precision (bf16 MFMA) 3x3 forward (conv_bf16.hip) ----
 long bf16_pack_elems(int K, int nout, int ksize = 3);
+long bf16_stage_elems(int nout, int ksize);  // bf16 per weight stage of the image (-1: no tile)
 // ---- fp32 3x3 conv on the bf16 matrix cores by three-way operand splitting (conv_x6.hip) ----
 long x6_pack_elems(int K, int nout, int zc);  // bf16 elements of a pre-split weight image
 hipError_t launch_pack_x6(const WView& wv, int K, int nout, int zc, void* out, hipStream_t s,

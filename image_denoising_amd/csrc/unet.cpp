@@ -429,7 +429,16 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   static const bool head_x6_env = !getenv("DN_X6_HEAD") || atoi(getenv("DN_X6_HEAD")) != 0;
   const bool sel = x6 && sel_rd && !p.with_bwd && p.OC <= X6_HEAD_OCMAX;
   const bool head_x6 = x6 && (head_x6_env || sel) && p.OC <= X6_HEAD_OCMAX;
-  auto deconv_x6_layer = [&](int i) { return x6 && x6_deconv && p.packUX[i] >= 0; };
+  // bf16 base (inference only): the fused bf16x6 head instead of nin_a / nin_b as two bf16 1x1
+  // launches + an fp32 nin_c (two 96-channel round trips through HBM saved; DN_BF16_HEAD_X6=0)
+  static const bool bf16_head_env = !getenv("DN_BF16_HEAD_X6") || atoi(getenv("DN_BF16_HEAD_X6")) != 0;
+  const bool bf16_head_x6 = bf16 && bf16_head_env && !p.with_bwd && p.OC <= X6_HEAD_OCMAX;
+  // the 96-channel deconvs on the persistent bf16x6 kernel, also in the bf16 base (one pass over
+  // the input instead of a bf16 1x1 launch per output parity; DN_BF16_DECONV_X6=0 keeps those)
+  static const bool bf16_dx6_env = !getenv("DN_BF16_DECONV_X6") || atoi(getenv("DN_BF16_DECONV_X6")) != 0;
+  auto deconv_x6_layer = [&](int i) {
+    return (x6 || (bf16 && bf16_dx6_env)) && x6_deconv && p.packUX[i] >= 0;
+  };
   // ConvTranspose2d(2,2): fp32 kernel, or the bf16 1x1 kernel per output parity
   auto deconv_forward = [&](const View& xin, int Nn, int h, int w, int cin, const float* wp,
                             const float* b, int cout, const View& out, hipStream_t st) -> hipError_t {
@@ -454,25 +463,36 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     return launch_fwd_bf16(a, st, 1);
   };
 
-  // every weight image of the pass in one launch (the bf16 images on their own kernel)
+  // every weight image of the pass (fp32, bf16x6 and bf16 alike) in one pack launch
   PackBatch pb;
   auto add = [&](bool ok, const PackJob& j) { return ok ? pack_add(pb, j, s) : hipErrorInvalidValue; };
   for (int i = ENC1; i < NINA; ++i) {
     const Layer& L = p.P.L[i];
     const float* w = prm + L.woff;
     PackJob j;
-    if (L.deconv && bf16) DN_TRY(launch_pack_bf16_deconv(w, L.cin, L.cout, ws + p.packBF[i], s));
-    else if (L.deconv && deconv_x6_layer(i)) DN_TRY(add(true, pack_job_deconv_x6(w, ws + p.packUX[i])));
-    else if (L.deconv) DN_TRY(add(pack_job(G_UP, deconv_fwd_view(w, L.cout), L.cin, L.cout, 4,
-                                            ws + p.packF[i], 0, 0, j), j));
-    else if (bf16) DN_TRY(launch_pack_bf16(conv_fwd_view(w, L.cin, 3), L.cin, L.cout,
-                                           ws + p.packBF[i], s));
+    if (L.deconv && deconv_x6_layer(i)) {
+      DN_TRY(add(true, pack_job_deconv_x6(w, ws + p.packUX[i])));
+    } else if (L.deconv && bf16) {  // ConvTranspose2d [cin][cout][2][2]: a 1x1 image per parity
+      const long img = bf16_pack_elems(L.cin, L.cout, 1);
+      for (int ab = 0; ab < 4; ++ab) {
+        WView v{};
+        v.w = w; v.off = ab; v.sK = (long)L.cout * 4; v.sN = 4; v.taps = 1;
+        DN_TRY(add(pack_job_bf16(v, L.cin, L.cout, 1,
+                                 reinterpret_cast<unsigned short*>(ws + p.packBF[i]) + ab * img, j), j));
+      }
+    } else if (L.deconv) {
+      DN_TRY(add(pack_job(G_UP, deconv_fwd_view(w, L.cout), L.cin, L.cout, 4, ws + p.packF[i], 0, 0, j),
+                 j));
+    } else if (bf16) DN_TRY(add(pack_job_bf16(conv_fwd_view(w, L.cin, 3), L.cin, L.cout, 3,
+                                            ws + p.packBF[i], j), j));
     else if (x6) DN_TRY(add(pack_job_x6(conv_fwd_view(w, L.cin, 3), L.cin, L.cout, 0,
                                         ws + p.packX[i], x6_tail_f(i), j), j));
     else DN_TRY(add(pack_job(L.k == 3 ? G_C3 : G_C1, conv_fwd_view(w, L.cin, L.k), L.cin, L.cout, 1,
                              ws + p.packF[i], 0, 0, j), j));
   }
-  if (bf16) {  // nin_a, nin_b on the bf16 kernel, nin_c (96 -> out_nc) on the fp32 one
+  if (bf16_head_x6) {
+    DN_TRY(add(true, pack_job_head_x6(prm + p.P.L[NINA].woff, prm + p.P.L[NINB].woff, ws + p.packH)));
+  } else if (bf16) {  // nin_a, nin_b on the bf16 kernel, nin_c (96 -> out_nc) on the fp32 one
     for (int i = NINA; i <= NINB; ++i)
       DN_TRY(launch_pack_bf16(conv_fwd_view(prm + p.P.L[i].woff, 96, 1), 96, 96,
                               ws + p.packBF[i], s, 1));
@@ -534,6 +554,18 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   if (bf16) {  // dec_conv1b, nin_a, nin_b on the bf16 kernel, then nin_c (96 -> out_nc, fp32)
     DN_TRY(conv_forward(V(p.d1a, 96), N, H(0), Wd(0), 96, Wt(D1B), Bs(D1B), 96, 3, 1,
                         V(p.d1b, 96), OUT_NHWC, s));
+    if (bf16_head_x6) {
+      FwdArgs a{};
+      a.in = ws + p.d1b; a.in_stride = 96; a.in_off = 0; a.IHt = H(0); a.IWt = Wd(0);
+      a.N = N; a.OH = H(0); a.OW = Wd(0); a.K = 96; a.NOUT = 96;
+      HeadArgs h{};
+      h.wp = ws + p.packH;
+      h.ba = Bs(NINA); h.bb = Bs(NINB);
+      h.wc = prm + p.P.L[NINC].woff; h.bc = Bs(NINC); h.oc = p.OC;
+      h.y = y;
+      DN_TRY(launch_nin_head_x6(a, h, ws + p.packH, s));
+      return DN_OK;
+    }
     DN_TRY(conv_forward(V(p.d1b, 96), N, H(0), Wd(0), 96, Wt(NINA), Bs(NINA), 96, 1, 1,
                         V(p.na, 96), OUT_NHWC, s));
     DN_TRY(conv_forward(V(p.na, 96), N, H(0), Wd(0), 96, Wt(NINB), Bs(NINB), 96, 1, 1,

@@ -25,17 +25,18 @@ typedef float f32x2_t __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
-// split3 of two values at once on packed registers (v_cvt_pk_bf16_f32 / v_pk_add_f32): the
+// split3 of two values at once (v_cvt_pk_bf16_f32 for the conversions, scalar subtractions): the
 // three 32-bit words each hold the (a, b) pieces of one plane, low half = a
 __device__ __forceinline__ void split3x2(float a, float b, unsigned& h, unsigned& m,
                                          unsigned& l) {
   const f32x2_t v = {a, b};
   h = __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_t));
-  const f32x2_t hv = {__uint_as_float(h << 16), __uint_as_float(h & 0xffff0000u)};
-  const f32x2_t r = v - hv;
+  // scalar subtractions (see x6_acc_add)
+  const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
+  const f32x2_t r = {ra, rb};
   m = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2_t));
-  const f32x2_t mv = {__uint_as_float(m << 16), __uint_as_float(m & 0xffff0000u)};
-  l = __builtin_bit_cast(unsigned, __builtin_convertvector(r - mv, bf16x2_t));
+  const f32x2_t r2 = {ra - __uint_as_float(m << 16), rb - __uint_as_float(m & 0xffff0000u)};
+  l = __builtin_bit_cast(unsigned, __builtin_convertvector(r2, bf16x2_t));
 }
 
 // the three bf16x8 planes of eight fp32 values (element e = v[e])
@@ -55,6 +56,14 @@ __device__ __forceinline__ void split3x8(const float (&v)[8], bf16x8& p0, bf16x8
 
 __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// acc += hi + lo as scalar v_add_f32 (conv_x6.hip is built with -fno-slp-vectorize): a packed
+// v_pk_add_f32 beside MFMAs costs more issue cycles than the two scalar adds it replaces
+// (A/B on one box: k_wgrad3s 96->96 at 64 x 128^2 1.127 -> 1.050 ms, the step 25.2 -> 24.8-25.1 ms)
+__device__ __forceinline__ void x6_acc_add(f32x4& acc, const f32x4& hi, const f32x4& lo) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r] = acc[r] + (hi[r] + lo[r]);
 }
 
 // One 16x16x32 block of every fragment of a wave: acc[m][q] += sum_k A[m] B[q] at fp32 accuracy.
@@ -93,7 +102,7 @@ __device__ __forceinline__ void x6_group(f32x4 (&acc)[MT][NT], const bf16x8 (&av
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int g = 0; g < QG; ++g) acc[m][q0 + g] += hi[m][g] + lo[m][g];
+    for (int g = 0; g < QG; ++g) x6_acc_add(acc[m][q0 + g], hi[m][g], lo[m][g]);
 }
 
 template <int MT, int NT, int QG>

@@ -111,3 +111,44 @@ def test_config4_full_size_finetune_step_properties():
     assert rel_err(b["base"][:1].cpu().numpy(), emu.numpy()) < EMU_TOL
     pred = adapter_ref.adapter_forward(a0, noisy[:1], emu)
     assert rel_err(b["pred"][:1].cpu().numpy(), pred.detach().numpy()) < EMU_TOL
+
+
+def _conv_bf16(x, w, b, act, x_stride=None):
+    """dn_conv2d_forward_bf16 on an NCHW fp32 input (optionally a channel view of a wider
+    NHWC buffer: x_stride > Cin)."""
+    from image_denoising_amd import _lib
+
+    N, cin, H, W = x.shape
+    cout = w.shape[0]
+    xs = x_stride or cin
+    buf = torch.zeros(N, H, W, xs)
+    buf[..., :cin] = x.permute(0, 2, 3, 1)
+    xg, wg, bg = buf.to(DEV), w.to(DEV), b.to(DEV)
+    y = torch.empty(N, H, W, cout, device=DEV)
+    pk = _lib.scratch(_lib.lib().dn_conv2d_bf16_pack_size(cin, cout), DEV)
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.call("dn_conv2d_forward_bf16", xg.data_ptr(), xs, N, H, W, cin, wg.data_ptr(),
+              bg.data_ptr(), cout, act, y.data_ptr(), cout, pk.data_ptr(), pk.numel(), s)
+    return y.cpu().permute(0, 3, 1, 2)
+
+
+# >= 1024 16x16 tiles with float4-aligned views and K % 4 == 0: the pipelined kernel
+# (k_fwd_bf16p); the odd stride / K and the small grid: k_fwd_bf16
+@pytest.mark.parametrize("cin,cout,N,H,W,xs", [
+    (96, 96, 16, 128, 128, None), (48, 48, 16, 128, 128, None), (144, 96, 4, 256, 256, None),
+    (96, 48, 16, 128, 120, 100), (36, 96, 16, 128, 128, None), (97, 96, 16, 128, 128, None),
+    (96, 96, 2, 40, 40, None)])
+def test_conv_bf16_vs_fp64_of_rounded_operands(cin, cout, N, H, W, xs):
+    """bf16 products are exact in fp32, so against an fp64 conv of the bf16-rounded operands the
+    only error is the fp32 accumulation order."""
+    g = torch.Generator().manual_seed(cin * 7 + N)
+    x = torch.randn(N, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * 0.05
+    b = torch.randn(cout, generator=g) * 0.1
+    y = _conv_bf16(x, w, b, 1, xs)
+    y2 = _conv_bf16(x, w, b, 1, xs)
+    assert torch.equal(y, y2)
+    xr, wr = x.bfloat16().double(), w.bfloat16().double()
+    ref = torch.nn.functional.leaky_relu(
+        torch.nn.functional.conv2d(xr, wr, b.double(), padding=1), 0.2)
+    assert rel_err(y.numpy(), ref.numpy()) < 1e-5

@@ -20,7 +20,7 @@ fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"]) * 1024 * 2
 write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"]) * 1024
 bs, H, W, C = (16, 512, 512, 96) if kind == "bf16" else (64, 256, 256, 96)
 alg = bs * H * W * C * 4 * 2 + 96 * 96 * 9 * 4
-out = {"kernel": {"x6": "k_c3x6p<NT=6> (bf16x6 split fp32)", "bf16": "k_fwd_bf16<6,4> (bf16 base)"}
+out = {"kernel": {"x6": "k_c3x6p<NT=6> (bf16x6 split fp32)", "bf16": "k_fwd_bf16p<6,4> (bf16 base)"}
                  .get(kind, "k_fwd<G_C3,NT=6,MT=4>") + f" dec_conv1b-shaped 96->96 3x3, {bs}x{H}x{W}",
        "launches": len(vals["FETCH_SIZE"]), "fetch_bytes_corrected": fetch, "write_bytes": write,
        "traffic_bytes": fetch + write, "algorithmic_bytes": alg,
