@@ -117,8 +117,10 @@ __global__ __launch_bounds__(256) void k_adapter_fwd(const float* __restrict__ p
 template <int C>
 struct AdTasks {
   static constexpr int T1 = AD_HID * 2 * C * 3, T2 = C * AD_HID * 3, TB1 = AD_HID, TB2 = C;
-  static constexpr int NT = T1 + T2 + TB1 + TB2;
-  static constexpr int TPT = (NT + 255) / 256;  // tasks per thread
+  // slots: each task type starts on a wave boundary, so no wave runs two types' loops in turn
+  static constexpr int S2 = (T1 + 63) / 64 * 64, SB = (S2 + T2 + 63) / 64 * 64;
+  static constexpr int NS = SB + TB1 + TB2;     // slots used
+  static constexpr int TPT = (NS + 255) / 256;  // slots per thread
 };
 
 template <int C>
@@ -129,11 +131,13 @@ __global__ __launch_bounds__(256, 3) void k_adapter_bwd(const float* __restrict_
                                                      int W, float* __restrict__ slab) {
   using A = AdCfg<C>;
   using T = AdTasks<C>;
-  constexpr int XA = A::XE * A::XE, HA = A::HE * A::HE, TA = AD_T * AD_T;
+  // TP: dpre row pitch, padded so that the 16-float row reads of tasks with different h start
+  // on different banks (h * 256 floats would all hit the same ones)
+  constexpr int XA = A::XE * A::XE, HA = A::HE * A::HE, TA = AD_T * AD_T, TP = TA + 4;
   __shared__ __attribute__((aligned(16))) float sx[A::CI * XA];
   __shared__ __attribute__((aligned(16))) float sh[AD_HID * HA];
   __shared__ __attribute__((aligned(16))) float sdo[C * HA];
-  __shared__ __attribute__((aligned(16))) float sdp[AD_HID * TA];
+  __shared__ __attribute__((aligned(16))) float sdp[AD_HID * TP];
   const int tid = threadIdx.x;
   const int tiles_x = (W + AD_T - 1) / AD_T, tiles_y = (H + AD_T - 1) / AD_T;
   const long ntiles = (long)N * tiles_x * tiles_y;
@@ -173,19 +177,19 @@ __global__ __launch_bounds__(256, 3) void k_adapter_bwd(const float* __restrict_
             g = fmaf(pw[A::W2 + (c * AD_HID + h) * 9 + t],
                      sdo[c * HA + (qy + 2 - t / 3) * A::HE + qx + 2 - t % 3], g);
         const bool on = sh[h * HA + (qy + 1) * A::HE + qx + 1] > 0.f;  // relu'
-        sdp[h * TA + tt] = on ? g : 0.f;
+        sdp[h * TP + tt] = on ? g : 0.f;
       }
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < T::TPT; ++j) {
       const int k = tt + 256 * j;
-      if (k >= T::NT) continue;
+      if (k >= T::NS || (k >= T::T1 && k < T::S2) || (k >= T::S2 + T::T2 && k < T::SB)) continue;
       float a0 = acc[j][0], a1 = acc[j][1], a2 = acc[j][2];
       if (k < T::T1) {  // dW1[h][i][ky][kx] = sum_q dpre[h][q] * x[i][q + (ky-1, kx-1)]
         const int h = k / (A::CI * 3), i = (k / 3) % A::CI, ky = k % 3;
         const float* xs = sx + i * XA + (ky + 1) * A::XE;  // input row r+ky+1 (halo 2), cols 0..19
-        const float* ds = sdp + h * TA;
+        const float* ds = sdp + h * TP;
 #pragma unroll 1
         for (int rr = 0; rr < AD_T; ++rr) {
           f4 d[4], x[5];
@@ -201,8 +205,8 @@ __global__ __launch_bounds__(256, 3) void k_adapter_bwd(const float* __restrict_
             a2 = fmaf(dc, x[(c + 3) >> 2][(c + 3) & 3], a2);
           }
         }
-      } else if (k < T::T1 + T::T2) {  // dW2[c][h][ky][kx] = sum_p dout[c][p] * hid[h][p + (ky-1, kx-1)]
-        const int kk = k - T::T1;
+      } else if (k < T::SB) {  // dW2[c][h][ky][kx] = sum_p dout[c][p] * hid[h][p + (ky-1, kx-1)]
+        const int kk = k - T::S2;
         const int c = kk / (AD_HID * 3), h = (kk / 3) % AD_HID, ky = kk % 3;
         const float* hs = sh + h * HA + ky * A::HE;  // hidden row r+ky (halo 1), cols 0..17
         const float* os = sdo + c * HA + A::HE;      // dout row r+1, cols 0..17 (1..16 used)
@@ -222,14 +226,14 @@ __global__ __launch_bounds__(256, 3) void k_adapter_bwd(const float* __restrict_
             a2 = fmaf(oc, hv[(cc + 2) >> 1][(cc + 2) & 1], a2);
           }
         }
-      } else if (k < T::T1 + T::T2 + T::TB1) {  // db1
-        const float* ds = sdp + (k - T::T1 - T::T2) * TA;
+      } else if (k < T::SB + T::TB1) {  // db1
+        const float* ds = sdp + (k - T::SB) * TP;
         for (int q = 0; q < TA; q += 4) {
           const f4 v = *reinterpret_cast<const f4*>(ds + q);
           a0 += v[0]; a0 += v[1]; a0 += v[2]; a0 += v[3];
         }
       } else {  // db2
-        const float* os = sdo + (k - T::T1 - T::T2 - T::TB1) * HA + A::HE;
+        const float* os = sdo + (k - T::SB - T::TB1) * HA + A::HE;
         for (int rr = 0; rr < AD_T; ++rr)
 #pragma unroll
           for (int cc = 1; cc <= AD_T; ++cc) a0 += os[rr * A::HE + cc];
@@ -243,18 +247,18 @@ __global__ __launch_bounds__(256, 3) void k_adapter_bwd(const float* __restrict_
 #pragma unroll
   for (int j = 0; j < T::TPT; ++j) {
     const int k = tid + 256 * j;
-    if (k >= T::NT) continue;
+    if (k >= T::NS || (k >= T::T1 && k < T::S2) || (k >= T::S2 + T::T2 && k < T::SB)) continue;
     if (k < T::T1) {
       const int h = k / (A::CI * 3), i = (k / 3) % A::CI, ky = k % 3;
       for (int kx = 0; kx < 3; ++kx) row[(h * A::CI + i) * 9 + ky * 3 + kx] = acc[j][kx];
-    } else if (k < T::T1 + T::T2) {
-      const int kk = k - T::T1;
+    } else if (k < T::SB) {
+      const int kk = k - T::S2;
       const int c = kk / (AD_HID * 3), h = (kk / 3) % AD_HID, ky = kk % 3;
       for (int kx = 0; kx < 3; ++kx) row[A::W2 + (c * AD_HID + h) * 9 + ky * 3 + kx] = acc[j][kx];
-    } else if (k < T::T1 + T::T2 + T::TB1) {
-      row[A::B1 + k - T::T1 - T::T2] = acc[j][0];
+    } else if (k < T::SB + T::TB1) {
+      row[A::B1 + k - T::SB] = acc[j][0];
     } else {
-      row[A::B2 + k - T::T1 - T::T2 - T::TB1] = acc[j][0];
+      row[A::B2 + k - T::SB - T::TB1] = acc[j][0];
     }
   }
 }
@@ -345,9 +349,10 @@ long adapter_param_count(int C) {
   return -1;
 }
 
+// one round of resident workgroups (3 per CU, bound by LDS): 1024 left a second round of 256
 int adapter_bwd_blocks(int N, int H, int W) {
   const long tiles = (long)N * ((H + AD_T - 1) / AD_T) * ((W + AD_T - 1) / AD_T);
-  return (int)(tiles < 1024 ? tiles : 1024);
+  return (int)(tiles < 768 ? tiles : 768);
 }
 
 hipError_t launch_adapter_fwd(const float* prm, const float* noisy, const float* base, int N, int C,

@@ -1102,11 +1102,62 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                      (__attribute__((address_space(3))) void*)l, 16, 0, 0);
   };
-  auto issue = [&](long u, float* buf) {
-    const int n = (int)(u / ((long)uy * ux));
-    const int rem = (int)(u - (long)n * uy * ux);
-    const int py0 = (rem / ux) * sh, px0 = (rem % ux) * sw;
-    const float* gb = a.g + (long)n * a.KH * a.KW * a.g_stride + a.g_off;
+  // stage u = (image n, stage row block iy, column block ix), decoded incrementally (no 64-bit
+  // divisions per stage)
+  struct Pos { int n, iy, ix; };
+  auto pos_of = [&](long u) {
+    Pos q;
+    q.n = (int)(u / ((long)uy * ux));
+    const int rem = (int)(u - (long)q.n * uy * ux);
+    q.iy = rem / ux; q.ix = rem - q.iy * ux;
+    return q;
+  };
+  auto next = [&](Pos q) {
+    if (++q.ix == ux) { q.ix = 0; if (++q.iy == uy) { q.iy = 0; ++q.n; } }
+    return q;
+  };
+  // images whose sides are whole stage blocks (every UNet level): the per-lane parts of the DMA
+  // addresses are stage-invariant and precomputed; only the halo edges need a per-stage test
+  const bool exact = a.KW % sw == 0 && a.KH % sh == 0;
+  constexpr int JG = (C::LGP + C::NW - 1) / C::NW, JX = (C::LXP + C::NW - 1) / C::NW;
+  int goff[JG], xoff[JX], xedge[JX];
+#pragma unroll
+  for (int j = 0; j < JG; ++j) {
+    const int idx = (wave + j * C::NW) * 256 + lane * 4;
+    const int px = idx / C::GS, co = idx - px * C::GS;
+    goff[j] = (px < C::PC && co < a.Cout) ? ((px >> SWL) * a.KW + (px & (sw - 1))) * a.g_stride + co : -1;
+  }
+#pragma unroll
+  for (int j = 0; j < JX; ++j) {
+    const int idx = (wave + j * C::NW) * 256 + lane * 4;
+    const int px = idx / C::XS, q = idx - px * C::XS;
+    const int yy = px / xw, xx = px - yy * xw;
+    const bool ok = px < (sh + 2) * xw && q < C::CIB && ci0 + q < a.Cin;
+    xoff[j] = ((yy - 1) * a.KW + xx - 1) * a.x_stride + ci0 + q;
+    // halo edges: bit 0 top row, 1 bottom row, 2 left column, 3 right column; bit 4 unused slot
+    xedge[j] = (yy == 0) | ((yy == sh + 1) << 1) | ((xx == 0) << 2) | ((xx == sw + 1) << 3) | ((!ok) << 4);
+  }
+  auto issue = [&](Pos q, float* buf) {
+    const int py0 = q.iy * sh, px0 = q.ix * sw;
+    const float* gb = a.g + (long)q.n * a.KH * a.KW * a.g_stride + a.g_off;
+    const float* xb = a.x + (long)q.n * a.KH * a.KW * a.x_stride + a.x_off;
+    if (exact) {
+      const float* gs = gb + ((long)py0 * a.KW + px0) * a.g_stride;
+      const float* xs = xb + ((long)py0 * a.KW + px0) * a.x_stride;
+      const int emask = (py0 == 0) | ((py0 + sh >= a.KH) << 1) | ((px0 == 0) << 2) |
+                        ((px0 + sw >= a.KW) << 3) | (1 << 4);
+#pragma unroll
+      for (int j = 0; j < JG; ++j) {
+        const int p = wave + j * C::NW;
+        if (p < C::LGP) glds(goff[j] >= 0 ? gs + goff[j] : a.zeros, buf + p * 256);
+      }
+#pragma unroll
+      for (int j = 0; j < JX; ++j) {
+        const int p = wave + j * C::NW;
+        if (p < C::LXP) glds((xedge[j] & emask) ? a.zeros : xs + xoff[j], buf + C::LGF + p * 256);
+      }
+      return;
+    }
     for (int p = wave; p < C::LGP; p += C::NW) {
       const int idx = p * 256 + lane * 4;
       const int px = idx / C::GS, co = idx - px * C::GS;
@@ -1115,14 +1166,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
                              ? gb + ((long)gy * a.KW + gx) * a.g_stride + co : a.zeros;
       glds(src, buf + p * 256);
     }
-    const float* xb = a.x + (long)n * a.KH * a.KW * a.x_stride + a.x_off;
     const int xpix = (sh + 2) * xw;
     for (int p = wave; p < C::LXP; p += C::NW) {
       const int idx = p * 256 + lane * 4;
-      const int px = idx / C::XS, q = idx - px * C::XS;
+      const int px = idx / C::XS, q4 = idx - px * C::XS;
       const int yy = px / xw, xx = px - yy * xw;
-      const int gy = py0 - 1 + yy, gx = px0 - 1 + xx, ci = ci0 + q;
-      const bool ok = px < xpix && q < C::CIB && gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW &&
+      const int gy = py0 - 1 + yy, gx = px0 - 1 + xx, ci = ci0 + q4;
+      const bool ok = px < xpix && q4 < C::CIB && gy >= 0 && gy < a.KH && gx >= 0 && gx < a.KW &&
                       ci < a.Cin;
       const float* src = ok ? xb + ((long)gy * a.KW + gx) * a.x_stride + ci : a.zeros;
       glds(src, buf + C::LGF + p * 256);
@@ -1134,13 +1184,15 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
   // this lane group's 8 K pixels: stage row pr0, columns pc0 .. pc0 + 7
   const int pr0 = (8 * lg) >> SWL, pc0 = (8 * lg) & (sw - 1);
 
-  if (u_beg < u_end) issue(u_beg, lds);
+  Pos pn = pos_of(u_beg);
+  if (u_beg < u_end) issue(pn, lds);
   __syncthreads();
   for (long u = u_beg; u < u_end; ++u) {
     const int cb = (int)((u - u_beg) & 1);
     const float* lgs = lds + cb * C::LBUF;
     const float* lxs = lgs + C::LGF;
-    if (u + 1 < u_end) issue(u + 1, lds + (cb ^ 1) * C::LBUF);
+    pn = next(pn);
+    if (u + 1 < u_end) issue(pn, lds + (cb ^ 1) * C::LBUF);
     // A: the wave's MFW gradient fragments
     bf16x8 av[3][MFW];
 #pragma unroll
@@ -1263,8 +1315,10 @@ hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s) {
 // weights in LDS for the whole launch; wave-tiles are single 16-pixel rows, taken in a wave-
 // strided loop, the next row's input loaded into registers while the current one computes
 // (the images are read from L2 once per CU, not once per tile).
-// SAVE: na / nb written for the backward; PAIR: the input is a pair image (hd.rd)
-template <bool SAVE, bool PAIR>
+// SAVE: na / nb written for the backward; PAIR: the input is a pair image (hd.rd); B1: plain
+// bf16 products (the bf16 base's autocast arithmetic): the input rounded to bf16, the images'
+// leading planes (the weights rounded to bf16), one MFMA per block chained in fp32
+template <bool SAVE, bool PAIR, bool B1 = false>
 __global__ __launch_bounds__(512, 1) void k_nin_head_x6(FwdArgs a, HeadArgs hd, const __bf16* wimg,
                                                       int nwt) {
   __shared__ __attribute__((aligned(16))) __bf16 lw[2 * X6_HEAD_BF];
@@ -1325,6 +1379,17 @@ __global__ __launch_bounds__(512, 1) void k_nin_head_x6(FwdArgs a, HeadArgs hd, 
       bf16x8 xv[3][1];
       const float v8[8] = {in[2 * b][0], in[2 * b][1], in[2 * b][2], in[2 * b][3],
                            in[2 * b + 1][0], in[2 * b + 1][1], in[2 * b + 1][2], in[2 * b + 1][3]};
+      if constexpr (B1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[0][0][j] = (__bf16)v8[j];
+#pragma unroll
+        for (int f = 0; f < 6; ++f) {
+          const int row = b * 96 + f * 16 + li;
+          const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(img + row * 32 + x6_swz(row, lg) * 8);
+          out[f][0] = mfma_bf16(w0, xv[0][0], out[f][0]);
+        }
+        continue;
+      }
       split3x8(v8, xv[0][0], xv[1][0], xv[2][0]);
       bf16x8 wv[3][6];
 #pragma unroll
@@ -1415,8 +1480,9 @@ hipError_t launch_pack_head_x6(const float* wa, const float* wb, void* out, hipS
   return pack_flush(b, s);
 }
 
-hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* wimg, hipStream_t s) {
-  if (a.K != 96 || h.oc < 1 || h.oc > X6_HEAD_OCMAX || ((a.in_stride | a.in_off) & 3) ||
+hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* wimg, hipStream_t s,
+                              bool bf16) {
+  if ((bf16 && (h.rd || (h.na && h.nb))) || a.K != 96 || h.oc < 1 || h.oc > X6_HEAD_OCMAX || ((a.in_stride | a.in_off) & 3) ||
       (long)a.IWt * a.in_stride * 4 >= 0x7fffffffL || (long)a.OW * 96 * 4 * 2 >= 0x7fffffffL)
     return hipErrorInvalidValue;
   const long nwt = (long)a.N * a.OH * ((a.OW + 15) / 16);  // one 16-pixel row per wave-tile
@@ -1429,6 +1495,7 @@ hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* w
   if (save && h.rd) return hipErrorInvalidValue;  // the pair pass saves nothing
   if (h.rd) hipLaunchKernelGGL((k_nin_head_x6<false, true>), grid, block, 0, s, a, h, w, (int)nwt);
   else if (save) hipLaunchKernelGGL((k_nin_head_x6<true, false>), grid, block, 0, s, a, h, w, (int)nwt);
+  else if (bf16) hipLaunchKernelGGL((k_nin_head_x6<false, false, true>), grid, block, 0, s, a, h, w, (int)nwt);
   else hipLaunchKernelGGL((k_nin_head_x6<false, false>), grid, block, 0, s, a, h, w, (int)nwt);
   return hipGetLastError();
 }

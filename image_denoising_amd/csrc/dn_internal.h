@@ -231,7 +231,9 @@ hipError_t launch_pack_head(const WView& wa, const WView& wb, float* out, hipStr
                             PackBatch* pb = nullptr);  // pb: queued, not launched
 // bf16x6 nin head (conv_x6.hip): pre-split nin_a | nin_b images (2 x X6_HEAD_BF bf16)
 hipError_t launch_pack_head_x6(const float* wa, const float* wb, void* out, hipStream_t s);
-hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* wimg, hipStream_t s);
+// bf16: plain bf16 products (the bf16 base; no saved activations, no pair image)
+hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* wimg, hipStream_t s,
+                              bool bf16 = false);
 // dec_conv1b-shaped 3x3 forward (K = NOUT = 96, EPI_BIAS_ACT) on the two N2N pair pixels of every
 // 2x2 cell only (a.sel_rd): output = the "pair image" [N][OH/2][OW][96] NHWC, column 2j + s = pixel
 // pair[rd][s] of cell j (s = 0, 1), i.e. exactly the pixels training_script.md:141-144 reads

@@ -420,6 +420,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     FwdArgs a{};
     a.in = in.p; a.in_stride = in.stride; a.in_off = in.off; a.IHt = h; a.IWt = w;
     a.N = Nn; a.OH = h; a.OW = w; a.K = K; a.NOUT = cout;
+    if (i == D1A) a.K = p.c1s;  // the zero pad channel as in the x6 path: K % 4 == 0 (pipelined)
     a.wp = ws + p.packBF[i]; a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
     a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = layout;
     return launch_fwd_bf16(a, st, ksize);
@@ -429,8 +430,9 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   static const bool head_x6_env = !getenv("DN_X6_HEAD") || atoi(getenv("DN_X6_HEAD")) != 0;
   const bool sel = x6 && sel_rd && !p.with_bwd && p.OC <= X6_HEAD_OCMAX;
   const bool head_x6 = x6 && (head_x6_env || sel) && p.OC <= X6_HEAD_OCMAX;
-  // bf16 base (inference only): the fused bf16x6 head instead of nin_a / nin_b as two bf16 1x1
-  // launches + an fp32 nin_c (two 96-channel round trips through HBM saved; DN_BF16_HEAD_X6=0)
+  // bf16 base (inference only): the fused head kernel in plain bf16 products instead of nin_a /
+  // nin_b as two bf16 1x1 launches + an fp32 nin_c (two 96-channel round trips through HBM
+  // saved; DN_BF16_HEAD_X6=0 keeps the three launches)
   static const bool bf16_head_env = !getenv("DN_BF16_HEAD_X6") || atoi(getenv("DN_BF16_HEAD_X6")) != 0;
   const bool bf16_head_x6 = bf16 && bf16_head_env && !p.with_bwd && p.OC <= X6_HEAD_OCMAX;
   // the 96-channel deconvs on the persistent bf16x6 kernel, also in the bf16 base (one pass over
@@ -563,7 +565,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
       h.ba = Bs(NINA); h.bb = Bs(NINB);
       h.wc = prm + p.P.L[NINC].woff; h.bc = Bs(NINC); h.oc = p.OC;
       h.y = y;
-      DN_TRY(launch_nin_head_x6(a, h, ws + p.packH, s));
+      DN_TRY(launch_nin_head_x6(a, h, ws + p.packH, s, /*bf16=*/true));
       return DN_OK;
     }
     DN_TRY(conv_forward(V(p.d1b, 96), N, H(0), Wd(0), 96, Wt(NINA), Bs(NINA), 96, 1, 1,

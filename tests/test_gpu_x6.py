@@ -183,6 +183,8 @@ def _wgrad(dz, x, x6):
     (96, 96, 2, 32, 32), (144, 96, 2, 16, 32), (48, 96, 2, 64, 64), (97, 96, 1, 32, 32),
     (96, 96, 4, 16, 16), (96, 96, 8, 8, 8), (96, 96, 16, 4, 4), (96, 96, 64, 128, 128),
     (48, 48, 2, 32, 32), (144, 48, 4, 16, 16), (48, 48, 64, 128, 128),  # 48 outputs
+    # sides that are not whole stage blocks (the generic DMA addressing) and an exact 8-wide one
+    (96, 96, 2, 20, 36), (48, 48, 3, 24, 40), (96, 96, 2, 13, 16), (96, 96, 2, 12, 8),
 ])
 def test_x6_backward_weight_vs_fp64(cin, cout, N, H, W):
     g = torch.Generator().manual_seed(7)
