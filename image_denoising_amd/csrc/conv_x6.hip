@@ -75,11 +75,11 @@ __global__ __launch_bounds__(256, 2) void k_c3x6(FwdArgs a) {
   const int nch = (a.K + C::KC - 1) / C::KC;
   const int nst = 9 * nch;
 
-  f32x4 acc[MT][NT];
+  f32x4 acc[MT][NT], accl[MT][NT];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int q = 0; q < NT; ++q) acc[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < NT; ++q) acc[m][q] = accl[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   float4 xr[C::XITEMS];
   auto load_x = [&](int k0) {
@@ -163,13 +163,14 @@ __global__ __launch_bounds__(256, 2) void k_c3x6(FwdArgs a) {
 #pragma unroll
       for (int p = 0; p < 3; ++p) bv[p][q] = *reinterpret_cast<const bf16x8*>(lw + p * C::WPL + off);
     }
-    x6_block<MT, NT, x6_qg(MT, NT)>(acc, av, bv);
+    x6_block_c<MT, NT, x6_qgc(MT, NT)>(acc, accl, av, bv);
     if (t == 8 && c + 1 < nch) {  // every wave is done with this chunk's x tile
       __syncthreads();
       store_x();
     }
     __syncthreads();  // next stage's weights landed (vmcnt(0)); next x tile written
   }
+  x6_fold(acc, accl);
   fwd_epilogue<NT, MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
 }
 
@@ -210,16 +211,21 @@ __device__ __forceinline__ void x6_barrier() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-// SEL: a.sel_rd's N2N pair pixels only (launch_fwd_x6_sel): a wave's two tile rows are one row
-// of 2x2 cells, whose 16 selected pixels (2 per cell) form ONE M fragment (the lane of fragment
-// row 2j + s reads its A operand at the pixel pair[rd][s] of cell j): half the MFMAs, the same
-// staging, per-pixel arithmetic unchanged (bit-identical outputs); the epilogue writes the
-// fragment as row ty0/2 + wave of the [OH/2][OW] pair image.
+// SEL: a.sel_rd's N2N pair pixels only (launch_fwd_x6_sel): the 16 selected pixels (2 per cell)
+// of one row of 2x2 cells form ONE M fragment (the lane of fragment row 2j + s reads its A
+// operand at the pixel pair[rd][s] of cell j): half the MFMAs, the same staging, per-pixel
+// arithmetic unchanged (bit-identical outputs).  Wave w computes cell rows 2(w&3), 2(w&3)+1 of
+// the tile for output channels [NT/2 * 16 (w>>2), +NT/2 * 16): two M fragments x NT/2 B
+// fragments per stage (6 + 9 operand reads) instead of one cell row x NT (3 + 18) -- the B
+// reads had made the LDS array, not the matrix core, the limit.  The epilogue writes row
+// ty0/2 + 2(w&3) + m of the [OH/2][OW] pair image, channels of the wave's half.
 template <int NT, int TAIL, bool SEL = false>
 __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   using C = PCfg<NT>;
-  static_assert(!SEL || TAIL == 0, "selected pixels: full 32-channel chunks only");
-  constexpr int MTC = SEL ? 1 : C::MT;  // M fragments computed per wave
+  static_assert(!SEL || (TAIL == 0 && NT % 2 == 0 && C::MT == 2 && C::WAVES == 8),
+                "selected pixels: full 32-channel chunks, 8 waves of two cell rows x NT/2");
+  constexpr int MTC = C::MT;               // M fragments computed per wave
+  constexpr int NTW = SEL ? NT / 2 : NT;   // B fragments per wave
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
   __bf16* lx = reinterpret_cast<__bf16*>(lds_raw);
   __bf16* ring = lx + 3 * C::XPL;
@@ -240,20 +246,26 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   constexpr int tail_st = tail == 1 ? 2 : 5;
   const int nst = 9 * nch - (tail ? 9 - tail_st : 0);
 
-  f32x4 acc[MTC][NT];
+  f32x4 acc[MTC][NTW], accl[MTC][NTW];
 #pragma unroll
   for (int m = 0; m < MTC; ++m)
 #pragma unroll
-    for (int q = 0; q < NT; ++q) acc[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // SEL: x-tile pixel of this lane's fragment row (cell j = li / 2, pair member s = li % 2)
-  int selpix = 0;
+    for (int q = 0; q < NTW; ++q) acc[m][q] = accl[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int qoff = SEL ? (wave >> 2) * NTW : 0;  // first B fragment (16 channels) of this wave
+  // SEL: x-tile pixel of this lane's row of fragment m (tile cell row 2(w&3) + m, cell
+  // j = li / 2, pair member s = li % 2)
+  int selpix[MTC] = {};
   if constexpr (SEL) {
-    const int ci = ty0 / 2 + wave, cj = tx0 / 2 + (li >> 1);
-    const int r = (ci < a.OH / 2 && cj < a.OW / 2)
-                      ? a.sel_rd[((long)n * (a.OH / 2) + ci) * (a.OW / 2) + cj] & 7 : 0;
-    constexpr unsigned kPair = 0xB721ED84u;  // train.py:151-154, 4 bits (a | b << 2) per rd
-    const int k = (kPair >> (4 * r + 2 * (li & 1))) & 3;
-    selpix = (2 * wave + (k >> 1)) * C::IW + 2 * (li >> 1) + (k & 1);
+#pragma unroll
+    for (int m = 0; m < MTC; ++m) {
+      const int lc = 2 * (wave & 3) + m;
+      const int ci = ty0 / 2 + lc, cj = tx0 / 2 + (li >> 1);
+      const int r = (ci < a.OH / 2 && cj < a.OW / 2)
+                        ? a.sel_rd[((long)n * (a.OH / 2) + ci) * (a.OW / 2) + cj] & 7 : 0;
+      constexpr unsigned kPair = 0xB721ED84u;  // train.py:151-154, 4 bits (a | b << 2) per rd
+      const int k = (kPair >> (4 * r + 2 * (li & 1))) & 3;
+      selpix[m] = (2 * lc + (k >> 1)) * C::IW + 2 * (li >> 1) + (k & 1);
+    }
   }
 
   // Exactly XITEMS buffer loads per thread per chunk (items outside the tile or the image get
@@ -338,7 +350,7 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     const bool more = c + 1 < nch;
     const int st = 9 * c + t;
     const __bf16* lw = ring + (st % C::S) * C::WSTP;
-    bf16x8 av[3][MTC], bv[3][NT];
+    bf16x8 av[3][MTC], bv[3][NTW];
     // MODE 3: the last chunk's mode decided at run time (tail instantiations: one A-read path
     // with branches keeps them at <= 256 VGPRs; two peeled paths would spill)
     const int mode = MODE == 3 ? ((tail && c + 1 == nch) ? tail : 0) : MODE;
@@ -382,10 +394,14 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
       }
     } else if constexpr (SEL) {
       const int ky = t / 3, kx = t - 3 * ky;
-      const int pix = selpix + ky * C::IW + kx;
-      const int off = pix * C::KC + x6_swz(pix, lg) * 8;
 #pragma unroll
-      for (int p = 0; p < 3; ++p) av[p][0] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
+      for (int m = 0; m < MTC; ++m) {
+        const int pix = selpix[m] + ky * C::IW + kx;
+        const int off = pix * C::KC + x6_swz(pix, lg) * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          av[p][m] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
+      }
     } else {
       const int ky = t / 3, kx = t - 3 * ky;
 #pragma unroll
@@ -401,11 +417,11 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     // MFMAs: the reads of group g + LOOK are issued after group g's MFMAs (into its freed
     // registers), so every MFMA finds its operands in flight long enough, and the stage's
     // operands never all live at once (the kernel is at 2 waves per SIMD, 256 VGPRs)
-    constexpr int QG = x6_qg(MTC, NT), NG = NT / QG, LOOK = NG < 2 ? NG : 2;
+    constexpr int QG = x6_qgc(MTC, NTW), NG = NTW / QG, LOOK = NG < 2 ? NG : 2;
     auto read_b = [&](int g) {
 #pragma unroll
       for (int q = g * QG; q < (g + 1) * QG; ++q) {
-        const int row = q * 16 + li;
+        const int row = (qoff + q) * 16 + li;
         const int off = row * C::KC + x6_swz(row, lg) * 8;
 #pragma unroll
         for (int p = 0; p < 3; ++p)
@@ -417,7 +433,7 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      x6_group<MTC, NT, QG>(acc, av, bv, g * QG);
+      x6_group_c<MTC, NTW, QG>(acc, accl, av, bv, g * QG);
       __builtin_amdgcn_sched_barrier(0);
       if (g + LOOK < NG) read_b(g + LOOK);
       __builtin_amdgcn_sched_barrier(0);
@@ -453,10 +469,17 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   }
   X6_WAITCNT_VM(0);  // the trailing re-load DMAs must land before the LDS is reused
   x6_barrier();
-  if constexpr (SEL) {  // the pair image: OH/2 rows, row ty0/2 + wave, column tx0 + fragment row
+  x6_fold(acc, accl);
+  if constexpr (SEL) {
+    // the pair image: OH/2 rows, row ty0/2 + 2(w&3) + m, column tx0 + fragment row, the wave's
+    // NTW*16 channels (the epilogue places wave w's rows at its ty0 argument + w*MT + m)
     FwdArgs ap = a;
     ap.OH = a.OH / 2;
-    fwd_epilogue<NT, 1, C::PS, false>(ap, acc, reinterpret_cast<float*>(lds_raw), ty0 / 2, tx0, n);
+    ap.NOUT = NTW * 16;
+    ap.out_off = a.out_off + qoff * 16;
+    ap.bias = a.bias ? a.bias + qoff * 16 : nullptr;
+    fwd_epilogue<NTW, MTC, C::PS, false>(ap, acc, reinterpret_cast<float*>(lds_raw),
+                                         ty0 / 2 + 2 * (wave & 3) - MTC * wave, tx0, n);
   } else {
     fwd_epilogue<NT, C::MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
   }
@@ -494,6 +517,9 @@ struct HCfg {
   static_assert(2 * LBYTES <= 163840, "two workgroups per CU");
 };
 
+#ifndef DN_X6H_CARRY
+#define DN_X6H_CARRY 1  // A/B switch: 0 = per-block sums in k_c3x6h
+#endif
 template <int NT, int TAIL, int MT_ = 2>
 __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
   using C = HCfg<NT, MT_>;
@@ -517,11 +543,11 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
   constexpr int tail_st = tail == 1 ? 2 : 5;
   const int nst = 9 * nch - (tail ? 9 - tail_st : 0);
 
-  f32x4 acc[MT][NT];
+  f32x4 acc[MT][NT], accl[MT][NT];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int q = 0; q < NT; ++q) acc[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < NT; ++q) acc[m][q] = accl[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // input rows of this tile through a 32-bit buffer resource (see k_c3x6p)
   const int ry0 = iy0 > 0 ? iy0 : 0, ry1 = iy0 + C::IH < a.IHt ? iy0 + C::IH : a.IHt;
@@ -596,7 +622,7 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
     const int mode = (tail && c + 1 == nch) ? tail : 0;
     // MT = 4: the A pieces of two rows at a time (registers), the B fragments read once for all
     constexpr int MH = MT >= 4 ? 2 : MT;
-    constexpr int QG = MT >= 4 ? 1 : x6_qg(MT, NT), NG = NT / QG, LOOK = NG < 2 ? NG : 2;
+    constexpr int QG = MT >= 4 ? 1 : (DN_X6H_CARRY ? x6_qgc(MT, NT) : x6_qg(MT, NT)), NG = NT / QG, LOOK = NG < 2 ? NG : 2;
     bf16x8 bv[3][NT];
     auto read_b = [&](int g) {
 #pragma unroll
@@ -662,9 +688,12 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
       }
       __builtin_amdgcn_sched_barrier(0);
       f32x4(&acch)[MH][NT] = *reinterpret_cast<f32x4(*)[MH][NT]>(&acc[mh * MH]);
+      f32x4(&acclh)[MH][NT] = *reinterpret_cast<f32x4(*)[MH][NT]>(&accl[mh * MH]);
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
-        x6_group<MH, NT, QG>(acch, av, bv, g * QG);
+        // MT = 4 keeps the per-block form: its 2 x 48 accumulators leave no room for accl
+        if constexpr (MT >= 4 || !DN_X6H_CARRY) x6_group<MH, NT, QG>(acch, av, bv, g * QG);
+        else x6_group_c<MH, NT, QG>(acch, acclh, av, bv, g * QG);
         if constexpr (MT >= 4) {  // the block sums' adds here, not deferred (live MFMA results)
 #pragma unroll
           for (int i = 0; i < MH; ++i)
@@ -693,6 +722,7 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
 #pragma unroll 1
     for (int t = 0; t < ns; ++t) stage(c, t);
   }
+  x6_fold(acc, accl);
   fwd_epilogue<NT, MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
 }
 

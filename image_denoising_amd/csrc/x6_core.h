@@ -113,4 +113,74 @@ __device__ __forceinline__ void x6_block(f32x4 (&acc)[MT][NT], const bf16x8 (&av
   for (int q0 = 0; q0 < NT; q0 += QG) x6_group<MT, NT, QG>(acc, av, bv, q0);
 }
 
+// Carried-correction form (the 3x3 forward / data-gradient kernels): the leading product a0*b0
+// of a block is still summed from zero and added to the running sum `acc` by a round-to-nearest
+// VALU add, but the five corrections chain across blocks in their own accumulator `accl`
+// (added to acc once, before the epilogue).  The corrections are <= 2^-7 of the products they
+// correct, so the matrix core's alignment bias on that chain is <= 2^-7 of the bias a chained
+// leading sum would carry -- below one fp32 rounding of the output over a K = 864 dot product --
+// while the block costs 4 VALU adds per fragment instead of 8 and no fresh lo chain.
+// DN_X6_CARRY=0 builds the per-block form (accl stays zero) for A/B runs.
+#ifndef DN_X6_CARRY
+#define DN_X6_CARRY 1
+#endif
+// fragment-group width of the carried form: one chain per fragment is enough (a single
+// 16x16x32 bf16 accumulation chain issues back-to-back, MI355X_MICROARCH.md), and the narrow
+// group keeps the hi temporaries and the B look-ahead small enough for the extra accl registers
+#ifndef DN_X6_QGC
+#define DN_X6_QGC 1
+#endif
+constexpr int x6_qgc(int mt, int nt) {
+  return DN_X6_CARRY ? (DN_X6_QGC > 0 ? DN_X6_QGC : x6_qg(mt, nt)) : x6_qg(mt, nt);
+}
+template <int MT, int NT, int QG>
+__device__ __forceinline__ void x6_group_c(f32x4 (&acc)[MT][NT], f32x4 (&accl)[MT][NT],
+                                           const bf16x8 (&av)[3][MT], const bf16x8 (&bv)[3][NT],
+                                           int q0) {
+#if DN_X6_CARRY
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  constexpr int PA[5] = {0, 1, 0, 1, 2}, PB[5] = {1, 0, 2, 1, 0};
+  f32x4 hi[MT][QG];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int g = 0; g < QG; ++g) hi[m][g] = mfma_bf16(av[0][m], bv[0][q0 + g], z);
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int g = 0; g < QG; ++g)
+        accl[m][q0 + g] = mfma_bf16(av[PA[j]][m], bv[PB[j]][q0 + g], accl[m][q0 + g]);
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int g = 0; g < QG; ++g)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[m][q0 + g][r] = acc[m][q0 + g][r] + hi[m][g][r];
+#else
+  (void)accl;
+  x6_group<MT, NT, QG>(acc, av, bv, q0);
+#endif
+}
+
+template <int MT, int NT, int QG>
+__device__ __forceinline__ void x6_block_c(f32x4 (&acc)[MT][NT], f32x4 (&accl)[MT][NT],
+                                           const bf16x8 (&av)[3][MT], const bf16x8 (&bv)[3][NT]) {
+  static_assert(NT % QG == 0, "whole fragment groups");
+#pragma unroll
+  for (int q0 = 0; q0 < NT; q0 += QG) x6_group_c<MT, NT, QG>(acc, accl, av, bv, q0);
+}
+
+// acc += accl (the carried corrections), once before the epilogue
+template <int MT, int NT>
+__device__ __forceinline__ void x6_fold(f32x4 (&acc)[MT][NT], const f32x4 (&accl)[MT][NT]) {
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[m][q][r] = acc[m][q][r] + accl[m][q][r];
+}
+
 }  // namespace dn
