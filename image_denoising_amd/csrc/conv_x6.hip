@@ -219,6 +219,9 @@ __device__ __forceinline__ void x6_barrier() {
 // fragments per stage (6 + 9 operand reads) instead of one cell row x NT (3 + 18) -- the B
 // reads had made the LDS array, not the matrix core, the limit.  The epilogue writes row
 // ty0/2 + 2(w&3) + m of the [OH/2][OW] pair image, channels of the wave's half.
+#ifndef DN_X6P_LOOK
+#define DN_X6P_LOOK 2  // B fragment groups read ahead of their MFMAs in k_c3x6p
+#endif
 template <int NT, int TAIL, bool SEL = false>
 __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   using C = PCfg<NT>;
@@ -417,7 +420,7 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     // MFMAs: the reads of group g + LOOK are issued after group g's MFMAs (into its freed
     // registers), so every MFMA finds its operands in flight long enough, and the stage's
     // operands never all live at once (the kernel is at 2 waves per SIMD, 256 VGPRs)
-    constexpr int QG = x6_qgc(MTC, NTW), NG = NTW / QG, LOOK = NG < 2 ? NG : 2;
+    constexpr int QG = x6_qgc(MTC, NTW), NG = NTW / QG, LOOK = NG < DN_X6P_LOOK ? NG : DN_X6P_LOOK;
     auto read_b = [&](int g) {
 #pragma unroll
       for (int q = g * QG; q < (g + 1) * QG; ++q) {
@@ -517,6 +520,10 @@ struct HCfg {
   static_assert(2 * LBYTES <= 163840, "two workgroups per CU");
 };
 
+#ifndef DN_X6H_LOOK
+#define DN_X6H_LOOK 2  // B fragment groups read ahead of their MFMAs in k_c3x6h (NT = 6: 3,
+                      // 100->96 at 64 x 256^2 3.70 -> 3.59 ms, profiles/r2_ab_look.log)
+#endif
 #ifndef DN_X6H_CARRY
 #define DN_X6H_CARRY 1  // A/B switch: 0 = per-block sums in k_c3x6h
 #endif
@@ -622,7 +629,8 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
     const int mode = (tail && c + 1 == nch) ? tail : 0;
     // MT = 4: the A pieces of two rows at a time (registers), the B fragments read once for all
     constexpr int MH = MT >= 4 ? 2 : MT;
-    constexpr int QG = MT >= 4 ? 1 : (DN_X6H_CARRY ? x6_qgc(MT, NT) : x6_qg(MT, NT)), NG = NT / QG, LOOK = NG < 2 ? NG : 2;
+    constexpr int QG = MT >= 4 ? 1 : (DN_X6H_CARRY ? x6_qgc(MT, NT) : x6_qg(MT, NT)), NG = NT / QG,
+                  LOOK = NG < DN_X6H_LOOK ? NG : (NT == 6 && MT == 2 ? 3 : DN_X6H_LOOK);
     bf16x8 bv[3][NT];
     auto read_b = [&](int g) {
 #pragma unroll
