@@ -28,6 +28,10 @@
 
 namespace dn {
 
+#ifndef DN_X6_GDMA
+#define DN_X6_GDMA 0  // A/B switch: 1 = the 3x3 kernels' weight DMA as global_load_lds
+#endif
+
 // bf16 elements of one weight stage (one tap, three planes of NP x 32) in the packed image,
 // padded to whole rounds of the pipelined kernel's DMA (8 waves x 1 KiB global_load_lds_dwordx4;
 // the 12-byte form would fit 18 KiB exactly, but it writes lane x 16 B in LDS, not lane x 12)
@@ -127,13 +131,19 @@ __global__ __launch_bounds__(256, 2) void k_c3x6(FwdArgs a) {
       }
     }
   };
+  // (buffer loads to LDS, not global_load_lds: see k_c3x6p's load_w)
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__bf16*>(wimg), (short)0, nst * C::WSTP * 2, 0x00020000);
   auto load_w = [&](int st, __bf16* dst) {  // stage st = chunk * 9 + tap, whole KiB pieces
-    const __bf16* src = wimg + (long)st * C::WSTP;
 #pragma unroll
     for (int p = wave; p < C::WST / 512; p += 4) {
+#if DN_X6_GDMA
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(src + p * 512 + lane * 8),
+          (const __attribute__((address_space(1))) void*)(wimg + (long)st * C::WSTP + p * 512 + lane * 8),
           (__attribute__((address_space(3))) void*)(dst + p * 512), 16, 0, 0);
+#else
+      buf_lds16(wrs, dst + p * 512, (st * C::WSTP + p * 512 + lane * 8) * 2);
+#endif
     }
   };
 
@@ -204,6 +214,13 @@ struct PCfg {
 
 #define X6_WAITCNT_VM(n) \
   __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
+// the same with lgkmcnt(0): at a stage's end every LDS read has been consumed, so the wait is
+// free, and it clears the compiler's view of the stage's weight DMAs as pending LGKM events --
+// otherwise the next stage's first MFMA waits lgkmcnt(0) for all of its operand reads instead
+// of the counted lgkmcnt(N) for the first few (the waitcnt pass treats global_load_lds as an
+// out-of-order LGKM event)
+#define X6_WAITCNT_VM_LGKM0(n) \
+  __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4))
 
 __device__ __forceinline__ void x6_barrier() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no compiler motion of LDS accesses across it
@@ -219,6 +236,9 @@ __device__ __forceinline__ void x6_barrier() {
 // fragments per stage (6 + 9 operand reads) instead of one cell row x NT (3 + 18) -- the B
 // reads had made the LDS array, not the matrix core, the limit.  The epilogue writes row
 // ty0/2 + 2(w&3) + m of the [OH/2][OW] pair image, channels of the wave's half.
+#ifndef DN_X6P_STAGED
+#define DN_X6P_STAGED 1  // A/B switch: the pipelined first fragment group of a k_c3x6p stage
+#endif
 #ifndef DN_X6P_LOOK
 #define DN_X6P_LOOK 2  // B fragment groups read ahead of their MFMAs in k_c3x6p
 #endif
@@ -317,16 +337,25 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
       }
     }
   };
-  // weights of stage `src_st` into ring slot `slot`: PPW DMAs of 1 KiB per wave
+  // weights of stage `src_st` into ring slot `slot`: PPW DMAs of 1 KiB per wave, as buffer loads
+  // to LDS (MUBUF): the FLAT-encoded global_load_lds counts as a pending FLAT access, which makes
+  // the compiler's waitcnt pass treat every later LDS-read wait as out of order (lgkmcnt(0)
+  // instead of the counted wait) as long as any of those DMAs is outstanding -- i.e. always
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__bf16*>(wimg), (short)0, nst * C::WSTP * 2, 0x00020000);
   auto load_w = [&](int src_st, int slot) {
-    const unsigned char* src = reinterpret_cast<const unsigned char*>(wimg + (long)src_st * C::WSTP);
     unsigned char* dst = reinterpret_cast<unsigned char*>(ring + slot * C::WSTP);
 #pragma unroll
     for (int j = 0; j < C::PPW; ++j) {
       const int piece = wave * C::PPW + j;
+#if DN_X6_GDMA
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(src + piece * 1024 + lane * 16),
+          (const __attribute__((address_space(1))) void*)(reinterpret_cast<const unsigned char*>(wimg) +
+                                                          (long)src_st * C::WSTP * 2 + piece * 1024 + lane * 16),
           (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16, 0, 0);
+#else
+      buf_lds16(wrs, dst + piece * 1024, src_st * C::WSTP * 2 + piece * 1024 + lane * 16);
+#endif
     }
   };
 
@@ -357,7 +386,15 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     // MODE 3: the last chunk's mode decided at run time (tail instantiations: one A-read path
     // with branches keeps them at <= 256 VGPRs; two peeled paths would spill)
     const int mode = MODE == 3 ? ((tail && c + 1 == nch) ? tail : 0) : MODE;
-    if (mode == 1) {
+    constexpr int QG = x6_qgc(MTC, NTW), NG = NTW / QG, LOOK = NG < DN_X6P_LOOK ? NG : DN_X6P_LOOK;
+    // STAGED (full chunks, carried form): the stage's first fragment group is issued as a
+    // read/compute pipeline -- A plane p and B plane p of group 0 requested one step before the
+    // MFMAs that use them -- so the first MFMA waits for 3 reads, not for all 6 A + 6 B reads
+    // of a stage that all 8 waves issue together after the barrier (384 LDS cycles); the MFMA
+    // order per accumulator is that of x6_group_c (results unchanged bit for bit)
+    constexpr bool STAGED = MODE == 0 && DN_X6_CARRY && QG == 1 && NG >= 3 && DN_X6P_STAGED;
+    if constexpr (STAGED) {
+    } else if (mode == 1) {
       // im2col stage t: lane group lg holds k = 8lg..8lg+7 = channels 0..3 of taps
       // 8t+2lg and 8t+2lg+1 (taps past 8 are zero), read as 8 B from quad 0 of the pixel
       const int ta = 8 * t + 2 * lg, tb = ta + 1;
@@ -420,7 +457,6 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     // MFMAs: the reads of group g + LOOK are issued after group g's MFMAs (into its freed
     // registers), so every MFMA finds its operands in flight long enough, and the stage's
     // operands never all live at once (the kernel is at 2 waves per SIMD, 256 VGPRs)
-    constexpr int QG = x6_qgc(MTC, NTW), NG = NTW / QG, LOOK = NG < DN_X6P_LOOK ? NG : DN_X6P_LOOK;
     auto read_b = [&](int g) {
 #pragma unroll
       for (int q = g * QG; q < (g + 1) * QG; ++q) {
@@ -431,15 +467,67 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
           bv[p][q] = *reinterpret_cast<const bf16x8*>(lw + p * C::WPL + off);
       }
     };
+    if constexpr (STAGED) {
+      const int ky = t / 3, kx = t - 3 * ky;
+      auto read_a = [&](int p) {
 #pragma unroll
-    for (int g = 0; g < LOOK; ++g) read_b(g);
-    __builtin_amdgcn_sched_barrier(0);
+        for (int m = 0; m < MTC; ++m) {
+          int pix;
+          if constexpr (SEL) pix = selpix[m] + ky * C::IW + kx;
+          else pix = (wave * C::MT + m + ky) * C::IW + li + kx;
+          const int off = pix * C::KC + x6_swz(pix, lg) * 8;
+          av[p][m] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + off);
+        }
+      };
+      auto read_bp = [&](int p) {  // plane p of B fragment 0
+        const int row = qoff * 16 + li;
+        const int off = row * C::KC + x6_swz(row, lg) * 8;
+        bv[p][0] = *reinterpret_cast<const bf16x8*>(lw + p * C::WPL + off);
+      };
+      auto lo = [&](int pa, int pb) {
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      x6_group_c<MTC, NTW, QG>(acc, accl, av, bv, g * QG);
+        for (int m = 0; m < MTC; ++m) accl[m][0] = mfma_bf16(av[pa][m], bv[pb][0], accl[m][0]);
+      };
+      read_a(0); read_bp(0); read_bp(1);
       __builtin_amdgcn_sched_barrier(0);
-      if (g + LOOK < NG) read_b(g + LOOK);
+      read_a(1); read_bp(2);
       __builtin_amdgcn_sched_barrier(0);
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      f32x4 hi[MTC];
+#pragma unroll
+      for (int m = 0; m < MTC; ++m) hi[m] = mfma_bf16(av[0][m], bv[0][0], z);
+      lo(0, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      read_a(2); read_b(1);
+      __builtin_amdgcn_sched_barrier(0);
+      lo(1, 0); lo(0, 2); lo(1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      read_b(2);
+      __builtin_amdgcn_sched_barrier(0);
+      lo(2, 0);
+#pragma unroll
+      for (int m = 0; m < MTC; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[m][0][r] = acc[m][0][r] + hi[m][r];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 1; g < NG; ++g) {
+        x6_group_c<MTC, NTW, QG>(acc, accl, av, bv, g * QG);
+        __builtin_amdgcn_sched_barrier(0);
+        if (g + 2 < NG) read_b(g + 2);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < LOOK; ++g) read_b(g);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        x6_group_c<MTC, NTW, QG>(acc, accl, av, bv, g * QG);
+        __builtin_amdgcn_sched_barrier(0);
+        if (g + LOOK < NG) read_b(g + LOOK);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     const bool xstep = t == 8 && more;
     if (xstep) {
@@ -453,9 +541,9 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     // chunk's first stage) -- the x loads are not waited for here
     // (stages 0 and 1: the prologue's chunk-1 x loads are younger than their DMAs)
     if (xstep || (t == 0 && c > 0) || (c == 0 && t < 2))
-      X6_WAITCNT_VM(C::PPW * (C::S - 2) + C::XITEMS);
+      X6_WAITCNT_VM_LGKM0(C::PPW * (C::S - 2) + C::XITEMS);
     else
-      X6_WAITCNT_VM(C::PPW * (C::S - 2));
+      X6_WAITCNT_VM_LGKM0(C::PPW * (C::S - 2));
     if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
     x6_barrier();
   };
@@ -521,8 +609,7 @@ struct HCfg {
 };
 
 #ifndef DN_X6H_LOOK
-#define DN_X6H_LOOK 2  // B fragment groups read ahead of their MFMAs in k_c3x6h (NT = 6: 3,
-                      // 100->96 at 64 x 256^2 3.70 -> 3.59 ms, profiles/r2_ab_look.log)
+#define DN_X6H_LOOK 2  // B fragment groups read ahead of their MFMAs in k_c3x6h
 #endif
 #ifndef DN_X6H_CARRY
 #define DN_X6H_CARRY 1  // A/B switch: 0 = per-block sums in k_c3x6h
@@ -598,16 +685,23 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
   };
   // stage src_st's 18 pieces into slot `slot`: wave w copies pieces w, w+4, ...; a wave with
   // fewer than PPW repeats its last piece (same bytes, same place) so every wave issues PPW
+  // (buffer loads to LDS, not global_load_lds: see k_c3x6p's load_w)
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__bf16*>(wimg), (short)0, nst * C::WSTP * 2, 0x00020000);
   auto load_w = [&](int src_st, int slot) {
-    const unsigned char* src = reinterpret_cast<const unsigned char*>(wimg + (long)src_st * C::WSTP);
     unsigned char* dst = reinterpret_cast<unsigned char*>(ring + slot * C::WST);
 #pragma unroll
     for (int j = 0; j < C::PPW; ++j) {
       int piece = wave + j * C::WAVES;
       if (piece >= C::PIECES) piece -= C::WAVES;
+#if DN_X6_GDMA
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(src + piece * 1024 + lane * 16),
+          (const __attribute__((address_space(1))) void*)(reinterpret_cast<const unsigned char*>(wimg) +
+                                                          (long)src_st * C::WSTP * 2 + piece * 1024 + lane * 16),
           (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16, 0, 0);
+#else
+      buf_lds16(wrs, dst + piece * 1024, src_st * C::WSTP * 2 + piece * 1024 + lane * 16);
+#endif
     }
   };
 
@@ -630,7 +724,7 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
     // MT = 4: the A pieces of two rows at a time (registers), the B fragments read once for all
     constexpr int MH = MT >= 4 ? 2 : MT;
     constexpr int QG = MT >= 4 ? 1 : (DN_X6H_CARRY ? x6_qgc(MT, NT) : x6_qg(MT, NT)), NG = NT / QG,
-                  LOOK = NG < DN_X6H_LOOK ? NG : (NT == 6 && MT == 2 ? 3 : DN_X6H_LOOK);
+                  LOOK = NG < DN_X6H_LOOK ? NG : DN_X6H_LOOK;
     bf16x8 bv[3][NT];
     auto read_b = [&](int g) {
 #pragma unroll

@@ -54,6 +54,18 @@ __device__ __forceinline__ void split3x8(const float (&v)[8], bf16x8& p0, bf16x8
   p2 = __builtin_bit_cast(bf16x8, l);
 }
 
+// 16 bytes per lane from a buffer resource into LDS at lds + 16 * lane (buffer_load_dwordx4 ...
+// lds).  The builtin exists only for the device pass: in the host pass it would invalidate the
+// calling kernel templates and drop their host stubs without a diagnostic.
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, void* lds, int voffset) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 16,
+                                           voffset, 0, 0, 0);
+#else
+  (void)rs; (void)lds; (void)voffset;
+#endif
+}
+
 __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
