@@ -46,6 +46,18 @@ __device__ __forceinline__ void glds16b(const void* g, void* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
+// the same as a buffer load to LDS (k_fwd_bf16p): a pending global_load_lds (FLAT) keeps the
+// compiler's waitcnt pass from counting LDS-read waits (every wait becomes lgkmcnt(0)); the
+// builtin exists only for the device pass (see x6_core.h buf_lds16)
+__device__ __forceinline__ void blds16b(__amdgpu_buffer_rsrc_t rs, void* l, int voffset) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)l, 16,
+                                           voffset, 0, 0, 0);
+#else
+  (void)rs; (void)l; (void)voffset;
+#endif
+}
+
 // epilogue: stage each 16-pixel row through LDS, write whole pixels as float4 (NHWC; OUT_UP2:
 // the deconv parity scatter of blockIdx.z)
 template <int NT, int MT, int PS>
@@ -278,14 +290,15 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16p(FwdArgs a) {
       }
     }
   };
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__bf16*>(wimg), (short)0, nst * C::WST * 2, 0x00020000);
   auto load_w = [&](int st, int slot) {  // stage st = chunk * 3 + ky: PPW 1 KiB pieces per wave
-    const __bf16* src = wimg + (long)st * C::WST;
     __bf16* dst = ring + slot * C::WST;
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
       int p = wave + 4 * j;
       if (p >= PIECES) p -= 4;
-      glds16b(src + p * 512 + lane * 8, dst + p * 512);
+      blds16b(wrs, dst + p * 512, (st * C::WST + p * 512 + lane * 8) * 2);
     }
   };
 
