@@ -1697,16 +1697,32 @@ __global__ __launch_bounds__(512, 1) void k_deconv_x6(FwdArgs a, const __bf16* w
       const float v8[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
       bf16x8 xv[3][1];
       split3x8(v8, xv[0][0], xv[1][0], xv[2][0]);
-      bf16x8 wv[3][6];
-#pragma unroll
-      for (int f = 0; f < 6; ++f) {
+      // one output fragment at a time, its three weight planes read one fragment ahead: 24
+      // operand registers live instead of 72, which leaves room for the third input set below
+      bf16x8 wv[2][3];
+      auto read_w = [&](int f, bf16x8 (&w)[3]) {
         const int row = b * 96 + f * 16 + li;
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
-          wv[pl][f] = *reinterpret_cast<const bf16x8*>(img + (pl * 3 * 96 + row) * 32 + x6_swz(row, lg) * 8);
+          w[pl] = *reinterpret_cast<const bf16x8*>(img + (pl * 3 * 96 + row) * 32 + x6_swz(row, lg) * 8);
+      };
+      read_w(0, wv[0]);
+#pragma unroll
+      for (int f = 0; f < 6; ++f) {
+        if (f + 1 < 6) read_w(f + 1, wv[(f + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        // x6_group's product order (hi = w0 x0; lo = w0 x1, w1 x0, w0 x2, w1 x1, w2 x0)
+        const bf16x8(&w)[3] = wv[f & 1];
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 hi = mfma_bf16(w[0], xv[0][0], z);
+        f32x4 lo = mfma_bf16(w[0], xv[1][0], z);
+        lo = mfma_bf16(w[1], xv[0][0], lo);
+        lo = mfma_bf16(w[0], xv[2][0], lo);
+        lo = mfma_bf16(w[1], xv[1][0], lo);
+        lo = mfma_bf16(w[2], xv[0][0], lo);
+        x6_acc_add(out[f][0], hi, lo);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      x6_block<6, 1, 1>(out, wv, xv);
-      __builtin_amdgcn_sched_barrier(0);
     }
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         a.out + ((long)n * 2 * a.OH + 2 * gy + pa) * out_row + a.out_off, (short)0,
@@ -1720,16 +1736,23 @@ __global__ __launch_bounds__(512, 1) void k_deconv_x6(FwdArgs a, const __bf16* w
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rs, off + 64 * f, 0, 0);
     }
   };
+  // three input register sets: a wave-tile's input is requested two tiles before it is used
+  // (one tile of MFMA work did not cover the HBM latency: 0.8 ms at 64 x 128^2 -> 256^2 against
+  // ~0.4 ms of HBM traffic)
   int wt = grp * 4 + wq;
-  float4 xa[6], xb[6];
+  float4 xa[6], xb[6], xc[6];
   load(wt, xa);
+  load(wt + wstride, xb);
   __syncthreads();  // parity images and bias landed
-  for (; wt < nwt; wt += 2 * wstride) {
-    load(wt + wstride, xb);
+  for (; wt < nwt; wt += 3 * wstride) {
+    load(wt + 2 * wstride, xc);
     tile(wt, xa);
     if (wt + wstride >= nwt) break;
-    load(wt + 2 * wstride, xa);
+    load(wt + 3 * wstride, xa);
     tile(wt + wstride, xb);
+    if (wt + 2 * wstride >= nwt) break;
+    load(wt + 4 * wstride, xb);
+    tile(wt + 2 * wstride, xc);
   }
 }
 

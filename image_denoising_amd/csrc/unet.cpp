@@ -93,7 +93,16 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
     return o;
   };
   p.c1k = 2 * nf + p.C;             // [up1 | x] channels
-  p.c1s = (p.c1k + 3) / 4 * 4;      // stride padded to float4 (pad channels kept at zero)
+  p.c1kp = (p.c1k + 3) / 4 * 4;     // ... padded to float4 (pad channels kept at zero)
+  // pixel stride of forward-only plans (the N2N target pass, the frozen finetune base, eval): a
+  // multiple of 32 channels (128 B), so the deconv's 384-B pixel writes and dec_conv1a's 128-B
+  // chunk reads stay line-aligned (stride 100: 400-B pixels, every 64-B piece split over two
+  // lines; the 256^2 deconv measured 0.88 ms at stride 100, 0.64 at 96); channels [c1kp, c1s)
+  // are never written or read.  Plans with a backward keep the float4 stride (measured faster
+  // there).  DN_C1S_ALIGN=4 / 32 forces either.
+  static const int c1s_env = getenv("DN_C1S_ALIGN") ? atoi(getenv("DN_C1S_ALIGN")) : 0;
+  const int c1s_align = c1s_env > 0 ? c1s_env : (bwd ? 4 : 32);
+  p.c1s = (p.c1k + c1s_align - 1) / c1s_align * c1s_align;
   p.c1 = alloc(0, p.c1s);
   p.a0 = alloc(0, nf);
   p.a1 = alloc(0, nf);
@@ -396,7 +405,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   auto x6_tail_f = [&](int i) -> int {
     const Layer& L = p.P.L[i];
     const int l = layer_level(i);
-    return x6_pipelined(N, H(l), Wd(l), L.cout, 0) ? x6_tail_mode(i == D1A ? p.c1s : L.cin) : 0;
+    return x6_pipelined(N, H(l), Wd(l), L.cout, 0) ? x6_tail_mode(i == D1A ? p.c1kp : L.cin) : 0;
   };
   auto conv_forward = [&](const View& in, int Nn, int h, int w, int K, const float* wp,
                           const float* b, int cout, int ksize, int act, const View& out,
@@ -407,9 +416,9 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
       FwdArgs a{};
       a.in = in.p; a.in_stride = in.stride; a.in_off = in.off; a.IHt = h; a.IWt = w;
       a.N = Nn; a.OH = h; a.OW = w; a.K = K; a.NOUT = cout;
-      // dec_conv1a reads [up1 | x | zero pad] (c1s = c1k rounded to 4): taking the zero pad
+      // dec_conv1a reads [up1 | x | zero pad] (c1kp = c1k rounded to 4): taking the zero pad
       // channel as a reduction channel (its packed weights are zero) keeps K % 4 == 0
-      if (i == D1A) a.K = p.c1s;
+      if (i == D1A) a.K = p.c1kp;
       a.x6_tail = x6_tail_f(i);  // a partial last K chunk packed over fewer stages
       a.wp = ws + p.packX[i]; a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
       a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = layout;
@@ -420,7 +429,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     FwdArgs a{};
     a.in = in.p; a.in_stride = in.stride; a.in_off = in.off; a.IHt = h; a.IWt = w;
     a.N = Nn; a.OH = h; a.OW = w; a.K = K; a.NOUT = cout;
-    if (i == D1A) a.K = p.c1s;  // the zero pad channel as in the x6 path: K % 4 == 0 (pipelined)
+    if (i == D1A) a.K = p.c1kp;  // the zero pad channel as in the x6 path: K % 4 == 0 (pipelined)
     a.wp = ws + p.packBF[i]; a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
     a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = layout;
     return launch_fwd_bf16(a, st, ksize);
@@ -510,7 +519,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   DN_TRY(pack_flush(pb, s));
   // enc_conv0, fused with pool0 = x -> channels [2nf, 2nf+C) of the up1 concat buffer
   DN_TRY(launch_enc0_fwd(x, N, C, p.H, p.W, prm + p.P.L[ENC0].woff, Bs(ENC0), ws + p.a0,
-                         ws + p.c1, p.c1s, 2 * nf, p.c1s, p.with_bwd ? ws + p.xin : nullptr, s));
+                         ws + p.c1, p.c1s, 2 * nf, p.c1kp, p.with_bwd ? ws + p.xin : nullptr, s));
   DN_TRY(conv_forward(V(p.a0, nf), N, H(0), Wd(0), nf, Wt(ENC1), Bs(ENC1), nf, 3, 1, V(p.a1, nf),
                       OUT_NHWC, s));
   // pool1 -> skip slice of c2

@@ -31,7 +31,7 @@ struct Plan {
   int N, H, W, C, OC, nf;
   bool with_bwd;
   // forward activations (NHWC, offsets in floats)
-  int c1s, c1k;                 // up1 concat: stride (float4-padded) and real channels
+  int c1s, c1k, c1kp;           // up1 concat: pixel stride, real channels, float4-padded K
   long c1, a0, a1;
   long c[5]; int cs[5];         // concat buffers at levels 1..4
   long a[5];                    // a2..a5 at levels 1..4

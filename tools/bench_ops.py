@@ -37,6 +37,22 @@ def deconv(N, h, w, C, y_stride):
           f"{gb/ms:6.2f} TB/s(alg)  {fl/ms/1e9:6.1f} TF/s", flush=True)
 
 
+def deconv_x6(N, h, w, y_stride, y_off=0):
+    """the bf16x6 ConvTranspose2d(96, 96, 2, 2) of the training path (k_deconv_x6)"""
+    x = torch.randn(N, h, w, 96, device="cuda")
+    wt = torch.randn(96, 96, 2, 2, device="cuda") * 0.05
+    b = torch.zeros(96, device="cuda")
+    y = torch.empty(N, 2 * h, 2 * w, y_stride, device="cuda")
+    pk = _lib.scratch(_lib.lib().dn_deconv2x2_x6_pack_size(), "cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    f = lambda: _lib.call("dn_deconv2x2_forward_x6", x.data_ptr(), N, h, w, wt.data_ptr(),
+                          b.data_ptr(), y.data_ptr(), y_stride, y_off, pk.data_ptr(), pk.numel(), st)
+    ms = timeit(f)
+    gb = (x.numel() + N * 4 * h * w * 96) * 4 / 1e9
+    print(f"deconv_x6 N={N} {h}x{w} y_stride={y_stride}: {ms*1e3:8.1f} us  "
+          f"{gb/ms:6.2f} TB/s(alg)", flush=True)
+
+
 def conv(N, H, W, Cin, Cout, k, x_stride, y_stride):
     x = torch.randn(N, H, W, x_stride, device="cuda")
     wt = torch.randn(Cout, Cin, k, k, device="cuda") * 0.05
@@ -54,6 +70,10 @@ def conv(N, H, W, Cin, Cout, k, x_stride, y_stride):
 
 
 if __name__ == "__main__":
+    if os.environ.get("OPS") == "deconv_x6":
+        for (h, ys) in ((128, 100), (64, 144), (32, 144), (128, 96)):
+            deconv_x6(64, h, h, ys)
+        sys.exit(0)
     for ys in (96, 100, 128, 144):
         deconv(64, 128, 128, 96, ys)
     for ys in (96, 144):
