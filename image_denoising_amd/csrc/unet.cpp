@@ -107,7 +107,11 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
   p.a0 = alloc(0, nf);
   p.a1 = alloc(0, nf);
   for (int l = 1; l <= 4; ++l) {  // c2..c5 concat buffers (c5 is [u5 | p4] = 2nf)
-    p.cs[l] = (l == 4) ? 2 * nf : 3 * nf;
+    p.ck[l] = (l == 4) ? 2 * nf : 3 * nf;
+    // forward-only plans: pixel stride a multiple of 32 channels like c1 (144 -> 160: 640-B
+    // pixels, the deconv / pool writes and the 128-B chunk reads line-aligned)
+    const int a = c1s_env > 0 ? c1s_env : (bwd ? 1 : 32);
+    p.cs[l] = (p.ck[l] + a - 1) / a * a;
     p.c[l] = alloc(l, p.cs[l]);
   }
   for (int l = 1; l <= 4; ++l) p.a[l] = alloc(l, nf);  // a2..a5 live at levels 1..4
@@ -552,7 +556,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
                             s));
     }
     const int ia = da_idx[l], ib = da_idx[l] + 1;
-    DN_TRY(conv_forward(V(p.c[l], p.cs[l]), N, H(l), Wd(l), p.cs[l], Wt(ia), Bs(ia), 2 * nf, 3, 1,
+    DN_TRY(conv_forward(V(p.c[l], p.cs[l]), N, H(l), Wd(l), p.ck[l], Wt(ia), Bs(ia), 2 * nf, 3, 1,
                         V(p.da[l], 2 * nf), OUT_NHWC, s));
     DN_TRY(conv_forward(V(p.da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ib), Bs(ib), 2 * nf, 3, 1,
                         V(p.db[l], 2 * nf), OUT_NHWC, s));

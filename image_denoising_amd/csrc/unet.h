@@ -33,7 +33,7 @@ struct Plan {
   // forward activations (NHWC, offsets in floats)
   int c1s, c1k, c1kp;           // up1 concat: pixel stride, real channels, float4-padded K
   long c1, a0, a1;
-  long c[5]; int cs[5];         // concat buffers at levels 1..4
+  long c[5]; int cs[5], ck[5];  // concat buffers at levels 1..4: pixel stride, channels
   long a[5];                    // a2..a5 at levels 1..4
   long p5, a6;
   long da[5], db[5];            // decoder conv outputs at levels 1..4
