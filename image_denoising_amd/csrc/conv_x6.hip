@@ -14,7 +14,7 @@
 //   Workgroup = 4 waves, tile = 4*MT rows x 16 pixels x 16*NT output channels; wave w owns
 //   rows [w*MT, w*MT+MT).  K is staged 32 input channels (one MFMA K) at a time: the x tile
 //   (with halo) is split as it is staged (fp32 registers -> three bf16 planes in LDS, once
-//   per chunk), the pre-split weights arrive one tap per stage by global_load_lds, double
+//   per chunk), the pre-split weights arrive one tap per stage by LDS DMA, double
 //   buffered, one barrier per stage.  LDS rows are 32 bf16 (64 B) with the 16-B quad index
 //   XOR-swizzled by (row >> 1) & 3, which makes the per-lane ds_read_b128 operand reads
 //   conflict-free for every tap offset.
@@ -33,7 +33,7 @@ namespace dn {
 #endif
 
 // bf16 elements of one weight stage (one tap, three planes of NP x 32) in the packed image,
-// padded to whole rounds of the pipelined kernel's DMA (8 waves x 1 KiB global_load_lds_dwordx4;
+// padded to whole rounds of the pipelined kernel's DMA (8 waves x 1 KiB dwordx4 LDS loads;
 // the 12-byte form would fit 18 KiB exactly, but it writes lane x 16 B in LDS, not lane x 12)
 __host__ __device__ constexpr int x6_wst(int np) {
   return (3 * np * 32 * 2 + 8191) / 8192 * 8192 / 2;
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256, 2) void k_c3x6(FwdArgs a) {
 // ------------------------------------------------------------------------------------
 // Pipelined variant for large grids: 8 waves (2 per SIMD) share one 16 x 16 x 16*NT tile
 // (wave w: rows 2w, 2w+1), one workgroup per CU.  The weight stages stream through an
-// S-deep LDS ring by 1 KiB DMAs (global_load_lds_dwordx4, PPW per wave per stage),
+// S-deep LDS ring by 1 KiB DMAs (buffer_load_dwordx4 ... lds, PPW per wave per stage),
 // so a stage's weights are requested S-2 stages (~2 us) before they are read; the wait before
 // each stage's barrier counts only this wave's own DMAs (s_waitcnt vmcnt(N)), not the next
 // chunk's x tile, which is loaded into registers when a chunk starts and split into the
