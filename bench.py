@@ -157,6 +157,80 @@ def time_dominant_kernel_bf16(bs, H, W, device, reps=5):
     return e0.elapsed_time(e1) / reps, bs * conv_flops(H, W, 96, 96, 3)
 
 
+THREE_BY_THREE = ("fwd3", "fwd3sel", "dgrad3", "wgrad3")
+
+
+def step_profile(step, reps=2):
+    """`reps` extra steps after the timed region with every launch recorded (dn_profile_ops:
+    HIP events on the launch stream, executors and the step single-stream so each event pair
+    brackets one kernel).  Returns (records, reps)."""
+    from image_denoising_amd import _lib
+
+    old = os.environ.get("DN_STEP_STREAMS")
+    os.environ["DN_STEP_STREAMS"] = "0"
+    torch.cuda.synchronize()
+    _lib.profile_ops(True)
+    try:
+        for _ in range(reps):
+            step()
+        torch.cuda.synchronize()
+        recs = _lib.profile_ops_take()
+    finally:
+        _lib.profile_ops(False)
+        if old is None:
+            os.environ.pop("DN_STEP_STREAMS", None)
+        else:
+            os.environ["DN_STEP_STREAMS"] = old
+    return recs, reps
+
+
+def per_shape_roofline(recs, reps, peak):
+    """the step's 3x3 launches grouped by (op, K, NOUT, H, W, kernel): launches per step, mean
+    HIP-event ms, algorithmic FLOPs per launch (SEL: the pair pixels it computes) and the fraction
+    of `peak`; plus the time-weighted fraction over all of them and the per-op step breakdown"""
+    groups = {}
+    for r in recs:
+        if r["op"] not in THREE_BY_THREE:
+            continue
+        k = (r["op"], r["K"], r["NOUT"], r["H"], r["W"], r["N"], r["kernel"])
+        g = groups.setdefault(k, [0, 0.0, 0.0])
+        g[0] += 1
+        g[1] += r["ms"]
+        g[2] += r["flops"]
+    shapes = []
+    for (op, K, NO, H, W, N, kern), (n, ms, fl) in groups.items():
+        tf = fl / (ms * 1e-3) / 1e12
+        # HBM bytes the launch must move: input + output activations (fp32), weights aside
+        alg_bytes = N * H * W * (K + NO) * 4.0
+        shapes.append({"op": op, "kernel": kern, "shape": f"{K}->{NO} @{N}x{H}x{W}",
+                       "launches_per_step": n / reps, "avg_launch_ms": round(ms / n, 4),
+                       "flops_per_launch": fl / n, "tflops": round(tf, 2), "frac": round(tf / peak, 4),
+                       "ms_per_step": round(ms / reps, 4), "algorithmic_bytes_per_launch": alg_bytes})
+    shapes.sort(key=lambda d: -d["ms_per_step"])
+    tot_ms = sum(d["ms_per_step"] for d in shapes)
+    tot_fl = sum(d["flops_per_launch"] * d["launches_per_step"] for d in shapes)
+    weighted = (tot_fl / (tot_ms * 1e-3) / 1e12 / peak) if tot_ms else None
+    by_op = {}
+    for r in recs:
+        by_op[r["op"]] = by_op.get(r["op"], 0.0) + r["ms"] / reps
+    executed = sum(r["flops"] for r in recs) / reps
+    return shapes, weighted, tot_ms, {k: round(v, 4) for k, v in sorted(by_op.items(), key=lambda kv: -kv[1])}, executed
+
+
+def pmc_step_traffic(kernel):
+    """HBM bytes per launch of `kernel` inside the bench step, from the committed rocprofv3 PMC
+    summary (tools/pmc_step.py over separate FETCH_SIZE / WRITE_SIZE passes; gfx950 x2 FETCH
+    correction), or (None, None)"""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_step.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    k = d.get("kernels", {}).get(kernel)
+    return (k["traffic_bytes"] if k else None), os.path.relpath(files[-1], ROOT)
+
+
 def pmc_traffic(tag=""):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
     (tools/pmc.sh + tools/pmc_summary.py; FETCH_SIZE x2 gfx950 correction), or None."""
@@ -304,6 +378,8 @@ def main():
     ap.add_argument("--breakdown", action="store_true", help="per-phase HIP-event timing (stderr)")
     args = ap.parse_args()
 
+    from image_denoising_amd import dist as dp
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -312,12 +388,12 @@ def main():
     backend = os.environ.get("DN_DIST_BACKEND", "nccl")
     if backend != "nccl":
         local = local % torch.cuda.device_count()
-    if world > 1:
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+    torch.cuda.set_device(local)
+    # a process group whenever torchrun started us (world 1 included: a one-rank RCCL group runs
+    # the same broadcast + per-step all-reduce as N ranks) or world > 1
+    os.environ["LOCAL_RANK"] = str(local)
+    dp.init_from_env(backend)
+    grouped = dp.is_initialized()
     device = torch.device("cuda", local)
 
     from image_denoising_amd import N2NTrainer, StructureTrainer, UNet
@@ -347,15 +423,15 @@ def main():
             if iu:
                 raise SystemExit("--precision bf16 is built for the UNet base")
             model.base.set_inference_precision("bf16")
-        tr = FinetuneTrainer(model, lr=1e-4, lambda_grad=0.1)
+        tr = FinetuneTrainer(model, lr=1e-4, lambda_grad=0.1, distributed=grouped)
         g = torch.Generator(device="cpu").manual_seed(7 + rank)
         noisy = (clean + (25.0 / 255.0) * torch.randn(clean.shape, generator=g).to(device)).contiguous()
         step = lambda: tr.train_step(clean, noisy)
     elif args.mode == "n2n":
-        tr = N2NTrainer(net, lr=3e-4, n_epoch=100, increase_ratio=2.0, seed=0)
+        tr = N2NTrainer(net, lr=3e-4, n_epoch=100, increase_ratio=2.0, seed=0, distributed=grouped)
         step = lambda: tr.train_step(clean, epoch=1)
     else:
-        tr = StructureTrainer(net, lr=3e-4, n_epoch=100)
+        tr = StructureTrainer(net, lr=3e-4, n_epoch=100, distributed=grouped)
         g = torch.Generator(device="cpu").manual_seed(7 + rank)
         noisy = (clean + (25.0 / 255.0) * torch.randn(clean.shape, generator=g).to(device)).contiguous()
         step = lambda: tr.train_step(clean, noisy, epoch=1)
@@ -363,22 +439,24 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if grouped:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     loss_v = loss.cpu().tolist()
+    # one profiled pair of steps after the timed region, on EVERY rank (the step all-reduces)
+    recs, reps = step_profile(step) if not iu else ([], 1)
 
     if args.breakdown and rank == 0 and args.mode == "n2n":
         breakdown(tr, clean, device)
@@ -387,23 +465,29 @@ def main():
         ms_step = 1000.0 * elapsed / args.steps
         value = world * bs * args.steps / elapsed
         bf = ft and args.precision == "bf16"
-        timer = (time_dominant_kernel_bf16 if bf else
-                 time_dominant_kernel_x6 if x6 else time_dominant_kernel)
-        kms, kflops = timer(bs, H, H, device)
-        achieved = kflops / (kms * 1e-3) / 1e12
         peak = PEAK_BF16_TFLOPS if bf else (PEAK_X6_TFLOPS if x6 else PEAK_FP32_TFLOPS)
         if args.mode == "n2n":  # fwd 256 + fwd/bwd 128
-            step_flops = bs * (fwd_flops(H, H, C) + 3 * fwd_flops(H // 2, H // 2, C))
+            ref_flops = bs * (fwd_flops(H, H, C) + 3 * fwd_flops(H // 2, H // 2, C))
         elif ft:  # frozen base forward + adapter fwd (864 flop/px) and bwd (~1728 flop/px, C=1)
-            step_flops = bs * (fwd_flops(H, H, C) + 3 * 864.0 * C * H * H)
+            ref_flops = bs * (fwd_flops(H, H, C) + 3 * 864.0 * C * H * H)
         else:  # two fwd/bwd at full resolution
-            step_flops = bs * 2 * 3 * fwd_flops(H, H, C)
-        if (bs, H, C, iu, bf) == (64, 256, 1, False, False):
-            traffic, traffic_src = pmc_traffic("x6" if x6 else "")
-        elif bf and (bs, H, C, iu) == (16, 512, 1, False):
-            traffic, traffic_src = pmc_traffic("bf16")
-        else:
+            ref_flops = bs * 2 * 3 * fwd_flops(H, H, C)
+        shapes, weighted, ms3, by_op, executed = per_shape_roofline(recs, reps, peak)
+        # the FLOPs the step's launches execute (the pair-pixel no-grad pass computes dec_conv1b
+        # and the head at half the pixels): what step_tflops divides; ref_flops is SURVEY 8d's
+        step_flops = executed if executed > 0 and not ft else ref_flops
+        if shapes:  # the dominant in-step 3x3 launch shape (largest time per step)
+            dom = shapes[0]
+            kms, kflops = dom["avg_launch_ms"], dom["flops_per_launch"]
+            kdesc = f"{dom['kernel']} {dom['op']} {dom['shape']} (in-step launch)"
+            traffic, traffic_src = pmc_step_traffic(dom["kernel"])
+        else:  # no instrumented executor (ImprovedUNet): the isolated 96->96 shape
+            timer = (time_dominant_kernel_bf16 if bf else
+                     time_dominant_kernel_x6 if x6 else time_dominant_kernel)
+            kms, kflops = timer(bs, H, H, device)
+            kdesc = "96->96 3x3 @%dx%dx%d, isolated launch" % (bs, H, H)
             traffic, traffic_src = None, None
+        achieved = kflops / (kms * 1e-3) / 1e12
         model = "ImprovedUNet(n_feature=48)" if iu else "UNet(n_feature=48)"
         if iu and not ft:
             workload = (f"{args.mode} step with arch_unet.ImprovedUNet(n_feature=48, depth=4, noise=True) "
@@ -436,18 +520,29 @@ def main():
                       if x6 else "fp32"),
             "data": "synthetic",
             "config": {"workload": workload,
-                       "global_batch": bs * world, "patch": [H, H, C], "parallelism": f"dp{world}"},
+                       "global_batch": bs * world, "patch": [H, H, C], "parallelism": f"dp{world}",
+                       "collective": (f"{dist.get_backend()} all_reduce(sum) of the flat gradient per step"
+                                      if grouped else "none (single process)")},
             "step_tflops": round(step_flops / (ms_step * 1e-3) / 1e12, 2),
             "step_frac_of_fp32_peak": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
+            "step_flops_executed": step_flops, "step_flops_reference": ref_flops,
             "roofline": {"bound": "mfma",
-                         "kernel": ("k_fwd_bf16p<NT=6,MT=4> (96->96 3x3, bf16 MFMA)" if bf else
-                                    "k_c3x6p<NT=6> (dec_conv1b 96->96 3x3 @256^2, fp32 as 6 "
-                                    "split-bf16 products; peak = bf16 dense / 6)" if x6 else
-                                    "k_fwd<G_C3,NT=6,MT=4> (dec_conv1b 96->96 3x3 @256^2)"),
+                         "kernel": kdesc + ("; bf16 MFMA" if bf else "; fp32 as 6 split-bf16 "
+                                            "products, peak = bf16 dense / 6" if x6 else "; fp32 MFMA"),
                          "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic,
                          "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
-                         "avg_launch_ms": round(kms, 4), "flops_per_launch": kflops},
+                         "avg_launch_ms": round(kms, 4), "flops_per_launch": kflops,
+                         "weighted_frac": round(weighted, 4) if weighted else None,
+                         "weighted_over": "every 3x3 launch of the step (fwd, pair-pixel fwd, "
+                                          "data and weight gradients), time-weighted",
+                         "ms_3x3_per_step": round(ms3, 3),
+                         "per_shape": [{k: v for k, v in d.items() if k != "algorithmic_bytes_per_launch"}
+                                       for d in shapes],
+                         "method": "one profiled step pair after the timed region, every launch "
+                                   "bracketed by HIP events on its stream, single-stream "
+                                   "(dn_profile_ops)"},
+            "step_breakdown_ms": by_op,
             "loss": loss_v,
         }
         if args.mode == "n2n" and C == 1 and not iu:
@@ -466,7 +561,7 @@ def main():
             rec["eval"]["psnr_ref_cpu"] = round(ref_ps, 4)
             rec["eval"]["psnr_abs_diff"] = round(abs(ps - ref_ps), 6)
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

@@ -20,7 +20,7 @@ TAG = os.environ.get("DN_BUILD_TAG", "")
 BUILD = os.path.join(PKG, "_objs" + (f"_{TAG}" if TAG else ""))
 LIB = os.path.join(PKG, "libdenoise_hip" + (f"_{TAG}" if TAG else "") + ".so")
 SOURCES = ["conv.hip", "conv_bf16.hip", "conv_x6.hip", "elementwise.hip", "first_layer.hip", "eval.hip", "adapter.hip", "iunet_ops.hip", "unet.cpp",
-           "iunet.cpp", "capi.cpp"]
+           "iunet.cpp", "capi.cpp", "profile.cpp"]
 HEADERS = ["dn_internal.h", "conv_epi.h", "x6_core.h", "philox.h", "unet.h", "iunet.h", "iunet_ops.h"]
 ARCH = os.environ.get("DN_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -16,6 +16,15 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DN_LIB_PATH", os.path.join(_HERE, "libdenoise_hip.so"))
 
 
+ABI_VERSION = 3  # include/denoise_hip.h DN_ABI_VERSION
+
+
+class DnOpRecord(ctypes.Structure):  # include/denoise_hip.h dn_op_record
+    _fields_ = [("op", ctypes.c_char * 24), ("kernel", ctypes.c_char * 48), ("K", c_int),
+                ("NOUT", c_int), ("H", c_int), ("W", c_int), ("N", c_int),
+                ("flops", ctypes.c_double), ("ms", ctypes.c_double)]
+
+
 class DnCfg(ctypes.Structure):
     _fields_ = [("in_nc", c_int), ("out_nc", c_int), ("n_feature", c_int)]
 
@@ -26,6 +35,9 @@ _U8 = c_void_p  # uint8_t* (device)
 # name -> (restype, argtypes)
 SIGNATURES = {
     "dn_version": (c_char_p, []),
+    "dn_abi_version": (c_int, []),
+    "dn_profile_ops": (c_int, [c_int]),
+    "dn_profile_ops_read": (c_int, [c_void_p, c_int, POINTER(c_int)]),
     "dn_last_error": (c_int, [c_char_p, c_size_t]),
     "dn_unet_param_count": (c_int, [POINTER(DnCfg), POINTER(c_size_t)]),
     "dn_unet_param_info": (c_int, [POINTER(DnCfg), c_int, POINTER(c_size_t), POINTER(c_size_t),
@@ -139,6 +151,10 @@ def lib() -> ctypes.CDLL:
                 f"libdenoise_hip.so not found at {LIB_PATH}; build it with "
                 "`python -m image_denoising_amd._build` (hipcc --offload-arch=gfx950)")
         L = ctypes.CDLL(LIB_PATH)
+        L.dn_abi_version.restype = c_int
+        if L.dn_abi_version() != ABI_VERSION:  # the argument lists below are revision 3's
+            raise RuntimeError(f"{LIB_PATH}: ABI revision {L.dn_abi_version()}, the binding "
+                               f"expects {ABI_VERSION} (include/denoise_hip.h DN_ABI_VERSION)")
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res
@@ -188,3 +204,19 @@ def scratch(nbytes: int, device) -> torch.Tensor:
 
 def cfg(in_nc: int, out_nc: int, n_feature: int) -> DnCfg:
     return DnCfg(in_nc, out_nc, n_feature)
+
+
+def profile_ops(enable: bool) -> None:
+    """dn_profile_ops: record every launch of the executors (single-stream) until disabled"""
+    check(lib().dn_profile_ops(int(bool(enable))), "dn_profile_ops")
+
+
+def profile_ops_take(cap: int = 8192) -> list[dict]:
+    """waits for and returns the launch records since profile_ops(True), dropping them"""
+    buf = (DnOpRecord * cap)()
+    n = c_int(0)
+    check(lib().dn_profile_ops_read(buf, cap, ctypes.byref(n)), "dn_profile_ops_read")
+    if n.value > cap:
+        raise RuntimeError(f"{n.value} launch records, only {cap} read")
+    return [dict(op=r.op.decode(), kernel=r.kernel.decode(), K=r.K, NOUT=r.NOUT, H=r.H, W=r.W,
+                 N=r.N, flops=r.flops, ms=r.ms) for r in buf[:n.value]]

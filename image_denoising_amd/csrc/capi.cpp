@@ -35,7 +35,9 @@ extern "C" {
 #define DN_SRC_HASH "unknown"
 #endif
 // src= the sha256 prefix of the sources this library was compiled from (_build.source_hash)
-const char* dn_version(void) { return "denoise_hip 0.2.0 gfx950 src=" DN_SRC_HASH; }
+const char* dn_version(void) { return "denoise_hip 0.3.0 gfx950 src=" DN_SRC_HASH; }
+
+int dn_abi_version(void) { return DN_ABI_VERSION; }
 
 int dn_last_error(char* buf, size_t len) {
   const std::string& s = g_last_error;
@@ -101,8 +103,10 @@ dn_status dn_unet_forward_prec(const dn_unet_cfg* cfg, const float* params, cons
   if (!cfg || !params || !x || !y || !ws) return fail(DN_ERR_ARG, "null argument");
   Plan p;
   std::string err;
-  // A workspace sized for the backward has the same forward offsets; only then does the
-  // forward save the activations the backward reads (the fused head writes d1b/na/nb).
+  // The workspace's size decides the plan: one sized with_backward=1 gets the backward plan
+  // (dense concat strides, the layout dn_unet_backward reads) and the forward saves the
+  // activations the backward needs (the fused head writes d1b/na/nb); a smaller one gets the
+  // forward-only plan, whose concat strides are padded to 128-B lines (a different layout).
   if (!build_plan(*cfg, N, H, W, true, p, err)) return fail(DN_ERR_ARG, err);
   if (ws_bytes < (size_t)p.total_floats * sizeof(float) &&
       !build_plan(*cfg, N, H, W, false, p, err))
@@ -217,6 +221,7 @@ dn_status dn_n2n_subsample(const float* img, int N, int C, int H, int W, const u
     return fail(DN_ERR_ARG, "H and W must be even");
   if ((long)N * H * W == 0) return DN_OK;
   if (!img || !sub1 || !sub2) return fail(DN_ERR_ARG, "null argument");
+  const OpTimer timer((hipStream_t)stream, "subsample", 0, C, C, H, W, N);
   return hip_status(launch_subsample(img, N, C, H, W, rd_idx_in, seed, offset, cell_base, sub1,
                                      sub2, rd_idx_out, (hipStream_t)stream),
                     "dn_n2n_subsample");
@@ -246,6 +251,7 @@ dn_status dn_add_gauss_noise(const float* clean, int N, int64_t per_image, float
   if (N < 0 || per_image < 0) return fail(DN_ERR_ARG, "negative size");
   if ((long)N * per_image == 0) return DN_OK;
   if (!clean || !noisy) return fail(DN_ERR_ARG, "null argument");
+  const OpTimer timer((hipStream_t)stream, "noise", 0);
   return hip_status(launch_noise(clean, N, per_image, std_, std_per_image, seed, offset, elem_base,
                                  noisy, (hipStream_t)stream),
                     "dn_add_gauss_noise");
@@ -258,6 +264,7 @@ dn_status dn_add_poisson_noise(const float* clean, int N, int64_t per_image, flo
   if (!lam_per_image && !(lam > 0.f && lam <= 500.f)) return fail(DN_ERR_ARG, "lam must be in (0, 500]");
   if ((long)N * per_image == 0) return DN_OK;
   if (!clean || !noisy) return fail(DN_ERR_ARG, "null argument");
+  const OpTimer timer((hipStream_t)stream, "noise", 0);
   return hip_status(launch_poisson(clean, N, per_image, lam, lam_per_image, seed, offset, elem_base,
                                    noisy, (hipStream_t)stream),
                     "dn_add_poisson_noise");
@@ -271,6 +278,7 @@ dn_status dn_n2n_loss(const float* out, const float* sub2, const float* den, con
   if (!out || !sub2 || !den || !rd_idx || !dout || !loss3 || !partial_ws)
     return fail(DN_ERR_ARG, "null argument");
   if (N < 1 || C < 1 || h < 1 || w < 1) return fail(DN_ERR_ARG, "empty loss input");
+  const OpTimer timer((hipStream_t)stream, "loss", 0);
   return hip_status(launch_n2n_loss(out, sub2, den, rd_idx, N, C, h, w, lambda, dout, loss3,
                                     partial_ws, (hipStream_t)stream),
                     "dn_n2n_loss");
@@ -282,6 +290,7 @@ dn_status dn_structure_loss(const float* pred, const float* pred2, const float* 
   if (!pred || !pred2 || !target || !dpred || !dpred2 || !loss5 || !partial_ws)
     return fail(DN_ERR_ARG, "null argument");
   if (N < 1 || C < 1 || H < 2 || W < 2) return fail(DN_ERR_ARG, "Structure_loss needs H, W >= 2");
+  const OpTimer timer((hipStream_t)stream, "loss", 0);
   return hip_status(launch_structure_loss(pred, pred2, target, N, C, H, W, alpha, beta, gamma,
                                           dpred, dpred2, loss5, partial_ws, (hipStream_t)stream),
                     "dn_structure_loss");
@@ -298,6 +307,7 @@ dn_status dn_adam_step(float* param, const float* grad, float* exp_avg, float* e
   const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
   const double step_size = (double)lr / bc1;
   const double bc2s = std::sqrt(bc2);
+  const OpTimer timer((hipStream_t)stream, "adam", 0);
   return hip_status(launch_adam(param, grad, exp_avg, exp_avg_sq, n, (float)(1.0 - (double)beta1),
                                 beta2, (float)(1.0 - (double)beta2), (float)step_size,
                                 (float)bc2s, eps, grad_scale, (hipStream_t)stream),
@@ -308,6 +318,7 @@ dn_status dn_accumulate(float* dst, const float* src, int64_t n, void* stream) {
   if (n < 0) return fail(DN_ERR_ARG, "n < 0");
   if (n == 0) return DN_OK;
   if (!dst || !src) return fail(DN_ERR_ARG, "null argument");
+  const OpTimer timer((hipStream_t)stream, "accumulate", 0);
   return hip_status(launch_accumulate(dst, src, n, (hipStream_t)stream), "dn_accumulate");
 }
 

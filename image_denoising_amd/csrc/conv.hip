@@ -1003,6 +1003,7 @@ static hipError_t run_fwd(const FwdArgs& a, hipStream_t s) {
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
   const int nz = a.zc ? (a.NOUT + a.zc - 1) / a.zc : ((a.out_layout == OUT_UP2 && GATHER != G_UP) ? 4 : 1);
   dim3 grid(tx * ty, a.N, nz);
+  prof_kernel("k_fwd");
   hipLaunchKernelGGL((k_fwd<GATHER, NT, MT>), grid, dim3(256), 0, s, a, HeadArgs{});
   return hipGetLastError();
 }
@@ -1221,6 +1222,7 @@ static hipError_t run_wgrad3(const WgradArgs& a, int splits, hipStream_t s) {
   const int nz = a.zc > 0 ? (a.cout_total + a.zc - 1) / a.zc : 1;
   dim3 grid(splits, (a.Cin + C::CIB - 1) / C::CIB, nz);
   // K stage width: 32-pixel row segments, or 16 / 8 / 4 pixels x 2 / 4 / 8 rows for narrow images
+  prof_kernel("k_wgrad3");
   if (a.KW >= 32) hipLaunchKernelGGL((k_wgrad3<CO_FR, WM, WN, 5>), grid, dim3(C::NTHR), 0, s, a);
   else if (a.KW >= 16) hipLaunchKernelGGL((k_wgrad3<CO_FR, WM, WN, 4>), grid, dim3(C::NTHR), 0, s, a);
   else if (a.KW >= 8) hipLaunchKernelGGL((k_wgrad3<CO_FR, WM, WN, 3>), grid, dim3(C::NTHR), 0, s, a);

@@ -447,10 +447,13 @@ hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize) {
                     (long)BCfg<6, 4, true>::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL;
   if (pipe) {
     const int tx = (a.OW + 15) / 16, ty = (a.OH + 15) / 16;
-    if (nt == 3)
+    if (nt == 3) {
+      prof_kernel("k_fwd_bf16p<3,4>");
       hipLaunchKernelGGL((k_fwd_bf16p<3, 4>), dim3(tx * ty, a.N, 1), dim3(256), 0, s, a);
-    else
+    } else {
+      prof_kernel("k_fwd_bf16p<6,4>");
       hipLaunchKernelGGL((k_fwd_bf16p<6, 4>), dim3(tx * ty, a.N, 1), dim3(256), 0, s, a);
+    }
     return hipGetLastError();
   }
   if (nt == 3) return small ? run_bf16<3, 1, true>(a, s) : run_bf16<3, 4, true>(a, s);

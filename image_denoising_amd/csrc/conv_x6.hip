@@ -21,12 +21,26 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <type_traits>
 
 #include "conv_epi.h"
 #include "x6_core.h"
 
 namespace dn {
+
+// profiling label of a template instantiation ("k_c3x6p<6,0>"; -1 = parameter absent)
+static std::string x6_kname(const char* k, int p0, int p1, int p2) {
+  std::string n = std::string(k) + "<" + std::to_string(p0);
+  for (int v : {p1, p2})
+    if (v >= 0) n += "," + std::to_string(v);
+  return n + ">";
+}
+// the same with one more template argument spelled out: x6_kmore(x6_kname(...), "false")
+static std::string x6_kmore(std::string n, const char* last) {
+  n.back() = ',';
+  return n.append(last).append(">");
+}
 
 #ifndef DN_X6_GDMA
 #define DN_X6_GDMA 0  // A/B switch: 1 = the 3x3 kernels' weight DMA as global_load_lds
@@ -833,6 +847,9 @@ static hipError_t run_x6h(const FwdArgs& a, int nz, hipStream_t s) {
   using C = HCfg<NT, MT>;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
   const dim3 grid(tx * ty, a.N, nz), block(C::WAVES * 64);
+  static const std::string kn[3] = {x6_kname("k_c3x6h", NT, 0, MT), x6_kname("k_c3x6h", NT, 1, MT),
+                                    x6_kname("k_c3x6h", NT, 2, MT)};
+  prof_kernel(kn[a.x6_tail > 2 ? 0 : a.x6_tail].c_str());
   if (a.x6_tail == 1)
     hipLaunchKernelGGL((k_c3x6h<NT, 1, MT>), grid, block, 0, s, a);
   else if (a.x6_tail == 2)
@@ -1040,6 +1057,8 @@ template <int NT, int MT>
 static hipError_t run_x6(const FwdArgs& a, int nz, hipStream_t s) {
   using C = XCfg<NT, MT>;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
+  static const std::string kn = x6_kname("k_c3x6", NT, MT, -1);
+  prof_kernel(kn.c_str());
   hipLaunchKernelGGL((k_c3x6<NT, MT>), dim3(tx * ty, a.N, nz), dim3(256), 0, s, a);
   return hipGetLastError();
 }
@@ -1107,6 +1126,11 @@ static hipError_t run_x6p(const FwdArgs& a, int nz, hipStream_t s) {
   using C = PCfg<NT>;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
   const dim3 grid(tx * ty, a.N, nz), block(C::WAVES * 64);
+  // (labels as rocprofv3 prints the instantiations: SEL = false spelled out)
+  static const std::string kn[3] = {x6_kmore(x6_kname("k_c3x6p", NT, 0, -1), "false"),
+                                    x6_kmore(x6_kname("k_c3x6p", NT, 1, -1), "false"),
+                                    x6_kmore(x6_kname("k_c3x6p", NT, 2, -1), "false")};
+  prof_kernel(kn[a.x6_tail > 2 ? 0 : a.x6_tail].c_str());
   if (a.x6_tail == 1)
     hipLaunchKernelGGL((k_c3x6p<NT, 1>), grid, block, 0, s, a);
   else if (a.x6_tail == 2)
@@ -1123,6 +1147,7 @@ hipError_t launch_fwd_x6_sel(const FwdArgs& a, hipStream_t s) {
       ((a.in_stride | a.in_off) & 3) || (long)C::IH * a.IWt * a.in_stride * 4 >= 0x7fffffffL)
     return hipErrorInvalidValue;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
+  prof_kernel("k_c3x6p<6,0,true>");
   hipLaunchKernelGGL((k_c3x6p<6, 0, true>), dim3(tx * ty, a.N, 1), dim3(C::WAVES * 64), 0, s, a);
   return hipGetLastError();
 }
@@ -1422,6 +1447,10 @@ template <int CO_FR, int WM, int WN>
 static hipError_t run_wgrad3s(const WgradArgs& a, int splits, hipStream_t s) {
   using C = Ws3Cfg<CO_FR, WM, WN>;
   const dim3 grid(splits, (a.Cin + C::CIB - 1) / C::CIB, 1), block(C::NTHR);
+  static const std::string kn[3] = {x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "3"),
+                                    x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "4"),
+                                    x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "5")};
+  prof_kernel(kn[a.KW >= 32 ? 2 : (a.KW >= 16 ? 1 : 0)].c_str());
   if (a.KW >= 32) hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 5>), grid, block, 0, s, a);
   else if (a.KW >= 16) hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 4>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 3>), grid, block, 0, s, a);

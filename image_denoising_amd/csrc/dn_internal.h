@@ -6,6 +6,47 @@
 
 namespace dn {
 
+// Makes the device of stream s current for the lifetime of the guard (and restores the caller's
+// on exit): the executors launch onto side streams and create per-device objects, which must
+// happen on the device of the caller's stream, not whichever device the thread had selected.
+struct StreamDeviceGuard {
+  int prev = -1;
+  explicit StreamDeviceGuard(hipStream_t s) {
+    hipDevice_t dev = 0;
+    int cur = 0;
+    if (hipStreamGetDevice(s, &dev) == hipSuccess && hipGetDevice(&cur) == hipSuccess &&
+        cur != dev && hipSetDevice(dev) == hipSuccess)
+      prev = cur;
+  }
+  ~StreamDeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  StreamDeviceGuard(const StreamDeviceGuard&) = delete;
+  StreamDeviceGuard& operator=(const StreamDeviceGuard&) = delete;
+};
+
+// In-step launch profiler (profile.cpp, dn_profile_ops): prof_on() while enabled; an OpTimer
+// brackets one launch on its stream with HIP events and records op / shape / algorithmic FLOPs;
+// launchers name the kernel they picked with prof_kernel() (a string literal).
+bool prof_on();
+void prof_kernel(const char* k);
+struct OpTimer {
+  int idx = -1;
+  hipStream_t s = nullptr;
+  OpTimer(hipStream_t st, const char* op, double flops, int K = 0, int NOUT = 0, int H = 0,
+          int W = 0, int N = 0);
+  ~OpTimer();
+  OpTimer(const OpTimer&) = delete;
+  OpTimer& operator=(const OpTimer&) = delete;
+};
+
+// DN_TRY(call) bracketed by an OpTimer (statement form)
+#define DN_TIMED(st, op, flops, K, NO, h, w, n, call)          \
+  do {                                                        \
+    const ::dn::OpTimer dn_timer_(st, op, flops, K, NO, h, w, n); \
+    DN_TRY(call);                                             \
+  } while (0)
+
 // How an output pixel of the implicit-GEMM kernel gathers its input pixels.
 enum Gather {
   G_C3 = 0,   // 3x3, stride 1, pad 1: in(y+ky-1, x+kx-1), 9 taps     (conv fwd / conv dgrad)

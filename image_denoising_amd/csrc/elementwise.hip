@@ -203,7 +203,8 @@ __global__ __launch_bounds__(256) void k_noise(const float* __restrict__ clean, 
 // The count is drawn by inversion of the Poisson CDF in fp64 with one 53-bit uniform per element
 // (philox_uniform53): k = min{k : u <= F(k)}, F accumulated from p_0 = exp(-mu),
 // p_k = p_{k-1} mu / k.  mu = lam x is formed in fp32 as torch.poisson receives it; mu <= 500
-// (the host checks lam; the images are in [0, 1]), the loop is bounded at mu + 20 sqrt(mu) + 40.
+// (the host checks a scalar lam; a per-image lam outside (0, 500] makes that image's output NaN;
+// the images are in [0, 1]), the loop is bounded at mu + 20 sqrt(mu) + 40.
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_poisson(const float* __restrict__ clean, int N,
                                                  int64_t per_image, float lam,
@@ -213,6 +214,10 @@ __global__ __launch_bounds__(256) void k_poisson(const float* __restrict__ clean
   const long total = (long)N * per_image;
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
     const float l = lam_img ? lam_img[e / per_image] : lam;
+    if (!(l > 0.f && l <= 500.f)) {  // a per-image lam the host could not check: NaN, loudly
+      noisy[e] = __builtin_nanf("");
+      continue;
+    }
     const float muf = l * clean[e];
     const double mu = muf > 0.f ? (double)muf : 0.0;
     const double u = philox_uniform53(seed, offset, elem_base + (uint64_t)e);

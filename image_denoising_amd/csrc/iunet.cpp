@@ -506,6 +506,7 @@ WView thin_view(const float* w, int cin) {  // weight [o][cin][3][3] as W(o, k, 
 
 dn_status iunet_forward(const IPlan& p, const float* prm, const float* x, float* y, float* ws,
                         hipStream_t s, int prec) {
+  const StreamDeviceGuard device_guard(s);
   if (prec != DN_PREC_FP32 && prec != DN_PREC_FP32_X6) return DN_ERR_ARG;
   const Ctx c{p, prm, ws, s, prec};
   const IParams& P = p.P;
@@ -671,6 +672,7 @@ dn_status rdb_bwd(const Ctx& c, float* dprm, const IRdb& R, const IBlockBufs& b,
 
 dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, float* dprm, float* ws,
                          hipStream_t s, int prec) {
+  const StreamDeviceGuard device_guard(s);
   if (prec != DN_PREC_FP32 && prec != DN_PREC_FP32_X6) return DN_ERR_ARG;
   const Ctx c{p, prm, ws, s, prec};
   const IParams& P = p.P;

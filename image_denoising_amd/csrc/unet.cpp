@@ -371,6 +371,8 @@ hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, 
   a.N = N; a.KH = KH; a.KW = KW; a.Cout = cout; a.Cin = cin;
   const int taps = mode == W_C3 ? 9 : (mode == W_UP2 ? 4 : 1);
   const long n = (long)cout * cin * taps + cout;
+  const OpTimer timer(s, mode == W_C3 ? "wgrad3" : (mode == W_UP2 ? "wgrad_up" : "wgrad1"),
+                      2.0 * N * KH * KW * cout * cin * taps, cin, cout, KH, KW, N);
   // slab scratch layout: [64 floats | splits x (W + b)]
   a.zeros = zeros ? zeros : slab;
   a.slab = slab + 64; a.slab_stride = n;
@@ -392,6 +394,7 @@ hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, 
 // ------------------------------------------------------------------------------------
 dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
                        hipStream_t s, int prec, const uint8_t* sel_rd) {
+  const StreamDeviceGuard device_guard(s);
   const bool bf16 = prec == DN_PREC_BF16, x6 = prec == DN_PREC_FP32_X6;
   // bf16x6 96-channel deconvs (k_deconv_x6); DN_X6_DECONV=0 keeps the fp32 kernel (A/B)
   static const bool x6_deconv = !getenv("DN_X6_DECONV") || atoi(getenv("DN_X6_DECONV")) != 0;
@@ -414,6 +417,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   auto conv_forward = [&](const View& in, int Nn, int h, int w, int K, const float* wp,
                           const float* b, int cout, int ksize, int act, const View& out,
                           int layout, hipStream_t st) -> hipError_t {
+    const OpTimer timer(st, ksize == 3 ? "fwd3" : "fwd1",
+                        2.0 * Nn * h * w * K * cout * ksize * ksize, K, cout, h, w, Nn);
     int i = ENC1;
     while (i < NL && Wt(i) != wp) ++i;
     if (x6 && i < NL && p.packX[i] >= 0) {
@@ -457,6 +462,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // ConvTranspose2d(2,2): fp32 kernel, or the bf16 1x1 kernel per output parity
   auto deconv_forward = [&](const View& xin, int Nn, int h, int w, int cin, const float* wp,
                             const float* b, int cout, const View& out, hipStream_t st) -> hipError_t {
+    const OpTimer timer(st, "deconv", 2.0 * Nn * h * w * cin * cout * 4, cin, cout, h, w, Nn);
     int i = ENC1;
     while (i < NL && Wt(i) != wp) ++i;
     if (i < NL && deconv_x6_layer(i)) {  // bf16x6 parity GEMMs on the layer's pre-split images
@@ -520,14 +526,18 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     DN_TRY(launch_pack_head(conv_fwd_view(prm + p.P.L[NINA].woff, 96, 1),
                             conv_fwd_view(prm + p.P.L[NINB].woff, 96, 1), ws + p.packH, s, &pb));
   }
-  DN_TRY(pack_flush(pb, s));
+  {
+    const OpTimer timer(s, "pack", 0);
+    DN_TRY(pack_flush(pb, s));
+  }
   // enc_conv0, fused with pool0 = x -> channels [2nf, 2nf+C) of the up1 concat buffer
-  DN_TRY(launch_enc0_fwd(x, N, C, p.H, p.W, prm + p.P.L[ENC0].woff, Bs(ENC0), ws + p.a0,
-                         ws + p.c1, p.c1s, 2 * nf, p.c1kp, p.with_bwd ? ws + p.xin : nullptr, s));
+  DN_TIMED(s, "enc0", 2.0 * N * p.H * p.W * C * nf * 9, C, nf, p.H, p.W, N,
+           launch_enc0_fwd(x, N, C, p.H, p.W, prm + p.P.L[ENC0].woff, Bs(ENC0), ws + p.a0,
+                           ws + p.c1, p.c1s, 2 * nf, p.c1kp, p.with_bwd ? ws + p.xin : nullptr, s));
   DN_TRY(conv_forward(V(p.a0, nf), N, H(0), Wd(0), nf, Wt(ENC1), Bs(ENC1), nf, 3, 1, V(p.a1, nf),
                       OUT_NHWC, s));
   // pool1 -> skip slice of c2
-  DN_TRY(launch_pool_fwd(ws + p.a1, N, H(0), Wd(0), nf, ws + p.c[1], p.cs[1], 2 * nf, s));
+  DN_TIMED(s, "pool", 0, 0, 0, 0, 0, 0, launch_pool_fwd(ws + p.a1, N, H(0), Wd(0), nf, ws + p.c[1], p.cs[1], 2 * nf, s));
   // enc_conv2..5 + pool2..5 (pool_k -> skip slice of c_{k+1}; pool5 -> p5)
   for (int l = 1; l <= 4; ++l) {
     const int li = ENC2 + (l - 1);
@@ -536,10 +546,10 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
                         s));
     if (l < 4) {
       const int tgt_off = (l + 1 == 4) ? nf : 2 * nf;
-      DN_TRY(launch_pool_fwd(ws + p.a[l], N, H(l), Wd(l), nf, ws + p.c[l + 1], p.cs[l + 1],
+      DN_TIMED(s, "pool", 0, 0, 0, 0, 0, 0, launch_pool_fwd(ws + p.a[l], N, H(l), Wd(l), nf, ws + p.c[l + 1], p.cs[l + 1],
                              tgt_off, s));
     } else {
-      DN_TRY(launch_pool_fwd(ws + p.a[4], N, H(4), Wd(4), nf, ws + p.p5, nf, 0, s));
+      DN_TIMED(s, "pool", 0, 0, 0, 0, 0, 0, launch_pool_fwd(ws + p.a[4], N, H(4), Wd(4), nf, ws + p.p5, nf, 0, s));
     }
   }
   DN_TRY(conv_forward(V(p.p5, nf), N, H(5), Wd(5), nf, Wt(ENC6), Bs(ENC6), nf, 3, 1, V(p.a6, nf),
@@ -578,7 +588,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
       h.ba = Bs(NINA); h.bb = Bs(NINB);
       h.wc = prm + p.P.L[NINC].woff; h.bc = Bs(NINC); h.oc = p.OC;
       h.y = y;
-      DN_TRY(launch_nin_head_x6(a, h, ws + p.packH, s, /*bf16=*/true));
+      DN_TIMED(s, "head", 2.0 * N * H(0) * Wd(0) * 96 * (2 * 96 + p.OC), 96, p.OC, H(0), Wd(0), N,
+               launch_nin_head_x6(a, h, ws + p.packH, s, /*bf16=*/true));
       return DN_OK;
     }
     DN_TRY(conv_forward(V(p.d1b, 96), N, H(0), Wd(0), 96, Wt(NINA), Bs(NINA), 96, 1, 1,
@@ -598,7 +609,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     a.wp = ws + p.packX[D1B]; a.bias = Bs(D1B); a.epi = EPI_BIAS_ACT;
     a.out = ws + p.d1b; a.out_stride = 96; a.out_off = 0; a.out_layout = OUT_NHWC;
     a.sel_rd = sel_rd;
-    DN_TRY(launch_fwd_x6_sel(a, s));
+    DN_TIMED(s, "fwd3sel", 2.0 * N * (H(0) / 2) * Wd(0) * 96 * 96 * 9, 96, 96, H(0) / 2, Wd(0), N,
+             launch_fwd_x6_sel(a, s));
     FwdArgs ah{};
     ah.in = ws + p.d1b; ah.in_stride = 96; ah.in_off = 0; ah.IHt = H(0) / 2; ah.IWt = Wd(0);
     ah.N = N; ah.OH = H(0) / 2; ah.OW = Wd(0); ah.K = 96; ah.NOUT = 96;
@@ -607,7 +619,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     h.wc = prm + p.P.L[NINC].woff; h.bc = Bs(NINC); h.oc = p.OC;
     h.y = y;
     h.rd = sel_rd;
-    DN_TRY(launch_nin_head_x6(ah, h, ws + p.packH, s));
+    DN_TIMED(s, "head", 2.0 * N * (H(0) / 2) * Wd(0) * 96 * (2 * 96 + p.OC), 96, p.OC, H(0) / 2,
+             Wd(0), N, launch_nin_head_x6(ah, h, ws + p.packH, s));
     return DN_OK;
   }
   if (x6) {  // dec_conv1b on the bf16x6 kernel, then the fused nin_a -> nin_b -> nin_c head
@@ -622,7 +635,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     h.wc = prm + p.P.L[NINC].woff; h.bc = Bs(NINC); h.oc = p.OC;
     h.y = y;
     if (p.with_bwd) { h.na = ws + p.na; h.nb = ws + p.nb; }
-    DN_TRY(head_x6 ? launch_nin_head_x6(a, h, ws + p.packH, s) : launch_nin_head(a, h, s));
+    DN_TIMED(s, "head", 2.0 * N * H(0) * Wd(0) * 96 * (2 * 96 + p.OC), 96, p.OC, H(0), Wd(0), N,
+             head_x6 ? launch_nin_head_x6(a, h, ws + p.packH, s) : launch_nin_head(a, h, s));
     return DN_OK;
   }
   // dec_conv1b + nin_a + nin_b + nin_c in one kernel (arch_unet.py:251-257); the
@@ -639,7 +653,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     h.wc = prm + p.P.L[NINC].woff; h.bc = Bs(NINC); h.oc = p.OC;
     h.y = y;
     if (p.with_bwd) { h.d1b = ws + p.d1b; h.na = ws + p.na; h.nb = ws + p.nb; }
-    DN_TRY(launch_head(a, h, s));
+    DN_TIMED(s, "fwd3+head", 2.0 * N * H(0) * Wd(0) * 96 * (9 * 96 + 2 * 96 + p.OC), 96, 96, H(0),
+             Wd(0), N, launch_head(a, h, s));
   }
   return DN_OK;
 }
@@ -660,26 +675,32 @@ struct SideStream {
   hipEvent_t fork = nullptr, join = nullptr;
 };
 
-static SideStream* side_stream() {
-  static std::mutex mu;
-  static std::map<int, SideStream> per_device;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lock(mu);
+// One side stream (and its fork / join events) per host thread and device: keyed on the
+// device of the caller's stream (not hipGetDevice(), which a caller need not have set to it) and
+// created under a guard for that device; thread-local, so two host threads running backwards on
+// one device never share the events between a record and its wait.
+static SideStream* side_stream(hipStream_t s) {
+  thread_local std::map<int, SideStream> per_device;
+  hipDevice_t dev = 0;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess) return nullptr;
   SideStream& ss = per_device[dev];
   if (!ss.st) {
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
     if (hipStreamCreateWithFlags(&ss.st, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess)
       ss = SideStream{};
-      return nullptr;
-    }
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (!ss.st) return nullptr;
   }
   return &ss;
 }
 
 dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* dx,
                         float* ws, hipStream_t s, int prec) {
+  const StreamDeviceGuard device_guard(s);
   const bool x6 = prec == DN_PREC_FP32_X6;
   // bf16x6 3x3 weight gradients (k_wgrad3s, split at the operand read); DN_X6_WGRAD=0 keeps the
   // fp32 k_wgrad3 (A/B: 26.7 vs 27.9 ms per step)
@@ -701,6 +722,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   auto x6_dgrad_deconv = [&](int i) { return x6 && x6_deconv && p.packUXB[i] >= 0; };
   auto deconv_dgrad = [&](const View& dy, int Nn, int h, int w, int cout, int i, int cin,
                           const View& mask, int epi, const View& dx, hipStream_t st) -> hipError_t {
+    const OpTimer timer(st, "deconv_dgrad", 2.0 * Nn * h * w * cin * cout * 4, cout, cin, h, w, Nn);
     if (!x6_dgrad_deconv(i))
       return dn::deconv_dgrad(dy, Nn, h, w, cout, Wt(i), cin, mask, epi, dx, st);
     FwdArgs a{};
@@ -736,12 +758,13 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     DN_TRY(launch_pack_head(conv_dgrad_view(prm + p.P.L[NINB].woff, 96, 1),
                             conv_dgrad_view(prm + p.P.L[NINA].woff, 96, 1), ws + p.packHB, s, &pb));
     DN_TRY(add(true, pack_job_zero(ws + p.zeros, 64)));
-    DN_TRY(pack_flush(pb, s));
+    DN_TIMED(s, "pack", 0, 0, 0, 0, 0, 0, pack_flush(pb, s));
   }
   RedBatch rb;  // every weight gradient's reduction, launched together at the end
   const float* Z = ws + p.zeros;
   static const bool two_env = !getenv("DN_BWD_STREAMS") || atoi(getenv("DN_BWD_STREAMS")) != 0;
-  SideStream* side = two_env ? side_stream() : nullptr;
+  // (profiling: one stream, so each launch's event pair brackets that kernel alone)
+  SideStream* side = two_env && !prof_on() ? side_stream(s) : nullptr;
   hipStream_t s2 = side ? side->st : s;
   auto fork = [&]() -> hipError_t {  // the side stream continues after main's work so far
     if (!side) return hipSuccess;
@@ -753,6 +776,8 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   auto conv_dgrad = [&](const View& dz, int Nn, int h, int w, int cout, const float* wp, int nout,
                         int ksize, int epi, const View& mask, const View& dx,
                         hipStream_t st) -> hipError_t {
+    const OpTimer timer(st, ksize == 3 ? "dgrad3" : "dgrad1",
+                        2.0 * Nn * h * w * cout * nout * ksize * ksize, cout, nout, h, w, Nn);
     int i = ENC1;
     while (i < NL && Wt(i) != wp) ++i;
     if (!x6 || i == NL || p.packXB[i] < 0 || ksize != 3)
@@ -789,11 +814,13 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     h.nb = ws + p.nb; h.na = ws + p.na; h.d1b = ws + p.d1b;
     h.g_nb = ws + p.g_nb; h.g_na = ws + p.g_na; h.g_d1b = ws + p.g_d1b;
     h.npx = (long)N * H(0) * Wd(0);
-    DN_TRY(launch_head_bwd(h, s));
+    DN_TIMED(s, "head_bwd", 2.0 * h.npx * 96 * (2 * 96 + OC), OC, 96, H(0), Wd(0), N,
+             launch_head_bwd(h, s));
   }
   DN_TRY(fork());
   if (OC <= 4)
-    DN_TRY(launch_wgrad_thin(dyv.p, dyv.stride, OC, ws + p.nb, (long)N * H(0) * Wd(0),
+    DN_TIMED(s2, "wgrad1", 2.0 * N * H(0) * Wd(0) * 96 * OC, 96, OC, H(0), Wd(0), N,
+             launch_wgrad_thin(dyv.p, dyv.stride, OC, ws + p.nb, (long)N * H(0) * Wd(0),
                              SL(NINC) + 64, p.splits[NINC], G(NINC), s2, &rb));
   else
     DN_TRY(wgrad(W_C1, dyv, V(p.nb, 96), N, H(0), Wd(0), OC, 96, G(NINC), SL(NINC),
@@ -823,7 +850,8 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     a.wlayout = 0; a.cin_total = p.c1k; a.ci_base = 0; a.bias = 1;
     const int sp = x6w ? wgrad_splits_x6(a, p.splits[D1A]) : p.splits[D1A];
     DN_TRY(fork());
-    DN_TRY(launch_wgrad(W_C3, a, sp, s2, x6w));
+    DN_TIMED(s2, "wgrad3", 2.0 * N * H(0) * Wd(0) * 96 * 2 * nf * 9, 2 * nf, 96, H(0), Wd(0), N,
+             launch_wgrad(W_C3, a, sp, s2, x6w));
     RedJob j = red_job(slab, n, sp, 96L * 2 * nf * 9, G(D1A));  // W[co][ci < 2nf][t]
     j.ig = j.og = 2 * nf * 9;
     j.is1 = j.os1 = p.c1k * 9;
@@ -834,8 +862,9 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     float* thin = slab + (long)p.splits[D1A] * n;
     const long nt = 96L * C * 9;
     const int st = enc0_wgrad_splits(N, H(0), Wd(0));
-    DN_TRY(launch_wgrad_c3_thin(ws + p.g_d1a, 96, ws + p.xin, N, C, H(0), Wd(0), thin, nt, C, 0,
-                                0, st, s2));
+    DN_TIMED(s2, "wgrad3_thin", 2.0 * N * H(0) * Wd(0) * 96 * C * 9, C, 96, H(0), Wd(0), N,
+             launch_wgrad_c3_thin(ws + p.g_d1a, 96, ws + p.xin, N, C, H(0), Wd(0), thin, nt, C, 0,
+                                  0, st, s2));
     DN_TRY(launch_reduce_scatter(thin, nt, st, nt, G(D1A), 9L * C, 9L * p.c1k, 9L * 2 * nf, s,
                                  &rb));
   }
@@ -862,9 +891,11 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     DN_TRY(conv_dgrad(V(p.g_db[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ib), 2 * nf, 3,
                       EPI_MASK, V(p.da[l], 2 * nf), V(p.g_da[l], 2 * nf), s));
     DN_TRY(fork());
-    DN_TRY(wgrad(W_C3, V(p.g_da[l], 2 * nf), V(p.c[l], p.cs[l]), N, H(l), Wd(l), 2 * nf, p.cs[l],
+    // channel count ck (the layer's cin, what G(ia) and the dgrad pack are sized for); cs is
+    // only the pixel stride (larger under a DN_C1S_ALIGN override)
+    DN_TRY(wgrad(W_C3, V(p.g_da[l], 2 * nf), V(p.c[l], p.cs[l]), N, H(l), Wd(l), 2 * nf, p.ck[l],
                  G(ia), SL(ia), p.splits[ia], s2, x6w, Z, &rb));
-    DN_TRY(conv_dgrad(V(p.g_da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ia), p.cs[l], 3,
+    DN_TRY(conv_dgrad(V(p.g_da[l], 2 * nf), N, H(l), Wd(l), 2 * nf, Wt(ia), p.ck[l], 3,
                       EPI_PLAIN, none, V(p.g_c[l], p.cs[l]), s));
     dU = V(p.g_c[l], p.cs[l], 0);  // [u_{l+1} grad | skip grad]
   }
@@ -881,7 +912,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   DN_TRY(conv_dgrad(V(p.g_a6, nf), N, H(5), Wd(5), nf, Wt(ENC6), nf, 3, EPI_PLAIN, none,
                     V(p.g_p5, nf), s));
   // pool5 backward -> g_a5 (level 4)
-  DN_TRY(launch_pool_bwd(ws + p.a[4], N, H(4), Wd(4), nf, ws + p.g_p5, nf, 0, 1, ws + p.g_a[4], s));
+  DN_TIMED(s, "pool_bwd", 0, 0, 0, 0, 0, 0, launch_pool_bwd(ws + p.a[4], N, H(4), Wd(4), nf, ws + p.g_p5, nf, 0, 1, ws + p.g_a[4], s));
   // enc_conv5..2: input p_{l} = skip slice of c_l; gradient accumulates into g_c_l's skip slice
   for (int l = 4; l >= 1; --l) {
     const int li = ENC2 + (l - 1);
@@ -893,10 +924,10 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                       V(p.g_c[l], p.cs[l], skip), s));
     // pool_l backward: d p_l (skip slice) -> gradient of the level l-1 activation
     if (l > 1) {
-      DN_TRY(launch_pool_bwd(ws + p.a[l - 1], N, H(l - 1), Wd(l - 1), nf, ws + p.g_c[l], p.cs[l],
+      DN_TIMED(s, "pool_bwd", 0, 0, 0, 0, 0, 0, launch_pool_bwd(ws + p.a[l - 1], N, H(l - 1), Wd(l - 1), nf, ws + p.g_c[l], p.cs[l],
                              skip, 1, ws + p.g_a[l - 1], s));
     } else {
-      DN_TRY(launch_pool_bwd(ws + p.a1, N, H(0), Wd(0), nf, ws + p.g_c[1], p.cs[1], skip, 1,
+      DN_TIMED(s, "pool_bwd", 0, 0, 0, 0, 0, 0, launch_pool_bwd(ws + p.a1, N, H(0), Wd(0), nf, ws + p.g_c[1], p.cs[1], skip, 1,
                              ws + p.g_a1, s));
     }
   }
@@ -907,16 +938,17 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   DN_TRY(conv_dgrad(V(p.g_a1, nf), N, H(0), Wd(0), nf, Wt(ENC1), nf, 3, EPI_MASK, V(p.a0, nf),
                     V(p.g_a0, nf), s));
   DN_TRY(fork());
-  DN_TRY(launch_enc0_wgrad(ws + p.g_a0, nf, ws + p.xin, N, C, H(0), Wd(0), SL(ENC0) + 64,
-                           p.splits[ENC0], G(ENC0), s2, &rb));
+  DN_TIMED(s2, "wgrad3_thin", 2.0 * N * H(0) * Wd(0) * nf * C * 9, C, nf, H(0), Wd(0), N,
+           launch_enc0_wgrad(ws + p.g_a0, nf, ws + p.xin, N, C, H(0), Wd(0), SL(ENC0) + 64,
+                             p.splits[ENC0], G(ENC0), s2, &rb));
   if (side) {  // join the weight-gradient branch before the reduction reads the slabs
     DN_TRY(hipEventRecord(side->join, s2));
     DN_TRY(hipStreamWaitEvent(s, side->join, 0));
   }
-  DN_TRY(red_flush(rb, s));
+  DN_TIMED(s, "reduce", 0, 0, 0, 0, 0, 0, red_flush(rb, s));
   // dL/dx: the network input feeds enc_conv0 and (as pool0) dec_conv1a's last C channels
   if (dx)
-    DN_TRY(launch_dgrad_input(ws + p.g_a0, prm + p.P.L[ENC0].woff, ws + p.g_d1a,
+    DN_TIMED(s, "dgrad_input", 0, 0, 0, 0, 0, 0, launch_dgrad_input(ws + p.g_a0, prm + p.P.L[ENC0].woff, ws + p.g_d1a,
                               prm + p.P.L[D1A].woff, p.c1k, 2 * nf, N, C, H(0), Wd(0), dx, s));
   return DN_OK;
 }

@@ -24,23 +24,50 @@ import torch
 import torch.distributed as dist
 
 
+def is_initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
 def is_distributed() -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    """a process group with more than one rank: what a trainer built with distributed=None
+    (auto) takes as "run data-parallel".  A trainer built with distributed=True runs its
+    collectives on any initialised group, world 1 included (a one-rank RCCL group exercises the
+    same broadcast / all-reduce calls as eight)."""
+    return is_initialized() and dist.get_world_size() > 1
+
+
+def require_group(distributed: bool | None) -> bool:
+    """resolve a trainer's `distributed` argument: None -> is_distributed(); True -> an
+    initialised process group is required (ValueError otherwise)"""
+    if distributed is None:
+        return is_distributed()
+    if distributed and not is_initialized():
+        raise ValueError("distributed=True needs an initialised torch.distributed process group "
+                         "(image_denoising_amd.dist.init_from_env)")
+    return bool(distributed)
+
+
+def launched_by_torchrun() -> bool:
+    """torchrun / torch.distributed.run sets TORCHELASTIC_RUN_ID for every rank it starts"""
+    return "TORCHELASTIC_RUN_ID" in os.environ
 
 
 def world_and_rank() -> tuple[int, int]:
-    if dist.is_available() and dist.is_initialized():
+    if is_initialized():
         return dist.get_world_size(), dist.get_rank()
     return 1, 0
 
 
-def init_from_env(backend: str = "nccl") -> tuple[int, int, int]:
+def init_from_env(backend: str = "nccl", force: bool = False) -> tuple[int, int, int]:
     """torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT) -> process group.
-    Returns (world, rank, local_rank); a single process stays non-distributed."""
+    Returns (world, rank, local_rank).  The group is created when world > 1, when torchrun
+    started this process (any world size: `torchrun --nproc-per-node 1` runs a one-rank RCCL
+    group) or when `force` is set; a plain single process stays non-distributed."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not dist.is_initialized():
+    want = world > 1 or force or launched_by_torchrun()
+    if want and not dist.is_initialized():
         if backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -58,14 +85,16 @@ def shard_bases(rank: int, local_batch: int, channels: int, height: int, width: 
 
 
 def broadcast_params(flat: torch.Tensor, src: int = 0) -> None:
-    if is_distributed():
+    """rank src's parameters to every rank (any initialised group, world 1 included)"""
+    if is_initialized():
         dist.broadcast(flat, src=src)
 
 
 def allreduce_grads(flat_grad: torch.Tensor) -> float:
-    """Sum the flat gradient over ranks in place; returns the scale (1/world) the optimizer
-    applies, so the update uses the global-batch mean gradient."""
-    if not is_distributed():
+    """Sum the flat gradient over ranks in place (any initialised group, world 1 included);
+    returns the scale (1/world) the optimizer applies, so the update uses the global-batch mean
+    gradient."""
+    if not is_initialized():
         return 1.0
     dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM)
     return 1.0 / dist.get_world_size()
@@ -73,7 +102,7 @@ def allreduce_grads(flat_grad: torch.Tensor) -> float:
 
 def allreduce_mean_(t: torch.Tensor) -> torch.Tensor:
     """mean of a (small) tensor over ranks, e.g. the logged loss (no host sync involved)"""
-    if is_distributed():
+    if is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         t /= dist.get_world_size()
     return t

@@ -142,9 +142,12 @@ class FinetuneTrainer:
             raise TypeError("FinetuneTrainer drives a DenoiserWithAdapter")
         self.model = model
         self.lambda_grad = lambda_grad
-        self.distributed = dp.is_distributed() if distributed is None else distributed
+        self.distributed = dp.require_group(distributed)
         ad = model.adapter
-        if self.distributed:
+        if self.distributed:  # identical replicas, as nn.DataParallel's per-forward broadcast
+            base_flat = getattr(model.base, "flat_params", None)
+            if base_flat is not None:  # the frozen base (loaded per rank from one checkpoint)
+                dp.broadcast_params(base_flat.data)
             dp.broadcast_params(ad.flat_params)
         self.opt = FlatAdam(ad.flat_params, lr=lr)
         self.grad = torch.zeros_like(ad.flat_params)

@@ -45,7 +45,7 @@ class N2NTrainer:
         self.noise_std = noise_std
         self.noise = AugmentNoise(noise_style) if noise_style else None
         self.seed = seed
-        self.distributed = dp.is_distributed() if distributed is None else distributed
+        self.distributed = dp.require_group(distributed)
         self.world, self.rank = dp.world_and_rank() if self.distributed else (1, 0)
         if self.distributed:  # identical replicas: broadcast rank 0's initial weights
             dp.broadcast_params(net.flat_params)
@@ -162,7 +162,7 @@ class StructureTrainer:
         self.net = net
         self.base_lr, self.n_epoch, self.gamma = lr, n_epoch, gamma
         self.weights = alpha_beta_gamma
-        self.distributed = dp.is_distributed() if distributed is None else distributed
+        self.distributed = dp.require_group(distributed)
         if self.distributed:
             dp.broadcast_params(net.flat_params)
         self.opt = FlatAdam(net.flat_params, lr=lr)

@@ -59,6 +59,12 @@ typedef struct dn_unet_cfg {
 /* "denoise_hip <version> gfx950 src=<16 hex>": the hash identifies the sources the library was
    built from (image_denoising_amd/_build.py source_hash) */
 const char* dn_version(void);
+/* The ABI revision of this header; a caller compiled against another revision must not bind.
+   Revision 3 (library 0.3.x): dn_unet_backward / dn_unet_backward_prec gained the nullable
+   `float* dx` argument after `dparams` (revision 2 had no dx: an old caller's arguments would
+   be shifted, so check dn_abi_version() == DN_ABI_VERSION before binding). */
+#define DN_ABI_VERSION 3
+int dn_abi_version(void);
 /* copies the last error message of this thread into buf (NUL-terminated); returns its length */
 int dn_last_error(char* buf, size_t len);
 
@@ -70,9 +76,34 @@ dn_status dn_unet_param_count(const dn_unet_cfg* cfg, size_t* count);
 dn_status dn_unet_param_info(const dn_unet_cfg* cfg, int index, size_t* w_off, size_t* w_count,
                              size_t* b_count);
 
+/* ---- in-step launch profiler (bench.py's per-shape roofline) ------------------------- */
+/* One launch recorded while profiling is enabled: op ("fwd3", "fwd3sel", "dgrad3", "wgrad3",
+   "fwd1", "deconv", "deconv_dgrad", "wgrad1", "wgrad_up", "head", "head_bwd", "enc0", "pool",
+   "pool_bwd", "pack", "reduce", "noise", "subsample", "loss", "adam", ...), the kernel the
+   launcher picked (may be empty), the GEMM shape (K reduction channels -> NOUT outputs over N x H
+   x W pixels), its algorithmic FLOPs (0 for byte-moving ops) and its HIP-event time on the
+   stream it was launched on. */
+typedef struct dn_op_record {
+  char op[24];
+  char kernel[48];
+  int K, NOUT, H, W, N;
+  double flops;
+  double ms;
+} dn_op_record;
+/* enable (1) / disable (0) recording; either call drops earlier records.  While enabled the
+   U-Net executors run every launch on the caller's stream (no side streams), so each record's
+   event pair brackets one kernel.  Not for production steps (one event pair per launch). */
+dn_status dn_profile_ops(int enable);
+/* waits for the recorded events, copies up to cap records into out, sets *count to the number
+   recorded (may exceed cap) and drops them. */
+dn_status dn_profile_ops_read(dn_op_record* out, int cap, int* count);
+
 /* ---- U-Net forward / backward: arch_unet.py:194-260 (UNet.forward) + autograd ---- */
 /* bytes of workspace for a batch N x H x W (H, W multiples of 32).  with_backward=1 sizes the
-   saved activations, gradient buffers and weight-gradient slabs needed by dn_unet_backward. */
+   saved activations, gradient buffers and weight-gradient slabs needed by dn_unet_backward.
+   The LAYOUT inside the workspace depends on with_backward (forward-only plans pad the concat
+   buffers' pixel strides to 128-B lines; backward plans keep them dense), so offsets read with
+   dn_unet_debug_buffers apply only to a workspace of the same with_backward. */
 dn_status dn_unet_workspace_size(const dn_unet_cfg* cfg, int N, int H, int W, int with_backward,
                                  size_t* bytes);
 /* y[N,out_nc,H,W] = UNet(x[N,in_nc,H,W]).  Activations are kept in ws for a later backward
@@ -149,7 +180,8 @@ dn_status dn_add_gauss_noise(const float* clean, int N, int64_t per_image, float
    torch.poisson(lam * x, generator) / lam): noisy = Poisson(lam * clean) / lam, lam per image
    from lam_per_image when not null.  Counts by fp64 CDF inversion of one 53-bit Philox uniform
    per element (same global-index stream convention as the Gaussian).  0 < lam <= 500 and clean
-   in [0, 1] (lam * clean <= 500). */
+   in [0, 1] (lam * clean <= 500): a scalar lam outside that range is rejected (DN_ERR_ARG); a
+   per-image lam outside it (device memory, not checked by the host) makes that image NaN. */
 dn_status dn_add_poisson_noise(const float* clean, int N, int64_t per_image, float lam,
                                const float* lam_per_image, uint64_t seed, uint64_t offset,
                                uint64_t elem_base, float* noisy, void* stream);

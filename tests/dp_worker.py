@@ -6,7 +6,15 @@ PRODUCT N2NTrainer(distributed=True) -- broadcast at init, one all-reduce of the
 per step, 1/world folded into the fused Adam kernel -- for two steps on its contiguous shard of
 a fixed global batch, then rank 0 writes what the test compares.
 
-    python tests/dp_worker.py OUT.npz PRECISION
+    python tests/dp_worker.py OUT.npz PRECISION            (two ranks, gloo)
+    python tests/dp_worker.py OUT.npz PRECISION nccl       (one rank, RCCL)
+    python tests/dp_worker.py OUT.npz PRECISION local      (no group; env-selected streams)
+    python tests/dp_worker.py OUT.npz PRECISION grad       (one UNet forward + backward)
+
+The `nccl` form is a ONE-rank RCCL group on the box's one GPU (RCCL does not put two ranks on
+one device): the product trainer's broadcast and per-step all-reduce run through RCCL for real,
+and the rank then repeats the two steps with distributed=False, so the test can require the two
+runs to agree bit for bit (a one-rank all-reduce is the identity, the scale 1/world = 1).
 """
 import os
 import sys
@@ -53,8 +61,61 @@ def run(tr, rank, world):
     return torch.stack(losses)
 
 
+def main_rccl(out, prec):
+    from image_denoising_amd import N2NTrainer
+    from image_denoising_amd import dist as dp
+
+    world, rank, _ = dp.init_from_env("nccl", force=True)
+    assert world == 1 and dp.is_initialized() and not dp.is_distributed()
+    backend = dist.get_backend()
+    net = build(prec, 0)
+    tr = N2NTrainer(net, distributed=True)  # broadcast + all-reduce on the RCCL group
+    assert tr.distributed
+    losses = run(tr, 0, 1)
+    grad, flat = tr.grad.cpu().numpy(), net.flat_params.detach().cpu().numpy()
+    net2 = build(prec, 0)
+    tr2 = N2NTrainer(net2, distributed=False)
+    losses2 = run(tr2, 0, 1)
+    torch.cuda.synchronize()
+    np.savez(out, backend=np.array(backend), losses=losses.cpu().numpy(), grad=grad, flat=flat,
+             losses_local=losses2.cpu().numpy(), grad_local=tr2.grad.cpu().numpy(),
+             flat_local=net2.flat_params.detach().cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def main_local(out, prec):
+    """one process, no group: the two steps under whatever DN_*_STREAMS the env sets"""
+    from image_denoising_amd import N2NTrainer
+
+    net = build(prec, 0)
+    tr = N2NTrainer(net, distributed=False)
+    losses = run(tr, 0, 1)
+    torch.cuda.synchronize()
+    np.savez(out, losses=losses.cpu().numpy(), grad=tr.grad.cpu().numpy(),
+             flat=net.flat_params.detach().cpu().numpy())
+
+
+def main_grad(out, prec):
+    """one forward + backward of the product UNet (parameter and input gradients) under the
+    env's plan overrides (DN_C1S_ALIGN)"""
+    net = build(prec, 0)
+    clean, noisy, _ = global_inputs()
+    x = noisy.cuda().requires_grad_(True)
+    y = net(x)
+    (y ** 2).mean().backward()
+    g = torch.cat([p.grad.reshape(-1) for p in net.parameters()])
+    np.savez(out, y=y.detach().cpu().numpy(), g=g.cpu().numpy(), dx=x.grad.cpu().numpy())
+
+
 def main():
     out, prec = sys.argv[1], sys.argv[2]
+    if len(sys.argv) > 3 and sys.argv[3] == "grad":
+        return main_grad(out, prec)
+    if len(sys.argv) > 3 and sys.argv[3] == "nccl":
+        return main_rccl(out, prec)
+    if len(sys.argv) > 3 and sys.argv[3] == "local":
+        return main_local(out, prec)
     from image_denoising_amd import N2NTrainer
     from image_denoising_amd import dist as dp
 

@@ -201,9 +201,37 @@ def _trainer_inputs():
     return clean, noisy, rd
 
 
+def _finetune_stand_ins(model):
+    """FinetuneTrainer's device launches on the CPU oracle: the frozen UNet base, the adapter
+    forward / backward (autograd over oracle.adapter_ref) and finetune.py's loss"""
+    import image_denoising_amd.finetune as ft_mod
+    from oracle import adapter_ref
+
+    ad = model.adapter
+
+    def ad_forward(noisy, base_out, out):
+        with torch.no_grad():
+            out.copy_(adapter_ref.adapter_forward(ad.flat_params, noisy, base_out))
+
+    def ad_backward(noisy, base_out, dout, dflat):
+        p = ad.flat_params.detach().clone().requires_grad_(True)
+        adapter_ref.adapter_forward(p, noisy, base_out).backward(dout)
+        dflat.copy_(p.grad)
+
+    def loss(pred, target, lam):
+        p = pred.detach().clone().requires_grad_(True)
+        l1, lg, l = adapter_ref.finetune_loss(p, target, lam)
+        l.backward()
+        return torch.stack([l1, lg, l]).detach(), p.grad
+
+    ad._run_forward, ad._run_backward = ad_forward, ad_backward
+    ft_mod.finetune_loss = loss
+
+
 def _run_trainer(kind, rank, world, steps=2):
-    """steps of N2NTrainer / StructureTrainer on this rank's shard; returns per-step losses,
-    the (all-reduced) gradient of the last step / world, and the final flat parameters"""
+    """steps of N2NTrainer / StructureTrainer / FinetuneTrainer on this rank's shard; returns
+    per-step losses, the (all-reduced) gradient of the last step / world, and the final flat
+    parameters (finetune: the adapter's, with the frozen base's appended)"""
     from image_denoising_amd import UNet
     from image_denoising_amd.trainer import N2NTrainer, StructureTrainer
 
@@ -213,6 +241,26 @@ def _run_trainer(kind, rank, world, steps=2):
         with torch.no_grad():
             net.flat_params.add_(0.5)
     dist_on = world > 1
+    if kind == "finetune":  # finetune.py:255-256 (DataParallel over the adapter model)
+        from image_denoising_amd.adapter import DenoiserWithAdapter
+        from image_denoising_amd.finetune import FinetuneTrainer
+
+        model = DenoiserWithAdapter(net, in_channels=1, hidden_channels=16)
+        with torch.no_grad():  # a non-trivial adapter, perturbed on rank 1 like the base
+            g = torch.Generator().manual_seed(5)
+            model.adapter.flat_params.copy_(0.1 * torch.randn(model.adapter.flat_params.shape,
+                                                              generator=g))
+            if rank == 1:
+                model.adapter.flat_params.add_(0.5)
+        tr = FinetuneTrainer(model, lr=1e-4, lambda_grad=0.1, distributed=dist_on)
+        _cpu_stand_ins(net, tr)
+        _finetune_stand_ins(model)
+        clean, noisy, _ = _trainer_inputs()
+        b = TB // world
+        sl = slice(rank * b, (rank + 1) * b)
+        losses = [tr.train_step(clean[sl], noisy[sl]).clone() for _ in range(steps)]
+        flat = torch.cat([model.adapter.flat_params, net.flat_params]).clone()
+        return torch.stack(losses), tr.grad / world, flat
     tr = (N2NTrainer(net, distributed=dist_on) if kind == "n2n"
           else StructureTrainer(net, distributed=dist_on))
     _cpu_stand_ins(net, tr)
@@ -280,9 +328,10 @@ def _spawn(target, args, nproc):
     return got
 
 
-@pytest.mark.parametrize("kind", ["n2n", "structure"])
+@pytest.mark.parametrize("kind", ["n2n", "structure", "finetune"])
 def test_two_rank_product_trainer_equals_full_batch(kind):
-    """N2NTrainer / StructureTrainer(distributed=True) on 2 gloo ranks == the single-process
+    """N2NTrainer / StructureTrainer / FinetuneTrainer(distributed=True) on 2 gloo ranks == the
+    single-process
     trainer on the concatenated batch: broadcast (rank 1 starts perturbed), gradient all-reduce
     and the 1/world grad_scale into Adam, over two steps (Adam state carried)."""
     losses_dp, grad_dp, flats = _spawn(_trainer_worker, (2, _free_port(), kind), 2)

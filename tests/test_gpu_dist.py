@@ -72,3 +72,62 @@ def test_two_rank_n2n_trainer_equals_full_batch(tmp_path, prec):
     d = np.abs(r["flat0"] - flat)
     assert (d > 1e-6).mean() < 2e-3, (d > 1e-6).mean()
     assert d.max() <= 2 * 2 * 3e-4 + 1e-6
+
+
+def test_one_rank_rccl_n2n_trainer_bit_exact(tmp_path):
+    """The RCCL path itself (BASELINE configs[2]'s collective, train.py:324-326): a ONE-rank
+    "nccl" process group on the box's GPU, started in a fresh process before any GPU call.
+    N2NTrainer(distributed=True) broadcasts and all-reduces through RCCL every step; the
+    one-rank sum is the identity and the scale 1, so two steps must equal a distributed=False
+    run bit for bit."""
+    out = str(tmp_path / "rccl.npz")
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()), PYTHONUNBUFFERED="1")
+    p = subprocess.run([sys.executable, os.path.join(HERE, "dp_worker.py"), out, "fp32_x6",
+                        "nccl"], env=env, cwd=ROOT, timeout=240)
+    assert p.returncode == 0
+    r = np.load(out)
+    assert str(r["backend"]) == "nccl"
+    assert np.array_equal(r["losses"], r["losses_local"])
+    assert np.array_equal(r["grad"], r["grad_local"])
+    assert np.array_equal(r["flat"], r["flat_local"])
+
+
+def test_single_stream_step_equals_two_stream_default(tmp_path):
+    """DN_STEP_STREAMS=0 (the no-grad target pass on the main stream) and DN_BWD_STREAMS=0 (the
+    weight gradients on the main stream) give the default two-stream step's results bit for bit
+    (every kernel writes its own buffers; the streams only reorder independent launches).  The
+    C++ side reads DN_BWD_STREAMS once per process, hence a fresh process per setting."""
+    res = {}
+    for tag, extra in (("two", {}), ("one", {"DN_STEP_STREAMS": "0", "DN_BWD_STREAMS": "0"})):
+        out = str(tmp_path / f"{tag}.npz")
+        env = dict(os.environ, PYTHONUNBUFFERED="1", **extra)
+        for k in ("DN_STEP_STREAMS", "DN_BWD_STREAMS"):
+            if k not in extra:
+                env.pop(k, None)
+        p = subprocess.run([sys.executable, os.path.join(HERE, "dp_worker.py"), out, "fp32_x6",
+                            "local"], env=env, cwd=ROOT, timeout=240)
+        assert p.returncode == 0, tag
+        res[tag] = np.load(out)
+    for k in ("losses", "grad", "flat"):
+        assert np.array_equal(res["one"][k], res["two"][k]), k
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp32_x6"])
+def test_backward_with_padded_concat_strides(tmp_path, prec):
+    """DN_C1S_ALIGN=32 pads every concat buffer's pixel stride (144 -> 160, 100 -> 128) in the
+    backward plan too: the backward must take the channel count from the layer (ck), not from
+    the stride, so outputs and every gradient equal the dense-stride plan's."""
+    res = {}
+    for tag, extra in (("dense", {}), ("pad32", {"DN_C1S_ALIGN": "32"})):
+        out = str(tmp_path / f"{tag}.npz")
+        env = dict(os.environ, PYTHONUNBUFFERED="1", **extra)
+        if not extra:
+            env.pop("DN_C1S_ALIGN", None)
+        p = subprocess.run([sys.executable, os.path.join(HERE, "dp_worker.py"), out, prec, "grad"],
+                           env=env, cwd=ROOT, timeout=240)
+        assert p.returncode == 0, tag
+        res[tag] = np.load(out)
+    for k in ("y", "g", "dx"):
+        a, b = res["dense"][k], res["pad32"][k]
+        assert np.abs(a - b).max() <= 1e-5 * np.abs(a).max(), (k, np.abs(a - b).max())
