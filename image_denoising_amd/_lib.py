@@ -116,6 +116,7 @@ SIGNATURES = {
     "dn_quantize_u8": (c_int, [_F, c_int64, c_int, _U8, c_void_p]),
     "dn_psnr_u8": (c_int, [_U8, _U8, c_int64, c_void_p, c_void_p, c_void_p]),
     "dn_ssim_u8": (c_int, [_U8, _U8, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "dn_l1_mean_batched": (c_int, [_F, _F, c_int64, c_int64, c_void_p, c_void_p]),
     "dn_l1_mean": (c_int, [_F, _F, c_int64, c_void_p, c_void_p, c_void_p]),
     "dn_iunet_param_count": (c_int, [POINTER(DnCfg), POINTER(c_size_t)]),
     "dn_iunet_workspace_size": (c_int, [POINTER(DnCfg), c_int, c_int, c_int, c_int,

@@ -394,6 +394,15 @@ dn_status dn_l1_mean(const float* a, const float* b, int64_t n, void* part, doub
                     "dn_l1_mean");
 }
 
+dn_status dn_l1_mean_batched(const float* a, const float* b, int64_t P, int64_t n, double* l1,
+                             void* stream) {
+  if (P < 0 || n < 1) return fail(DN_ERR_ARG, "P >= 0 and n >= 1 required");
+  if (P == 0) return DN_OK;
+  if (P > 0x7fffffffL) return fail(DN_ERR_ARG, "P too large");
+  if (!a || !b || !l1) return fail(DN_ERR_ARG, "null argument");
+  return hip_status(launch_l1_batched(a, b, P, n, l1, (hipStream_t)stream), "dn_l1_mean_batched");
+}
+
 // ---- op-level entry points ------------------------------------------------------------
 size_t dn_conv2d_pack_size(int Cin, int Cout, int ksize, int backward_data) {
   if ((ksize != 1 && ksize != 3) || Cin < 1 || Cout < 1) return 0;

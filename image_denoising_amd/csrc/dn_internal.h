@@ -254,6 +254,8 @@ hipError_t launch_psnr(const uint8_t* a, const uint8_t* b, long n, double* part,
                        hipStream_t s);
 hipError_t launch_ssim(const uint8_t* a, const uint8_t* b, int C, int H, int W, int hwc,
                        double* part, double* out, hipStream_t s);
+hipError_t launch_l1_batched(const float* a, const float* b, long P, long n, double* out,
+                             hipStream_t s);
 hipError_t launch_l1(const float* a, const float* b, long n, double* part, double* out,
                      hipStream_t s);
 hipError_t launch_head_bwd(const HeadBwdArgs& h, hipStream_t s);

@@ -147,6 +147,20 @@ __global__ __launch_bounds__(256) void k_l1_part(const float* __restrict__ a,
   if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
+// mean |a_p - b_p| of P items of n floats each (the per-tile criterion of evaluation_704.py:98),
+// one workgroup per item: fp64 per-thread sums in a fixed order, fixed-tree block sum
+__global__ __launch_bounds__(256) void k_l1_batched(const float* __restrict__ a,
+                                                    const float* __restrict__ b, long n,
+                                                    double* __restrict__ out) {
+  __shared__ double sh[256];
+  const float* pa = a + (long)blockIdx.x * n;
+  const float* pb = b + (long)blockIdx.x * n;
+  double s = 0.0;
+  for (long i = threadIdx.x; i < n; i += 256) s += fabs((double)pa[i] - (double)pb[i]);
+  const double tot = block_sum_d(s, sh);
+  if (threadIdx.x == 0) out[blockIdx.x] = tot / (double)n;
+}
+
 // img [C,H,W] or [H,W,C] (hwc=1) uint8; one SSIM map per channel over the valid region
 __global__ __launch_bounds__(256) void k_ssim_part(const uint8_t* __restrict__ a,
                                                    const uint8_t* __restrict__ b, int C, int H,
@@ -257,6 +271,12 @@ hipError_t launch_ssim(const uint8_t* a, const uint8_t* b, int C, int H, int W, 
   hipLaunchKernelGGL(k_ssim_part, dim3(nb), dim3(256), 0, s, a, b, C, H, W, hwc, part);
   hipLaunchKernelGGL(k_eval_finalize, dim3(1), dim3(256), 0, s, part, (int)nb, (double)total, 1,
                      out);
+  return hipGetLastError();
+}
+
+hipError_t launch_l1_batched(const float* a, const float* b, long P, long n, double* out,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(k_l1_batched, dim3((unsigned)P), dim3(256), 0, s, a, b, n, out);
   return hipGetLastError();
 }
 

@@ -142,10 +142,12 @@ def denoise_tiled(net, noisy, patch: int = PATCH, overlap: int = OVERLAP, max_ba
     pred = torch.empty((P, net.out_nc, patch, patch), dtype=torch.float32, device=dev)
     for b0 in range(0, P, max_batch):
         pred[b0:b0 + max_batch] = net(tiles[b0:b0 + max_batch])
-    parts = _parts(dev)
+    # criterion(prediction_patch, noisy_input) of every tile (evaluation_704.py:98), one launch
+    if net.out_nc != C:
+        raise ValueError("tiled evaluation compares the prediction with its input: out_nc == C")
     l1s = torch.empty(P, dtype=torch.float64, device=dev)
-    for p in range(P):  # criterion(prediction_patch, noisy_input) per tile
-        _l1(pred[p], tiles[p], parts, l1s[p:p + 1])
+    _lib.call("dn_l1_mean_batched", _lib.ptr(pred), _lib.ptr(tiles), P, C * patch * patch,
+              _lib.ptr(l1s), st)
     wm = torch.from_numpy(weight_mask(patch)).to(dev)
     out = torch.empty((net.out_nc, H, W), dtype=torch.float32, device=dev)
     p8 = torch.empty((net.out_nc, H, W), dtype=torch.uint8, device=dev)
@@ -189,8 +191,24 @@ def validation_denoise(dataset_dir):
     return im1, im2, clean, noise
 
 
-def main(argv=None):
+def build_network(log_name: str, n_channel: int, n_feature: int):
+    """evaluation.py:32-50's choice of network by --log_name, in the reference's branch order
+    ('UNET' is matched case-sensitively, so 'UNetImproved' reaches the ImprovedUNet branch)"""
     from .arch_unet import UNet
+    from .improved_unet import ImprovedUNet
+
+    if "UNET" in log_name and "blindspot" in log_name:
+        raise SystemExit("the blind-spot UNet is out of scope on this path (DESIGN.md §8)")
+    if "UNET" in log_name:
+        return UNet(in_nc=n_channel, out_nc=n_channel, n_feature=n_feature)
+    if "RESNET" in log_name:
+        raise SystemExit("RESNET is out of scope on this path (DESIGN.md §8)")
+    if "UNetImproved" in log_name:
+        return ImprovedUNet(in_nc=n_channel, out_nc=n_channel, n_feature=n_feature)
+    raise SystemExit(f"--log_name {log_name!r} names no network (evaluation.py:32-50)")
+
+
+def main(argv=None):
     from .checkpoint import load_checkpoint
 
     ap = argparse.ArgumentParser(description="evaluation.py / evaluation_704.py on the HIP path")
@@ -199,18 +217,17 @@ def main(argv=None):
     ap.add_argument("--save_dir", type=str, default="./eval_results")
     ap.add_argument("--n_feature", type=int, default=48)
     ap.add_argument("--n_channel", type=int, default=1)
-    ap.add_argument("--log_name", type=str, default="UNET")
+    ap.add_argument("--log_name", type=str, default="UNetImproved")  # evaluation.py:19
     ap.add_argument("--gpu_devices", default="0", type=str)
     ap.add_argument("--tiled", action="store_true", help="evaluation_704.py tiling")
     ap.add_argument("--patch", type=int, default=PATCH)
     ap.add_argument("--overlap", type=int, default=OVERLAP)
     ap.add_argument("--save_images", action="store_true")
     opt = ap.parse_args(argv)
-    if "UNET" not in opt.log_name.upper() or "blindspot" in opt.log_name:
-        raise SystemExit("only the UNet (non-blind-spot) architecture is on this path")
+    net = build_network(opt.log_name, opt.n_channel, opt.n_feature)
     os.makedirs(opt.save_dir, exist_ok=True)
     clean, noisy, clean_paths, noisy_paths = validation_denoise(opt.data_dir)
-    net = UNet(in_nc=opt.n_channel, out_nc=opt.n_channel, n_feature=opt.n_feature).to(_device())
+    net = net.to(_device())
     load_checkpoint(net, opt.checkpoint)
     net.eval()
     print(f"Loaded checkpoint from {opt.checkpoint}")

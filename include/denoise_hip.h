@@ -322,6 +322,10 @@ dn_status dn_ssim_u8(const uint8_t* a, const uint8_t* b, int C, int H, int W, in
 /* mean |a - b| (nn.L1Loss, evaluation.py:74) */
 dn_status dn_l1_mean(const float* a, const float* b, int64_t n, void* part, double* l1,
                      void* stream);
+/* l1[p] = mean |a[p] - b[p]| for P consecutive items of n floats (evaluation_704.py:98's
+   criterion(prediction_patch, noisy_input) for every tile at once, one launch; fp64 sums) */
+dn_status dn_l1_mean_batched(const float* a, const float* b, int64_t P, int64_t n, double* l1,
+                             void* stream);
 
 /* ---- adapter finetune: adapter.py:5-67 (OutputAdapter / DenoiserWithAdapter),
    finetune.py:153-162 (gradient_loss), finetune.py:269-289 (the step) ------------------------
