@@ -217,18 +217,19 @@ def per_shape_roofline(recs, reps, peak):
     return shapes, weighted, tot_ms, {k: round(v, 4) for k, v in sorted(by_op.items(), key=lambda kv: -kv[1])}, executed
 
 
-def pmc_step_traffic(kernel):
+def pmc_step_traffic(kernel, mode_tag):
     """HBM bytes per launch of `kernel` inside the bench step, from the committed rocprofv3 PMC
-    summary (tools/pmc_step.py over separate FETCH_SIZE / WRITE_SIZE passes; gfx950 x2 FETCH
-    correction), or (None, None)"""
+    summaries profiles/<round>_<mode_tag>_pmc_step.json (tools/gpu_run.sh pmc: separate
+    FETCH_SIZE / WRITE_SIZE passes over this bench configuration; gfx950 x2 FETCH correction),
+    newest round first; (None, None) if no summary holds the kernel"""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_step.json")))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    k = d.get("kernels", {}).get(kernel)
-    return (k["traffic_bytes"] if k else None), os.path.relpath(files[-1], ROOT)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{mode_tag}_pmc_step.json")), reverse=True)
+    for f in files:
+        k = json.load(open(f)).get("kernels", {}).get(kernel)
+        if k:
+            return k["traffic_bytes"], os.path.relpath(f, ROOT)
+    return None, None
 
 
 def pmc_traffic(tag=""):
@@ -480,7 +481,9 @@ def main():
             dom = shapes[0]
             kms, kflops = dom["avg_launch_ms"], dom["flops_per_launch"]
             kdesc = f"{dom['kernel']} {dom['op']} {dom['shape']} (in-step launch)"
-            traffic, traffic_src = pmc_step_traffic(dom["kernel"])
+            mode_tag = ("bf16" if bf else args.mode) + ("_iunet" if iu else "") + \
+                (f"_c{C}" if C != 1 else "")
+            traffic, traffic_src = pmc_step_traffic(dom["kernel"], mode_tag)
         else:  # no instrumented executor (ImprovedUNet): the isolated 96->96 shape
             timer = (time_dominant_kernel_bf16 if bf else
                      time_dominant_kernel_x6 if x6 else time_dominant_kernel)

@@ -256,6 +256,31 @@ __device__ __forceinline__ void x6_barrier() {
 #ifndef DN_X6P_LOOK
 #define DN_X6P_LOOK 2  // B fragment groups read ahead of their MFMAs in k_c3x6p
 #endif
+// DN_X6_STAMPS=1 (diagnostic builds only): s_memtime stamps of waves 0 and 4 (one per SIMD pair
+// half) of the first 64 tiles of image 0 -- kernel start, per stage after its opening barrier /
+// after its last MFMA / before its closing barrier, end of the main loop, end of the epilogue --
+// read back with dn_debug_x6_stamps (tools/x6_stamps.py).  Stamps sit where no LDS read is in
+// flight, so the counted lgkmcnt waits of the stage are unchanged.
+#ifndef DN_X6_STAMPS
+#define DN_X6_STAMPS 0
+#endif
+#if DN_X6_STAMPS
+constexpr int X6_STAMP_SLOTS = 128;
+__device__ unsigned long long g_x6_stamps[64 * 2 * X6_STAMP_SLOTS];
+#define X6_STAMP(slot)                                                                         \
+  do {                                                                                         \
+    if (blockIdx.y == 0 && blockIdx.z == 0 && blockIdx.x < 64 && (wave & 3) == 0 &&            \
+        (slot) < X6_STAMP_SLOTS) {                                                             \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                              \
+      if (lane == 0) g_x6_stamps[(blockIdx.x * 2 + (wave >> 2)) * X6_STAMP_SLOTS + (slot)] = t_; \
+    }                                                                                          \
+  } while (0)
+#else
+#define X6_STAMP(slot) \
+  do {                 \
+  } while (0)
+#endif
+
 template <int NT, int TAIL, bool SEL = false>
 __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   using C = PCfg<NT>;
@@ -391,10 +416,12 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   // for the x registers then only ever cover DMAs issued a stage or more earlier.
   // MODE 0: a full 32-channel chunk tap, with the operand reads of a stage in one basic block
   // (the MFMAs then wait for them with counted lgkmcnt); MODE 3: the tail instantiations.
+  X6_STAMP(0);
   auto stage = [&](auto mode_tag, int c, int t) {
     constexpr int MODE = decltype(mode_tag)::value;
     const bool more = c + 1 < nch;
     const int st = 9 * c + t;
+    X6_STAMP(1 + 3 * st);
     const __bf16* lw = ring + (st % C::S) * C::WSTP;
     bf16x8 av[3][MTC], bv[3][NTW];
     // MODE 3: the last chunk's mode decided at run time (tail instantiations: one A-read path
@@ -543,6 +570,7 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    X6_STAMP(2 + 3 * st);
     const bool xstep = t == 8 && more;
     if (xstep) {
       x6_barrier();  // every wave is done with this chunk's x tile
@@ -559,6 +587,7 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     else
       X6_WAITCNT_VM_LGKM0(C::PPW * (C::S - 2));
     if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
+    X6_STAMP(3 + 3 * st);
     x6_barrier();
   };
   // TAIL: the instantiation's last-chunk packing (the host passes a.x6_tail == TAIL)
@@ -574,6 +603,7 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   }
   X6_WAITCNT_VM(0);  // the trailing re-load DMAs must land before the LDS is reused
   x6_barrier();
+  X6_STAMP(1 + 3 * nst);
   x6_fold(acc, accl);
   if constexpr (SEL) {
     // the pair image: OH/2 rows, row ty0/2 + 2(w&3) + m, column tx0 + fragment row, the wave's
@@ -588,7 +618,20 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   } else {
     fwd_epilogue<NT, C::MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
   }
+#if DN_X6_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  X6_STAMP(2 + 3 * nst);
+#endif
 }
+
+#if DN_X6_STAMPS
+// host copy of the stamp buffer (diagnostic builds only; not part of include/denoise_hip.h)
+extern "C" int dn_debug_x6_stamps(unsigned long long* host, int n) {
+  const int cap = 64 * 2 * X6_STAMP_SLOTS;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_x6_stamps),
+                                  sizeof(unsigned long long) * (n < cap ? n : cap));
+}
+#endif
 
 // ------------------------------------------------------------------------------------
 // Two-workgroups-per-CU variant for large grids (k_c3x6h): 4 waves on an 8 x 16 x 16*NT tile

@@ -6,7 +6,8 @@
 #       bench           default bench line, CPU baseline included      -> gpurun_out/bench.log
 #       quick           bench line without the CPU baseline            -> gpurun_out/quick.log
 #       stats:TAG       rocprofv3 --kernel-trace --stats over a 3-step bench -> gpurun_out/prof/TAG
-#       pmc             FETCH_SIZE / WRITE_SIZE passes over a 2-step bench -> gpurun_out/pmc_step
+#       pmc:TAG[:ARGS]  FETCH_SIZE / WRITE_SIZE passes over a 2-step bench -> profiles/TAG_pmc_step.json
+#       stamps:K+N+H    k_c3x6p stage timeline from the DN_X6_STAMPS build (tools/x6_stamps.py)
 #       sq:NAME:CTRS    one SQ counter pass (<= 8 SQ counters, '+'-separated) over a 2-step bench
 #       micro           tools/x6_micro.py (isolated 3x3 shapes)         -> gpurun_out/micro.log
 #       torchrun1       torchrun --nproc-per-node 1 bench (a one-rank RCCL group) -> gpurun_out/torchrun1.log
@@ -52,18 +53,24 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/$arg -o run \
         -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof/$arg.log 2>&1 || fail "$step" $?
       summ_stats gpurun_out/prof/$arg ;;
-    pmc)
-      rm -rf gpurun_out/pmc_step
+    pmc)  # pmc:TAG[:bench args, '+'-separated]
+      tag=${arg%%:*}; bargs=${arg#*:}; [ "$bargs" = "$arg" ] && bargs=""; bargs=${bargs//+/ }
+      rm -rf gpurun_out/pmc_step_$tag
       for c in FETCH_SIZE WRITE_SIZE; do
-        timeout -s KILL 200 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc_step/$c -o run \
-          -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_step/$c.log 2>&1 || fail "$step $c" $?
+        timeout -s KILL 200 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc_step_$tag/$c -o run \
+          -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $bargs > gpurun_out/pmc_step_$tag/$c.log 2>&1 || fail "$step $c" $?
       done
-      python3 tools/pmc_step.py r3 || fail "$step summary" $? ;;
+      python3 tools/pmc_step.py $tag gpurun_out/pmc_step_$tag || fail "$step summary" $? ;;
+    stamps)  # stamps:K+NOUT+H (needs libdenoise_hip_stamps.so, tools/x6_stamps.py)
+      DN_LIB_PATH=image_denoising_amd/libdenoise_hip_stamps.so timeout -k 10 120 python -u tools/x6_stamps.py ${arg//+/ } \
+        > gpurun_out/stamps_${arg//+/_}.log 2>&1 || fail "$step" $?
+      cat gpurun_out/stamps_${arg//+/_}.log | grep -v amdgpu.ids ;;
     sq)
       out=${arg%%:*}; ctrs=${arg#*:}; ctrs=${ctrs//+/ }
       rm -rf gpurun_out/pmc_sq/$out; mkdir -p gpurun_out/pmc_sq
       timeout -s KILL 200 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d gpurun_out/pmc_sq/$out -o run \
         -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ${SQ_ARGS:-} > gpurun_out/pmc_sq/$out.log 2>&1 || fail "$step" $?
+      # (SQ_ARGS: extra bench arguments, e.g. SQ_ARGS="--mode finetune --precision bf16")
       python3 tools/pmc_sq_summary.py gpurun_out/pmc_sq/$out ;;
     micro)
       timeout -k 10 300 python -u tools/x6_micro.py > gpurun_out/micro.log 2>&1 || fail "$step" $?
