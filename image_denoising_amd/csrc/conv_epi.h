@@ -30,8 +30,8 @@ __device__ __forceinline__ WgradArgs wg_block(const WgradArgs& a0) {
 // UP: deconv forward, wave = parity (a,b) and every wave covers all MT rows; else wave w owns
 // rows [w*MT, w*MT+MT) and blockIdx.z is the output-channel block (zc) or the scatter parity.
 template <int NT, int MT, int PS, bool UP>
-__device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, const f32x4 (&acc)[MT][NT],
-                                             float* lds, int ty0, int tx0, int n) {
+__device__ __forceinline__ void fwd_epilogue_generic(const FwdArgs& a, const f32x4 (&acc)[MT][NT],
+                                                     float* lds, int ty0, int tx0, int n) {
   constexpr int NP = 16 * NT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 15, lg = lane >> 4;
@@ -149,6 +149,114 @@ __device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, const f32x4 (&acc
       }
     }
   }
+}
+
+
+// NHWC float4 epilogue specialised on the epilogue kind EPI (compile time): every load of the
+// wave's rows -- the staged tile read back from LDS, the mask / residual / old output -- is
+// issued before the first global store.  The generic epilogue decides the kind at run time, so
+// the compiler had to place a conservative s_waitcnt vmcnt(0) at the merge of each row's
+// conditional loads -- behind the previous row's stores, i.e. one full store round trip per row
+// (~15k cycles of a ~115k-cycle 16x16x96 tile with every CU storing at once, DN_X6_STAMPS).
+// Requires vec_out (OUT_NHWC, float4-aligned strides / offsets); rows are staged one at a time
+// through the wave's own LDS area (a wave's LDS accesses complete in order).
+template <int NT, int MT, int PS, int EPI>
+__device__ __forceinline__ void fwd_epilogue_vec(const FwdArgs& a, const f32x4 (&acc)[MT][NT],
+                                                 float* lds, int ty0, int tx0, int n) {
+  constexpr int NP = 16 * NT;
+  constexpr bool BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_ACT || EPI == EPI_BIAS_ADD;
+  constexpr bool MASKL = EPI == EPI_MASK || EPI == EPI_BIAS_ADD;  // reads a.mask
+  constexpr bool OLDL = EPI == EPI_ACCUM;                         // reads a.out
+  constexpr int NIT = (16 * NP / 4 + 63) / 64;  // float4 items per lane per row
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int wrow = wave * MT;
+  const int cz = a.zc ? (int)blockIdx.z * a.zc : 0;
+  const int nout = a.zc ? min(NP, a.NOUT - cz) : a.NOUT;
+  const int NQ = nout >> 2;
+  float* st = lds + wave * 16 * PS;
+  const bool has_bias = BIAS && a.bias != nullptr;
+  float4 bvec[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int e = lane + 64 * k;
+    bvec[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (has_bias && e < 16 * NQ)
+      bvec[k] = *reinterpret_cast<const float4*>(a.bias + cz + 4 * (e - (e / NQ) * NQ));
+  }
+  float4 vv[MT][NIT], rr[MT][NIT];
+  long oi[MT][NIT];
+  bool ok[MT][NIT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {  // phase 1: stage, read back, auxiliary loads
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) st[(4 * lg + r) * PS + q * 16 + li] = acc[m][q][r];
+    const int gy = ty0 + wrow + m;
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int e = lane + 64 * k;
+      const int p = e / NQ, c = 4 * (e - p * NQ);
+      const int gx = tx0 + p;
+      ok[m][k] = e < 16 * NQ && gx < a.OW && gy < a.OH;
+      vv[m][k] = rr[m][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      const long pix = ((long)n * a.OH + gy) * a.OW + gx;
+      oi[m][k] = pix * a.out_stride + a.out_off + cz + c;
+      if (e < 16 * NQ) vv[m][k] = *reinterpret_cast<const float4*>(st + p * PS + c);
+      if (MASKL && ok[m][k])
+        rr[m][k] = *reinterpret_cast<const float4*>(a.mask + pix * a.mask_stride + a.mask_off + cz + c);
+      if (OLDL && ok[m][k]) rr[m][k] = *reinterpret_cast<const float4*>(a.out + oi[m][k]);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)  // phase 2: arithmetic and stores
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      if (!ok[m][k]) continue;
+      float4 v = vv[m][k];
+      const float4 r = rr[m][k];
+      if (BIAS) {
+        v.x += bvec[k].x; v.y += bvec[k].y; v.z += bvec[k].z; v.w += bvec[k].w;
+      }
+      if (EPI == EPI_BIAS_ACT) {
+        v.x = v.x > 0.f ? v.x : v.x * 0.2f; v.y = v.y > 0.f ? v.y : v.y * 0.2f;
+        v.z = v.z > 0.f ? v.z : v.z * 0.2f; v.w = v.w > 0.f ? v.w : v.w * 0.2f;
+      } else if (EPI == EPI_BIAS_ADD) {
+        v.x = r.x + v.x; v.y = r.y + v.y; v.z = r.z + v.z; v.w = r.w + v.w;
+      } else if (EPI == EPI_MASK) {
+        v.x = r.x > 0.f ? v.x : v.x * 0.2f; v.y = r.y > 0.f ? v.y : v.y * 0.2f;
+        v.z = r.z > 0.f ? v.z : v.z * 0.2f; v.w = r.w > 0.f ? v.w : v.w * 0.2f;
+      } else if (EPI == EPI_ACCUM) {
+        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+      }
+      *reinterpret_cast<float4*>(a.out + oi[m][k]) = v;
+    }
+}
+
+// the epilogue: the specialised float4 NHWC path where it applies, else the generic one
+template <int NT, int MT, int PS, bool UP>
+__device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, const f32x4 (&acc)[MT][NT],
+                                             float* lds, int ty0, int tx0, int n) {
+  const bool aux = a.epi == EPI_MASK || a.epi == EPI_BIAS_ADD;
+  const bool vec_nhwc = !UP && a.out_layout == OUT_NHWC &&
+                        ((a.out_stride | a.out_off | a.NOUT) & 3) == 0 &&
+                        (!aux || ((a.mask_stride | a.mask_off) & 3) == 0);
+#ifndef DN_EPI_VEC
+#define DN_EPI_VEC 1  // A/B switch: 0 = the generic run-time-kind epilogue everywhere
+#endif
+  if (DN_EPI_VEC && vec_nhwc) {
+    switch (a.epi) {
+      case EPI_BIAS: return fwd_epilogue_vec<NT, MT, PS, EPI_BIAS>(a, acc, lds, ty0, tx0, n);
+      case EPI_BIAS_ACT: return fwd_epilogue_vec<NT, MT, PS, EPI_BIAS_ACT>(a, acc, lds, ty0, tx0, n);
+      case EPI_PLAIN: return fwd_epilogue_vec<NT, MT, PS, EPI_PLAIN>(a, acc, lds, ty0, tx0, n);
+      case EPI_MASK: return fwd_epilogue_vec<NT, MT, PS, EPI_MASK>(a, acc, lds, ty0, tx0, n);
+      case EPI_ACCUM: return fwd_epilogue_vec<NT, MT, PS, EPI_ACCUM>(a, acc, lds, ty0, tx0, n);
+      case EPI_BIAS_ADD: return fwd_epilogue_vec<NT, MT, PS, EPI_BIAS_ADD>(a, acc, lds, ty0, tx0, n);
+      default: break;
+    }
+  }
+  fwd_epilogue_generic<NT, MT, PS, UP>(a, acc, lds, ty0, tx0, n);
 }
 
 }  // namespace dn

@@ -256,6 +256,18 @@ __device__ __forceinline__ void x6_barrier() {
 #ifndef DN_X6P_LOOK
 #define DN_X6P_LOOK 2  // B fragment groups read ahead of their MFMAs in k_c3x6p
 #endif
+// A/B switches of the k_c3x6p stage schedule (full chunks): DMAI = the next weight stage's DMA
+// pieces issued between the first fragment groups instead of after the last MFMA; PIN = each
+// group's round-to-nearest hi adds pinned behind its MFMAs instead of sunk to the stage end
+#ifndef DN_X6P_DMAI
+#define DN_X6P_DMAI 1
+#endif
+#ifndef DN_X6P_PIN
+#define DN_X6P_PIN 1
+#endif
+#ifndef DN_X6P_ABL_NODMA
+#define DN_X6P_ABL_NODMA 0  // diagnostic ablation: no weight DMA in the stage loop (wrong results)
+#endif
 // DN_X6_STAMPS=1 (diagnostic builds only): s_memtime stamps of waves 0 and 4 (one per SIMD pair
 // half) of the first 64 tiles of image 0 -- kernel start, per stage after its opening barrier /
 // after its last MFMA / before its closing barrier, end of the main loop, end of the epilogue --
@@ -382,6 +394,12 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   // instead of the counted wait) as long as any of those DMAs is outstanding -- i.e. always
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<__bf16*>(wimg), (short)0, nst * C::WSTP * 2, 0x00020000);
+  auto load_w_piece = [&](int src_st, int slot, int j) {
+    if (DN_X6P_ABL_NODMA) return;  // diagnostic ablation only: stale weights
+    unsigned char* dst = reinterpret_cast<unsigned char*>(ring + slot * C::WSTP);
+    const int piece = wave * C::PPW + j;
+    buf_lds16(wrs, dst + piece * 1024, src_st * C::WSTP * 2 + piece * 1024 + lane * 16);
+  };
   auto load_w = [&](int src_st, int slot) {
     unsigned char* dst = reinterpret_cast<unsigned char*>(ring + slot * C::WSTP);
 #pragma unroll
@@ -508,7 +526,21 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
           bv[p][q] = *reinterpret_cast<const bf16x8*>(lw + p * C::WPL + off);
       }
     };
+    // next weight stage (st + S - 1) into the slot every wave left at the previous barrier
+    const int wsrc = st + C::S - 1 < nst ? st + C::S - 1 : nst - 1, wslot = (st + C::S - 1) % C::S;
+    // the group's hi adds materialised here (an empty asm reading and writing the sums): the
+    // compiler had sunk all of them to the stage end, behind the last MFMA, keeping 12 hi
+    // temporaries live and adding 48 dependent adds to the tail the partner wave waits on
+    auto pin_group = [&](int g) {
+      if constexpr (DN_X6P_PIN) {
+#pragma unroll
+        for (int m = 0; m < MTC; ++m)
+#pragma unroll
+          for (int q = g * QG; q < (g + 1) * QG; ++q) asm volatile("" : "+v"(acc[m][q]));
+      }
+    };
     if constexpr (STAGED) {
+      static_assert(!DN_X6P_DMAI || C::PPW <= NG, "one DMA piece per early fragment group");
       const int ky = t / 3, kx = t - 3 * ky;
       auto read_a = [&](int p) {
 #pragma unroll
@@ -536,7 +568,8 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       f32x4 hi[MTC];
 #pragma unroll
-      for (int m = 0; m < MTC; ++m) hi[m] = mfma_bf16(av[0][m], bv[0][0], z);
+      for (int m = 0; m < MTC; ++m)
+        hi[m] = mfma_bf16(av[0][m], bv[0][0], DN_X6_ABL_CHAIN ? acc[m][0] : z);
       lo(0, 1);
       __builtin_amdgcn_sched_barrier(0);
       read_a(2); read_b(1);
@@ -549,12 +582,17 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
 #pragma unroll
       for (int m = 0; m < MTC; ++m)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[m][0][r] = acc[m][0][r] + hi[m][r];
+        for (int r = 0; r < 4; ++r) acc[m][0][r] = DN_X6_ABL_CHAIN ? hi[m][r] : acc[m][0][r] + hi[m][r];
+      pin_group(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (DN_X6P_DMAI) load_w_piece(wsrc, wslot, 0);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int g = 1; g < NG; ++g) {
         x6_group_c<MTC, NTW, QG>(acc, accl, av, bv, g * QG);
+        pin_group(g);
         __builtin_amdgcn_sched_barrier(0);
+        if (DN_X6P_DMAI && g < C::PPW) load_w_piece(wsrc, wslot, g);
         if (g + 2 < NG) read_b(g + 2);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -577,12 +615,15 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
       store_x();
       load_x((c + 2 < nch ? c + 2 : nch - 1) * C::KC);  // uniform count: re-load at the end
     }
-    load_w(st + C::S - 1 < nst ? st + C::S - 1 : nst - 1, (st + C::S - 1) % C::S);
+    constexpr bool DMAI = STAGED && DN_X6P_DMAI;
+    if (!DMAI) load_w(wsrc, wslot);
     // own DMAs of stage st+1 landed: issued after them are those of stages st+2, st+S-1 and the
     // next-but-one chunk's x loads when issued in this stage (xstep) or the previous one (a
     // chunk's first stage) -- the x loads are not waited for here
     // (stages 0 and 1: the prologue's chunk-1 x loads are younger than their DMAs)
-    if (xstep || (t == 0 && c > 0) || (c == 0 && t < 2))
+    // DMAI: a stage's weight DMAs precede its x loads, so the x loads of stage st-2 (a chunk's
+    // second stage, t == 1) are younger than stage st+1's DMAs too
+    if (xstep || (t == 0 && c > 0) || (DMAI && t == 1 && c > 0) || (c == 0 && t < 2))
       X6_WAITCNT_VM_LGKM0(C::PPW * (C::S - 2) + C::XITEMS);
     else
       X6_WAITCNT_VM_LGKM0(C::PPW * (C::S - 2));
@@ -619,8 +660,9 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
     fwd_epilogue<NT, C::MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
   }
 #if DN_X6_STAMPS
+  X6_STAMP(3 + 3 * nst);  // epilogue issued (stores in flight)
   __builtin_amdgcn_s_waitcnt(0);
-  X6_STAMP(2 + 3 * nst);
+  X6_STAMP(2 + 3 * nst);  // stores complete
 #endif
 }
 

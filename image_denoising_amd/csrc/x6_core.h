@@ -136,6 +136,9 @@ __device__ __forceinline__ void x6_block(f32x4 (&acc)[MT][NT], const bf16x8 (&av
 #ifndef DN_X6_CARRY
 #define DN_X6_CARRY 1
 #endif
+#ifndef DN_X6_ABL_CHAIN
+#define DN_X6_ABL_CHAIN 0
+#endif
 // fragment-group width of the carried form: one chain per fragment is enough (a single
 // 16x16x32 bf16 accumulation chain issues back-to-back, MI355X_MICROARCH.md), and the narrow
 // group keeps the hi temporaries and the B look-ahead small enough for the extra accl registers
@@ -152,6 +155,20 @@ __device__ __forceinline__ void x6_group_c(f32x4 (&acc)[MT][NT], f32x4 (&accl)[M
 #if DN_X6_CARRY
   const f32x4 z = {0.f, 0.f, 0.f, 0.f};
   constexpr int PA[5] = {0, 1, 0, 1, 2}, PB[5] = {1, 0, 2, 1, 0};
+#if DN_X6_ABL_CHAIN  // diagnostic ablation only (biased sums): the leading product chained into acc
+  (void)z;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int g = 0; g < QG; ++g) acc[m][q0 + g] = mfma_bf16(av[0][m], bv[0][q0 + g], acc[m][q0 + g]);
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int g = 0; g < QG; ++g)
+        accl[m][q0 + g] = mfma_bf16(av[PA[j]][m], bv[PB[j]][q0 + g], accl[m][q0 + g]);
+#else
   f32x4 hi[MT][QG];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
@@ -170,6 +187,7 @@ __device__ __forceinline__ void x6_group_c(f32x4 (&acc)[MT][NT], f32x4 (&accl)[M
     for (int g = 0; g < QG; ++g)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[m][q0 + g][r] = acc[m][q0 + g][r] + hi[m][g][r];
+#endif
 #else
   (void)accl;
   x6_group<MT, NT, QG>(acc, av, bv, q0);

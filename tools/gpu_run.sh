@@ -7,7 +7,7 @@
 #       quick           bench line without the CPU baseline            -> gpurun_out/quick.log
 #       stats:TAG       rocprofv3 --kernel-trace --stats over a 3-step bench -> gpurun_out/prof/TAG
 #       pmc:TAG[:ARGS]  FETCH_SIZE / WRITE_SIZE passes over a 2-step bench -> profiles/TAG_pmc_step.json
-#       stamps:K+N+H    k_c3x6p stage timeline from the DN_X6_STAMPS build (tools/x6_stamps.py)
+#       stamps:TAG:K+N+H  k_c3x6p stage timeline from a DN_X6_STAMPS build (tools/x6_stamps.py)
 #       sq:NAME:CTRS    one SQ counter pass (<= 8 SQ counters, '+'-separated) over a 2-step bench
 #       micro           tools/x6_micro.py (isolated 3x3 shapes)         -> gpurun_out/micro.log
 #       torchrun1       torchrun --nproc-per-node 1 bench (a one-rank RCCL group) -> gpurun_out/torchrun1.log
@@ -61,10 +61,11 @@ for step in "$@"; do
           -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $bargs > gpurun_out/pmc_step_$tag/$c.log 2>&1 || fail "$step $c" $?
       done
       python3 tools/pmc_step.py $tag gpurun_out/pmc_step_$tag || fail "$step summary" $? ;;
-    stamps)  # stamps:K+NOUT+H (needs libdenoise_hip_stamps.so, tools/x6_stamps.py)
-      DN_LIB_PATH=image_denoising_amd/libdenoise_hip_stamps.so timeout -k 10 120 python -u tools/x6_stamps.py ${arg//+/ } \
-        > gpurun_out/stamps_${arg//+/_}.log 2>&1 || fail "$step" $?
-      cat gpurun_out/stamps_${arg//+/_}.log | grep -v amdgpu.ids ;;
+    stamps)  # stamps:TAG:K+NOUT+H (a DN_X6_STAMPS=1 build libdenoise_hip_TAG.so, tools/x6_stamps.py)
+      tag=${arg%%:*}; shp=${arg#*:}
+      DN_LIB_PATH=image_denoising_amd/libdenoise_hip_$tag.so timeout -k 10 120 python -u tools/x6_stamps.py ${shp//+/ } \
+        > gpurun_out/stamps_${tag}_${shp//+/_}.log 2>&1 || fail "$step" $?
+      sed "s/^/$tag: /" gpurun_out/stamps_${tag}_${shp//+/_}.log | grep -v amdgpu.ids ;;
     sq)
       out=${arg%%:*}; ctrs=${arg#*:}; ctrs=${ctrs//+/ }
       rm -rf gpurun_out/pmc_sq/$out; mkdir -p gpurun_out/pmc_sq

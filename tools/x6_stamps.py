@@ -41,13 +41,15 @@ C = st[:, :, 2:2 + 3 * nst:3]
 E = st[:, :, 3:3 + 3 * nst:3]
 loop_end = st[:, :, 1 + 3 * nst]
 epi_end = st[:, :, 2 + 3 * nst]
+epi_issued = st[:, :, 3 + 3 * nst]
 start = st[:, :, 0]
 nxt = np.concatenate([A[:, :, 1:], loop_end[:, :, None]], axis=2)
 comp, tail, barw = C - A, E - C, nxt - E
 tile = epi_end - start
 print(f"k_c3x6p {K}->{NO} @{N}x{H}x{H}: {nst} stages, shader cycles (mean over 64 tiles x waves 0/4)")
 print(f"  tile {tile.mean():9.0f}   prologue {(A[:, :, 0] - start).mean():7.0f}   "
-      f"main loop {(loop_end - A[:, :, 0]).mean():9.0f}   epilogue {(epi_end - loop_end).mean():7.0f}")
+      f"main loop {(loop_end - A[:, :, 0]).mean():9.0f}   epilogue {(epi_end - loop_end).mean():7.0f} "
+      f"(issued {(epi_issued - loop_end).mean():7.0f}, store drain {(epi_end - epi_issued).mean():6.0f})")
 print(f"  per stage: compute {comp.mean():6.0f}  tail {tail.mean():5.0f}  barrier {barw.mean():5.0f}"
       f"  (stage {(nxt - A).mean():6.0f}; MFMA floor 2 waves x 72 x 16 = 2304)")
 for t in range(9):
