@@ -676,6 +676,231 @@ extern "C" int dn_debug_x6_stamps(unsigned long long* host, int n) {
 #endif
 
 // ------------------------------------------------------------------------------------
+// The N2N pair-pixel pass with 32-row tiles (k_c3x6s, launch_fwd_x6_sel): the 16-row SEL tile of
+// k_c3x6p has half the MFMAs of a full tile for the same x staging, barriers and weight DMAs per
+// stage (measured 0.34 of the bf16/6 ceiling against the full kernel's 0.47).  Here a 32 x 16
+// tile's 16 cell rows give every wave two M fragments (cell rows 2w, 2w+1) of all 96 channels,
+// as many MFMAs per stage as the full kernel; the 34-row x tile (117.5 KB, three planes) leaves
+// room for a 2-slot ring of unpadded 18 KiB weight stages: stage st+1's 18 DMA pieces (3 per
+// wave, the short waves repeating one) are issued during stage st, between its first fragment
+// groups, and waited for at its end.
+// ------------------------------------------------------------------------------------
+struct SCfg {
+  static constexpr int WAVES = 8, MT = 2, S = 2, NT = 6;
+  static constexpr int TW = 16, TH = 32, IH = TH + 2, IW = TW + 2, KC = 32, NP = 96;
+  static constexpr int XPIX = IH * IW;
+  static constexpr int XPL = XPIX * KC;
+  static constexpr int WPL = NP * KC;
+  static constexpr int WST = 3 * WPL;                 // bf16 per LDS stage (unpadded)
+  static constexpr int WSTP = x6_wst(NP);             // stage stride of the packed image
+  static constexpr int PIECES = WST * 2 / 1024;       // 18
+  static constexpr int PPW = (PIECES + WAVES - 1) / WAVES;
+  static_assert(PIECES * 1024 == WST * 2 && PPW == 3, "stage = 18 whole KiB pieces");
+  static constexpr int XQ = XPIX * (KC / 4);
+  static constexpr int XITEMS = (XQ + WAVES * 64 - 1) / (WAVES * 64);
+  static constexpr int PS = NP + 4;
+  static constexpr int LBYTES_MAIN = 2 * 3 * XPL + 2 * S * WST;
+  static constexpr int LEPI = 4 * WAVES * 16 * PS;
+  static constexpr int LBYTES = LBYTES_MAIN > LEPI ? LBYTES_MAIN : LEPI;
+  static_assert(LBYTES <= 163840, "one workgroup per CU");
+};
+
+__global__ __launch_bounds__(512, 1) void k_c3x6s(FwdArgs a) {
+  using C = SCfg;
+  constexpr int MT = C::MT, NT = C::NT;
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
+  __bf16* lx = reinterpret_cast<__bf16*>(lds_raw);
+  __bf16* ring = lx + 3 * C::XPL;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lg = lane >> 4;
+  const int tiles_x = (a.OW + C::TW - 1) / C::TW;
+  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
+  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
+  const int n = blockIdx.y;
+  const int iy0 = ty0 - 1, ix0 = tx0 - 1;
+  const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
+  const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp);
+  const int nch = a.K / C::KC;
+  const int nst = 9 * nch;
+
+  f32x4 acc[MT][NT], accl[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < NT; ++q) acc[m][q] = accl[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // x-tile pixel of this lane's row of fragment m: tile cell row 2w + m, cell j = li / 2, pair
+  // member s = li % 2 at pair[rd][s] of the cell (train.py:151-154)
+  int selpix[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int lc = 2 * wave + m;
+    const int ci = ty0 / 2 + lc, cj = tx0 / 2 + (li >> 1);
+    const int r = (ci < a.OH / 2 && cj < a.OW / 2)
+                      ? a.sel_rd[((long)n * (a.OH / 2) + ci) * (a.OW / 2) + cj] & 7 : 0;
+    constexpr unsigned kPair = 0xB721ED84u;  // 4 bits (a | b << 2) per rd
+    const int k = (kPair >> (4 * r + 2 * (li & 1))) & 3;
+    selpix[m] = (2 * lc + (k >> 1)) * C::IW + 2 * (li >> 1) + (k & 1);
+  }
+
+  // x tile rows through a 32-bit buffer resource (see k_c3x6p)
+  const int ry0 = iy0 > 0 ? iy0 : 0, ry1 = iy0 + C::IH < a.IHt ? iy0 + C::IH : a.IHt;
+  const long row_floats = (long)a.IWt * a.in_stride;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(inb + ry0 * row_floats), (short)0,
+      (int)((ry1 - ry0) * row_floats * 4), 0x00020000);
+  f32x4 xr[C::XITEMS];
+  auto load_x = [&](int k0) {
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * C::WAVES * 64;
+      const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+      const int iy = pix / C::IW, ix = pix - iy * C::IW;
+      const int gy = iy0 + iy, gx = ix0 + ix, k = k0 + 4 * q;
+      const bool ok = e < C::XQ && gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt && k < a.K;
+      const int off = ok ? (((gy - ry0) * a.IWt + gx) * a.in_stride + k) * 4 : 0x7fffffff;
+      xr[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int it = 0; it < C::XITEMS; ++it) {
+      const int e = tid + it * C::WAVES * 64;
+      if (e < C::XQ) {
+        const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+        const float f[4] = {xr[it][0], xr[it][1], xr[it][2], xr[it][3]};
+        bf16x4 h, m, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          __bf16 hj, mj, lj;
+          split3(f[j], hj, mj, lj);
+          h[j] = hj; m[j] = mj; l[j] = lj;
+        }
+        const int off = pix * C::KC + x6_swz(pix, q >> 1) * 8 + (q & 1) * 4;
+        *reinterpret_cast<bf16x4*>(lx + off) = h;
+        *reinterpret_cast<bf16x4*>(lx + C::XPL + off) = m;
+        *reinterpret_cast<bf16x4*>(lx + 2 * C::XPL + off) = l;
+      }
+    }
+  };
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__bf16*>(wimg), (short)0, nst * C::WSTP * 2, 0x00020000);
+  // piece j of stage src_st into slot `slot`: pieces w, w + 8, w + 16 (waves 2..7 repeat w + 8:
+  // the same bytes to the same place), so every wave issues PPW DMAs per stage
+  auto load_w_piece = [&](int src_st, int slot, int j) {
+    int piece = wave + j * C::WAVES;
+    if (piece >= C::PIECES) piece -= C::WAVES;
+    unsigned char* dst = reinterpret_cast<unsigned char*>(ring + slot * C::WST);
+    buf_lds16(wrs, dst + piece * 1024, src_st * C::WSTP * 2 + piece * 1024 + lane * 16);
+  };
+
+  // prologue: stage 0's weights, chunk 0's x tile into LDS, chunk 1's x into registers
+#pragma unroll
+  for (int j = 0; j < C::PPW; ++j) load_w_piece(0, 0, j);
+  load_x(0);
+  store_x();
+  load_x((nch > 1 ? 1 : 0) * C::KC);
+  X6_WAITCNT_VM(C::XITEMS);            // own stage-0 DMAs landed (older than the x loads)
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
+  x6_barrier();
+
+  constexpr int NG = NT;  // fragment groups of one B fragment (carried form, QG = 1)
+#pragma unroll 1
+  for (int st = 0; st < nst; ++st) {
+    const int c = st / 9, t = st - 9 * c;
+    const bool more = c + 1 < nch;
+    const int ky = t / 3, kx = t - 3 * ky;
+    const __bf16* lw = ring + (st % C::S) * C::WST;
+    const int wsrc = st + 1 < nst ? st + 1 : nst - 1, wslot = (st + 1) % C::S;
+    bf16x8 av[3][MT], bv[3][NT];
+    auto read_a = [&](int p) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int pix = selpix[m] + ky * C::IW + kx;
+        av[p][m] = *reinterpret_cast<const bf16x8*>(lx + p * C::XPL + pix * C::KC + x6_swz(pix, lg) * 8);
+      }
+    };
+    auto read_b = [&](int q) {
+      const int row = q * 16 + li;
+      const int off = row * C::KC + x6_swz(row, lg) * 8;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bv[p][q] = *reinterpret_cast<const bf16x8*>(lw + p * C::WPL + off);
+    };
+    auto read_bp = [&](int p) {
+      const int off = li * C::KC + x6_swz(li, lg) * 8;
+      bv[p][0] = *reinterpret_cast<const bf16x8*>(lw + p * C::WPL + off);
+    };
+    auto lo = [&](int pa, int pb) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) accl[m][0] = mfma_bf16(av[pa][m], bv[pb][0], accl[m][0]);
+    };
+    auto pin_group = [&](int g) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) asm volatile("" : "+v"(acc[m][g]));
+    };
+    // group 0 as a read/compute pipeline (k_c3x6p's STAGED order), then groups 1..5 with B read
+    // two groups ahead; the next stage's DMA pieces after groups 0, 1, 2
+    read_a(0); read_bp(0); read_bp(1);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(1); read_bp(2);
+    __builtin_amdgcn_sched_barrier(0);
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    f32x4 hi[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) hi[m] = mfma_bf16(av[0][m], bv[0][0], z);
+    lo(0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(2); read_b(1);
+    __builtin_amdgcn_sched_barrier(0);
+    lo(1, 0); lo(0, 2); lo(1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    read_b(2);
+    __builtin_amdgcn_sched_barrier(0);
+    lo(2, 0);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[m][0][r] = acc[m][0][r] + hi[m][r];
+    pin_group(0);
+    __builtin_amdgcn_sched_barrier(0);
+    load_w_piece(wsrc, wslot, 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 1; g < NG; ++g) {
+      x6_group_c<MT, NT, 1>(acc, accl, av, bv, g);
+      pin_group(g);
+      __builtin_amdgcn_sched_barrier(0);
+      if (g < C::PPW) load_w_piece(wsrc, wslot, g);
+      if (g + 2 < NG) read_b(g + 2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const bool xstep = t == 8 && more;
+    if (xstep) {
+      x6_barrier();  // every wave is done with this chunk's x tile
+      store_x();
+      load_x((c + 2 < nch ? c + 2 : nch - 1) * C::KC);  // uniform count: re-load at the end
+    }
+    // own DMAs of stage st+1 landed (issued in this stage); the x loads issued after them (an
+    // xstep) are not waited for -- those of the previous xstep are (one stage after their issue)
+    if (xstep)
+      X6_WAITCNT_VM_LGKM0(C::XITEMS);
+    else
+      X6_WAITCNT_VM_LGKM0(0);
+    if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
+    x6_barrier();
+  }
+  X6_WAITCNT_VM(0);  // trailing re-load DMAs / x loads land before the LDS is reused
+  x6_barrier();
+  x6_fold(acc, accl);
+  // the pair image: OH/2 rows, row ty0/2 + 2w + m (the epilogue places wave w's rows at its ty0
+  // argument + w*MT + m), all 96 channels
+  FwdArgs ap = a;
+  ap.OH = a.OH / 2;
+  fwd_epilogue<NT, MT, C::PS, false>(ap, acc, reinterpret_cast<float*>(lds_raw), ty0 / 2, tx0, n);
+}
+
+// ------------------------------------------------------------------------------------
 // Two-workgroups-per-CU variant for large grids (k_c3x6h): 4 waves on an 8 x 16 x 16*NT tile
 // (wave w: rows 2w, 2w+1), 70 KB of LDS (the x tile's three planes + a 2-slot ring of unpadded
 // 18 KiB weight stages), so two workgroups share a CU and one's prologue (x tile from HBM) and
@@ -1231,6 +1456,14 @@ hipError_t launch_fwd_x6_sel(const FwdArgs& a, hipStream_t s) {
       a.out_layout != OUT_NHWC || a.epi != EPI_BIAS_ACT || (a.OH | a.OW) & 1 ||
       ((a.in_stride | a.in_off) & 3) || (long)C::IH * a.IWt * a.in_stride * 4 >= 0x7fffffffL)
     return hipErrorInvalidValue;
+  // 32-row tiles (k_c3x6s) unless DN_X6_SEL32=0 (the 16-row k_c3x6p<6,0,true>, A/B)
+  static const bool sel32_env = !getenv("DN_X6_SEL32") || atoi(getenv("DN_X6_SEL32")) != 0;
+  if (sel32_env && (long)SCfg::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL) {
+    const int tx = (a.OW + SCfg::TW - 1) / SCfg::TW, ty = (a.OH + SCfg::TH - 1) / SCfg::TH;
+    prof_kernel("k_c3x6s");
+    hipLaunchKernelGGL(k_c3x6s, dim3(tx * ty, a.N, 1), dim3(SCfg::WAVES * 64), 0, s, a);
+    return hipGetLastError();
+  }
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
   prof_kernel("k_c3x6p<6,0,true>");
   hipLaunchKernelGGL((k_c3x6p<6, 0, true>), dim3(tx * ty, a.N, 1), dim3(C::WAVES * 64), 0, s, a);
