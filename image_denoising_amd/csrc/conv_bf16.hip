@@ -15,6 +15,7 @@
 //   8-element operand (k = 8*(lane>>4) .. +7) is one ds_read_b128.
 #include <cstdlib>
 
+#include "conv_epi.h"
 #include "dn_internal.h"
 
 namespace dn {
@@ -56,50 +57,6 @@ __device__ __forceinline__ void blds16b(__amdgpu_buffer_rsrc_t rs, void* l, int 
 #else
   (void)rs; (void)l; (void)voffset;
 #endif
-}
-
-// epilogue: stage each 16-pixel row through LDS, write whole pixels as float4 (NHWC; OUT_UP2:
-// the deconv parity scatter of blockIdx.z)
-template <int NT, int MT, int PS>
-__device__ __forceinline__ void bf_epilogue(const FwdArgs& a, const f32x4b (&acc)[MT][NT],
-                                            unsigned char* lds_raw, int ty0, int tx0, int n,
-                                            int wave, int lane) {
-  const int li = lane & 15, lg = lane >> 4;
-  float* stg = reinterpret_cast<float*>(lds_raw) + wave * 16 * PS;
-  const int NQ = a.NOUT >> 2;
-#pragma unroll
-  for (int m = 0; m < MT; ++m) {
-#pragma unroll
-    for (int q = 0; q < NT; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) stg[(4 * lg + r) * PS + q * 16 + li] = acc[m][q][r];
-    __syncthreads();
-    const int gy = ty0 + wave * MT + m;
-    if (gy < a.OH) {
-      for (int e = lane; e < 16 * NQ; e += 64) {
-        const int p = e / NQ, cc = 4 * (e - p * NQ);
-        const int gx = tx0 + p;
-        if (gx >= a.OW) continue;
-        float4 v = *reinterpret_cast<const float4*>(stg + p * PS + cc);
-        const float4 b = *reinterpret_cast<const float4*>(a.bias + cc);
-        v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
-        if (a.epi == EPI_BIAS_ACT) {
-          v.x = v.x > 0.f ? v.x : v.x * 0.2f; v.y = v.y > 0.f ? v.y : v.y * 0.2f;
-          v.z = v.z > 0.f ? v.z : v.z * 0.2f; v.w = v.w > 0.f ? v.w : v.w * 0.2f;
-        }
-        long oi;
-        if (a.out_layout == OUT_UP2) {  // ConvTranspose2d(2,2) scatter: pixel (2y+a, 2x+b)
-          const int ab = (int)blockIdx.z;
-          oi = (((long)n * 2 * a.OH + 2 * gy + (ab >> 1)) * 2 * a.OW + 2 * gx + (ab & 1)) *
-                   a.out_stride + a.out_off + cc;
-        } else {
-          oi = (((long)n * a.OH + gy) * a.OW + gx) * a.out_stride + a.out_off + cc;
-        }
-        *reinterpret_cast<float4*>(a.out + oi) = v;
-      }
-    }
-    __syncthreads();
-  }
 }
 
 template <int NT, int MT, bool K3>
@@ -206,7 +163,9 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16(FwdArgs a) {
     __syncthreads();  // next stage's weights landed (vmcnt(0)), next x tile written
   }
 
-  bf_epilogue<NT, MT, C::PS>(a, acc, lds_raw, ty0, tx0, n, wave, lane);
+  // the shared LDS-staged epilogue (conv_epi.h): loads of all rows before any store, no
+  // per-row barriers (each wave stages its own rows)
+  fwd_epilogue<NT, MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
 }
 
 // ------------------------------------------------------------------------------------
@@ -344,7 +303,9 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16p(FwdArgs a) {
     bf_barrier();
   }
   __syncthreads();
-  bf_epilogue<NT, MT, C::PS>(a, acc, lds_raw, ty0, tx0, n, wave, lane);
+  // the shared LDS-staged epilogue (conv_epi.h): loads of all rows before any store, no
+  // per-row barriers (each wave stages its own rows)
+  fwd_epilogue<NT, MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
 }
 
 // bf16 weight image: [chunk][ky][kx][n][WS] (k = chunk*32 + kk for kk < 32; zero padded), each

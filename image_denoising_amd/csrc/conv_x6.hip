@@ -938,6 +938,9 @@ struct HCfg {
 #ifndef DN_X6H_CARRY
 #define DN_X6H_CARRY 1  // A/B switch: 0 = per-block sums in k_c3x6h
 #endif
+#ifndef DN_X6H_PIN
+#define DN_X6H_PIN 1  // A/B switch: 0 = MT = 2's hi adds left to the compiler (sunk to the stage end)
+#endif
 template <int NT, int TAIL, int MT_ = 2>
 __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
   using C = HCfg<NT, MT_>;
@@ -1120,7 +1123,7 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
         // MT = 4 keeps the per-block form: its 2 x 48 accumulators leave no room for accl
         if constexpr (MT >= 4 || !DN_X6H_CARRY) x6_group<MH, NT, QG>(acch, av, bv, g * QG);
         else x6_group_c<MH, NT, QG>(acch, acclh, av, bv, g * QG);
-        if constexpr (MT >= 4) {  // the block sums' adds here, not deferred (live MFMA results)
+        if constexpr (MT >= 4 || DN_X6H_PIN) {  // the block sums' adds here, not sunk to the stage end
 #pragma unroll
           for (int i = 0; i < MH; ++i)
 #pragma unroll

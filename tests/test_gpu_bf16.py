@@ -13,6 +13,9 @@ DEV = "cuda"
 # fp32 ulp of a bf16 rounding boundary and rounds the other way (2^-8 relative on that element,
 # which reaches the output attenuated but, with ~1e6 activations per layer, not rarely)
 EMU_TOL = 1e-2
+# ... and element by element: a flip moves few outputs, so all but a small fraction of the
+# elements must agree to 1e-3 of max |y| (an indexing error confined to a region would not)
+EMU_ELEM_TOL, EMU_ELEM_FRAC = 1e-3, 2e-3
 # vs the fp32 reference: the bf16 rounding itself (8-bit mantissa) through ~20 layers
 FP32_TOL = 5e-2
 
@@ -21,6 +24,18 @@ def rel_err(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def assert_emulation_match(y, emu):
+    """max error within EMU_TOL and at most EMU_ELEM_FRAC of the elements beyond EMU_ELEM_TOL
+    (both relative to max |emu|)"""
+    y = np.asarray(y, dtype=np.float64)
+    emu = np.asarray(emu, dtype=np.float64)
+    scale = max(np.abs(emu).max(), 1e-30)
+    d = np.abs(y - emu) / scale
+    frac = float((d > EMU_ELEM_TOL).mean())
+    assert d.max() < EMU_TOL, d.max()
+    assert frac <= EMU_ELEM_FRAC, (frac, d.max())
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -45,7 +60,7 @@ def test_unet_bf16_forward_vs_emulation(C, shape):
     with torch.no_grad():
         emu = unet_ref.forward(flat, x.double(), C, C, bf16_3x3=True)
         ref = unet_ref.forward(flat, x.double(), C, C)
-    assert rel_err(y.numpy(), emu.numpy()) < EMU_TOL
+    assert_emulation_match(y.numpy(), emu.numpy())
     assert rel_err(y.numpy(), ref.numpy()) < FP32_TOL
     # and the fp32 path stays the fp32 path
     net.set_inference_precision("fp32")
@@ -108,9 +123,9 @@ def test_config4_full_size_finetune_step_properties():
     with torch.no_grad():
         emu = unet_ref.forward(base.flat_params.cpu().double(), noisy[:1].double(), 1, 1,
                                bf16_3x3=True).float()
-    assert rel_err(b["base"][:1].cpu().numpy(), emu.numpy()) < EMU_TOL
+    assert_emulation_match(b["base"][:1].cpu().numpy(), emu.numpy())
     pred = adapter_ref.adapter_forward(a0, noisy[:1], emu)
-    assert rel_err(b["pred"][:1].cpu().numpy(), pred.detach().numpy()) < EMU_TOL
+    assert_emulation_match(b["pred"][:1].cpu().numpy(), pred.detach().numpy())
 
 
 def _conv_bf16(x, w, b, act, x_stride=None):

@@ -4,7 +4,7 @@
 #                                              the first failure ends the call (no retries)
 # STEP: tests[:FILES]   pytest -m gpu (all, or comma-separated files)  -> gpurun_out/pytest_gpu.log
 #       bench           default bench line, CPU baseline included      -> gpurun_out/bench.log
-#       quick           bench line without the CPU baseline            -> gpurun_out/quick.log
+#       quick[:ARGS]    bench line without the CPU baseline ('+'-separated bench args) -> gpurun_out/quick.log
 #       stats:TAG       rocprofv3 --kernel-trace --stats over a 3-step bench -> gpurun_out/prof/TAG
 #       pmc:TAG[:ARGS]  FETCH_SIZE / WRITE_SIZE passes over a 2-step bench -> profiles/TAG_pmc_step.json
 #       stamps:TAG:K+N+H  k_c3x6p stage timeline from a DN_X6_STAMPS build (tools/x6_stamps.py)
@@ -46,7 +46,7 @@ for step in "$@"; do
       timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2>&1 || fail "$step" $?
       grep '^{' gpurun_out/bench.log | cut -c1-400 ;;
     quick)
-      timeout -k 10 240 python -u bench.py --no-cpu-baseline ${arg//,/ } > gpurun_out/quick.log 2>&1 || fail "$step" $?
+      timeout -k 10 240 python -u bench.py --no-cpu-baseline ${arg//+/ } > gpurun_out/quick.log 2>&1 || fail "$step" $?
       grep '^{' gpurun_out/quick.log | cut -c1-400 ;;
     stats)
       rm -rf gpurun_out/prof/$arg; mkdir -p gpurun_out/prof
@@ -55,7 +55,7 @@ for step in "$@"; do
       summ_stats gpurun_out/prof/$arg ;;
     pmc)  # pmc:TAG[:bench args, '+'-separated]
       tag=${arg%%:*}; bargs=${arg#*:}; [ "$bargs" = "$arg" ] && bargs=""; bargs=${bargs//+/ }
-      rm -rf gpurun_out/pmc_step_$tag
+      rm -rf gpurun_out/pmc_step_$tag; mkdir -p gpurun_out/pmc_step_$tag
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 200 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc_step_$tag/$c -o run \
           -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $bargs > gpurun_out/pmc_step_$tag/$c.log 2>&1 || fail "$step $c" $?
@@ -68,7 +68,7 @@ for step in "$@"; do
       sed "s/^/$tag: /" gpurun_out/stamps_${tag}_${shp//+/_}.log | grep -v amdgpu.ids ;;
     sq)
       out=${arg%%:*}; ctrs=${arg#*:}; ctrs=${ctrs//+/ }
-      rm -rf gpurun_out/pmc_sq/$out; mkdir -p gpurun_out/pmc_sq
+      rm -rf gpurun_out/pmc_sq/$out; mkdir -p gpurun_out/pmc_sq/$out
       timeout -s KILL 200 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d gpurun_out/pmc_sq/$out -o run \
         -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ${SQ_ARGS:-} > gpurun_out/pmc_sq/$out.log 2>&1 || fail "$step" $?
       # (SQ_ARGS: extra bench arguments, e.g. SQ_ARGS="--mode finetune --precision bf16")
