@@ -457,7 +457,7 @@ def main():
         elapsed = float(t)
     loss_v = loss.cpu().tolist()
     # one profiled pair of steps after the timed region, on EVERY rank (the step all-reduces)
-    recs, reps = step_profile(step) if not iu else ([], 1)
+    recs, reps = step_profile(step)
 
     if args.breakdown and rank == 0 and args.mode == "n2n":
         breakdown(tr, clean, device)
@@ -484,7 +484,7 @@ def main():
             mode_tag = ("bf16" if bf else args.mode) + ("_iunet" if iu else "") + \
                 (f"_c{C}" if C != 1 else "")
             traffic, traffic_src = pmc_step_traffic(dom["kernel"], mode_tag)
-        else:  # no instrumented executor (ImprovedUNet): the isolated 96->96 shape
+        else:  # no 3x3 launch recorded: the isolated 96->96 shape
             timer = (time_dominant_kernel_bf16 if bf else
                      time_dominant_kernel_x6 if x6 else time_dominant_kernel)
             kms, kflops = timer(bs, H, H, device)

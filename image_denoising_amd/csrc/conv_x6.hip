@@ -939,7 +939,7 @@ struct HCfg {
 #define DN_X6H_CARRY 1  // A/B switch: 0 = per-block sums in k_c3x6h
 #endif
 #ifndef DN_X6H_PIN
-#define DN_X6H_PIN 1  // A/B switch: 0 = MT = 2's hi adds left to the compiler (sunk to the stage end)
+#define DN_X6H_PIN 0  // A/B switch: 1 = MT = 2's hi adds pinned per group (100->96 @256^2: 1-2 % slower)
 #endif
 template <int NT, int TAIL, int MT_ = 2>
 __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
@@ -1765,9 +1765,9 @@ int wgrad_splits_x6(const WgradArgs& a, int splits) {
 }
 
 template <int CO_FR, int WM, int WN>
-static hipError_t run_wgrad3s(const WgradArgs& a, int splits, hipStream_t s) {
+static hipError_t run_wgrad3s(const WgradArgs& a, int splits, hipStream_t s, int nz = 1) {
   using C = Ws3Cfg<CO_FR, WM, WN>;
-  const dim3 grid(splits, (a.Cin + C::CIB - 1) / C::CIB, 1), block(C::NTHR);
+  const dim3 grid(splits, (a.Cin + C::CIB - 1) / C::CIB, nz), block(C::NTHR);
   static const std::string kn[3] = {x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "3"),
                                     x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "4"),
                                     x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "5")};
@@ -1781,6 +1781,53 @@ static hipError_t run_wgrad3s(const WgradArgs& a, int splits, hipStream_t s) {
 hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s) {
   if (!wgrad3_x6_ok(a)) return hipErrorInvalidValue;
   return a.Cout == 96 ? run_wgrad3s<6, 2, 2>(a, splits, s) : run_wgrad3s<3, 1, 3>(a, splits, s);
+}
+
+// The blocked 3x3 weight gradient (the ImprovedUNet executor: any Cout, output-channel blocks of
+// 96 / 48 / 32 over blockIdx.z, as launch_gwgrad) on the bf16x6 kernel.  32-wide blocks (the RDB
+// growth convs, the 24-channel level) take 32 / 48 / 64 input channels per workgroup, whichever
+// pads Cin least; every block of a layer uses the same split count.
+static int gw6_block(int cout) { return cout <= 32 ? 32 : (cout <= 48 ? 48 : 96); }
+static int gw6_cib(int cb, int Cin) {
+  if (cb == 96) return 32;
+  if (cb == 48) return 48;
+  int best = 48;
+  long pad = 1L << 30;
+  for (int t : {64, 48, 32}) {
+    const long p = (long)(Cin + t - 1) / t * t;
+    if (p < pad) { pad = p; best = t; }
+  }
+  return best;
+}
+
+bool gwgrad_x6_ok(const WgradArgs& a) {
+  if (a.Cin < 16 || a.KW < 8 || !a.zeros || a.zc > 0) return false;
+  if ((a.g_stride | a.g_off | a.x_stride | a.x_off) & 3) return false;
+  return a.x_off + ((a.Cin + 3) & ~3) <= a.x_stride && a.g_off + ((a.Cout + 3) & ~3) <= a.g_stride;
+}
+
+// split count of the x6 launch: at most `splits` (what the slab was sized for), and splits x
+// input-channel blocks x output blocks within one round of 512 resident workgroups
+int gwgrad_x6_splits(const WgradArgs& a, int splits) {
+  const int cb = gw6_block(a.Cout), nz = (a.Cout + cb - 1) / cb;
+  const int cib = gw6_cib(cb, a.Cin);
+  const int cap = 512 / (nz * ((a.Cin + cib - 1) / cib));
+  return splits < cap ? splits : (cap < 1 ? 1 : cap);
+}
+
+hipError_t launch_gwgrad_x6(const WgradArgs& a0, int splits, hipStream_t s) {
+  if (!gwgrad_x6_ok(a0)) return hipErrorInvalidValue;
+  const int cb = gw6_block(a0.Cout), nz = (a0.Cout + cb - 1) / cb;
+  WgradArgs a = a0;
+  a.zc = cb;
+  a.cout_total = a0.Cout;
+  a.co_base = 0;
+  if (cb == 96) return run_wgrad3s<6, 2, 2>(a, splits, s, nz);
+  if (cb == 48) return run_wgrad3s<3, 1, 3>(a, splits, s, nz);
+  const int ct = gw6_cib(cb, a.Cin);
+  if (ct == 64) return run_wgrad3s<2, 1, 4>(a, splits, s, nz);
+  if (ct == 32) return run_wgrad3s<2, 1, 2>(a, splits, s, nz);
+  return run_wgrad3s<2, 1, 3>(a, splits, s, nz);
 }
 
 // ------------------------------------------------------------------------------------

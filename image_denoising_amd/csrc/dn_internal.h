@@ -309,6 +309,10 @@ bool fwd_supported(int gather, int nout);
 int gwgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout);
 bool gwgrad_ok(int mode, int Cin, int Cout, const View& g, const View& x);
 hipError_t launch_gwgrad(int mode, const WgradArgs& a, int splits, hipStream_t s);
+// the same 3x3 weight gradient on the bf16x6 kernel (conv_x6.hip)
+bool gwgrad_x6_ok(const WgradArgs& a);
+int gwgrad_x6_splits(const WgradArgs& a, int splits);
+hipError_t launch_gwgrad_x6(const WgradArgs& a, int splits, hipStream_t s);
 bool wgrad_supported(int mode, int cout, int cin);
 
 // ---- elementwise launchers (elementwise.hip) ----

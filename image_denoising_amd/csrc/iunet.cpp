@@ -78,6 +78,11 @@ bool ggeom(int ksize, int K, int nout, GGeom& g) {
 bool x6_shape(int nout) { return nout == 32 || nout % 48 == 0; }
 bool x6_takes(int K, int nout, int tail) {
   if (nout == 32 && K < 80) return false;  // 32-wide tiles: staging-bound, no gain (32x48, 32x56)
+  // 32-wide RDB growth convs with K >= 80 take a zero-padded last chunk when it cannot be
+  // tail-packed (88, 120: 3 / 4 chunks, 9 / 7 % padding; on the fp32 kernel they ran at ~60 %
+  // of the x6 rate of their 80- / 112-channel neighbours); DN_IU_X6_PAD32=0 keeps them on fp32
+  static const bool pad32 = !getenv("DN_IU_X6_PAD32") || atoi(getenv("DN_IU_X6_PAD32")) != 0;
+  if (pad32 && nout == 32 && K % 4 == 0) return true;
   return x6_shape(nout) && (K % 32 == 0 || K >= 128 || tail) && (K > 32 || nout % 96 == 0);
 }
 // output-channel blocks of the wide layers: 96, or 48 where 96 would pad (144 = 3 x 48)
@@ -416,11 +421,24 @@ struct OpProf {
 };
 OpProf g_prof;
 
+// dn_profile_ops op name of an OpScope kind ("fwd" + k = 3 -> "fwd3", the bench's 3x3 ops)
+inline const char* prof_op(const char* kind, int k) {
+  const std::string kd(kind);
+  if (kd == "fwd") return k == 3 ? "fwd3" : "fwd1";
+  if (kd == "wgrad") return k == 3 ? "wgrad3" : "wgrad1";
+  if (kd == "dgrad") return k == 3 ? "dgrad3" : "dgrad1";
+  return kind;
+}
+
 struct OpScope {
   hipStream_t s;
   bool on;
+  OpTimer timer;  // the in-step launch record (dn_profile_ops), when enabled
   OpScope(hipStream_t st, const char* kind, int cout, int cin, int k, int h, int w, int N,
-          double flop_mult) : s(st), on(g_prof.on) {
+          double flop_mult)
+      : s(st), on(g_prof.on),
+        timer(st, prof_op(kind, k), flop_mult * 2.0 * N * h * w * (double)cout * cin * k * k,
+              cin, cout, h, w, N) {
     if (!on) return;
     char b[128];
     snprintf(b, sizeof(b), "%-6s %dx%d k%d @%dx%d", kind, cout, cin, k, h, w);
@@ -592,9 +610,16 @@ dn_status wgrad_g(const Ctx& c, float* dprm, int mode, const IConv& L, const Vie
   a.N = c.p.N; a.KH = h; a.KW = w; a.Cout = L.cout; a.Cin = L.cin;
   a.zeros = slab; a.slab = slab + 64; a.slab_stride = n;
   a.wlayout = 0; a.cin_total = L.cin; a.ci_base = 0; a.bias = bias ? 1 : 0;
-  const int sp = gwgrad_splits(mode, c.p.N, h, w, L.cin, L.cout);
+  int sp = gwgrad_splits(mode, c.p.N, h, w, L.cin, L.cout);
   IU_TRY(hipMemsetAsync(slab, 0, 64 * sizeof(float), c.s));
-  IU_TRY(launch_gwgrad(mode, a, sp, c.s));
+  // fp32_x6: the 3x3 weight gradients on the bf16x6 kernel too (DN_IU_X6_WGRAD=0: fp32, A/B)
+  static const bool x6w_env = !getenv("DN_IU_X6_WGRAD") || atoi(getenv("DN_IU_X6_WGRAD")) != 0;
+  if (x6w_env && c.prec == DN_PREC_FP32_X6 && mode == W_C3 && gwgrad_x6_ok(a)) {
+    sp = gwgrad_x6_splits(a, sp);
+    IU_TRY(launch_gwgrad_x6(a, sp, c.s));
+  } else {
+    IU_TRY(launch_gwgrad(mode, a, sp, c.s));
+  }
   IU_TRY(launch_reduce(slab + 64, n, sp, n, dprm + L.w, c.s));
   return DN_OK;
 }
