@@ -189,23 +189,32 @@ def per_shape_roofline(recs, reps, peak):
     HIP-event ms, algorithmic FLOPs per launch (SEL: the pair pixels it computes) and the fraction
     of `peak`; plus the time-weighted fraction over all of them and the per-op step breakdown"""
     groups = {}
+    seen = {}  # launches of each kernel so far: a record's position in its kernel's sequence
+    per_kernel = {}
     for r in recs:
+        per_kernel[r["kernel"]] = per_kernel.get(r["kernel"], 0) + 1
+    for r in recs:
+        i = seen.get(r["kernel"], 0)
+        seen[r["kernel"]] = i + 1
         if r["op"] not in THREE_BY_THREE:
             continue
         k = (r["op"], r["K"], r["NOUT"], r["H"], r["W"], r["N"], r["kernel"])
-        g = groups.setdefault(k, [0, 0.0, 0.0])
+        g = groups.setdefault(k, [0, 0.0, 0.0, set()])
         g[0] += 1
         g[1] += r["ms"]
         g[2] += r["flops"]
+        g[3].add(i % max(1, per_kernel[r["kernel"]] // reps))
     shapes = []
-    for (op, K, NO, H, W, N, kern), (n, ms, fl) in groups.items():
+    for (op, K, NO, H, W, N, kern), (n, ms, fl, pos) in groups.items():
         tf = fl / (ms * 1e-3) / 1e12
         # HBM bytes the launch must move: input + output activations (fp32), weights aside
         alg_bytes = N * H * W * (K + NO) * 4.0
         shapes.append({"op": op, "kernel": kern, "shape": f"{K}->{NO} @{N}x{H}x{W}",
                        "launches_per_step": n / reps, "avg_launch_ms": round(ms / n, 4),
                        "flops_per_launch": fl / n, "tflops": round(tf, 2), "frac": round(tf / peak, 4),
-                       "ms_per_step": round(ms / reps, 4), "algorithmic_bytes_per_launch": alg_bytes})
+                       "ms_per_step": round(ms / reps, 4), "algorithmic_bytes_per_launch": alg_bytes,
+                       "alg_gbs": round(alg_bytes / (ms / n * 1e-3) / 1e9, 1),
+                       "_positions": sorted(pos), "_kernel_per_step": per_kernel[kern] // reps})
     shapes.sort(key=lambda d: -d["ms_per_step"])
     tot_ms = sum(d["ms_per_step"] for d in shapes)
     tot_fl = sum(d["flops_per_launch"] * d["launches_per_step"] for d in shapes)
@@ -217,19 +226,28 @@ def per_shape_roofline(recs, reps, peak):
     return shapes, weighted, tot_ms, {k: round(v, 4) for k, v in sorted(by_op.items(), key=lambda kv: -kv[1])}, executed
 
 
-def pmc_step_traffic(kernel, mode_tag):
-    """HBM bytes per launch of `kernel` inside the bench step, from the committed rocprofv3 PMC
+def pmc_step_traffic(shape, mode_tag):
+    """HBM bytes per launch of the dominant in-step shape, from the committed rocprofv3 PMC
     summaries profiles/<round>_<mode_tag>_pmc_step.json (tools/gpu_run.sh pmc: separate
-    FETCH_SIZE / WRITE_SIZE passes over this bench configuration; gfx950 x2 FETCH correction),
-    newest round first; (None, None) if no summary holds the kernel"""
+    FETCH_SIZE / WRITE_SIZE passes over this bench configuration, one stream; gfx950 x2 FETCH
+    correction), newest round first.  The shape's launches are picked out of the summary's last
+    step by their positions in the kernel's launch sequence (the dn_profile_ops order); a summary
+    without per-launch bytes, or whose launch count does not fit, gives the kernel's mean over
+    all its shapes.  Returns (bytes, source, "shape" | "kernel mean") or (None, None, None)."""
     import glob
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{mode_tag}_pmc_step.json")), reverse=True)
     for f in files:
-        k = json.load(open(f)).get("kernels", {}).get(kernel)
-        if k:
-            return k["traffic_bytes"], os.path.relpath(f, ROOT)
-    return None, None
+        k = json.load(open(f)).get("kernels", {}).get(shape["kernel"])
+        if not k:
+            continue
+        per, n = k.get("per_launch_bytes"), shape["_kernel_per_step"]
+        if per and n and len(per) >= n and max(shape["_positions"]) < n:
+            last = per[len(per) - n:]
+            sel = [last[i] for i in shape["_positions"]]
+            return sum(sel) / len(sel), os.path.relpath(f, ROOT), "shape"
+        return k["traffic_bytes"], os.path.relpath(f, ROOT), "kernel mean"
+    return None, None, None
 
 
 def pmc_traffic(tag=""):
@@ -376,6 +394,9 @@ def main():
     ap.add_argument("--arch", choices=["UNet", "UNetImproved"], default="UNet",
                     help="network (train.py:305-313 / finetune.py --arch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-eval", action="store_true",
+                    help="skip the eval-PSNR leg (and the CPU baseline that shares its image): "
+                         "under rocprofv3 --pmc the profiled step pair is then the run's last launches")
     ap.add_argument("--breakdown", action="store_true", help="per-phase HIP-event timing (stderr)")
     args = ap.parse_args()
 
@@ -483,14 +504,19 @@ def main():
             kdesc = f"{dom['kernel']} {dom['op']} {dom['shape']} (in-step launch)"
             mode_tag = ("bf16" if bf else args.mode) + ("_iunet" if iu else "") + \
                 (f"_c{C}" if C != 1 else "")
-            traffic, traffic_src = pmc_step_traffic(dom["kernel"], mode_tag)
+            traffic, traffic_src, traffic_by = pmc_step_traffic(dom, mode_tag)
         else:  # no 3x3 launch recorded: the isolated 96->96 shape
             timer = (time_dominant_kernel_bf16 if bf else
                      time_dominant_kernel_x6 if x6 else time_dominant_kernel)
             kms, kflops = timer(bs, H, H, device)
             kdesc = "96->96 3x3 @%dx%dx%d, isolated launch" % (bs, H, H)
-            traffic, traffic_src = None, None
+            traffic, traffic_src, traffic_by = None, None, None
         achieved = kflops / (kms * 1e-3) / 1e12
+        # the bound of the dominant launch: its arithmetic intensity (algorithmic FLOPs over the
+        # fp32 activations it must move) against the machine balance peak / 8 TB/s -- the bf16
+        # base's 3x3 convs (~217 FLOP/B against 312) are HBM-bound, the bf16x6 ones (52) are not
+        alg_bytes = shapes[0]["algorithmic_bytes_per_launch"] if shapes else None
+        hbm_bound = bool(alg_bytes) and kflops / alg_bytes < peak * 1e12 / (PEAK_HBM_GBS * 1e9)
         model = "ImprovedUNet(n_feature=48)" if iu else "UNet(n_feature=48)"
         if iu and not ft:
             workload = (f"{args.mode} step with arch_unet.ImprovedUNet(n_feature=48, depth=4, noise=True) "
@@ -529,18 +555,27 @@ def main():
             "step_tflops": round(step_flops / (ms_step * 1e-3) / 1e12, 2),
             "step_frac_of_fp32_peak": round(step_flops / (ms_step * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
             "step_flops_executed": step_flops, "step_flops_reference": ref_flops,
-            "roofline": {"bound": "mfma",
+            "roofline": {"bound": "hbm" if hbm_bound else "mfma",
                          "kernel": kdesc + ("; bf16 MFMA" if bf else "; fp32 as 6 split-bf16 "
                                             "products, peak = bf16 dense / 6" if x6 else "; fp32 MFMA"),
-                         "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": traffic,
+                         **({"achieved": round(alg_bytes / (kms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
+                             "unit": "GB/s", "frac": round(alg_bytes / (kms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                             "mfma_achieved_tflops": round(achieved, 2), "mfma_peak_tflops": peak,
+                             "mfma_frac": round(achieved / peak, 4)} if hbm_bound else
+                            {"achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                             "frac": round(achieved / peak, 4)}),
+                         "traffic": traffic,
                          "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                         "traffic_of": traffic_by,
+                         "algorithmic_bytes_per_launch": shapes[0]["algorithmic_bytes_per_launch"]
+                         if shapes else None,
                          "avg_launch_ms": round(kms, 4), "flops_per_launch": kflops,
                          "weighted_frac": round(weighted, 4) if weighted else None,
                          "weighted_over": "every 3x3 launch of the step (fwd, pair-pixel fwd, "
                                           "data and weight gradients), time-weighted",
                          "ms_3x3_per_step": round(ms3, 3),
-                         "per_shape": [{k: v for k, v in d.items() if k != "algorithmic_bytes_per_launch"}
+                         "per_shape": [{k: v for k, v in d.items()
+                                        if k != "algorithmic_bytes_per_launch" and not k.startswith("_")}
                                        for d in shapes],
                          "method": "one profiled step pair after the timed region, every launch "
                                    "bracketed by HIP events on its stream, single-stream "
@@ -548,7 +583,7 @@ def main():
             "step_breakdown_ms": by_op,
             "loss": loss_v,
         }
-        if args.mode == "n2n" and C == 1 and not iu:
+        if args.mode == "n2n" and C == 1 and not iu and not args.no_eval:
             # "eval PSNR vs ref" (BASELINE metric): the trained weights denoise one 512x512 image
             # on the HIP path; the CPU leg runs the reference restatement on the same weights
             clean8, noisy8 = eval_image()
@@ -557,7 +592,7 @@ def main():
                            "image": "512x512 synthetic, gauss25, after the timed steps",
                            "noisy_psnr": round(float(10 * __import__("math").log10(
                                255.0 ** 2 / float(((noisy8.astype("f8") - clean8) ** 2).mean()))), 4)}
-        if not args.no_cpu_baseline and world == 1 and args.mode == "n2n" and C == 1 and not iu:
+        if not args.no_cpu_baseline and not args.no_eval and world == 1 and args.mode == "n2n" and C == 1 and not iu:
             rec["cpu_baseline"] = cpu_baseline()
             ref_ps = oracle_eval_psnr(net.flat_params, clean8, noisy8)
             rec["cpu_baseline"]["eval_psnr"] = round(ref_ps, 4)

@@ -77,12 +77,22 @@ bool ggeom(int ksize, int K, int nout, GGeom& g) {
 // faster matrix cores give (measured per shape)
 bool x6_shape(int nout) { return nout == 32 || nout % 48 == 0; }
 bool x6_takes(int K, int nout, int tail) {
-  if (nout == 32 && K < 80) return false;  // 32-wide tiles: staging-bound, no gain (32x48, 32x56)
+  // 32-wide tiles with K < 80 were staging-bound on round 2's 8-row kernels (no gain for 32x48,
+  // 32x56); the 16-row ones take K >= 48 at 0.33-0.37 of the x6 peak against the fp32 kernel's
+  // 0.25-0.27 (48->32 @256^2: 1.05 -> 0.79 ms); DN_IU_X6_SMALL32=0 keeps them on fp32
+  static const bool small32 = !getenv("DN_IU_X6_SMALL32") || atoi(getenv("DN_IU_X6_SMALL32")) != 0;
+  if (nout == 32 && K < 80 && !(small32 && K % 4 == 0 && K >= 48)) return false;
   // 32-wide RDB growth convs with K >= 80 take a zero-padded last chunk when it cannot be
   // tail-packed (88, 120: 3 / 4 chunks, 9 / 7 % padding; on the fp32 kernel they ran at ~60 %
   // of the x6 rate of their 80- / 112-channel neighbours); DN_IU_X6_PAD32=0 keeps them on fp32
   static const bool pad32 = !getenv("DN_IU_X6_PAD32") || atoi(getenv("DN_IU_X6_PAD32")) != 0;
   if (pad32 && nout == 32 && K % 4 == 0) return true;
+  // likewise the data gradients of those convs (K = 32 = the growth, nout = 80..144 of the dense
+  // concatenation: 48-channel output blocks, the last one partial) and the 24-channel top
+  // level's 72 -> 24 (a 32-wide tile, 8 outputs idle): the fp32 kernel ran them at 0.19-0.22 of
+  // the x6 ceiling
+  if (pad32 && K == 32 && nout >= 80 && nout % 8 == 0) return true;
+  if (pad32 && nout == 24 && K >= 72 && K % 4 == 0) return true;
   return x6_shape(nout) && (K % 32 == 0 || K >= 128 || tail) && (K > 32 || nout % 96 == 0);
 }
 // output-channel blocks of the wide layers: 96, or 48 where 96 would pad (144 = 3 x 48)
@@ -313,7 +323,7 @@ bool iunet_build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, IPlan
   long x6max = 0;
   auto pf = [&](int k, int K, int nout) {
     pk = std::max(pk, gpack_floats(k, K, nout));
-    if (k == 3 && x6_shape(nout))
+    if (k == 3)  // every shape x6_takes may route (-1 where the x6 kernels have no tile)
       x6max = std::max(x6max, (x6_pack_elems(K, nout, x6_zc(nout)) + 1) / 2);
   };
   for (int i = 0; i < 4; ++i) {

@@ -57,8 +57,8 @@ for step in "$@"; do
       tag=${arg%%:*}; bargs=${arg#*:}; [ "$bargs" = "$arg" ] && bargs=""; bargs=${bargs//+/ }
       rm -rf gpurun_out/pmc_step_$tag; mkdir -p gpurun_out/pmc_step_$tag
       for c in FETCH_SIZE WRITE_SIZE; do
-        timeout -s KILL 200 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc_step_$tag/$c -o run \
-          -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $bargs > gpurun_out/pmc_step_$tag/$c.log 2>&1 || fail "$step $c" $?
+        DN_STEP_STREAMS=0 timeout -s KILL 200 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc_step_$tag/$c -o run \
+          -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-eval $bargs > gpurun_out/pmc_step_$tag/$c.log 2>&1 || fail "$step $c" $?
       done
       python3 tools/pmc_step.py $tag gpurun_out/pmc_step_$tag || fail "$step summary" $? ;;
     stamps)  # stamps:TAG:K+NOUT+H (a DN_X6_STAMPS=1 build libdenoise_hip_TAG.so, tools/x6_stamps.py)

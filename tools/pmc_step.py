@@ -35,19 +35,26 @@ def main():
             if r["Counter_Name"] != c:
                 continue
             k = norm(r["Kernel_Name"])
-            per.setdefault(k, {}).setdefault(c, []).append(float(r["Counter_Value"]))
+            per.setdefault(k, {}).setdefault(c, []).append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     out = {}
     for k, v in per.items():
         if "FETCH_SIZE" not in v or "WRITE_SIZE" not in v:
             continue
-        fetch = sum(v["FETCH_SIZE"]) / len(v["FETCH_SIZE"]) * 1024 * 2
-        write = sum(v["WRITE_SIZE"]) / len(v["WRITE_SIZE"]) * 1024
-        out[k] = {"launches": len(v["FETCH_SIZE"]), "fetch_bytes_corrected": fetch,
+        f = [x for _, x in sorted(v["FETCH_SIZE"])]
+        w = [x for _, x in sorted(v["WRITE_SIZE"])]
+        fetch = sum(f) / len(f) * 1024 * 2
+        write = sum(w) / len(w) * 1024
+        out[k] = {"launches": len(f), "fetch_bytes_corrected": fetch,
                   "write_bytes": write, "traffic_bytes": fetch + write}
+        # per launch in dispatch order (the two passes run the same single-stream launch
+        # sequence): bench.py picks the dominant shape's launches out of the last step
+        if len(f) == len(w):
+            out[k]["per_launch_bytes"] = [round(a * 2048 + b * 1024) for a, b in zip(f, w)]
     doc = {"method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes with "
                      "--kernel-trace over `bench.py --steps 2 --warmup 1 --no-cpu-baseline` "
                      "(tools/gpu_run.sh pmc); per-launch means over every dispatch of the kernel "
-                     "(all its shapes); FETCH x2 gfx950 correction",
+                     "(all its shapes); FETCH x2 gfx950 correction; per_launch_bytes in dispatch order "
+                     "(DN_STEP_STREAMS=0: one stream, the launch order of dn_profile_ops)",
            "kernels": dict(sorted(out.items(), key=lambda kv: -kv[1]["traffic_bytes"]))}
     dst = os.path.join(ROOT, "profiles", f"{tag}_pmc_step.json")
     json.dump(doc, open(dst, "w"), indent=1)
