@@ -186,9 +186,11 @@ __global__ __launch_bounds__(256, (GATHER == G_C3 && NT == 6) ? 3 : 2) void k_fw
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
-  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
-  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
-  const int n = blockIdx.y;
+  int bxr, byr;  // XCD-aware tile order (conv_epi.h xcd_tile)
+  xcd_tile(bxr, byr);
+  const int ty0 = (bxr / tiles_x) * C::TH;
+  const int tx0 = (bxr % tiles_x) * C::TW;
+  const int n = byr;
   const int iy0 = GATHER == G_C3 ? ty0 - 1 : (GATHER == G_DN2 ? 2 * ty0 : ty0);
   const int ix0 = GATHER == G_C3 ? tx0 - 1 : (GATHER == G_DN2 ? 2 * tx0 : tx0);
   const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;

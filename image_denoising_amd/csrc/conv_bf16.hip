@@ -70,9 +70,11 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16(FwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
-  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
-  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
-  const int n = blockIdx.y;
+  int bxr, byr;  // XCD-aware tile order (conv_epi.h xcd_tile)
+  xcd_tile(bxr, byr);
+  const int ty0 = (bxr / tiles_x) * C::TH;
+  const int tx0 = (bxr % tiles_x) * C::TW;
+  const int n = byr;
   const int iy0 = ty0 - (K3 ? 1 : 0), ix0 = tx0 - (K3 ? 1 : 0);
   const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
   const bool vec = ((a.in_stride | a.in_off) & 3) == 0;
@@ -201,9 +203,11 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16p(FwdArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lg = lane >> 4;
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
-  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
-  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
-  const int n = blockIdx.y;
+  int bxr, byr;  // XCD-aware tile order (conv_epi.h xcd_tile)
+  xcd_tile(bxr, byr);
+  const int ty0 = (bxr / tiles_x) * C::TH;
+  const int tx0 = (bxr % tiles_x) * C::TW;
+  const int n = byr;
   const int iy0 = ty0 - 1, ix0 = tx0 - 1;
   const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
   const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp);

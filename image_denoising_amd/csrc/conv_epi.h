@@ -11,6 +11,36 @@ namespace dn {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// XCD-aware tile order of the tiled conv kernels: the hardware deals workgroups round-robin
+// over the 8 XCDs (linear block b -> XCD b % 8, MI355X_MICROARCH.md §Workgroup dispatch), so in
+// launch order neighbouring tiles land on different XCDs and each re-fetches the halo rows the
+// other already holds in its own L2.  Remapped, XCD x walks one contiguous run of
+// (tile, image) indices -- vertical and horizontal neighbours are in flight on the same XCD --
+// without changing which tiles are computed.  Over (blockIdx.x, blockIdx.y) of one z slab
+// (the epilogue reads blockIdx.z itself); a bijection for any slab size (uneven runs when it
+// is not a multiple of 8).  DN_XCD_REMAP=0 builds the launch order (A/B).
+#ifndef DN_XCD_REMAP
+#define DN_XCD_REMAP 1
+#endif
+__device__ __forceinline__ void xcd_tile(int& bx, int& by) {
+  const unsigned gx = gridDim.x, tot = gx * gridDim.y;
+  const unsigned l = blockIdx.x + gx * blockIdx.y;
+  if (!DN_XCD_REMAP || tot < 16) {
+    bx = (int)blockIdx.x; by = (int)blockIdx.y;
+    return;
+  }
+  // global block l + z*tot sits on XCD (l + z0) % 8; XCD x holds the slab blocks
+  // first(x), first(x) + 8, ... and gets the run [start(x), start(x) + count(x)) of the order
+  const unsigned z0 = (blockIdx.z * tot) % 8, x = (l + z0) % 8;
+  unsigned start = 0;
+  for (unsigned xx = 0; xx < x; ++xx) {
+    const unsigned f = (xx + 8 - z0) % 8;
+    start += f < tot ? (tot - 1 - f) / 8 + 1 : 0u;
+  }
+  const unsigned lp = start + (l - (x + 8 - z0) % 8) / 8;
+  bx = (int)(lp % gx); by = (int)(lp / gx);
+}
+
 // weight gradients: output-channel block of a wide layer (a.zc > 0): blockIdx.z selects
 // channels [z*zc, z*zc+zc)
 __device__ __forceinline__ WgradArgs wg_block(const WgradArgs& a0) {

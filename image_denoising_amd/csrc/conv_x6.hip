@@ -83,9 +83,11 @@ __global__ __launch_bounds__(256, 2) void k_c3x6(FwdArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int li = lane & 15, lg = lane >> 4;
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
-  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
-  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
-  const int n = blockIdx.y;
+  int bxr, byr;  // XCD-aware tile order (conv_epi.h xcd_tile)
+  xcd_tile(bxr, byr);
+  const int ty0 = (bxr / tiles_x) * C::TH;
+  const int tx0 = (bxr % tiles_x) * C::TW;
+  const int n = byr;
   const int iy0 = ty0 - 1, ix0 = tx0 - 1;
   const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
   const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp) + (long)blockIdx.z * a.wp_z;
@@ -207,9 +209,12 @@ __global__ __launch_bounds__(256, 2) void k_c3x6(FwdArgs a) {
 // chunk's x tile, which is loaded into registers when a chunk starts and split into the
 // three LDS planes when it ends.  Requires float4-aligned input views with K % 4 == 0.
 // ------------------------------------------------------------------------------------
-template <int NT>
+template <int NT, int WV = 8>
 struct PCfg {
-  static constexpr int WAVES = 8, MT = 2, S = 4;
+  // WV = 8: two waves per SIMD, MT = 2 rows each.  WV = 4 (one wave per SIMD, 4 rows, 392-462
+  // registers with the accumulators in AGPRs, no spills) measured 8-15 % slower on the 96-channel
+  // shapes (profiles/r3_ab_w4_not_kept.log): not launched
+  static constexpr int WAVES = WV, MT = 16 / WV, S = 4;
   static constexpr int TW = 16, TH = WAVES * MT, IH = TH + 2, IW = TW + 2, KC = 32, NP = 16 * NT;
   static constexpr int XPIX = IH * IW;
   static constexpr int XPL = XPIX * KC;
@@ -276,6 +281,11 @@ __device__ __forceinline__ void x6_barrier() {
 #ifndef DN_X6_STAMPS
 #define DN_X6_STAMPS 0
 #endif
+// A/B switch: static priority 1 for waves 4-7 (the second-dispatched half, the arbitration
+// loser of every stage) before the main loop (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+#ifndef DN_X6_PRIO
+#define DN_X6_PRIO 0
+#endif
 #if DN_X6_STAMPS
 constexpr int X6_STAMP_SLOTS = 128;
 __device__ unsigned long long g_x6_stamps[64 * 2 * X6_STAMP_SLOTS];
@@ -293,9 +303,9 @@ __device__ unsigned long long g_x6_stamps[64 * 2 * X6_STAMP_SLOTS];
   } while (0)
 #endif
 
-template <int NT, int TAIL, bool SEL = false>
-__global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
-  using C = PCfg<NT>;
+template <int NT, int TAIL, bool SEL = false, int WV = 8>
+__global__ __launch_bounds__(64 * WV, 1) void k_c3x6p(FwdArgs a) {
+  using C = PCfg<NT, WV>;
   static_assert(!SEL || (TAIL == 0 && NT % 2 == 0 && C::MT == 2 && C::WAVES == 8),
                 "selected pixels: full 32-channel chunks, 8 waves of two cell rows x NT/2");
   constexpr int MTC = C::MT;               // M fragments computed per wave
@@ -308,9 +318,12 @@ __global__ __launch_bounds__(512, 1) void k_c3x6p(FwdArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int li = lane & 15, lg = lane >> 4;
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
-  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
-  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
-  const int n = blockIdx.y;
+  int bxr, byr;  // XCD-aware tile order (conv_epi.h xcd_tile)
+  xcd_tile(bxr, byr);
+  const int ty0 = (bxr / tiles_x) * C::TH;
+  if (DN_X6_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  const int tx0 = (bxr % tiles_x) * C::TW;
+  const int n = byr;
   const int iy0 = ty0 - 1, ix0 = tx0 - 1;
   const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
   const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp) + (long)blockIdx.z * a.wp_z;
@@ -715,10 +728,13 @@ __global__ __launch_bounds__(512, 1) void k_c3x6s(FwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lg = lane >> 4;
+  if (DN_X6_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
-  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
-  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
-  const int n = blockIdx.y;
+  int bxr, byr;  // XCD-aware tile order (conv_epi.h xcd_tile)
+  xcd_tile(bxr, byr);
+  const int ty0 = (bxr / tiles_x) * C::TH;
+  const int tx0 = (bxr % tiles_x) * C::TW;
+  const int n = byr;
   const int iy0 = ty0 - 1, ix0 = tx0 - 1;
   const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
   const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp);
@@ -953,9 +969,11 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int li = lane & 15, lg = lane >> 4;
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
-  const int ty0 = (blockIdx.x / tiles_x) * C::TH;
-  const int tx0 = (blockIdx.x % tiles_x) * C::TW;
-  const int n = blockIdx.y;
+  int bxr, byr;  // XCD-aware tile order (conv_epi.h xcd_tile)
+  xcd_tile(bxr, byr);
+  const int ty0 = (bxr / tiles_x) * C::TH;
+  const int tx0 = (bxr % tiles_x) * C::TW;
+  const int n = byr;
   const int iy0 = ty0 - 1, ix0 = tx0 - 1;
   const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
   const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp) + (long)blockIdx.z * a.wp_z;

@@ -25,13 +25,13 @@ struct Rec {
 std::mutex g_mu;
 std::vector<Rec> g_recs;
 bool g_on = false;
-thread_local const char* g_kernel = "";
+thread_local char g_kernel[48] = "";  // copied: callers may pass a temporary's c_str()
 }  // namespace
 
 bool prof_on() { return g_on; }
 
 void prof_kernel(const char* k) {
-  if (g_on) g_kernel = k;
+  if (g_on) std::snprintf(g_kernel, sizeof g_kernel, "%s", k ? k : "");
 }
 
 OpTimer::OpTimer(hipStream_t st, const char* op, double flops, int K, int NOUT, int H, int W,
@@ -46,7 +46,7 @@ OpTimer::OpTimer(hipStream_t st, const char* op, double flops, int K, int NOUT, 
     (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b);
     return;
   }
-  g_kernel = "";
+  g_kernel[0] = '\0';
   std::lock_guard<std::mutex> lock(g_mu);
   idx = (int)g_recs.size();
   s = st;
@@ -58,7 +58,7 @@ OpTimer::~OpTimer() {
   std::lock_guard<std::mutex> lock(g_mu);
   if (idx >= (int)g_recs.size()) return;  // cleared meanwhile
   Rec& r = g_recs[idx];
-  std::snprintf(r.kernel, sizeof r.kernel, "%s", g_kernel ? g_kernel : "");
+  std::snprintf(r.kernel, sizeof r.kernel, "%s", g_kernel);
   (void)hipEventRecord(r.b, s);
 }
 
