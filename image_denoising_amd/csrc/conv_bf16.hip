@@ -182,6 +182,9 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16(FwdArgs a) {
 // is hidden behind two weight stages instead of stalling the stage it was issued in (k_fwd_bf16
 // waits for it at that stage's barrier).
 // ------------------------------------------------------------------------------------
+#ifndef DN_BF_ABL_XWAIT
+#define DN_BF_ABL_XWAIT 0
+#endif
 #define BF_WAITCNT_VM(n) \
   __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
 
@@ -301,7 +304,9 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16p(FwdArgs a) {
       store_x();
     }
     // own DMAs of stage st+1 landed; younger: the next chunk's x loads (issued at ky == 0)
-    if (ky == 0 && more) BF_WAITCNT_VM(C::XITEMS);
+    // (DN_BF_ABL_XWAIT: diagnostic ablation, wrong results -- stage ky == 1 does not wait for the
+    // next chunk's x loads, so its weight DMA for ky == 2 may not have landed; timing only)
+    if ((ky == 0 || (DN_BF_ABL_XWAIT && ky == 1)) && more) BF_WAITCNT_VM(C::XITEMS);
     else BF_WAITCNT_VM(0);
     if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
     bf_barrier();
