@@ -485,8 +485,8 @@ dn_status dn_conv2d_forward_x6(const float* x, int x_stride, int N, int H, int W
   if (dn_status st = need_pack(pack_ws, pack_bytes, need)) return st;
   hipStream_t s = (hipStream_t)stream;
   // large grids with a partial last 32-channel chunk: the pipelined kernel's tail packing
-  const int tail = (x_stride % 4 == 0 && Cin % 4 == 0 && x6_pipelined(N, H, W, Cout, 0))
-                       ? x6_tail_mode(Cin) : 0;
+  const int tail = x6_image_mode(N, H, W, Cin, Cout, 0,
+                                 x_stride % 4 == 0 && Cin % 4 == 0 && y_stride % 4 == 0);
   hipError_t e = launch_pack_x6(conv_fwd_view(w, Cin, 3), Cin, Cout, 0, pack_ws, s, tail);
   if (e == hipSuccess) {
     FwdArgs a{};
@@ -512,7 +512,8 @@ dn_status dn_conv2d_backward_data_x6(const float* dz, int N, int H, int W, int C
   if (dn_status st = need_pack(pack_ws, pack_bytes, need)) return st;
   hipStream_t s = (hipStream_t)stream;
   const int zc = x6_dgrad_zc(Cin);
-  const int tail = (Cout % 4 == 0 && x6_pipelined(N, H, W, Cin, zc)) ? x6_tail_mode(Cout) : 0;
+  const int tail = x6_image_mode(N, H, W, Cout, Cin, zc,
+                                 Cout % 4 == 0 && dx_stride % 4 == 0 && (!mask || mask_stride % 4 == 0));
   hipError_t e = launch_pack_x6(conv_dgrad_view(w, Cin, 3), Cout, Cin, zc, pack_ws, s, tail);
   if (e == hipSuccess) {
     FwdArgs a{};

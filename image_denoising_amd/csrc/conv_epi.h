@@ -190,21 +190,20 @@ __device__ __forceinline__ void fwd_epilogue_generic(const FwdArgs& a, const f32
 // (~15k cycles of a ~115k-cycle 16x16x96 tile with every CU storing at once, DN_X6_STAMPS).
 // Requires vec_out (OUT_NHWC, float4-aligned strides / offsets); rows are staged one at a time
 // through the wave's own LDS area (a wave's LDS accesses complete in order).
+// (fwd_epilogue_vec_at: the wave's rows start at tile row wrow, its channels at cz (nout of
+// them), its staging area is `st` (16 * PS floats) -- for kernels whose waves split the channels)
 template <int NT, int MT, int PS, int EPI>
-__device__ __forceinline__ void fwd_epilogue_vec(const FwdArgs& a, const f32x4 (&acc)[MT][NT],
-                                                 float* lds, int ty0, int tx0, int n) {
+__device__ __forceinline__ void fwd_epilogue_vec_at(const FwdArgs& a, const f32x4 (&acc)[MT][NT],
+                                                    float* st, int ty0, int tx0, int n, int wrow,
+                                                    int cz, int nout) {
   constexpr int NP = 16 * NT;
   constexpr bool BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_ACT || EPI == EPI_BIAS_ADD;
   constexpr bool MASKL = EPI == EPI_MASK || EPI == EPI_BIAS_ADD;  // reads a.mask
   constexpr bool OLDL = EPI == EPI_ACCUM;                         // reads a.out
   constexpr int NIT = (16 * NP / 4 + 63) / 64;  // float4 items per lane per row
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
   const int li = lane & 15, lg = lane >> 4;
-  const int wrow = wave * MT;
-  const int cz = a.zc ? (int)blockIdx.z * a.zc : 0;
-  const int nout = a.zc ? min(NP, a.NOUT - cz) : a.NOUT;
   const int NQ = nout >> 2;
-  float* st = lds + wave * 16 * PS;
   const bool has_bias = BIAS && a.bias != nullptr;
   float4 bvec[NIT];
 #pragma unroll
@@ -262,6 +261,33 @@ __device__ __forceinline__ void fwd_epilogue_vec(const FwdArgs& a, const f32x4 (
       }
       *reinterpret_cast<float4*>(a.out + oi[m][k]) = v;
     }
+}
+
+template <int NT, int MT, int PS, int EPI>
+__device__ __forceinline__ void fwd_epilogue_vec(const FwdArgs& a, const f32x4 (&acc)[MT][NT],
+                                                 float* lds, int ty0, int tx0, int n) {
+  const int wave = threadIdx.x >> 6;
+  const int cz = a.zc ? (int)blockIdx.z * a.zc : 0;
+  const int nout = a.zc ? min(16 * NT, a.NOUT - cz) : a.NOUT;
+  fwd_epilogue_vec_at<NT, MT, PS, EPI>(a, acc, lds + wave * 16 * PS, ty0, tx0, n, wave * MT, cz,
+                                       nout);
+}
+
+// the float4 NHWC epilogue of a wave that owns rows [wrow, wrow + MT) and channels [cz, cz +
+// nout) of the tile, the kind dispatched at run time (the caller checked vec_nhwc)
+template <int NT, int MT, int PS>
+__device__ __forceinline__ void fwd_epilogue_at(const FwdArgs& a, const f32x4 (&acc)[MT][NT],
+                                                float* st, int ty0, int tx0, int n, int wrow,
+                                                int cz, int nout) {
+  switch (a.epi) {
+    case EPI_BIAS: return fwd_epilogue_vec_at<NT, MT, PS, EPI_BIAS>(a, acc, st, ty0, tx0, n, wrow, cz, nout);
+    case EPI_BIAS_ACT: return fwd_epilogue_vec_at<NT, MT, PS, EPI_BIAS_ACT>(a, acc, st, ty0, tx0, n, wrow, cz, nout);
+    case EPI_PLAIN: return fwd_epilogue_vec_at<NT, MT, PS, EPI_PLAIN>(a, acc, st, ty0, tx0, n, wrow, cz, nout);
+    case EPI_MASK: return fwd_epilogue_vec_at<NT, MT, PS, EPI_MASK>(a, acc, st, ty0, tx0, n, wrow, cz, nout);
+    case EPI_ACCUM: return fwd_epilogue_vec_at<NT, MT, PS, EPI_ACCUM>(a, acc, st, ty0, tx0, n, wrow, cz, nout);
+    case EPI_BIAS_ADD: return fwd_epilogue_vec_at<NT, MT, PS, EPI_BIAS_ADD>(a, acc, st, ty0, tx0, n, wrow, cz, nout);
+    default: break;
+  }
 }
 
 // the epilogue: the specialised float4 NHWC path where it applies, else the generic one

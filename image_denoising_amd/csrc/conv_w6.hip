@@ -1,0 +1,439 @@
+// bf16x6 3x3 convolution through the 1-D Winograd transform F(2,3) along x (k_c3w6): the
+// 96-output-channel forward / data-gradient shapes of the N2N step with 2/3 of the MFMAs.
+//
+// Along x, two outputs of a kernel row are y0 = d0 g0 + d1 g1 + d2 g2 and y1 = d1 g0 + d2 g1 +
+// d3 g2 (d = four consecutive inputs of a tile of two output pixels, g = the row's three taps).
+// F(2,3) computes them from four products of transformed operands,
+//   v = (d0 - d2, d1 + d2, d2 - d1, d1 - d3),   u = (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2),
+//   m_p = v_p u_p,   y0 = m0 + m1 + m2,   y1 = m1 - m2 - m3,
+// so a tile row costs 3 kernel rows x 4 positions = 12 products per two output pixels instead of
+// 18 (every product here a 32-channel dot product on the matrix cores).  The four positions are
+// four independent GEMMs over (input channel, kernel row): M = tiles, N = output channels,
+// K = 32 channels x 3 rows; y is formed in registers after the last K chunk.
+// Arithmetic: v (fp32 adds) and u (rounded once from fp64 by the packer) are split exactly into
+// three bf16 pieces and multiplied as in the bf16x6 kernels (six piece products, fp32 sums), so
+// each m_p has the accuracy of an fp32 dot product; the transforms add one rounding of v and u
+// (measured against fp64 in tests/test_gpu_x6.py like the direct kernels).
+//
+//   Workgroup = 8 waves, one per CU (LDS), tile = 16 rows x 16 pixels (8 Winograd tiles per
+//   row) x 96 output channels.  Wave (mg, nh, ph) = (w & 1, (w >> 1) & 1, w >> 2): tile rows
+//   8mg .. 8mg+7 (four M fragments of 16 Winograd tiles = two rows each) x output channels
+//   48nh .. +47 (three N fragments) x positions 2ph, 2ph+1.  Per K chunk a wave runs 6 stages
+//   (kernel row ky, position p) of 4 x 3 fragments x 6 products = 72 MFMAs.
+//   * The transformed x tile V (18 input rows x 8 tiles x 4 positions x 32 channels, three bf16
+//     planes, 108 KiB) is built per chunk from a raw fp32 staging copy (the next chunk's raw x is
+//     loaded into registers and written to the staging area during the current chunk).
+//   * Weights come straight from the pre-split image (k_pack_batch PK_W6) into registers: each
+//     N fragment of the next stage is requested right after its last use in this one.
+//   * After the last chunk the two position halves exchange partial output sums through LDS.
+#include <cstdlib>
+#include <string>
+#include <type_traits>
+
+#include "conv_epi.h"
+#include "x6_core.h"
+
+namespace dn {
+
+struct WCfg {
+  static constexpr int WAVES = 8, MT = 4, NTW = 3, NP = 96, NPOS = 4, NJ = 8;
+  static constexpr int TW = 16, TH = 16, IH = TH + 2, IW = TW + 2, KC = 32;
+  static constexpr int SPC = 12;                       // weight stages per full chunk (ky, p)
+  static constexpr int VPL = IH * 4 * NJ * NPOS * 8;   // bf16 per plane of V (quads of 8)
+  static constexpr int VBYTES = 3 * VPL * 2;
+  static constexpr int XS = 36;                        // floats per pixel of the raw staging
+  static constexpr int RAWB = IH * IW * XS * 4;
+  static constexpr int WPL = NP * KC;
+  static constexpr int WSTP = x6_wst(NP);
+  static constexpr int XQ = IH * IW * (KC / 4);        // float4 items of a raw x tile
+  static constexpr int XITEMS = (XQ + WAVES * 64 - 1) / (WAVES * 64);
+  static constexpr int VITEMS = (IH * NJ * 8 + WAVES * 64 - 1) / (WAVES * 64);  // transform items
+  static constexpr int PS = 16 * NTW + 4;
+  static constexpr int LBYTES = VBYTES + RAWB;
+  static_assert(LBYTES <= 163840, "one workgroup per CU");
+  static_assert(WAVES * 16 * PS * 4 <= RAWB, "epilogue staging inside the raw area");
+  static_assert(WAVES * 2 * NTW * 2 * 4 * 64 * 4 <= VBYTES, "exchange inside V");
+};
+
+// 16-B quad index of V element (row, kq, j, p): p is XOR-swizzled by j >> 2 and row & 1, so the
+// 16 tiles (two rows x 8) that lanes li = 0..15 read at one (p, kq) fall on 16 distinct quads of
+// a 256-B window (conflict-free ds_read_b128)
+__device__ __forceinline__ int w6_vq(int row, int kq, int j, int p) {
+  return ((row * 4 + kq) * 8 + j) * 4 + (p ^ (j >> 2) ^ ((row & 1) << 1));
+}
+
+__device__ __forceinline__ void w6_barrier() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+#ifndef DN_W6_GM
+#define DN_W6_GM 1
+#endif
+
+template <int I0, int N, class F>
+__device__ __forceinline__ void w6_for(F&& f) {
+  if constexpr (I0 < N) {
+    f(std::integral_constant<int, I0>{});
+    w6_for<I0 + 1, N>(f);
+  }
+}
+
+// TAIL (x6_tail_mode of K) packs the last chunk's channels: 1 (<= 4 channels): one stage per
+// position, k = 4 ky + channel; 2 (<= 16 channels): two stages per position, k = 16 (ky - 2s) +
+// channel.  Full chunks: stage 4 ky + p, k = channel.
+template <int TAIL>
+__global__ __launch_bounds__(512, 1) void k_c3w6(FwdArgs a) {
+  using C = WCfg;
+  constexpr int MT = C::MT, NTW = C::NTW;
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
+  __bf16* lv = reinterpret_cast<__bf16*>(lds_raw);
+  float* lraw = reinterpret_cast<float*>(lds_raw + C::VBYTES);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lg = lane >> 4;
+  const int mg = wave & 1, nh = (wave >> 1) & 1, ph = wave >> 2;
+  const int tiles_x = (a.OW + C::TW - 1) / C::TW;
+  int bxr, byr;
+  xcd_tile(bxr, byr);
+  const int ty0 = (bxr / tiles_x) * C::TH, tx0 = (bxr % tiles_x) * C::TW, n = byr;
+  const int iy0 = ty0 - 1, ix0 = tx0 - 1;
+  const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
+  const int nch = (a.K + C::KC - 1) / C::KC;
+
+  // acc[pi][f][q]: position 2ph + pi, M fragment f, N fragment q
+  f32x4 acc[2][MT][NTW];
+#pragma unroll
+  for (int pi = 0; pi < 2; ++pi)
+#pragma unroll
+    for (int f = 0; f < MT; ++f)
+#pragma unroll
+      for (int q = 0; q < NTW; ++q) acc[pi][f][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // raw x tile of a chunk: XITEMS float4 per thread (out-of-range offsets read zeros)
+  const int ry0 = iy0 > 0 ? iy0 : 0, ry1 = iy0 + C::IH < a.IHt ? iy0 + C::IH : a.IHt;
+  const long row_floats = (long)a.IWt * a.in_stride;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(inb + ry0 * row_floats), (short)0, (int)((ry1 - ry0) * row_floats * 4),
+      0x00020000);
+  f32x4 xr[C::XITEMS];
+  auto load_x = [&](int k0, int tid, int i0, int i1) {
+#pragma unroll
+    for (int it = i0; it < i1; ++it) {
+      const int e = tid + it * C::WAVES * 64;
+      const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+      const int iy = pix / C::IW, ix = pix - iy * C::IW;
+      const int gy = iy0 + iy, gx = ix0 + ix, k = k0 + 4 * q;
+      const bool ok = e < C::XQ && gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt && k < a.K;
+      const int off = ok ? (((gy - ry0) * a.IWt + gx) * a.in_stride + k) * 4 : 0x7fffffff;
+      xr[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    }
+  };
+  auto store_raw = [&](int tid, int i0, int i1) {
+#pragma unroll
+    for (int it = i0; it < i1; ++it) {
+      const int e = tid + it * C::WAVES * 64;
+      if (e < C::XQ) {
+        const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+        *reinterpret_cast<f32x4*>(lraw + pix * C::XS + 4 * q) = xr[it];
+      }
+    }
+  };
+  // raw staging -> V: item (row, j, c4) transforms channels 4c4 .. 4c4+3 of Winograd tile j
+  auto transform = [&](int tid) {
+#pragma unroll
+    for (int it = 0; it < C::VITEMS; ++it) {
+      const int e = tid + it * C::WAVES * 64;
+      if (e < C::IH * C::NJ * 8) {
+        const int c4 = e & 7, j = (e >> 3) & 7, row = e >> 6;
+        const float* r = lraw + (row * C::IW + 2 * j) * C::XS + 4 * c4;
+        const f32x4 d0 = *reinterpret_cast<const f32x4*>(r);
+        const f32x4 d1 = *reinterpret_cast<const f32x4*>(r + C::XS);
+        const f32x4 d2 = *reinterpret_cast<const f32x4*>(r + 2 * C::XS);
+        const f32x4 d3 = *reinterpret_cast<const f32x4*>(r + 3 * C::XS);
+        f32x4 v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          v[0][c] = d0[c] - d2[c];
+          v[1][c] = d1[c] + d2[c];
+          v[2][c] = d2[c] - d1[c];
+          v[3][c] = d1[c] - d3[c];
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          unsigned h0, m0, l0, h1, m1, l1;
+          split3x2(v[p][0], v[p][1], h0, m0, l0);
+          split3x2(v[p][2], v[p][3], h1, m1, l1);
+          const int o = w6_vq(row, c4 >> 1, j, p) * 8 + (c4 & 1) * 4;  // bf16 index in a plane
+          typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<u32x2_t*>(lv + o) = u32x2_t{h0, h1};
+          *reinterpret_cast<u32x2_t*>(lv + C::VPL + o) = u32x2_t{m0, m1};
+          *reinterpret_cast<u32x2_t*>(lv + 2 * C::VPL + o) = u32x2_t{l0, l1};
+        }
+      }
+    }
+  };
+
+  // weights: fragment q = output channels 48nh + 16q .. +15 of stage st, plane pl
+  const int nst_img = nch * C::SPC;
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.wp), (short)0, nst_img * C::WSTP * 2, 0x00020000);
+  int woff[NTW];
+#pragma unroll
+  for (int q = 0; q < NTW; ++q) {
+    const int row = (NTW * nh + q) * 16 + li;
+    woff[q] = (row * C::KC + x6_swz(row, lg) * 8) * 2;
+  }
+  bf16x8 w[3][NTW];
+  auto load_wq = [&](int st, int q) {
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      w[pl][q] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, (st * C::WSTP + pl * C::WPL) * 2 + woff[q], 0, 0));
+  };
+
+  // stage list of this wave for chunk c (image stage index); tail chunks per TAIL
+  auto stage_of = [&](int c, int s, bool tailc) -> int {
+    if (!tailc) return c * C::SPC + (s >> 1) * 4 + 2 * ph + (s & 1);  // s = 2 ky + pi
+    if (TAIL == 1) return c * C::SPC + 2 * ph + s;                     // s = pi
+    return c * C::SPC + 2 * (2 * ph + (s >> 1)) + (s & 1);             // s = 2 pi + half
+  };
+
+  // one stage: A fragments of the 4 M fragments (three planes each) read from V, then per N
+  // fragment q: 2 x 2 M fragments x 6 products, its adds pinned, and the next stage's fragment q
+  // requested into the registers it frees
+  auto stage = [&](auto mode_tag, int s, int nxt, int liv, int lgv) {
+    constexpr int MODE = decltype(mode_tag)::value;  // 0 full, 1 / 2 tail
+    int pi, ky0;
+    if (MODE == 0) { pi = s & 1; ky0 = s >> 1; }
+    else if (MODE == 1) { pi = s; ky0 = 0; }
+    else { pi = s >> 1; ky0 = 2 * (s & 1); }
+    const int p = 2 * ph + pi;
+    bf16x8 av[3][MT];
+#pragma unroll
+    for (int f = 0; f < MT; ++f) {
+      const int row0 = 8 * mg + 2 * f + (liv >> 3), j = liv & 7;
+      if constexpr (MODE == 0) {
+        const int o = w6_vq(row0 + ky0, lgv, j, p) * 8;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) av[pl][f] = *reinterpret_cast<const bf16x8*>(lv + pl * C::VPL + o);
+      } else if constexpr (MODE == 1) {
+        // lane group 0: channels 0..3 of ky 0 and 1; group 1: ky 2 and zeros; 2, 3: zeros
+        const int ka = 2 * lgv, kb = ka + 1;
+        const int oa = w6_vq(row0 + (ka < 3 ? ka : 0), 0, j, p) * 8;
+        const int ob = w6_vq(row0 + (kb < 3 ? kb : 0), 0, j, p) * 8;
+        const bf16x4 z4 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          bf16x4 va = *reinterpret_cast<const bf16x4*>(lv + pl * C::VPL + oa);
+          bf16x4 vb = *reinterpret_cast<const bf16x4*>(lv + pl * C::VPL + ob);
+          if (ka > 2) va = z4;
+          if (kb > 2) vb = z4;
+          av[pl][f] = __builtin_shufflevector(va, vb, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      } else {
+        // lane groups 0, 1: channels 0..15 of ky0 (quads 0, 1); 2, 3: those of ky0 + 1
+        const int ky = ky0 + (lgv >> 1);
+        const int o = w6_vq(row0 + (ky < 3 ? ky : 0), lgv & 1, j, p) * 8;
+        const bf16x8 z8 = {};
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(lv + pl * C::VPL + o);
+          av[pl][f] = ky > 2 ? z8 : v;
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    auto run = [&](auto pic) {
+      constexpr int PI = decltype(pic)::value;
+#pragma unroll
+      for (int q = 0; q < NTW; ++q) {
+        constexpr int GM = DN_W6_GM;  // M fragments per MFMA group
+#pragma unroll
+        for (int mp = 0; mp < MT / GM; ++mp) {
+          f32x4(&ah)[GM][NTW] = *reinterpret_cast<f32x4(*)[GM][NTW]>(&acc[PI][GM * mp]);
+          bf16x8 a2[3][GM];
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+            for (int i = 0; i < GM; ++i) a2[pl][i] = av[pl][GM * mp + i];
+          x6_group<GM, NTW, 1>(ah, a2, w, q);
+#pragma unroll
+          for (int i = 0; i < GM; ++i) asm volatile("" : "+v"(ah[i][q]));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (nxt >= 0) load_wq(nxt, q);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    if (pi == 0) run(std::integral_constant<int, 0>{});
+    else run(std::integral_constant<int, 1>{});
+  };
+
+  // prologue: stage 0's weights, chunk 0's x tile -> raw -> V
+  const bool tail_only = TAIL && nch == 1;
+#pragma unroll
+  for (int q = 0; q < NTW; ++q) load_wq(stage_of(0, 0, tail_only), q);
+  load_x(0, tid, 0, C::XITEMS);
+  store_raw(tid, 0, C::XITEMS);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  w6_barrier();
+  transform(tid);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  w6_barrier();
+
+  constexpr int XG = 3, XPG = (C::XITEMS + XG - 1) / XG;
+#pragma unroll 1
+  for (int c = 0; c < nch; ++c) {
+    int liv = li, lgv = lg, tidv = tid;
+    asm volatile("" : "+v"(liv), "+v"(lgv), "+v"(tidv));
+    const bool more = c + 1 < nch;
+    const bool tailc = TAIL && !more;
+    const bool next_tail = TAIL && c + 2 == nch;
+    if (tailc) {
+      constexpr int NS = TAIL == 1 ? 2 : 4;
+      using MD = std::integral_constant<int, TAIL == 1 ? 1 : 2>;
+      w6_for<0, NS>([&](auto si) {
+        constexpr int s = decltype(si)::value;
+        stage(MD{}, s, s + 1 < NS ? stage_of(c, s + 1, true) : -1, liv, lgv);
+      });
+      break;
+    }
+    // a full chunk: 6 stages; the next chunk's raw x in three groups (loaded at stages 0, 2, 4
+    // after the stage's weight requests, written to the staging area two stages later)
+    w6_for<0, 6>([&](auto si) {
+      constexpr int s = decltype(si)::value;
+      const int nxt = s + 1 < 6 ? stage_of(c, s + 1, false) : (more ? stage_of(c + 1, 0, next_tail) : -1);
+      if constexpr (s >= 2 && s % 2 == 0) {
+        constexpr int g = s / 2 - 1;
+        if (more) store_raw(tidv, g * XPG, (g + 1) * XPG < C::XITEMS ? (g + 1) * XPG : C::XITEMS);
+      }
+      stage(std::integral_constant<int, 0>{}, s, nxt, liv, lgv);
+      if constexpr (s % 2 == 0) {
+        constexpr int g = s / 2;
+        if (more) load_x((c + 1) * C::KC, tidv, g * XPG, (g + 1) * XPG < C::XITEMS ? (g + 1) * XPG : C::XITEMS);
+      }
+    });
+    if (more) {
+      store_raw(tidv, 2 * XPG, C::XITEMS);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      w6_barrier();  // every wave done with V; the raw tile complete
+      transform(tidv);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      w6_barrier();  // V of the next chunk complete
+    }
+  }
+
+  // output transform: ph 0 holds m0, m1, ph 1 holds m2, m3.  Partial sums per tile:
+  //   ph 0: (y0, y1) += (m0 + m1, m1);   ph 1: (y0, y1) += (m2, -m2 - m3)
+  // wave ph keeps M fragments 2ph, 2ph+1 (tile rows 8mg + 4ph .. +3) and hands the other two's
+  // partials to its partner (same mg, nh) through LDS
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  w6_barrier();  // every wave is done with V: it becomes the exchange area
+  f32x4 y[2][2][NTW];  // [f - 2ph][output parity][q]
+  {
+    float* xo = reinterpret_cast<float*>(lds_raw) + (wave * 2 * NTW * 2) * 4 * 64;  // mine, out
+    const int pw = wave ^ 4;                                                        // partner
+    const float* xi = reinterpret_cast<const float*>(lds_raw) + (pw * 2 * NTW * 2) * 4 * 64;
+    // compile-time fragment indices per position half (a run-time index would put acc in memory)
+    auto part = [&](auto phc) {
+      constexpr int PH = decltype(phc)::value;
+#pragma unroll
+      for (int ff = 0; ff < 2; ++ff)
+#pragma unroll
+        for (int q = 0; q < NTW; ++q) {
+          constexpr int FO = 2 * (1 - PH), FK = 2 * PH;  // the partner's fragments, mine
+          f32x4 o0, o1, k0, k1;
+          if constexpr (PH == 0) {
+            o0 = acc[0][FO + ff][q] + acc[1][FO + ff][q]; o1 = acc[1][FO + ff][q];
+            k0 = acc[0][FK + ff][q] + acc[1][FK + ff][q]; k1 = acc[1][FK + ff][q];
+          } else {
+            o0 = acc[0][FO + ff][q]; o1 = -acc[0][FO + ff][q] - acc[1][FO + ff][q];
+            k0 = acc[0][FK + ff][q]; k1 = -acc[0][FK + ff][q] - acc[1][FK + ff][q];
+          }
+          *reinterpret_cast<f32x4*>(xo + ((ff * NTW + q) * 2 + 0) * 256 + lane * 4) = o0;
+          *reinterpret_cast<f32x4*>(xo + ((ff * NTW + q) * 2 + 1) * 256 + lane * 4) = o1;
+          y[ff][0][q] = k0;
+          y[ff][1][q] = k1;
+        }
+    };
+    if (ph == 0) part(std::integral_constant<int, 0>{});
+    else part(std::integral_constant<int, 1>{});
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    w6_barrier();
+#pragma unroll
+    for (int ff = 0; ff < 2; ++ff)
+#pragma unroll
+      for (int q = 0; q < NTW; ++q) {
+        // y0 = (m0 + m1) + m2, y1 = m1 + (-m2 - m3): ph 0's part first in both
+        const f32x4 i0 = *reinterpret_cast<const f32x4*>(xi + ((ff * NTW + q) * 2 + 0) * 256 + lane * 4);
+        const f32x4 i1 = *reinterpret_cast<const f32x4*>(xi + ((ff * NTW + q) * 2 + 1) * 256 + lane * 4);
+        if (ph == 0) { y[ff][0][q] = y[ff][0][q] + i0; y[ff][1][q] = y[ff][1][q] + i1; }
+        else { y[ff][0][q] = i0 + y[ff][0][q]; y[ff][1][q] = i1 + y[ff][1][q]; }
+      }
+  }
+  // epilogue: this wave's 4 tile rows 8mg + 4ph + r (fragment 2ph + r/2, half r%2), channels
+  // 48nh .. +47; the fragment's lane (li, lg) holds tiles 4lg .. 4lg+3 of the fragment's 16,
+  // i.e. row half lg >> 1, tiles 4 (lg & 1) + e -> pixels 2 (4 (lg & 1) + e) + parity
+  float* st = lraw + wave * 16 * C::PS;
+  f32x4 outr[4][NTW];  // rows as the vec epilogue's acc: pixel 4lg' + r of row m
+  // stage each row through LDS in the C/D map the epilogue expects: write the row's 16 pixels
+  // x 48 channels, read back as acc-layout registers
+#pragma unroll
+  for (int r4 = 0; r4 < 4; ++r4) {
+    const int ff = r4 >> 1, hf = r4 & 1;
+    if ((lg >> 1) == hf) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int t = 4 * (lg & 1) + e;
+#pragma unroll
+        for (int q = 0; q < NTW; ++q) {
+          st[(2 * t) * C::PS + 16 * q + li] = y[ff][0][q][e];
+          st[(2 * t + 1) * C::PS + 16 * q + li] = y[ff][1][q][e];
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+    for (int q = 0; q < NTW; ++q)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) outr[r4][q][rr] = st[(4 * lg + rr) * C::PS + 16 * q + li];
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+#ifdef DN_W6_NOEPI
+  float sum = 0.f;
+  for (int r4 = 0; r4 < 4; ++r4) for (int q = 0; q < NTW; ++q) for (int rr = 0; rr < 4; ++rr) sum += outr[r4][q][rr];
+  a.out[tid] = sum;
+#else
+  fwd_epilogue_at<NTW, 4, C::PS>(a, outr, st, ty0, tx0, n, 8 * mg + 4 * ph, nh * 16 * NTW, 16 * NTW);
+#endif
+}
+
+int w6_stages_per_chunk() { return WCfg::SPC; }
+
+// k_c3w6 for a 96-output-channel forward / data gradient on a PK_W6 image (a.x6_tail & X6_W6)
+hipError_t launch_fwd_w6(const FwdArgs& a, hipStream_t s) {
+  using C = WCfg;
+  const bool aux = a.epi == EPI_MASK || a.epi == EPI_BIAS_ADD;
+  const int tail = a.x6_tail & 7;
+  if (a.NOUT != 96 || a.zc || a.out_layout != OUT_NHWC || a.sel_rd ||
+      ((a.out_stride | a.out_off | a.NOUT) & 3) || (aux && ((a.mask_stride | a.mask_off) & 3)) ||
+      a.epi < EPI_BIAS || a.epi > EPI_BIAS_ADD || ((a.in_stride | a.in_off | a.K) & 3) ||
+      (long)C::IH * a.IWt * a.in_stride * 4 >= 0x7fffffffL || tail != x6_tail_mode(a.K))
+    return hipErrorInvalidValue;
+  const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
+  const dim3 grid(tx * ty, a.N, 1), block(C::WAVES * 64);
+  static const char* kn[3] = {"k_c3w6<0>", "k_c3w6<1>", "k_c3w6<2>"};
+  prof_kernel(kn[tail]);
+  if (tail == 1)
+    hipLaunchKernelGGL(k_c3w6<1>, grid, block, 0, s, a);
+  else if (tail == 2)
+    hipLaunchKernelGGL(k_c3w6<2>, grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL(k_c3w6<0>, grid, block, 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace dn

@@ -46,13 +46,6 @@ static std::string x6_kmore(std::string n, const char* last) {
 #define DN_X6_GDMA 0  // A/B switch: 1 = the 3x3 kernels' weight DMA as global_load_lds
 #endif
 
-// bf16 elements of one weight stage (one tap, three planes of NP x 32) in the packed image,
-// padded to whole rounds of the pipelined kernel's DMA (8 waves x 1 KiB dwordx4 LDS loads;
-// the 12-byte form would fit 18 KiB exactly, but it writes lane x 16 B in LDS, not lane x 12)
-__host__ __device__ constexpr int x6_wst(int np) {
-  return (3 * np * 32 * 2 + 8191) / 8192 * 8192 / 2;
-}
-
 template <int NT, int MT>
 struct XCfg {
   static constexpr int TW = 16, TH = 4 * MT, IH = TH + 2, IW = TW + 2, KC = 32, NP = 16 * NT;
@@ -1231,6 +1224,44 @@ __device__ __forceinline__ void pk_x6(const PackJob& j, long e) {
   if ((int)(r % (32L * NP)) < pad) st[3 * NP * 32 + (int)(r % (32L * NP))] = (__bf16)0.f;
 }
 
+// Winograd F(2,3) image of k_c3w6 (conv_w6.hip): [chunk][stage][piece][n < 96][32 k] as pk_x6,
+// stage 4 ky + p holding u_p = G g of kernel row ky (g = the three kx taps of (k, n)):
+// u = (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2), each rounded once from fp64, then split.
+// Last chunk (tail): 1: stage p, k = 4 ky + channel; 2: stage 2p + h, k = 16 (ky - 2h) + channel.
+__device__ __forceinline__ void pk_w6(const PackJob& j, long e) {
+  const int NP = j.g0, nch = j.nch, wst = x6_wst(NP), pad = wst - 3 * NP * 32;
+  const int kk = (int)(e % 32), nn = (int)((e / 32) % NP);
+  const int cs = (int)(e / (32L * NP)), c = cs / 12, s = cs % 12;
+  int ky = s >> 2, p = s & 3, k = c * 32 + kk;
+  bool live = true;
+  if (j.tail == 1 && c == nch - 1) {
+    p = s; ky = kk >> 2; k = c * 32 + (kk & 3);
+    live = s < 4 && kk < 12;
+  } else if (j.tail == 2 && c == nch - 1) {
+    p = s >> 1; ky = 2 * (s & 1) + (kk >> 4); k = c * 32 + (kk & 15);
+    live = s < 8 && ky < 3;
+  }
+  float v = 0.f;
+  if (live && k < j.K && nn < j.NOUT) {
+    double g[3];
+    for (int kx = 0; kx < 3; ++kx) {
+      const int t = 3 * ky + kx, tm = j.flip ? j.taps - 1 - t : t;
+      g[kx] = j.w[(long)k * j.sK + (long)nn * j.sN + (long)tm * j.sT];
+    }
+    const double u = p == 0 ? g[0] : (p == 1 ? (g[0] + g[1] + g[2]) * 0.5
+                                             : (p == 2 ? (g[0] - g[1] + g[2]) * 0.5 : g[2]));
+    v = (float)u;
+  }
+  __bf16 h, m, l;
+  split3(v, h, m, l);
+  __bf16* st = static_cast<__bf16*>(j.out) + (long)cs * wst;
+  const int o = nn * 32 + x6_swz(nn, kk >> 3) * 8 + (kk & 7);
+  st[o] = h;
+  st[NP * 32 + o] = m;
+  st[2 * NP * 32 + o] = l;
+  if ((int)(e % (32L * NP)) < pad) st[3 * NP * 32 + (int)(e % (32L * NP))] = (__bf16)0.f;
+}
+
 // the forward-family kernel's per-chunk LDS image [chunk][tap][k][n] (zero padded), one image
 // set per z (deconv forward: one per (a,b))
 __device__ __forceinline__ void pk_f32(const PackJob& j, long e) {
@@ -1313,6 +1344,7 @@ __global__ __launch_bounds__(256) void k_pack_batch(PackBatch b) {
     switch (j.kind) {
       case PK_F32: pk_f32(j, e); break;
       case PK_X6: pk_x6(j, e); break;
+      case PK_W6: pk_w6(j, e); break;
       case PK_DECONV_X6: pk_deconv_x6(j, e); break;
       case PK_HEAD_X6: pk_head_x6(j, e); break;
       case PK_DECONV_DGRAD_X6: pk_deconv_dgrad_x6(j, e); break;
@@ -1404,7 +1436,26 @@ long x6_pack_elems(int K, int nout, int zc) {
   const int np = x6_np(nout, zc);
   if (np == 0 || (zc > 0 && zc != np)) return -1;
   const int nz = zc > 0 ? (nout + zc - 1) / zc : 1;
-  return (long)nz * ((K + 31) / 32) * 9 * x6_wst(np);
+  // 96 outputs in one block: room for the Winograd image (12 stages per chunk) as well
+  const int spc = (np == 96 && nz == 1) ? 12 : 9;
+  return (long)nz * ((K + 31) / 32) * spc * x6_wst(np);
+}
+
+// DN_X6_W6=1/0: 96-output-channel large-grid launches on the Winograd kernel or not (default
+// DN_X6_W6_DEFAULT)
+#ifndef DN_X6_W6_DEFAULT
+#define DN_X6_W6_DEFAULT 0
+#endif
+static bool w6_enabled() {
+  static const bool on = getenv("DN_X6_W6") ? atoi(getenv("DN_X6_W6")) != 0 : DN_X6_W6_DEFAULT != 0;
+  return on;
+}
+
+int x6_image_mode(int N, int H, int W, int K, int nout, int zc, bool aligned) {
+  if (!aligned || !x6_pipelined(N, H, W, nout, zc)) return 0;
+  const int tail = x6_tail_mode(K);
+  const bool w6 = w6_enabled() && nout == 96 && zc == 0 && (tail != 0 || K % 32 == 0);
+  return tail | (w6 ? X6_W6 : 0);
 }
 
 int x6_tail_mode(int K) {
@@ -1412,9 +1463,13 @@ int x6_tail_mode(int K) {
   return r == 0 ? 0 : (r <= 4 ? 1 : (r <= 16 ? 2 : 0));
 }
 
-bool pack_job_x6(const WView& wv, int K, int nout, int zc, void* out, int tail, PackJob& j) {
+bool pack_job_x6(const WView& wv, int K, int nout, int zc, void* out, int mode, PackJob& j) {
   const long total = x6_pack_elems(K, nout, zc);
-  if (total < 0 || wv.taps != 9 || (tail && tail != x6_tail_mode(K))) return false;
+  const int tail = mode & 7;
+  const bool w6 = (mode & X6_W6) != 0;
+  if (total < 0 || wv.taps != 9 || (tail && tail != x6_tail_mode(K)) ||
+      (w6 && (nout != 96 || zc != 0)))
+    return false;
   WView v = wv;
   if (zc > 0) v.sZ = (long)zc * wv.sN;  // block z = output channels [z*zc, z*zc + zc)
   j = PackJob{};
@@ -1422,6 +1477,7 @@ bool pack_job_x6(const WView& wv, int K, int nout, int zc, void* out, int tail, 
   j.kind = PK_X6; j.out = out;
   j.K = K; j.NOUT = zc > 0 ? zc : nout; j.g0 = x6_np(nout, zc); j.nch = (K + 31) / 32;
   j.nz = zc > 0 ? (nout + zc - 1) / zc : 1; j.zc = zc; j.ntot = nout; j.tail = tail;
+  if (w6) j.kind = PK_W6;
   return true;
 }
 
@@ -1502,6 +1558,12 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
   const int np = x6_np(a.NOUT, a.zc);
   if (np == 0 || (a.zc > 0 && a.zc != np)) return hipErrorInvalidValue;
   const int nz = a.zc > 0 ? (a.NOUT + a.zc - 1) / a.zc : 1;
+  if (a.x6_tail & X6_W6) return launch_fwd_w6(a, s);  // a Winograd image (x6_image_mode)
+  // DN_X6_REG=1: the 96-channel large-grid shapes on k_c3x6r (weights in registers, conv_x6r.hip)
+  if (x6r_enabled() && np == 96 && (a.x6_tail || x6_pipelined(a.N, a.OH, a.OW, a.NOUT, a.zc))) {
+    hipError_t e = hipSuccess;
+    if (launch_fwd_x6r(a, s, e)) return e;
+  }
   // large grids: the pipelined 16-row kernel (one workgroup per CU, >= 2 rounds of tiles)
   static const bool no_pipe = getenv("DN_X6_NOPIPE") != nullptr;  // A/B probe
   // the pipelined kernel addresses one tile's 18 input rows through a 32-bit buffer resource

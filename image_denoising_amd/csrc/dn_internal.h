@@ -161,7 +161,7 @@ struct FwdGeom { int KC, TAPS, WNS, LW; };
 // images of a 96-channel deconv, the two bf16x6 head images, and a zero fill (the weight
 // gradients' 64-float DMA padding).  Strides of the weight view are element strides (< 2^31).
 enum PackKind { PK_F32 = 0, PK_X6 = 1, PK_DECONV_X6 = 2, PK_HEAD_X6 = 3, PK_ZERO = 4,
-                PK_DECONV_DGRAD_X6 = 5, PK_BF16 = 6 };
+                PK_DECONV_DGRAD_X6 = 5, PK_BF16 = 6, PK_W6 = 7 };
 struct PackJob {
   const float* w;   // view origin (WView.w + off); PK_HEAD_X6: nin_a, PK_DECONV_X6: raw weight
   const float* w2;  // PK_HEAD_X6: nin_b
@@ -182,6 +182,7 @@ __host__ __device__ inline long pack_job_elems(const PackJob& j) {
   switch (j.kind) {
     case PK_F32: return (long)j.nch * j.g3 * j.nz;
     case PK_X6: return (long)j.nz * j.nch * 9 * j.g0 * 32;
+    case PK_W6: return (long)j.nch * 12 * j.g0 * 32;
     case PK_DECONV_X6: return 4L * 3 * 3 * 96 * 32;
     case PK_HEAD_X6: return 2L * 3 * 3 * 96 * 32;
     case PK_DECONV_DGRAD_X6: return 4L * 3 * 3 * 96 * 32;
@@ -359,6 +360,17 @@ int x6_tail_mode(int K);
 // the launch takes the pipelined kernel (large grid), so a tail-packed image may be used
 bool x6_pipelined(int N, int H, int W, int nout, int zc);
 hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s);
+// k_c3x6r (conv_x6r.hip): 96-output-channel forward / data gradient with the weights in
+// registers; false = the arguments are not its case (err untouched)
+bool x6r_enabled();
+// k_c3w6 (conv_w6.hip): the 1-D Winograd F(2,3) bf16x6 kernel for 96 output channels, on a PK_W6
+// image; FwdArgs::x6_tail carries X6_W6 | x6_tail_mode(K) for it (see x6_image_mode)
+constexpr int X6_W6 = 8;
+hipError_t launch_fwd_w6(const FwdArgs& a, hipStream_t s);
+// the weight-image mode of a split-bf16 3x3 launch (pack and launch agree on it): the tail
+// packing of the last chunk on large grids with aligned views, | X6_W6 for the Winograd kernel
+int x6_image_mode(int N, int H, int W, int K, int nout, int zc, bool aligned);
+bool launch_fwd_x6r(const FwdArgs& a, hipStream_t s, hipError_t& err);
 hipError_t launch_pack_bf16(const WView& wv, int K, int nout, void* out, hipStream_t s,
                             int ksize = 3);
 hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize = 3);

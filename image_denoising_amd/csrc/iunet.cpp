@@ -143,6 +143,7 @@ hipError_t grun(int ksize, const View& in, int N, int H, int W, int K, const flo
 // tail packing of a partial last K chunk when the launch takes the pipelined kernel
 int x6_tail_for(const View& in, int N, int H, int W, int K, int nout) {
   const bool aligned = ((in.stride | in.off | K) & 3) == 0;
+  // (the direct kernels only: the Winograd image, x6_image_mode's X6_W6, is not used here)
   return aligned && x6_pipelined(N, H, W, nout, x6_zc(nout)) ? x6_tail_mode(K) : 0;
 }
 

@@ -409,10 +409,13 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // bias / activation / storage)
   // the pipelined split-bf16 kernel takes a partial last K chunk (dec_conv1a's x channels,
   // the 48-channel encoder's second chunk) packed over fewer stages (x6_tail_mode)
+  // (x6_image_mode: | X6_W6 for the Winograd kernel on the 96-output layers; dec_conv1b keeps
+  // the direct image in the N2N no-grad pass, whose pair-pixel kernel reads it)
   auto x6_tail_f = [&](int i) -> int {
     const Layer& L = p.P.L[i];
     const int l = layer_level(i);
-    return x6_pipelined(N, H(l), Wd(l), L.cout, 0) ? x6_tail_mode(i == D1A ? p.c1kp : L.cin) : 0;
+    const int m = x6_image_mode(N, H(l), Wd(l), i == D1A ? p.c1kp : L.cin, L.cout, 0, true);
+    return (i == D1B && sel_rd) ? (m & ~X6_W6) : m;
   };
   auto conv_forward = [&](const View& in, int Nn, int h, int w, int K, const float* wp,
                           const float* b, int cout, int ksize, int act, const View& out,
@@ -714,8 +717,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   auto V = [&](long off, int stride, int coff = 0) { return View{ws + off, stride, coff}; };
   auto x6_tail_b = [&](int i) -> int {  // as x6_tail_f in the forward, for the data gradients
     const int l = layer_level(i), nout = dgrad_nout(p, i);
-    return x6_pipelined(N, H(l), Wd(l), nout, x6_dgrad_zc(nout)) ? x6_tail_mode(p.P.L[i].cout)
-                                                                  : 0;
+    return x6_image_mode(N, H(l), Wd(l), p.P.L[i].cout, nout, x6_dgrad_zc(nout), true);
   };
   // bf16x6 data gradients of the 96-channel deconvs (DN_X6_DECONV=0: the fp32 kernel, A/B)
   static const bool x6_deconv = !getenv("DN_X6_DECONV") || atoi(getenv("DN_X6_DECONV")) != 0;

@@ -10,6 +10,13 @@ namespace dn {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
+// bf16 elements of one weight stage (one tap, three planes of NP x 32) in the packed image,
+// padded to whole rounds of the pipelined kernel's DMA (8 waves x 1 KiB dwordx4 LDS loads;
+// the 12-byte form would fit 18 KiB exactly, but it writes lane x 16 B in LDS, not lane x 12)
+__host__ __device__ constexpr int x6_wst(int np) {
+  return (3 * np * 32 * 2 + 8191) / 8192 * 8192 / 2;
+}
+
 // 16-B quad q of LDS row `row` lives at quad q ^ ((row >> 1) & 3)
 __device__ __forceinline__ int x6_swz(int row, int q) { return q ^ ((row >> 1) & 3); }
 
