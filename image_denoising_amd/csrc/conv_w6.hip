@@ -15,14 +15,14 @@
 // each m_p has the accuracy of an fp32 dot product; the transforms add one rounding of v and u
 // (measured against fp64 in tests/test_gpu_x6.py like the direct kernels).
 //
-//   Workgroup = 8 waves, one per CU (LDS), tile = 16 rows x 16 pixels (8 Winograd tiles per
-//   row) x 96 output channels.  Wave (mg, nh, ph) = (w & 1, (w >> 1) & 1, w >> 2): tile rows
-//   8mg .. 8mg+7 (four M fragments of 16 Winograd tiles = two rows each) x output channels
-//   48nh .. +47 (three N fragments) x positions 2ph, 2ph+1.  Per K chunk a wave runs 6 stages
-//   (kernel row ky, position p) of 4 x 3 fragments x 6 products = 72 MFMAs.
-//   * The transformed x tile V (18 input rows x 8 tiles x 4 positions x 32 channels, three bf16
-//     planes, 108 KiB) is built per chunk from a raw fp32 staging copy (the next chunk's raw x is
-//     loaded into registers and written to the staging area during the current chunk).
+//   Workgroup = 4 waves, two workgroups per CU, tile = 8 rows x 16 pixels (8 Winograd tiles per
+//   row) x 96 output channels.  Wave (nh, ph) = (w & 1, w >> 1): all 8 tile rows (four M
+//   fragments of 16 Winograd tiles = two rows each) x output channels 48nh .. +47 (three N
+//   fragments) x positions 2ph, 2ph+1.  Per K chunk a wave runs 6 stages (kernel row ky,
+//   position p) of 4 x 3 fragments x 6 products = 72 MFMAs.
+//   * Per chunk the workgroup first builds the transformed x tile V (10 input rows x 8 tiles x 4
+//     positions x 32 channels, three bf16 planes, 60 KiB) straight from global loads, between two
+//     barriers; the other workgroup on the CU keeps the matrix cores busy meanwhile.
 //   * Weights come straight from the pre-split image (k_pack_batch PK_W6) into registers: each
 //     N fragment of the next stage is requested right after its last use in this one.
 //   * After the last chunk the two position halves exchange partial output sums through LDS.
@@ -36,23 +36,19 @@
 namespace dn {
 
 struct WCfg {
-  static constexpr int WAVES = 8, MT = 4, NTW = 3, NP = 96, NPOS = 4, NJ = 8;
-  static constexpr int TW = 16, TH = 16, IH = TH + 2, IW = TW + 2, KC = 32;
+  static constexpr int WAVES = 4, MT = 4, NTW = 3, NP = 96, NPOS = 4, NJ = 8;
+  static constexpr int TW = 16, TH = 8, IH = TH + 2, IW = TW + 2, KC = 32;
   static constexpr int SPC = 12;                       // weight stages per full chunk (ky, p)
   static constexpr int VPL = IH * 4 * NJ * NPOS * 8;   // bf16 per plane of V (quads of 8)
   static constexpr int VBYTES = 3 * VPL * 2;
-  static constexpr int XS = 36;                        // floats per pixel of the raw staging
-  static constexpr int RAWB = IH * IW * XS * 4;
   static constexpr int WPL = NP * KC;
   static constexpr int WSTP = x6_wst(NP);
-  static constexpr int XQ = IH * IW * (KC / 4);        // float4 items of a raw x tile
-  static constexpr int XITEMS = (XQ + WAVES * 64 - 1) / (WAVES * 64);
   static constexpr int VITEMS = (IH * NJ * 8 + WAVES * 64 - 1) / (WAVES * 64);  // transform items
   static constexpr int PS = 16 * NTW + 4;
-  static constexpr int LBYTES = VBYTES + RAWB;
-  static_assert(LBYTES <= 163840, "one workgroup per CU");
-  static_assert(WAVES * 16 * PS * 4 <= RAWB, "epilogue staging inside the raw area");
-  static_assert(WAVES * 2 * NTW * 2 * 4 * 64 * 4 <= VBYTES, "exchange inside V");
+  static constexpr int XCH = WAVES * 2 * NTW * 2 * 4 * 64;  // floats of the exchange area
+  static constexpr int LEND = (XCH + WAVES * 16 * PS) * 4;  // exchange + epilogue staging (over V)
+  static constexpr int LBYTES = VBYTES > LEND ? VBYTES : LEND;
+  static_assert(2 * LBYTES <= 163840, "two workgroups per CU");
 };
 
 // 16-B quad index of V element (row, kq, j, p): p is XOR-swizzled by j >> 2 and row & 1, so the
@@ -68,6 +64,17 @@ __device__ __forceinline__ void w6_barrier() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
+// diagnostic ablations (wrong results, timing only): NOT = V built for the first chunk only,
+// NOW = no weight loads in the stage loop
+#ifndef DN_W6_ABL_NOT
+#define DN_W6_ABL_NOT 0
+#endif
+#ifndef DN_W6_ABL_NOW
+#define DN_W6_ABL_NOW 0
+#endif
+#ifndef DN_W6_TG
+#define DN_W6_TG 3  // transform items whose x loads are in flight together
+#endif
 #ifndef DN_W6_GM
 #define DN_W6_GM 1
 #endif
@@ -84,17 +91,16 @@ __device__ __forceinline__ void w6_for(F&& f) {
 // position, k = 4 ky + channel; 2 (<= 16 channels): two stages per position, k = 16 (ky - 2s) +
 // channel.  Full chunks: stage 4 ky + p, k = channel.
 template <int TAIL>
-__global__ __launch_bounds__(512, 1) void k_c3w6(FwdArgs a) {
+__global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   using C = WCfg;
   constexpr int MT = C::MT, NTW = C::NTW;
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
   __bf16* lv = reinterpret_cast<__bf16*>(lds_raw);
-  float* lraw = reinterpret_cast<float*>(lds_raw + C::VBYTES);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lg = lane >> 4;
-  const int mg = wave & 1, nh = (wave >> 1) & 1, ph = wave >> 2;
+  const int nh = wave & 1, ph = wave >> 1;
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
   int bxr, byr;
   xcd_tile(bxr, byr);
@@ -112,54 +118,45 @@ __global__ __launch_bounds__(512, 1) void k_c3w6(FwdArgs a) {
 #pragma unroll
       for (int q = 0; q < NTW; ++q) acc[pi][f][q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // raw x tile of a chunk: XITEMS float4 per thread (out-of-range offsets read zeros)
+  // x rows of the tile through a 32-bit buffer resource (out-of-range offsets read zeros)
   const int ry0 = iy0 > 0 ? iy0 : 0, ry1 = iy0 + C::IH < a.IHt ? iy0 + C::IH : a.IHt;
   const long row_floats = (long)a.IWt * a.in_stride;
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(inb + ry0 * row_floats), (short)0, (int)((ry1 - ry0) * row_floats * 4),
       0x00020000);
-  f32x4 xr[C::XITEMS];
-  auto load_x = [&](int k0, int tid, int i0, int i1) {
+  // chunk k0's V: item (row, j, c4) = channels 4c4 .. 4c4+3 of Winograd tile j of input row row,
+  // from the four input pixels 2j .. 2j+3 of the halo tile (loaded for all of a thread's items
+  // first, so their latencies overlap)
+  auto transform = [&](int k0, int tid) {
 #pragma unroll
-    for (int it = i0; it < i1; ++it) {
-      const int e = tid + it * C::WAVES * 64;
-      const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
-      const int iy = pix / C::IW, ix = pix - iy * C::IW;
-      const int gy = iy0 + iy, gx = ix0 + ix, k = k0 + 4 * q;
-      const bool ok = e < C::XQ && gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt && k < a.K;
-      const int off = ok ? (((gy - ry0) * a.IWt + gx) * a.in_stride + k) * 4 : 0x7fffffff;
-      xr[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-    }
-  };
-  auto store_raw = [&](int tid, int i0, int i1) {
+    for (int ig = 0; ig < C::VITEMS; ig += DN_W6_TG) {
+    f32x4 d[C::VITEMS][4];
 #pragma unroll
-    for (int it = i0; it < i1; ++it) {
+    for (int it = ig; it < ig + DN_W6_TG && it < C::VITEMS; ++it) {
       const int e = tid + it * C::WAVES * 64;
-      if (e < C::XQ) {
-        const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
-        *reinterpret_cast<f32x4*>(lraw + pix * C::XS + 4 * q) = xr[it];
+      const int c4 = e & 7, j = (e >> 3) & 7, row = e >> 6;
+      const int gy = iy0 + row, k = k0 + 4 * c4;
+      const bool rok = e < C::IH * C::NJ * 8 && gy >= 0 && gy < a.IHt && k < a.K;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int gx = ix0 + 2 * j + i;
+        const bool ok = rok && gx >= 0 && gx < a.IWt;
+        const int off = ok ? (((gy - ry0) * a.IWt + gx) * a.in_stride + k) * 4 : 0x7fffffff;
+        d[it][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
       }
     }
-  };
-  // raw staging -> V: item (row, j, c4) transforms channels 4c4 .. 4c4+3 of Winograd tile j
-  auto transform = [&](int tid) {
 #pragma unroll
-    for (int it = 0; it < C::VITEMS; ++it) {
+    for (int it = ig; it < ig + DN_W6_TG && it < C::VITEMS; ++it) {
       const int e = tid + it * C::WAVES * 64;
       if (e < C::IH * C::NJ * 8) {
         const int c4 = e & 7, j = (e >> 3) & 7, row = e >> 6;
-        const float* r = lraw + (row * C::IW + 2 * j) * C::XS + 4 * c4;
-        const f32x4 d0 = *reinterpret_cast<const f32x4*>(r);
-        const f32x4 d1 = *reinterpret_cast<const f32x4*>(r + C::XS);
-        const f32x4 d2 = *reinterpret_cast<const f32x4*>(r + 2 * C::XS);
-        const f32x4 d3 = *reinterpret_cast<const f32x4*>(r + 3 * C::XS);
         f32x4 v[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          v[0][c] = d0[c] - d2[c];
-          v[1][c] = d1[c] + d2[c];
-          v[2][c] = d2[c] - d1[c];
-          v[3][c] = d1[c] - d3[c];
+          v[0][c] = d[it][0][c] - d[it][2][c];
+          v[1][c] = d[it][1][c] + d[it][2][c];
+          v[2][c] = d[it][2][c] - d[it][1][c];
+          v[3][c] = d[it][1][c] - d[it][3][c];
         }
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
@@ -173,6 +170,7 @@ __global__ __launch_bounds__(512, 1) void k_c3w6(FwdArgs a) {
           *reinterpret_cast<u32x2_t*>(lv + 2 * C::VPL + o) = u32x2_t{l0, l1};
         }
       }
+    }
     }
   };
 
@@ -214,7 +212,7 @@ __global__ __launch_bounds__(512, 1) void k_c3w6(FwdArgs a) {
     bf16x8 av[3][MT];
 #pragma unroll
     for (int f = 0; f < MT; ++f) {
-      const int row0 = 8 * mg + 2 * f + (liv >> 3), j = liv & 7;
+      const int row0 = 2 * f + (liv >> 3), j = liv & 7;
       if constexpr (MODE == 0) {
         const int o = w6_vq(row0 + ky0, lgv, j, p) * 8;
 #pragma unroll
@@ -264,7 +262,7 @@ __global__ __launch_bounds__(512, 1) void k_c3w6(FwdArgs a) {
           for (int i = 0; i < GM; ++i) asm volatile("" : "+v"(ah[i][q]));
           __builtin_amdgcn_sched_barrier(0);
         }
-        if (nxt >= 0) load_wq(nxt, q);
+        if (nxt >= 0 && !DN_W6_ABL_NOW) load_wq(nxt, q);
         __builtin_amdgcn_sched_barrier(0);
       }
     };
@@ -272,70 +270,53 @@ __global__ __launch_bounds__(512, 1) void k_c3w6(FwdArgs a) {
     else run(std::integral_constant<int, 1>{});
   };
 
-  // prologue: stage 0's weights, chunk 0's x tile -> raw -> V
+  // first stage's weights; then per chunk: V built between two barriers, then its stages
   const bool tail_only = TAIL && nch == 1;
 #pragma unroll
   for (int q = 0; q < NTW; ++q) load_wq(stage_of(0, 0, tail_only), q);
-  load_x(0, tid, 0, C::XITEMS);
-  store_raw(tid, 0, C::XITEMS);
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  w6_barrier();
-  transform(tid);
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  w6_barrier();
-
-  constexpr int XG = 3, XPG = (C::XITEMS + XG - 1) / XG;
+  const int nfull = TAIL ? nch - 1 : nch;  // full chunks; a tail-packed last one after the loop
 #pragma unroll 1
-  for (int c = 0; c < nch; ++c) {
+  for (int c = 0; c < nfull; ++c) {
     int liv = li, lgv = lg, tidv = tid;
     asm volatile("" : "+v"(liv), "+v"(lgv), "+v"(tidv));
     const bool more = c + 1 < nch;
-    const bool tailc = TAIL && !more;
     const bool next_tail = TAIL && c + 2 == nch;
-    if (tailc) {
-      constexpr int NS = TAIL == 1 ? 2 : 4;
-      using MD = std::integral_constant<int, TAIL == 1 ? 1 : 2>;
-      w6_for<0, NS>([&](auto si) {
-        constexpr int s = decltype(si)::value;
-        stage(MD{}, s, s + 1 < NS ? stage_of(c, s + 1, true) : -1, liv, lgv);
-      });
-      break;
-    }
-    // a full chunk: 6 stages; the next chunk's raw x in three groups (loaded at stages 0, 2, 4
-    // after the stage's weight requests, written to the staging area two stages later)
+    if (c > 0) w6_barrier();  // every wave is done with the previous chunk's V
+    if (!DN_W6_ABL_NOT || c == 0) transform(c * C::KC, tidv);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own V stores done
+    w6_barrier();
     w6_for<0, 6>([&](auto si) {
       constexpr int s = decltype(si)::value;
       const int nxt = s + 1 < 6 ? stage_of(c, s + 1, false) : (more ? stage_of(c + 1, 0, next_tail) : -1);
-      if constexpr (s >= 2 && s % 2 == 0) {
-        constexpr int g = s / 2 - 1;
-        if (more) store_raw(tidv, g * XPG, (g + 1) * XPG < C::XITEMS ? (g + 1) * XPG : C::XITEMS);
-      }
       stage(std::integral_constant<int, 0>{}, s, nxt, liv, lgv);
-      if constexpr (s % 2 == 0) {
-        constexpr int g = s / 2;
-        if (more) load_x((c + 1) * C::KC, tidv, g * XPG, (g + 1) * XPG < C::XITEMS ? (g + 1) * XPG : C::XITEMS);
-      }
     });
-    if (more) {
-      store_raw(tidv, 2 * XPG, C::XITEMS);
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      w6_barrier();  // every wave done with V; the raw tile complete
-      transform(tidv);
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      w6_barrier();  // V of the next chunk complete
-    }
+  }
+  if constexpr (TAIL != 0) {
+    const int c = nch - 1;
+    int liv = li, lgv = lg, tidv = tid;
+    asm volatile("" : "+v"(liv), "+v"(lgv), "+v"(tidv));
+    if (c > 0) w6_barrier();
+    transform(c * C::KC, tidv);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    w6_barrier();
+    constexpr int NS = TAIL == 1 ? 2 : 4;
+    using MD = std::integral_constant<int, TAIL == 1 ? 1 : 2>;
+    w6_for<0, NS>([&](auto si) {
+      constexpr int s = decltype(si)::value;
+      stage(MD{}, s, s + 1 < NS ? stage_of(c, s + 1, true) : -1, liv, lgv);
+    });
   }
 
   // output transform: ph 0 holds m0, m1, ph 1 holds m2, m3.  Partial sums per tile:
   //   ph 0: (y0, y1) += (m0 + m1, m1);   ph 1: (y0, y1) += (m2, -m2 - m3)
-  // wave ph keeps M fragments 2ph, 2ph+1 (tile rows 8mg + 4ph .. +3) and hands the other two's
-  // partials to its partner (same mg, nh) through LDS
+  // wave ph keeps M fragments 2ph, 2ph+1 (tile rows 4ph .. 4ph+3) and hands the other two's
+  // partials to its partner (same nh) through LDS
   __builtin_amdgcn_s_waitcnt(0xC07F);
   w6_barrier();  // every wave is done with V: it becomes the exchange area
   f32x4 y[2][2][NTW];  // [f - 2ph][output parity][q]
   {
     float* xo = reinterpret_cast<float*>(lds_raw) + (wave * 2 * NTW * 2) * 4 * 64;  // mine, out
-    const int pw = wave ^ 4;                                                        // partner
+    const int pw = wave ^ 2;                                                        // partner
     const float* xi = reinterpret_cast<const float*>(lds_raw) + (pw * 2 * NTW * 2) * 4 * 64;
     // compile-time fragment indices per position half (a run-time index would put acc in memory)
     auto part = [&](auto phc) {
@@ -374,10 +355,10 @@ __global__ __launch_bounds__(512, 1) void k_c3w6(FwdArgs a) {
         else { y[ff][0][q] = i0 + y[ff][0][q]; y[ff][1][q] = i1 + y[ff][1][q]; }
       }
   }
-  // epilogue: this wave's 4 tile rows 8mg + 4ph + r (fragment 2ph + r/2, half r%2), channels
+  // epilogue: this wave's 4 tile rows 4ph + r (fragment 2ph + r/2, half r%2), channels
   // 48nh .. +47; the fragment's lane (li, lg) holds tiles 4lg .. 4lg+3 of the fragment's 16,
   // i.e. row half lg >> 1, tiles 4 (lg & 1) + e -> pixels 2 (4 (lg & 1) + e) + parity
-  float* st = lraw + wave * 16 * C::PS;
+  float* st = reinterpret_cast<float*>(lds_raw) + C::XCH + wave * 16 * C::PS;
   f32x4 outr[4][NTW];  // rows as the vec epilogue's acc: pixel 4lg' + r of row m
   // stage each row through LDS in the C/D map the epilogue expects: write the row's 16 pixels
   // x 48 channels, read back as acc-layout registers
@@ -407,7 +388,7 @@ __global__ __launch_bounds__(512, 1) void k_c3w6(FwdArgs a) {
   for (int r4 = 0; r4 < 4; ++r4) for (int q = 0; q < NTW; ++q) for (int rr = 0; rr < 4; ++rr) sum += outr[r4][q][rr];
   a.out[tid] = sum;
 #else
-  fwd_epilogue_at<NTW, 4, C::PS>(a, outr, st, ty0, tx0, n, 8 * mg + 4 * ph, nh * 16 * NTW, 16 * NTW);
+  fwd_epilogue_at<NTW, 4, C::PS>(a, outr, st, ty0, tx0, n, 4 * ph, nh * 16 * NTW, 16 * NTW);
 #endif
 }
 

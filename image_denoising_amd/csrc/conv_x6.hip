@@ -1444,7 +1444,7 @@ long x6_pack_elems(int K, int nout, int zc) {
 // DN_X6_W6=1/0: 96-output-channel large-grid launches on the Winograd kernel or not (default
 // DN_X6_W6_DEFAULT)
 #ifndef DN_X6_W6_DEFAULT
-#define DN_X6_W6_DEFAULT 0
+#define DN_X6_W6_DEFAULT 1
 #endif
 static bool w6_enabled() {
   static const bool on = getenv("DN_X6_W6") ? atoi(getenv("DN_X6_W6")) != 0 : DN_X6_W6_DEFAULT != 0;
