@@ -127,16 +127,20 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   // chunk k0's V: item (row, j, c4) = channels 4c4 .. 4c4+3 of Winograd tile j of input row row,
   // from the four input pixels 2j .. 2j+3 of the halo tile (loaded for all of a thread's items
   // first, so their latencies overlap)
-  auto transform = [&](int k0, int tid) {
+  // (C4: channel quads transformed -- 8 for a full chunk, the ones a tail stage reads for the
+  // tail chunk: 1 for mode 1, 4 for mode 2)
+  auto transform = [&](auto c4tag, int k0, int tid) {
+    constexpr int C4 = decltype(c4tag)::value, NIT = C::IH * C::NJ * C4;
+    constexpr int VIT = (NIT + C::WAVES * 64 - 1) / (C::WAVES * 64);
 #pragma unroll
-    for (int ig = 0; ig < C::VITEMS; ig += DN_W6_TG) {
+    for (int ig = 0; ig < VIT; ig += DN_W6_TG) {
     f32x4 d[C::VITEMS][4];
 #pragma unroll
-    for (int it = ig; it < ig + DN_W6_TG && it < C::VITEMS; ++it) {
+    for (int it = ig; it < ig + DN_W6_TG && it < VIT; ++it) {
       const int e = tid + it * C::WAVES * 64;
-      const int c4 = e & 7, j = (e >> 3) & 7, row = e >> 6;
+      const int c4 = e % C4, j = (e / C4) & 7, row = e / (8 * C4);
       const int gy = iy0 + row, k = k0 + 4 * c4;
-      const bool rok = e < C::IH * C::NJ * 8 && gy >= 0 && gy < a.IHt && k < a.K;
+      const bool rok = e < NIT && gy >= 0 && gy < a.IHt && k < a.K;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int gx = ix0 + 2 * j + i;
@@ -146,10 +150,10 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
       }
     }
 #pragma unroll
-    for (int it = ig; it < ig + DN_W6_TG && it < C::VITEMS; ++it) {
+    for (int it = ig; it < ig + DN_W6_TG && it < VIT; ++it) {
       const int e = tid + it * C::WAVES * 64;
-      if (e < C::IH * C::NJ * 8) {
-        const int c4 = e & 7, j = (e >> 3) & 7, row = e >> 6;
+      if (e < NIT) {
+        const int c4 = e % C4, j = (e / C4) & 7, row = e / (8 * C4);
         f32x4 v[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -282,7 +286,7 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
     const bool more = c + 1 < nch;
     const bool next_tail = TAIL && c + 2 == nch;
     if (c > 0) w6_barrier();  // every wave is done with the previous chunk's V
-    if (!DN_W6_ABL_NOT || c == 0) transform(c * C::KC, tidv);
+    if (!DN_W6_ABL_NOT || c == 0) transform(std::integral_constant<int, 8>{}, c * C::KC, tidv);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own V stores done
     w6_barrier();
     w6_for<0, 6>([&](auto si) {
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
     int liv = li, lgv = lg, tidv = tid;
     asm volatile("" : "+v"(liv), "+v"(lgv), "+v"(tidv));
     if (c > 0) w6_barrier();
-    transform(c * C::KC, tidv);
+    transform(std::integral_constant<int, TAIL == 1 ? 1 : 4>{}, c * C::KC, tidv);
     __builtin_amdgcn_s_waitcnt(0xC07F);
     w6_barrier();
     constexpr int NS = TAIL == 1 ? 2 : 4;

@@ -409,15 +409,15 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // bias / activation / storage)
   // the pipelined split-bf16 kernel takes a partial last K chunk (dec_conv1a's x channels,
   // the 48-channel encoder's second chunk) packed over fewer stages (x6_tail_mode)
-  // (x6_image_mode: | X6_W6 for the Winograd kernel on the 96-output layers.  dec_conv1b's
-  // forward stays on the direct kernel: the N2N no-grad pass evaluates it at the pair pixels only
-  // (k_c3x6s, direct arithmetic), and that pass is bit-identical to the full forward only if the
-  // full forward's dec_conv1b is the direct kernel too -- test_unet_forward_n2n_pair_pixels_bit_identical)
+  // (x6_image_mode: | X6_W6 for the Winograd kernel on the 96-output layers.  In forward-only
+  // plans dec_conv1b stays on the direct kernel: the N2N no-grad pass evaluates it at the pair
+  // pixels only (k_c3x6s, direct arithmetic), bit-identical to the full no-grad forward only if
+  // that one's dec_conv1b is direct too -- test_unet_forward_n2n_pair_pixels_bit_identical)
   auto x6_tail_f = [&](int i) -> int {
     const Layer& L = p.P.L[i];
     const int l = layer_level(i);
     const int m = x6_image_mode(N, H(l), Wd(l), i == D1A ? p.c1kp : L.cin, L.cout, 0, true);
-    return i == D1B ? (m & ~X6_W6) : m;
+    return (i == D1B && !p.with_bwd) ? (m & ~X6_W6) : m;
   };
   auto conv_forward = [&](const View& in, int Nn, int h, int w, int K, const float* wp,
                           const float* b, int cout, int ksize, int act, const View& out,
