@@ -204,6 +204,37 @@ __device__ __forceinline__ void fwd_epilogue_vec_at(const FwdArgs& a, const f32x
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, lg = lane >> 4;
   const int NQ = nout >> 2;
+  if constexpr (EPI == EPI_BIAS_ACT && MT % 2 == 0) {
+    // fused 2x2 max-pool (FwdArgs::pool_out): rows m, m+1 of the wave and pixels 4lg + 2h, +1
+    // of a lane are one window; each member activated exactly as below, then k_pool_fwd's
+    // window order (TL, TR, BL, BR; a later member wins only if greater or NaN)
+    if (a.pool_out) {
+      const int OH2 = a.OH >> 1, OW2 = a.OW >> 1;
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        const int c = 16 * q + li;
+        const float b = (c < nout && a.bias) ? a.bias[cz + c] : 0.f;
+#pragma unroll
+        for (int m = 0; m < MT; m += 2)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            float v[4] = {acc[m][q][2 * h], acc[m][q][2 * h + 1], acc[m + 1][q][2 * h],
+                          acc[m + 1][q][2 * h + 1]};
+            float mx = 0.f;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              float x = v[t] + b;
+              x = x > 0.f ? x : x * 0.2f;
+              mx = (t == 0 || x > mx || __builtin_isnan(x)) ? x : mx;
+            }
+            const int gy2 = (ty0 + wrow + m) >> 1, gx2 = (tx0 >> 1) + 2 * lg + h;
+            if (c < nout && gy2 < OH2 && gx2 < OW2)
+              a.pool_out[((long)n * OH2 + gy2) * OW2 * a.pool_stride + (long)gx2 * a.pool_stride +
+                         a.pool_off + cz + c] = mx;
+          }
+      }
+    }
+  }
   const bool has_bias = BIAS && a.bias != nullptr;
   float4 bvec[NIT];
 #pragma unroll

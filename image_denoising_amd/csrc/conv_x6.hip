@@ -1452,10 +1452,12 @@ static bool w6_enabled() {
 }
 
 int x6_image_mode(int N, int H, int W, int K, int nout, int zc, bool aligned) {
-  if (!aligned || !x6_pipelined(N, H, W, nout, zc)) return 0;
-  const int tail = x6_tail_mode(K);
-  const bool w6 = w6_enabled() && nout == 96 && zc == 0 && (tail != 0 || K % 32 == 0);
-  return tail | (w6 ? X6_W6 : 0);
+  if (!aligned) return 0;
+  // k_c3w6 (8 x 16 tiles, two workgroups per CU) from one full round of resident workgroups
+  const long t8 = (long)N * ((H + 7) / 8) * ((W + 15) / 16);
+  const bool w6 = w6_enabled() && nout == 96 && zc == 0 && t8 >= 512;
+  if (!w6 && !x6_pipelined(N, H, W, nout, zc)) return 0;
+  return x6_tail_mode(K) | (w6 ? X6_W6 : 0);
 }
 
 int x6_tail_mode(int K) {
@@ -1557,6 +1559,10 @@ bool x6_pipelined(int N, int H, int W, int nout, int zc) {
 hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
   const int np = x6_np(a.NOUT, a.zc);
   if (np == 0 || (a.zc > 0 && a.zc != np)) return hipErrorInvalidValue;
+  // a fused pool: the float4 epilogue of a tiled kernel (k_c3w6 has none), even sides
+  if (a.pool_out && (a.epi != EPI_BIAS_ACT || a.out_layout != OUT_NHWC || (a.x6_tail & X6_W6) ||
+                     ((a.out_stride | a.out_off | a.NOUT) & 3) || ((a.OH | a.OW) & 1)))
+    return hipErrorInvalidValue;
   const int nz = a.zc > 0 ? (a.NOUT + a.zc - 1) / a.zc : 1;
   if (a.x6_tail & X6_W6) return launch_fwd_w6(a, s);  // a Winograd image (x6_image_mode)
   // DN_X6_REG=1: the 96-channel large-grid shapes on k_c3x6r (weights in registers, conv_x6r.hip)
@@ -1595,11 +1601,13 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
     return run();
   }
   if (!no_pipe && x6_pipelined(a.N, a.OH, a.OW, a.NOUT, a.zc) && aligned) return run();
+  // (a fused pool needs an even number of tile rows per wave: MT = 2)
+  const bool pool = a.pool_out != nullptr;
   if (np == 32)
-    return x6_pick_mt<2>(a, nz) == 2 ? run_x6<2, 2>(a, nz, s) : run_x6<2, 1>(a, nz, s);
+    return pool || x6_pick_mt<2>(a, nz) == 2 ? run_x6<2, 2>(a, nz, s) : run_x6<2, 1>(a, nz, s);
   if (np == 48)
-    return x6_pick_mt<3>(a, nz) == 2 ? run_x6<3, 2>(a, nz, s) : run_x6<3, 1>(a, nz, s);
-  return x6_pick_mt<6>(a, nz) == 2 ? run_x6<6, 2>(a, nz, s) : run_x6<6, 1>(a, nz, s);
+    return pool || x6_pick_mt<3>(a, nz) == 2 ? run_x6<3, 2>(a, nz, s) : run_x6<3, 1>(a, nz, s);
+  return pool || x6_pick_mt<6>(a, nz) == 2 ? run_x6<6, 2>(a, nz, s) : run_x6<6, 1>(a, nz, s);
 }
 
 
@@ -1617,6 +1625,9 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
 // added to the fp32 accumulators.  Wave (wm, wn): MFW output-channel fragments x 16 input
 // channels x 9 taps; the bias gradient is the G pieces against a ones fragment.
 // ------------------------------------------------------------------------------------
+#ifndef DN_WG_ABL_NOSPLIT
+#define DN_WG_ABL_NOSPLIT 0
+#endif
 template <int CO_FR, int WM, int WN>
 struct Ws3Cfg {
   static constexpr int COUT = 16 * CO_FR, MFW = CO_FR / WM, CIB = 16 * WN;
@@ -1758,7 +1769,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
       float v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = lgs[(8 * lg + j) * C::GS + (wm * MFW + i) * 16 + li];
+#if DN_WG_ABL_NOSPLIT  // diagnostic ablation (wrong results): one bf16 plane, no split VALU
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { av[0][i][j] = (__bf16)v[j]; av[1][i][j] = av[0][i][j]; av[2][i][j] = av[0][i][j]; }
+#else
       split3x8(v, av[0][i], av[1][i], av[2][i]);
+#endif
 #pragma unroll
       for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(av[p][i]));  // kept, not re-split per tap
     }
@@ -1771,7 +1787,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
       for (int m = 0; m < 10; ++m) w[m] = xr[m * C::XS];
       unsigned P[3][5];
 #pragma unroll
-      for (int d = 0; d < 5; ++d) split3x2(w[2 * d], w[2 * d + 1], P[0][d], P[1][d], P[2][d]);
+      for (int d = 0; d < 5; ++d) {
+#if DN_WG_ABL_NOSPLIT
+        P[0][d] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t{w[2 * d], w[2 * d + 1]}), bf16x2_t));
+        P[1][d] = P[0][d]; P[2][d] = P[0][d];
+#else
+        split3x2(w[2 * d], w[2 * d + 1], P[0][d], P[1][d], P[2][d]);
+#endif
+      }
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         bf16x8 bv[3][1];

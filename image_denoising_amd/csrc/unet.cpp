@@ -413,15 +413,22 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // plans dec_conv1b stays on the direct kernel: the N2N no-grad pass evaluates it at the pair
   // pixels only (k_c3x6s, direct arithmetic), bit-identical to the full no-grad forward only if
   // that one's dec_conv1b is direct too -- test_unet_forward_n2n_pair_pixels_bit_identical)
+  // the encoder's 2x2 max-pools fused into the x6 convs' epilogues (DN_POOL_FUSE=0: separate
+  // k_pool_fwd launches, A/B)
+  static const bool pool_fuse = !getenv("DN_POOL_FUSE") || atoi(getenv("DN_POOL_FUSE")) != 0;
   auto x6_tail_f = [&](int i) -> int {
     const Layer& L = p.P.L[i];
     const int l = layer_level(i);
     const int m = x6_image_mode(N, H(l), Wd(l), i == D1A ? p.c1kp : L.cin, L.cout, 0, true);
     return (i == D1B && !p.with_bwd) ? (m & ~X6_W6) : m;
   };
+  // pool (x6 path, EPI_BIAS_ACT): the 2x2 max-pool of `out` fused into the conv's epilogue into
+  // that view (*pooled set); otherwise the caller pools
   auto conv_forward = [&](const View& in, int Nn, int h, int w, int K, const float* wp,
                           const float* b, int cout, int ksize, int act, const View& out,
-                          int layout, hipStream_t st) -> hipError_t {
+                          int layout, hipStream_t st, const View* pool = nullptr,
+                          bool* pooled = nullptr) -> hipError_t {
+    if (pooled) *pooled = false;
     const OpTimer timer(st, ksize == 3 ? "fwd3" : "fwd1",
                         2.0 * Nn * h * w * K * cout * ksize * ksize, K, cout, h, w, Nn);
     int i = ENC1;
@@ -436,6 +443,10 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
       a.x6_tail = x6_tail_f(i);  // a partial last K chunk packed over fewer stages
       a.wp = ws + p.packX[i]; a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
       a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = layout;
+      if (pool && pool_fuse && act && layout == OUT_NHWC && !(a.x6_tail & X6_W6)) {
+        a.pool_out = pool->p; a.pool_stride = pool->stride; a.pool_off = pool->off;
+        if (pooled) *pooled = true;
+      }
       return launch_fwd_x6(a, st);
     }
     if (!bf16 || i == NL || p.packBF[i] < 0)
@@ -539,23 +550,25 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   DN_TIMED(s, "enc0", 2.0 * N * p.H * p.W * C * nf * 9, C, nf, p.H, p.W, N,
            launch_enc0_fwd(x, N, C, p.H, p.W, prm + p.P.L[ENC0].woff, Bs(ENC0), ws + p.a0,
                            ws + p.c1, p.c1s, 2 * nf, p.c1kp, p.with_bwd ? ws + p.xin : nullptr, s));
-  DN_TRY(conv_forward(V(p.a0, nf), N, H(0), Wd(0), nf, Wt(ENC1), Bs(ENC1), nf, 3, 1, V(p.a1, nf),
-                      OUT_NHWC, s));
-  // pool1 -> skip slice of c2
-  DN_TIMED(s, "pool", 0, 0, 0, 0, 0, 0, launch_pool_fwd(ws + p.a1, N, H(0), Wd(0), nf, ws + p.c[1], p.cs[1], 2 * nf, s));
+  {  // enc_conv1 + pool1 -> skip slice of c2
+    const View pv = V(p.c[1], p.cs[1], 2 * nf);
+    bool pooled = false;
+    DN_TRY(conv_forward(V(p.a0, nf), N, H(0), Wd(0), nf, Wt(ENC1), Bs(ENC1), nf, 3, 1,
+                        V(p.a1, nf), OUT_NHWC, s, &pv, &pooled));
+    if (!pooled)
+      DN_TIMED(s, "pool", 0, 0, 0, 0, 0, 0, launch_pool_fwd(ws + p.a1, N, H(0), Wd(0), nf, ws + p.c[1], p.cs[1], 2 * nf, s));
+  }
   // enc_conv2..5 + pool2..5 (pool_k -> skip slice of c_{k+1}; pool5 -> p5)
   for (int l = 1; l <= 4; ++l) {
     const int li = ENC2 + (l - 1);
     const View in = (l == 4) ? V(p.c[4], p.cs[4], nf) : V(p.c[l], p.cs[l], 2 * nf);
+    const View pv = l < 4 ? V(p.c[l + 1], p.cs[l + 1], (l + 1 == 4) ? nf : 2 * nf) : V(p.p5, nf, 0);
+    bool pooled = false;
     DN_TRY(conv_forward(in, N, H(l), Wd(l), nf, Wt(li), Bs(li), nf, 3, 1, V(p.a[l], nf), OUT_NHWC,
-                        s));
-    if (l < 4) {
-      const int tgt_off = (l + 1 == 4) ? nf : 2 * nf;
-      DN_TIMED(s, "pool", 0, 0, 0, 0, 0, 0, launch_pool_fwd(ws + p.a[l], N, H(l), Wd(l), nf, ws + p.c[l + 1], p.cs[l + 1],
-                             tgt_off, s));
-    } else {
-      DN_TIMED(s, "pool", 0, 0, 0, 0, 0, 0, launch_pool_fwd(ws + p.a[4], N, H(4), Wd(4), nf, ws + p.p5, nf, 0, s));
-    }
+                        s, &pv, &pooled));
+    if (pooled) continue;
+    DN_TIMED(s, "pool", 0, 0, 0, 0, 0, 0,
+             launch_pool_fwd(ws + p.a[l], N, H(l), Wd(l), nf, pv.p, pv.stride, pv.off, s));
   }
   DN_TRY(conv_forward(V(p.p5, nf), N, H(5), Wd(5), nf, Wt(ENC6), Bs(ENC6), nf, 3, 1, V(p.a6, nf),
                       OUT_NHWC, s));
