@@ -27,6 +27,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 B, H, W, STEPS = 4, 64, 64, 2
+if os.environ.get("DPW_SHAPE"):  # "B,H,W": sizes on the large-grid kernels (k_c3w6, pipelined)
+    B, H, W = (int(v) for v in os.environ["DPW_SHAPE"].split(","))
 
 
 def global_inputs():

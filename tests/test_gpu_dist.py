@@ -131,3 +131,42 @@ def test_backward_with_padded_concat_strides(tmp_path, prec):
     for k in ("y", "g", "dx"):
         a, b = res["dense"][k], res["pad32"][k]
         assert np.abs(a - b).max() <= 1e-5 * np.abs(a).max(), (k, np.abs(a - b).max())
+
+
+def _worker_env_run(tmp_path, tag, extra, mode, prec="fp32_x6"):
+    """dp_worker.py on 8 x 128^2 (the 96-output convs at 128^2 take k_c3w6, the 48-channel
+    encoder the pipelined kernels with the fused pool)"""
+    out = str(tmp_path / f"{tag}.npz")
+    env = dict(os.environ, PYTHONUNBUFFERED="1", DPW_SHAPE="8,128,128", **extra)
+    for k in ("DN_POOL_FUSE", "DN_X6_W6"):
+        if k not in extra:
+            env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(HERE, "dp_worker.py"), out, prec, mode],
+                       env=env, cwd=ROOT, timeout=240)
+    assert p.returncode == 0, tag
+    return np.load(out)
+
+
+def test_fused_pool_step_equals_separate_pool(tmp_path):
+    """The encoder's 2x2 max-pools fused into the x6 convs' epilogue (default) give the N2N step
+    of separate k_pool_fwd launches (DN_POOL_FUSE=0) bit for bit: the same activated values,
+    the same window order."""
+    fused = _worker_env_run(tmp_path, "fused", {}, "local")
+    sep = _worker_env_run(tmp_path, "sep", {"DN_POOL_FUSE": "0"}, "local")
+    for k in ("losses", "grad", "flat"):
+        assert np.array_equal(fused[k], sep[k]), k
+
+
+def test_winograd_step_matches_direct_kernels(tmp_path):
+    """The 96-output 3x3 convs on the 1-D Winograd kernel k_c3w6 (default) against the direct
+    bf16x6 kernels (DN_X6_W6=0): the same arithmetic class (fp32-accurate dot products; the
+    transform adds one rounding of v and u), so outputs and every gradient agree to fp32
+    rounding.  Tolerance: 2e-5 of the max magnitude for the output and the parameter gradients
+    (LeakyReLU's slope switch at 0 can move a gradient element by rounding, as between any two
+    fp32 implementations).  dL/dx of this random-init net is ~1e-16, i.e. a sum of much larger
+    terms that cancel to rounding level, so only its scale is compared (5e-2)."""
+    w6 = _worker_env_run(tmp_path, "w6", {}, "grad")
+    d = _worker_env_run(tmp_path, "direct", {"DN_X6_W6": "0"}, "grad")
+    for k, tol in (("y", 2e-5), ("g", 2e-5), ("dx", 5e-2)):
+        a, b = w6[k], d[k]
+        assert np.abs(a - b).max() <= tol * np.abs(a).max(), (k, np.abs(a - b).max())
