@@ -51,11 +51,13 @@ struct WCfg {
   static_assert(2 * LBYTES <= 163840, "two workgroups per CU");
 };
 
-// 16-B quad index of V element (row, kq, j, p): p is XOR-swizzled by j >> 2 and row & 1, so the
-// 16 tiles (two rows x 8) that lanes li = 0..15 read at one (p, kq) fall on 16 distinct quads of
-// a 256-B window (conflict-free ds_read_b128)
+// 16-B quad index of V element (row, kq, j, p): p is XOR-swizzled by j >> 2, row & 1 and kq, so
+// the 16 tiles (two rows x 8) that lanes li = 0..15 read at one (p, kq) fall on 16 distinct quads
+// of a 256-B window (conflict-free ds_read_b128), and so do the (kq, j & 3) pairs of the transform's
+// 8-B writes (without kq in the swizzle those were 4-way bank conflicts: SQ_LDS_BANK_CONFLICT 41 %
+// of the LDS-active cycles)
 __device__ __forceinline__ int w6_vq(int row, int kq, int j, int p) {
-  return ((row * 4 + kq) * 8 + j) * 4 + (p ^ (j >> 2) ^ ((row & 1) << 1));
+  return ((row * 4 + kq) * 8 + j) * 4 + (p ^ (j >> 2) ^ ((row & 1) << 1) ^ kq);
 }
 
 __device__ __forceinline__ void w6_barrier() {
