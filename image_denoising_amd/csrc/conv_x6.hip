@@ -1640,12 +1640,23 @@ struct Ws3Cfg {
   static constexpr int LBUF = LGF + LXF;
 };
 
-template <int CO_FR, int WM, int WN, int SWL>
+// PL (DN_WG_PLANES): the stage's operands split ONCE into bf16 planes in LDS between two
+// barriers (each was split once per reading wave pair at the operand read: 4.8 non-MFMA VALU per
+// MFMA), one fp32 DMA buffer (the next stage's DMA overlaps this stage's MFMAs); G planes
+// [piece][co][32 px] (swizzled quads), X planes [piece][stage row][ci][pixel pair]
+template <int CO_FR, int WM, int WN, int SWL, bool PL = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
   using C = Ws3Cfg<CO_FR, WM, WN>;
   constexpr int MFW = C::MFW;
   const WgradArgs a = wg_block(a0);
-  __shared__ __attribute__((aligned(16))) float lds[2 * C::LBUF];
+  constexpr int XPR = ((1 << SWL) + 2) / 2;                 // pixel pairs per X stage row
+  constexpr int XROWS = (C::PC >> SWL) + 2;
+  constexpr int GPLF = C::COUT * 16;                        // floats per G plane
+  constexpr int XPLF = XROWS * C::CIB * XPR;                // floats (dwords) per X plane
+  constexpr int LDSF = PL ? C::LBUF + 3 * (GPLF + XPLF) : 2 * C::LBUF;
+  __shared__ __attribute__((aligned(16))) float lds[LDSF];
+  __bf16* gpl = reinterpret_cast<__bf16*>(lds + C::LBUF);   // (PL) G planes
+  unsigned* xpl = reinterpret_cast<unsigned*>(lds + C::LBUF + 3 * GPLF);  // (PL) X planes
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
@@ -1755,17 +1766,53 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
 
   Pos pn = pos_of(u_beg);
   if (u_beg < u_end) issue(pn, lds);
-  __syncthreads();
+  if constexpr (!PL) __syncthreads();
   for (long u = u_beg; u < u_end; ++u) {
-    const int cb = (int)((u - u_beg) & 1);
+    const int cb = PL ? 0 : (int)((u - u_beg) & 1);
     const float* lgs = lds + cb * C::LBUF;
     const float* lxs = lgs + C::LGF;
     pn = next(pn);
-    if (u + 1 < u_end) issue(pn, lds + (cb ^ 1) * C::LBUF);
+    if constexpr (PL) {
+      __syncthreads();  // this stage's DMA landed (vmcnt(0)); every wave done with the planes
+      // G: rows co, pixel octet g -> three 16-B plane quads (lanes = consecutive co)
+      for (int t = tid; t < C::COUT * 4; t += C::NTHR) {
+        const int c = t % C::COUT, g = t / C::COUT;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = lgs[(8 * g + j) * C::GS + c];
+        bf16x8 p0, p1, p2;
+        split3x8(v, p0, p1, p2);
+        const int o = c * 32 + x6_swz(c, g) * 8;
+        *reinterpret_cast<bf16x8*>(gpl + o) = p0;
+        *reinterpret_cast<bf16x8*>(gpl + 2 * GPLF + o) = p1;
+        *reinterpret_cast<bf16x8*>(gpl + 4 * GPLF + o) = p2;
+      }
+      // X: (stage row, ci, pixel pair) -> one dword per plane (lanes = consecutive ci)
+      for (int t = tid; t < XROWS * C::CIB * XPR; t += C::NTHR) {
+        const int ci = t % C::CIB, r = t / C::CIB, d = r % XPR, yy = r / XPR;
+        const float* xp = lxs + (yy * (2 * XPR) + 2 * d) * C::XS + ci;
+        unsigned h, m, l;
+        split3x2(xp[0], xp[C::XS], h, m, l);
+        const int o = (yy * C::CIB + ci) * XPR + d;
+        xpl[o] = h; xpl[XPLF + o] = m; xpl[2 * XPLF + o] = l;
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own plane writes done
+      __syncthreads();                     // planes complete; the fp32 buffer is free
+      if (u + 1 < u_end) issue(pn, lds);
+    } else {
+      if (u + 1 < u_end) issue(pn, lds + (cb ^ 1) * C::LBUF);
+    }
     // A: the wave's MFW gradient fragments
     bf16x8 av[3][MFW];
 #pragma unroll
     for (int i = 0; i < MFW; ++i) {
+      if constexpr (PL) {
+        const int row = (wm * MFW + i) * 16 + li;
+        const int o = row * 32 + x6_swz(row, lg) * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) av[p][i] = *reinterpret_cast<const bf16x8*>(gpl + 2 * p * GPLF + o);
+        continue;
+      }
       float v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = lgs[(8 * lg + j) * C::GS + (wm * MFW + i) * 16 + li];
@@ -1781,11 +1828,18 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
       // the kernel row's 10-pixel window, split once: P[plane][d] = pieces of pixels 2d, 2d+1
+      unsigned P[3][5];
+      if constexpr (PL) {
+        const unsigned* xq = xpl + ((pr0 + ky) * C::CIB + wn * 16 + li) * XPR + (pc0 >> 1);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+          for (int d = 0; d < 5; ++d) P[pl][d] = xq[pl * XPLF + d];
+      } else {
       const float* xr = lxs + ((pr0 + ky) * xw + pc0) * C::XS + wn * 16 + li;
       float w[10];
 #pragma unroll
       for (int m = 0; m < 10; ++m) w[m] = xr[m * C::XS];
-      unsigned P[3][5];
 #pragma unroll
       for (int d = 0; d < 5; ++d) {
 #if DN_WG_ABL_NOSPLIT
@@ -1794,6 +1848,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
 #else
         split3x2(w[2 * d], w[2 * d + 1], P[0][d], P[1][d], P[2][d]);
 #endif
+      }
       }
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
@@ -1824,8 +1879,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
         x6_acc_add(accb[i][0], hi, lo);
       }
     }
-    __syncthreads();  // next stage landed (vmcnt(0)); everyone done with this buffer
+    if constexpr (!PL) __syncthreads();  // next stage landed (vmcnt(0)); everyone done with this buffer
   }
+  if constexpr (PL) __syncthreads();  // the trailing DMA (none issued past the last stage)
 
   float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
   const int ci = ci0 + wn * 16 + li;
@@ -1867,10 +1923,28 @@ int wgrad_splits_x6(const WgradArgs& a, int splits) {
   return splits < cap ? splits : (cap < 1 ? 1 : cap);
 }
 
+#ifndef DN_WG_PLANES_DEFAULT
+#define DN_WG_PLANES_DEFAULT 1
+#endif
+static bool wg_planes() {  // DN_WG_PLANES=0/1: k_wgrad3s with the split at the operand read / in LDS planes
+  static const bool on = getenv("DN_WG_PLANES") ? atoi(getenv("DN_WG_PLANES")) != 0 : DN_WG_PLANES_DEFAULT != 0;
+  return on;
+}
+
 template <int CO_FR, int WM, int WN>
 static hipError_t run_wgrad3s(const WgradArgs& a, int splits, hipStream_t s, int nz = 1) {
   using C = Ws3Cfg<CO_FR, WM, WN>;
   const dim3 grid(splits, (a.Cin + C::CIB - 1) / C::CIB, nz), block(C::NTHR);
+  if (wg_planes()) {
+    static const std::string kp[3] = {x6_kmore(x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "3"), "true"),
+                                      x6_kmore(x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "4"), "true"),
+                                      x6_kmore(x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "5"), "true")};
+    prof_kernel(kp[a.KW >= 32 ? 2 : (a.KW >= 16 ? 1 : 0)].c_str());
+    if (a.KW >= 32) hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 5, true>), grid, block, 0, s, a);
+    else if (a.KW >= 16) hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 4, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 3, true>), grid, block, 0, s, a);
+    return hipGetLastError();
+  }
   static const std::string kn[3] = {x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "3"),
                                     x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "4"),
                                     x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "5")};
