@@ -1924,7 +1924,7 @@ int wgrad_splits_x6(const WgradArgs& a, int splits) {
 }
 
 #ifndef DN_WG_PLANES_DEFAULT
-#define DN_WG_PLANES_DEFAULT 1
+#define DN_WG_PLANES_DEFAULT 0
 #endif
 static bool wg_planes() {  // DN_WG_PLANES=0/1: k_wgrad3s with the split at the operand read / in LDS planes
   static const bool on = getenv("DN_WG_PLANES") ? atoi(getenv("DN_WG_PLANES")) != 0 : DN_WG_PLANES_DEFAULT != 0;
