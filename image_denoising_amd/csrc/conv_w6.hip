@@ -181,9 +181,11 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   };
 
   // weights: fragment q = output channels 48nh + 16q .. +15 of stage st, plane pl
+  // (output-channel block z = blockIdx.z of 96 channels when a.zc: its own image, a.wp_z bf16)
   const int nst_img = nch * C::SPC;
+  const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp) + (long)blockIdx.z * a.wp_z;
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(a.wp), (short)0, nst_img * C::WSTP * 2, 0x00020000);
+      const_cast<__bf16*>(wimg), (short)0, nst_img * C::WSTP * 2, 0x00020000);
   int woff[NTW];
 #pragma unroll
   for (int q = 0; q < NTW; ++q) {
@@ -394,7 +396,11 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   for (int r4 = 0; r4 < 4; ++r4) for (int q = 0; q < NTW; ++q) for (int rr = 0; rr < 4; ++rr) sum += outr[r4][q][rr];
   a.out[tid] = sum;
 #else
-  fwd_epilogue_at<NTW, 4, C::PS>(a, outr, st, ty0, tx0, n, 4 * ph, nh * 16 * NTW, 16 * NTW);
+  {
+    const int cz = (a.zc ? (int)blockIdx.z * a.zc : 0) + nh * 16 * NTW;
+    const int nout = a.NOUT - cz < 16 * NTW ? a.NOUT - cz : 16 * NTW;
+    if (nout > 0) fwd_epilogue_at<NTW, 4, C::PS>(a, outr, st, ty0, tx0, n, 4 * ph, cz, nout);
+  }
 #endif
 }
 
@@ -405,13 +411,14 @@ hipError_t launch_fwd_w6(const FwdArgs& a, hipStream_t s) {
   using C = WCfg;
   const bool aux = a.epi == EPI_MASK || a.epi == EPI_BIAS_ADD;
   const int tail = a.x6_tail & 7;
-  if (a.NOUT != 96 || a.zc || a.out_layout != OUT_NHWC || a.sel_rd ||
+  const int nz = a.zc ? (a.NOUT + a.zc - 1) / a.zc : 1;
+  if ((a.zc ? a.zc != 96 : a.NOUT != 96) || a.out_layout != OUT_NHWC || a.sel_rd ||
       ((a.out_stride | a.out_off | a.NOUT) & 3) || (aux && ((a.mask_stride | a.mask_off) & 3)) ||
       a.epi < EPI_BIAS || a.epi > EPI_BIAS_ADD || ((a.in_stride | a.in_off | a.K) & 3) ||
       (long)C::IH * a.IWt * a.in_stride * 4 >= 0x7fffffffL || tail != x6_tail_mode(a.K))
     return hipErrorInvalidValue;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
-  const dim3 grid(tx * ty, a.N, 1), block(C::WAVES * 64);
+  const dim3 grid(tx * ty, a.N, nz), block(C::WAVES * 64);
   static const char* kn[3] = {"k_c3w6<0>", "k_c3w6<1>", "k_c3w6<2>"};
   prof_kernel(kn[tail]);
   if (tail == 1)

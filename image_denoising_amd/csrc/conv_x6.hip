@@ -1216,7 +1216,9 @@ __device__ __forceinline__ void pk_x6(const PackJob& j, long e) {
   }
   __bf16 h, m, l;
   split3(v, h, m, l);
-  __bf16* st = static_cast<__bf16*>(j.out) + ((long)z * nch * 9 + ct) * wst;
+  // (block z's image starts at z x x6_pack_elems / nz: 12 stage slots per chunk for 96-wide
+  // blocks, which have room for the Winograd image too)
+  __bf16* st = static_cast<__bf16*>(j.out) + ((long)z * nch * (NP == 96 ? 12 : 9) + ct) * wst;
   const int o = nn * 32 + x6_swz(nn, kk >> 3) * 8 + (kk & 7);
   st[o] = h;
   st[NP * 32 + o] = m;
@@ -1228,8 +1230,11 @@ __device__ __forceinline__ void pk_x6(const PackJob& j, long e) {
 // stage 4 ky + p holding u_p = G g of kernel row ky (g = the three kx taps of (k, n)):
 // u = (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2), each rounded once from fp64, then split.
 // Last chunk (tail): 1: stage p, k = 4 ky + channel; 2: stage 2p + h, k = 16 (ky - 2h) + channel.
-__device__ __forceinline__ void pk_w6(const PackJob& j, long e) {
+__device__ __forceinline__ void pk_w6(const PackJob& j, long e0) {
   const int NP = j.g0, nch = j.nch, wst = x6_wst(NP), pad = wst - 3 * NP * 32;
+  const long per_z = (long)nch * 12 * NP * 32;  // one image per output-channel block z (zc)
+  const int z = (int)(e0 / per_z);
+  const long e = e0 - (long)z * per_z;
   const int kk = (int)(e % 32), nn = (int)((e / 32) % NP);
   const int cs = (int)(e / (32L * NP)), c = cs / 12, s = cs % 12;
   int ky = s >> 2, p = s & 3, k = c * 32 + kk;
@@ -1242,11 +1247,11 @@ __device__ __forceinline__ void pk_w6(const PackJob& j, long e) {
     live = s < 8 && ky < 3;
   }
   float v = 0.f;
-  if (live && k < j.K && nn < j.NOUT) {
+  if (live && k < j.K && nn < j.NOUT && (j.zc == 0 || z * j.zc + nn < j.ntot)) {
     double g[3];
     for (int kx = 0; kx < 3; ++kx) {
       const int t = 3 * ky + kx, tm = j.flip ? j.taps - 1 - t : t;
-      g[kx] = j.w[(long)k * j.sK + (long)nn * j.sN + (long)tm * j.sT];
+      g[kx] = j.w[(long)z * j.sZ + (long)k * j.sK + (long)nn * j.sN + (long)tm * j.sT];
     }
     const double u = p == 0 ? g[0] : (p == 1 ? (g[0] + g[1] + g[2]) * 0.5
                                              : (p == 2 ? (g[0] - g[1] + g[2]) * 0.5 : g[2]));
@@ -1254,7 +1259,7 @@ __device__ __forceinline__ void pk_w6(const PackJob& j, long e) {
   }
   __bf16 h, m, l;
   split3(v, h, m, l);
-  __bf16* st = static_cast<__bf16*>(j.out) + (long)cs * wst;
+  __bf16* st = static_cast<__bf16*>(j.out) + ((long)z * nch * 12 + cs) * wst;
   const int o = nn * 32 + x6_swz(nn, kk >> 3) * 8 + (kk & 7);
   st[o] = h;
   st[NP * 32 + o] = m;
@@ -1436,8 +1441,8 @@ long x6_pack_elems(int K, int nout, int zc) {
   const int np = x6_np(nout, zc);
   if (np == 0 || (zc > 0 && zc != np)) return -1;
   const int nz = zc > 0 ? (nout + zc - 1) / zc : 1;
-  // 96 outputs in one block: room for the Winograd image (12 stages per chunk) as well
-  const int spc = (np == 96 && nz == 1) ? 12 : 9;
+  // 96-output blocks: room for the Winograd image (12 stages per chunk) as well
+  const int spc = np == 96 ? 12 : 9;
   return (long)nz * ((K + 31) / 32) * spc * x6_wst(np);
 }
 
@@ -1455,7 +1460,9 @@ int x6_image_mode(int N, int H, int W, int K, int nout, int zc, bool aligned) {
   if (!aligned) return 0;
   // k_c3w6 (8 x 16 tiles, two workgroups per CU) from one full round of resident workgroups
   const long t8 = (long)N * ((H + 7) / 8) * ((W + 15) / 16);
-  const bool w6 = w6_enabled() && nout == 96 && zc == 0 && t8 >= 512;
+  const int nz = zc > 0 ? (nout + zc - 1) / zc : 1;
+  const bool w6 = w6_enabled() && x6_np(nout, zc) == 96 && (zc == 0 ? nout == 96 : zc == 96) &&
+                  t8 * nz >= 512;
   if (!w6 && !x6_pipelined(N, H, W, nout, zc)) return 0;
   return x6_tail_mode(K) | (w6 ? X6_W6 : 0);
 }
@@ -1470,7 +1477,7 @@ bool pack_job_x6(const WView& wv, int K, int nout, int zc, void* out, int mode, 
   const int tail = mode & 7;
   const bool w6 = (mode & X6_W6) != 0;
   if (total < 0 || wv.taps != 9 || (tail && tail != x6_tail_mode(K)) ||
-      (w6 && (nout != 96 || zc != 0)))
+      (w6 && (zc == 0 ? nout != 96 : zc != 96)))
     return false;
   WView v = wv;
   if (zc > 0) v.sZ = (long)zc * wv.sN;  // block z = output channels [z*zc, z*zc + zc)

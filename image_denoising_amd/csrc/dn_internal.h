@@ -186,7 +186,7 @@ __host__ __device__ inline long pack_job_elems(const PackJob& j) {
   switch (j.kind) {
     case PK_F32: return (long)j.nch * j.g3 * j.nz;
     case PK_X6: return (long)j.nz * j.nch * 9 * j.g0 * 32;
-    case PK_W6: return (long)j.nch * 12 * j.g0 * 32;
+    case PK_W6: return (long)j.nz * j.nch * 12 * j.g0 * 32;
     case PK_DECONV_X6: return 4L * 3 * 3 * 96 * 32;
     case PK_HEAD_X6: return 2L * 3 * 3 * 96 * 32;
     case PK_DECONV_DGRAD_X6: return 4L * 3 * 3 * 96 * 32;

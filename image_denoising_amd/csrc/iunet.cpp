@@ -141,10 +141,16 @@ hipError_t grun(int ksize, const View& in, int N, int H, int W, int K, const flo
 
 // the same 3x3 conv on the split-bf16 kernels (image from launch_pack_x6 with zc = x6_zc(nout))
 // tail packing of a partial last K chunk when the launch takes the pipelined kernel
-int x6_tail_for(const View& in, int N, int H, int W, int K, int nout) {
+// (w6_ok: the launch's output / auxiliary views allow the Winograd kernel's float4 NHWC
+// epilogue; then x6_image_mode may add X6_W6 for the 96-channel blocks)
+int x6_tail_for(const View& in, int N, int H, int W, int K, int nout, bool w6_ok) {
   const bool aligned = ((in.stride | in.off | K) & 3) == 0;
-  // (the direct kernels only: the Winograd image, x6_image_mode's X6_W6, is not used here)
+  if (w6_ok && aligned) return x6_image_mode(N, H, W, K, nout, x6_zc(nout), true);
   return aligned && x6_pipelined(N, H, W, nout, x6_zc(nout)) ? x6_tail_mode(K) : 0;
+}
+static bool w6_views(const View& out, int layout, const View& aux, int nout) {
+  return layout == OUT_NHWC && ((out.stride | out.off | nout) & 3) == 0 &&
+         (!aux.p || ((aux.stride | aux.off) & 3) == 0);
 }
 
 hipError_t x6run(const View& in, int N, int H, int W, int K, const float* wp, int nout,
@@ -478,7 +484,7 @@ dn_status conv_fwd(const Ctx& c, const IConv& L, const View& in, int h, int w, i
                    const View& out, int layout = OUT_NHWC, const View& aux = kNone) {
   OpScope prof(c.s, "fwd", L.cout, L.cin, L.k, h, w, c.p.N, 1.0);
   float* pk = c.ws + c.p.pack;
-  const int tail = x6_tail_for(in, c.p.N, h, w, L.cin, L.cout);
+  const int tail = x6_tail_for(in, c.p.N, h, w, L.cin, L.cout, w6_views(out, layout, aux, L.cout));
   if (c.prec == DN_PREC_FP32_X6 && L.k == 3 && x6_takes(L.cin, L.cout, tail)) {
     IU_TRY(launch_pack_x6(conv_fwd_view(c.Wt(L), L.cin, 3), L.cin, L.cout, x6_zc(L.cout), pk,
                           c.s, tail));
@@ -640,7 +646,7 @@ dn_status dgrad_g(const Ctx& c, const IConv& L, const View& g, int h, int w, int
                   const View& aux, const View& dx) {
   OpScope prof(c.s, "dgrad", nout, L.cout, L.k, h, w, c.p.N, 1.0);
   float* pk = c.ws + c.p.pack;
-  const int tail = x6_tail_for(g, c.p.N, h, w, L.cout, nout);
+  const int tail = x6_tail_for(g, c.p.N, h, w, L.cout, nout, w6_views(dx, OUT_NHWC, aux, nout));
   if (c.prec == DN_PREC_FP32_X6 && L.k == 3 && x6_takes(L.cout, nout, tail)) {
     IU_TRY(launch_pack_x6(conv_dgrad_view(c.Wt(L), L.cin, 3), L.cout, nout, x6_zc(nout), pk,
                           c.s, tail));
