@@ -391,17 +391,11 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
       for (int rr = 0; rr < 4; ++rr) outr[r4][q][rr] = st[(4 * lg + rr) * C::PS + 16 * q + li];
     __builtin_amdgcn_s_waitcnt(0xC07F);
   }
-#ifdef DN_W6_NOEPI
-  float sum = 0.f;
-  for (int r4 = 0; r4 < 4; ++r4) for (int q = 0; q < NTW; ++q) for (int rr = 0; rr < 4; ++rr) sum += outr[r4][q][rr];
-  a.out[tid] = sum;
-#else
   {
     const int cz = (a.zc ? (int)blockIdx.z * a.zc : 0) + nh * 16 * NTW;
     const int nout = a.NOUT - cz < 16 * NTW ? a.NOUT - cz : 16 * NTW;
     if (nout > 0) fwd_epilogue_at<NTW, 4, C::PS>(a, outr, st, ty0, tx0, n, 4 * ph, cz, nout);
   }
-#endif
 }
 
 int w6_stages_per_chunk() { return WCfg::SPC; }

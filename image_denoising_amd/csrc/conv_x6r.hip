@@ -302,14 +302,7 @@ __global__ __launch_bounds__(512, 1) void k_c3x6r(FwdArgs a) {
 #endif
   // the staging areas sit past the two x buffers: no barrier before the epilogue
   float* st = reinterpret_cast<float*>(lds_raw + 2 * C::XBUF * 2) + wave * C::LEPI;
-#ifdef DN_X6R_NOEPI
-  if (tid < 0) fwd_epilogue_vec_at<NTW, MT, C::PS, EPI_BIAS>(a, acc, st, ty0, tx0, n, mq * MT, nh * 16 * NTW, 16 * NTW);
-  float sum = 0.f;
-  for (int m = 0; m < MT; ++m) for (int q = 0; q < NTW; ++q) for (int r = 0; r < 4; ++r) sum += acc[m][q][r];
-  a.out[tid] = sum;
-#else
   fwd_epilogue_at<NTW, MT, C::PS>(a, acc, st, ty0, tx0, n, mq * MT, nh * 16 * NTW, 16 * NTW);
-#endif
 }
 
 // A/B switch DN_X6_REG (default 0 until measured): the 96-channel shapes on k_c3x6r
