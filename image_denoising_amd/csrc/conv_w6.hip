@@ -74,6 +74,9 @@ __device__ __forceinline__ void w6_barrier() {
 #ifndef DN_W6_ABL_NOW
 #define DN_W6_ABL_NOW 0
 #endif
+#ifndef DN_W6_EARLY
+#define DN_W6_EARLY 0  // 1: the next chunk's x loads before the chunk-end barrier; 2: before its last stage
+#endif
 #ifndef DN_W6_TG
 #define DN_W6_TG 3  // transform items whose x loads are in flight together
 #endif
@@ -180,6 +183,54 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
     }
   };
 
+  // the same for a full chunk in two halves: its x loads (tload, into d) and the V writes
+  // (twrite) -- the loads of chunk c+1 issued before the barrier that ends chunk c (DN_W6_EARLY)
+  constexpr int NIT8 = C::IH * C::NJ * 8;
+  auto tload = [&](int k0, int tid, f32x4 (&d)[C::VITEMS][4]) {
+#pragma unroll
+    for (int it = 0; it < C::VITEMS; ++it) {
+      const int e = tid + it * C::WAVES * 64;
+      const int c4 = e & 7, j = (e >> 3) & 7, row = e >> 6;
+      const int gy = iy0 + row, k = k0 + 4 * c4;
+      const bool rok = e < NIT8 && gy >= 0 && gy < a.IHt && k < a.K;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int gx = ix0 + 2 * j + i;
+        const bool ok = rok && gx >= 0 && gx < a.IWt;
+        const int off = ok ? (((gy - ry0) * a.IWt + gx) * a.in_stride + k) * 4 : 0x7fffffff;
+        d[it][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      }
+    }
+  };
+  auto twrite = [&](int tid, const f32x4 (&d)[C::VITEMS][4]) {
+#pragma unroll
+    for (int it = 0; it < C::VITEMS; ++it) {
+      const int e = tid + it * C::WAVES * 64;
+      if (e < NIT8) {
+        const int c4 = e & 7, j = (e >> 3) & 7, row = e >> 6;
+        f32x4 v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          v[0][c] = d[it][0][c] - d[it][2][c];
+          v[1][c] = d[it][1][c] + d[it][2][c];
+          v[2][c] = d[it][2][c] - d[it][1][c];
+          v[3][c] = d[it][1][c] - d[it][3][c];
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          unsigned h0, m0, l0, h1, m1, l1;
+          split3x2(v[p][0], v[p][1], h0, m0, l0);
+          split3x2(v[p][2], v[p][3], h1, m1, l1);
+          const int o = w6_vq(row, c4 >> 1, j, p) * 8 + (c4 & 1) * 4;
+          typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<u32x2_t*>(lv + o) = u32x2_t{h0, h1};
+          *reinterpret_cast<u32x2_t*>(lv + C::VPL + o) = u32x2_t{m0, m1};
+          *reinterpret_cast<u32x2_t*>(lv + 2 * C::VPL + o) = u32x2_t{l0, l1};
+        }
+      }
+    }
+  };
+
   // weights: fragment q = output channels 48nh + 16q .. +15 of stage st, plane pl
   // (output-channel block z = blockIdx.z of 96 channels when a.zc: its own image, a.wp_z bf16)
   const int nst_img = nch * C::SPC;
@@ -283,21 +334,33 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
 #pragma unroll
   for (int q = 0; q < NTW; ++q) load_wq(stage_of(0, 0, tail_only), q);
   const int nfull = TAIL ? nch - 1 : nch;  // full chunks; a tail-packed last one after the loop
+  f32x4 dx[C::VITEMS][4];  // (DN_W6_EARLY) the next full chunk's x, loaded before its barrier
 #pragma unroll 1
   for (int c = 0; c < nfull; ++c) {
     int liv = li, lgv = lg, tidv = tid;
     asm volatile("" : "+v"(liv), "+v"(lgv), "+v"(tidv));
     const bool more = c + 1 < nch;
     const bool next_tail = TAIL && c + 2 == nch;
-    if (c > 0) w6_barrier();  // every wave is done with the previous chunk's V
-    if (!DN_W6_ABL_NOT || c == 0) transform(std::integral_constant<int, 8>{}, c * C::KC, tidv);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own V stores done
-    w6_barrier();
+    if (!DN_W6_EARLY || c == 0) {
+      if (c > 0) w6_barrier();  // every wave is done with the previous chunk's V
+      if (!DN_W6_ABL_NOT || c == 0) transform(std::integral_constant<int, 8>{}, c * C::KC, tidv);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own V stores done
+      w6_barrier();
+    }
     w6_for<0, 6>([&](auto si) {
       constexpr int s = decltype(si)::value;
       const int nxt = s + 1 < 6 ? stage_of(c, s + 1, false) : (more ? stage_of(c + 1, 0, next_tail) : -1);
+      if constexpr (DN_W6_EARLY == 2 && s == 5)
+        if (c + 1 < nfull) tload((c + 1) * C::KC, tidv, dx);
       stage(std::integral_constant<int, 0>{}, s, nxt, liv, lgv);
     });
+    if (DN_W6_EARLY && c + 1 < nfull) {
+      if (DN_W6_EARLY == 1) tload((c + 1) * C::KC, tidv, dx);
+      w6_barrier();  // every wave is done with this chunk's V
+      twrite(tidv, dx);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      w6_barrier();
+    }
   }
   if constexpr (TAIL != 0) {
     const int c = nch - 1;
