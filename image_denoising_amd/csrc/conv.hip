@@ -1275,7 +1275,12 @@ int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
   long want = 768 / cib;
   const long slab_cap = (64L << 20) / ((long)Cout * Cin * taps + Cout);  // <= 256 MB of slab
   if (want > slab_cap) want = slab_cap;
-  if (want > units / 2) want = units / 2;
+  // at least MU pixel chunks per split (DN_WG_MIN_UNITS, default 2): on the small levels the
+  // per-workgroup slab (up to 110 KB written, then re-read by the reduction) outweighs the work
+  // of a 2-chunk split
+  static const int mu_env = getenv("DN_WG_MIN_UNITS") ? atoi(getenv("DN_WG_MIN_UNITS")) : 2;
+  const int mu = mu_env < 1 ? 1 : mu_env;
+  if (want > units / mu) want = units / mu;
   if (want < 1) want = 1;
   return (int)want;
 }

@@ -920,9 +920,9 @@ __global__ __launch_bounds__(512, 1) void k_c3x6s(FwdArgs a) {
 // constant count); the next chunk's x tile is loaded into registers at the start of a chunk,
 // after that stage's DMA, and split into LDS at its end.  Stage reads and MFMAs as k_c3x6p.
 // ------------------------------------------------------------------------------------
-template <int NT, int MT_ = 2>
+template <int NT, int MT_ = 2, int S_ = 2>
 struct HCfg {
-  static constexpr int WAVES = 4, MT = MT_, S = 2;
+  static constexpr int WAVES = 4, MT = MT_, S = S_;
   static constexpr int TW = 16, TH = WAVES * MT, IH = TH + 2, IW = TW + 2, KC = 32, NP = 16 * NT;
   static constexpr int XPIX = IH * IW;
   static constexpr int XPL = XPIX * KC;
@@ -947,12 +947,17 @@ struct HCfg {
 #ifndef DN_X6H_CARRY
 #define DN_X6H_CARRY 1  // A/B switch: 0 = per-block sums in k_c3x6h
 #endif
+#ifndef DN_X6H_CARRY4
+#define DN_X6H_CARRY4 1  // A/B switch: 1 = MT = 4 with NT <= 3 carries the corrections too (96 acc VGPRs)
+#endif
 #ifndef DN_X6H_PIN
 #define DN_X6H_PIN 0  // A/B switch: 1 = MT = 2's hi adds pinned per group (100->96 @256^2: 1-2 % slower)
 #endif
-template <int NT, int TAIL, int MT_ = 2>
+// S_ = 3 (small grids, MT = 1): a 3-slot weight ring, stage st + 2 requested at the start of st,
+// so a stage waits on neither the L2 latency of its weights nor that of the next stage's
+template <int NT, int TAIL, int MT_ = 2, int S_ = 2>
 __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
-  using C = HCfg<NT, MT_>;
+  using C = HCfg<NT, MT_, S_>;
   constexpr int MT = C::MT;
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
   __bf16* lx = reinterpret_cast<__bf16*>(lds_raw);
@@ -1043,8 +1048,9 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
     }
   };
 
-  // prologue: stage 0's weights (L2) and chunk 0's x tile (HBM) in flight together
-  load_w(0, 0);
+  // prologue: the first S - 1 stages' weights (L2) and chunk 0's x tile (HBM) in flight together
+#pragma unroll
+  for (int j = 0; j + 1 < C::S; ++j) load_w(j < nst ? j : nst - 1, j);
   load_x(0);
   store_x();                           // waits for the x loads (and the older DMA)
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
@@ -1053,14 +1059,16 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
   auto stage = [&](int c, int t) {
     const bool more = c + 1 < nch;
     const int st = 9 * c + t;
-    const __bf16* lw = ring + (st & 1) * C::WST;
-    // stage st+1's weights into the other slot (every wave left it at the last barrier); past
-    // the end a re-load of the last stage
-    load_w(st + 1 < nst ? st + 1 : nst - 1, (st + 1) & 1);
+    const __bf16* lw = ring + (st % C::S) * C::WST;
+    // stage st+S-1's weights into the slot of stage st-1 (every wave left it at the last
+    // barrier); past the end a re-load of the last stage
+    load_w(st + C::S - 1 < nst ? st + C::S - 1 : nst - 1, (st + C::S - 1) % C::S);
     if (t == 0 && more) load_x((c + 1) * C::KC);  // the next chunk, after this stage's DMA
     const int mode = (tail && c + 1 == nch) ? tail : 0;
     // MT = 4: the A pieces of two rows at a time (registers), the B fragments read once for all
     constexpr int MH = MT >= 4 ? 2 : MT;
+    // MT = 4 keeps the per-block form (its 2 x 48 accumulators at NT = 6 leave no room for accl)
+    constexpr bool BLK = !DN_X6H_CARRY || (MT >= 4 && !(DN_X6H_CARRY4 && NT <= 3));
     constexpr int QG = MT >= 4 ? 1 : (DN_X6H_CARRY ? x6_qgc(MT, NT) : x6_qg(MT, NT)), NG = NT / QG,
                   LOOK = NG < DN_X6H_LOOK ? NG : DN_X6H_LOOK;
     bf16x8 bv[3][NT];
@@ -1131,8 +1139,7 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
       f32x4(&acclh)[MH][NT] = *reinterpret_cast<f32x4(*)[MH][NT]>(&accl[mh * MH]);
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
-        // MT = 4 keeps the per-block form: its 2 x 48 accumulators leave no room for accl
-        if constexpr (MT >= 4 || !DN_X6H_CARRY) x6_group<MH, NT, QG>(acch, av, bv, g * QG);
+        if constexpr (BLK) x6_group<MH, NT, QG>(acch, av, bv, g * QG);
         else x6_group_c<MH, NT, QG>(acch, acclh, av, bv, g * QG);
         if constexpr (MT >= 4 || DN_X6H_PIN) {  // the block sums' adds here, not sunk to the stage end
 #pragma unroll
@@ -1151,9 +1158,17 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
       x6_barrier();  // every wave is done with this chunk's x tile
       store_x();
     }
-    // own DMAs of stage st+1 landed; younger: this stage's x loads (chunk start)
-    if (t == 0 && more) X6_WAITCNT_VM(C::XITEMS);
-    else X6_WAITCNT_VM(0);
+    // own DMAs of stage st+1 landed; younger: those of stages st+2 .. st+S-1 and the chunk's x
+    // loads while they were issued after it (t <= S-2); after the last stage none in flight
+    // (the epilogue reuses the ring)
+    if constexpr (C::S == 2) {
+      if (t == 0 && more) X6_WAITCNT_VM(C::XITEMS);
+      else X6_WAITCNT_VM(0);
+    } else {
+      if (st + 1 == nst) X6_WAITCNT_VM(0);
+      else if (t <= C::S - 2 && more) X6_WAITCNT_VM((C::S - 2) * C::PPW + C::XITEMS);
+      else X6_WAITCNT_VM((C::S - 2) * C::PPW);
+    }
     if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
     x6_barrier();
   };
@@ -1180,6 +1195,17 @@ static hipError_t run_x6h(const FwdArgs& a, int nz, hipStream_t s) {
     hipLaunchKernelGGL((k_c3x6h<NT, 2, MT>), grid, block, 0, s, a);
   else
     hipLaunchKernelGGL((k_c3x6h<NT, 0, MT>), grid, block, 0, s, a);
+  return hipGetLastError();
+}
+
+// small grids (below one round of 16 x 16 tiles), plain image: the 3-slot ring
+template <int NT, int MT>
+static hipError_t run_x6h3(const FwdArgs& a, int nz, hipStream_t s) {
+  using C = HCfg<NT, MT, 3>;
+  const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
+  static const std::string kn = x6_kmore(x6_kname("k_c3x6h", NT, 0, MT), "3");
+  prof_kernel(kn.c_str());
+  hipLaunchKernelGGL((k_c3x6h<NT, 0, MT, 3>), dim3(tx * ty, a.N, nz), dim3(C::WAVES * 64), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1461,8 +1487,10 @@ int x6_image_mode(int N, int H, int W, int K, int nout, int zc, bool aligned) {
   // k_c3w6 (8 x 16 tiles, two workgroups per CU) from one full round of resident workgroups
   const long t8 = (long)N * ((H + 7) / 8) * ((W + 15) / 16);
   const int nz = zc > 0 ? (nout + zc - 1) / zc : 1;
+  // DN_W6_MIN_TILES: tuning probe for the smallest Winograd launch (default one full round)
+  static const long min_t = getenv("DN_W6_MIN_TILES") ? atol(getenv("DN_W6_MIN_TILES")) : 512;
   const bool w6 = w6_enabled() && x6_np(nout, zc) == 96 && (zc == 0 ? nout == 96 : zc == 96) &&
-                  t8 * nz >= 512;
+                  t8 * nz >= min_t;
   if (!w6 && !x6_pipelined(N, H, W, nout, zc)) return 0;
   return x6_tail_mode(K) | (w6 ? X6_W6 : 0);
 }
@@ -1610,6 +1638,14 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
   if (!no_pipe && x6_pipelined(a.N, a.OH, a.OW, a.NOUT, a.zc) && aligned) return run();
   // (a fused pool needs an even number of tile rows per wave: MT = 2)
   const bool pool = a.pool_out != nullptr;
+  // small grids: k_c3x6h with the 3-slot weight ring where the shape allows (float4 rows; two
+  // workgroups per CU: MT = 1 at 96 channels); DN_X6_RING3=0 keeps k_c3x6
+  static const bool ring3 = !getenv("DN_X6_RING3") || atoi(getenv("DN_X6_RING3")) != 0;
+  if (ring3 && aligned && half_fits) {
+    if (np == 96 && !pool) return run_x6h3<6, 1>(a, nz, s);
+    if (np == 48) return pool || x6_pick_mt<3>(a, nz) == 2 ? run_x6h3<3, 2>(a, nz, s) : run_x6h3<3, 1>(a, nz, s);
+    if (np == 32) return pool || x6_pick_mt<2>(a, nz) == 2 ? run_x6h3<2, 2>(a, nz, s) : run_x6h3<2, 1>(a, nz, s);
+  }
   if (np == 32)
     return pool || x6_pick_mt<2>(a, nz) == 2 ? run_x6<2, 2>(a, nz, s) : run_x6<2, 1>(a, nz, s);
   if (np == 48)
@@ -2228,6 +2264,9 @@ hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* w
 // 16 pixels -- so three of the four reads of an input row hit that XCD's L2.  The next row's
 // input is loaded into registers while the current one computes; the images are read from L2
 // once per workgroup.
+#ifndef DN_DECONV_CPOL
+#define DN_DECONV_CPOL 0  // A/B: cache policy bits of the output stores (2 = nt, streaming)
+#endif
 __global__ __launch_bounds__(512, 1) void k_deconv_x6(FwdArgs a, const __bf16* wimg, int nwt) {
   __shared__ __attribute__((aligned(16))) __bf16 lw[2 * X6_HEAD_BF];
   __shared__ __attribute__((aligned(16))) float lbias[96];
@@ -2314,7 +2353,8 @@ __global__ __launch_bounds__(512, 1) void k_deconv_x6(FwdArgs a, const __bf16* w
       const float4 bb = *reinterpret_cast<const float4*>(lbias + f * 16 + 4 * lg);
       const float4 o = make_float4(out[f][0][0] + bb.x, out[f][0][1] + bb.y, out[f][0][2] + bb.z,
                                    out[f][0][3] + bb.w);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rs, off + 64 * f, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rs, off + 64 * f, 0,
+                                             DN_DECONV_CPOL);
     }
   };
   // three input register sets: a wave-tile's input is requested two tiles before it is used
