@@ -138,7 +138,7 @@ def _worker_env_run(tmp_path, tag, extra, mode, prec="fp32_x6"):
     encoder the pipelined kernels with the fused pool)"""
     out = str(tmp_path / f"{tag}.npz")
     env = dict(os.environ, PYTHONUNBUFFERED="1", DPW_SHAPE="8,128,128", **extra)
-    for k in ("DN_POOL_FUSE", "DN_X6_W6"):
+    for k in ("DN_POOL_FUSE", "DN_X6_W6", "DN_X6_RING3"):
         if k not in extra:
             env.pop(k, None)
     p = subprocess.run([sys.executable, os.path.join(HERE, "dp_worker.py"), out, prec, mode],
@@ -155,6 +155,16 @@ def test_fused_pool_step_equals_separate_pool(tmp_path):
     sep = _worker_env_run(tmp_path, "sep", {"DN_POOL_FUSE": "0"}, "local")
     for k in ("losses", "grad", "flat"):
         assert np.array_equal(fused[k], sep[k]), k
+
+
+def test_small_grid_ring_step_equals_single_stage_prefetch(tmp_path):
+    """Below one round of 16 x 16 tiles (here every level under 64^2 of the 8 x 128^2 step) the
+    3x3 convs run on k_c3x6h with a 3-slot weight ring (default) instead of k_c3x6
+    (DN_X6_RING3=0): the same products in the same order, so the N2N step is bit-identical."""
+    ring = _worker_env_run(tmp_path, "ring3", {}, "local")
+    old = _worker_env_run(tmp_path, "noring", {"DN_X6_RING3": "0"}, "local")
+    for k in ("losses", "grad", "flat"):
+        assert np.array_equal(ring[k], old[k]), k
 
 
 def test_winograd_step_matches_direct_kernels(tmp_path):
