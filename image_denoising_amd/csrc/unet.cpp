@@ -872,8 +872,8 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     RedJob j = red_job(slab, n, sp, 96L * 2 * nf * 9, G(D1A));  // W[co][ci < 2nf][t]
     j.ig = j.og = 2 * nf * 9;
     j.is1 = j.os1 = p.c1k * 9;
-    DN_TRY(red_add(&rb, j, s));
-    DN_TRY(red_add(&rb, red_job(slab + 96L * p.c1k * 9, n, sp, 96, G(D1A) + 96L * p.c1k * 9), s));
+    DN_TRY(red_add(&rb, j, s2));  // (a full batch flushes on s2, behind the wgrads it reads)
+    DN_TRY(red_add(&rb, red_job(slab + 96L * p.c1k * 9, n, sp, 96, G(D1A) + 96L * p.c1k * 9), s2));
     // input-channel slice: compact [co][C][9] rows after the MFMA kernel's, own split count,
     // scattered into W[co][2nf + ci][t]
     float* thin = slab + (long)p.splits[D1A] * n;
@@ -882,7 +882,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     DN_TIMED(s2, "wgrad3_thin", 2.0 * N * H(0) * Wd(0) * 96 * C * 9, C, 96, H(0), Wd(0), N,
              launch_wgrad_c3_thin(ws + p.g_d1a, 96, ws + p.xin, N, C, H(0), Wd(0), thin, nt, C, 0,
                                   0, st, s2));
-    DN_TRY(launch_reduce_scatter(thin, nt, st, nt, G(D1A), 9L * C, 9L * p.c1k, 9L * 2 * nf, s,
+    DN_TRY(launch_reduce_scatter(thin, nt, st, nt, G(D1A), 9L * C, 9L * p.c1k, 9L * 2 * nf, s2,
                                  &rb));
   }
   // only the up1 part of the concat needs a gradient (pool0 is the network input)
@@ -916,6 +916,10 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                       EPI_PLAIN, none, V(p.g_c[l], p.cs[l]), s));
     dU = V(p.g_c[l], p.cs[l], 0);  // [u_{l+1} grad | skip grad]
   }
+  // the head's and the decoder's reductions on the side stream now, behind their weight
+  // gradients, overlapping the encoder's data gradients (DN_RED_EARLY=0: all at the end)
+  static const bool red_early = !getenv("DN_RED_EARLY") || atoi(getenv("DN_RED_EARLY")) != 0;
+  if (side && red_early) DN_TIMED(s2, "reduce", 0, 0, 0, 0, 0, 0, red_flush(rb, s2));
   // up5: x = a6 (level 5), dU = g_c5[0:nf]
   DN_TRY(fork());
   DN_TRY(wgrad(W_UP2, V(p.g_c[4], p.cs[4], 0), V(p.a6, nf), N, H(5), Wd(5), nf, nf, G(UP5), SL(UP5),
