@@ -280,6 +280,22 @@ class UNet(nn.Module):
                   _lib.ptr(dy), _lib.ptr(dflat), _lib.ptr(dx), N, H, W, ws.data_ptr(), ws.numel(),
                   self._prec(), _lib.stream_of(dy))
 
+    def _run_backward_split(self, dy, dflat, ws, N, H, W, tail_ready):
+        """_run_backward that records tail_ready (a torch.cuda.Event) once dflat[tail_begin():]
+        is final, while the encoder's gradients are still being computed
+        (dn_unet_backward_split: the data-parallel step all-reduces that range early)"""
+        _lib.call("dn_unet_backward_split", ctypes.byref(self._cfg), _lib.ptr(self._flat),
+                  _lib.ptr(dy), _lib.ptr(dflat), None, N, H, W, ws.data_ptr(), ws.numel(),
+                  self._prec(), _lib.stream_of(dy), ctypes.c_void_p(tail_ready.cuda_event), None)
+
+    def tail_begin(self) -> int:
+        """first flat-parameter index of the range (dec_conv5a .. nin_c, state_dict order) whose
+        gradient the backward finishes before the encoder's"""
+        t = ctypes.c_int64()
+        _lib.call("dn_unet_backward_split", ctypes.byref(self._cfg), None, None, None, None, 1, 32,
+                  32, None, 0, self._prec(), None, None, ctypes.byref(t))
+        return int(t.value)
+
     # ---- nn.Module API ----------------------------------------------------------------
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = x.contiguous()

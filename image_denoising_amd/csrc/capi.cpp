@@ -35,7 +35,7 @@ extern "C" {
 #define DN_SRC_HASH "unknown"
 #endif
 // src= the sha256 prefix of the sources this library was compiled from (_build.source_hash)
-const char* dn_version(void) { return "denoise_hip 0.3.0 gfx950 src=" DN_SRC_HASH; }
+const char* dn_version(void) { return "denoise_hip 0.4.0 gfx950 src=" DN_SRC_HASH; }
 
 int dn_abi_version(void) { return DN_ABI_VERSION; }
 
@@ -173,6 +173,30 @@ dn_status dn_unet_backward_prec(const dn_unet_cfg* cfg, const float* params, con
                 "workspace smaller than dn_unet_workspace_size(with_backward=1)");
   return unet_backward(p, params, dy, dparams, dx, static_cast<float*>(ws), (hipStream_t)stream,
                        precision);
+  DN_GUARD_END
+}
+
+dn_status dn_unet_backward_split(const dn_unet_cfg* cfg, const float* params, const float* dy,
+                                 float* dparams, float* dx, int N, int H, int W, void* ws,
+                                 size_t ws_bytes, int precision, void* stream, void* tail_ready,
+                                 int64_t* tail_begin_out) {
+  DN_GUARD_BEGIN
+  if (precision != DN_PREC_FP32 && precision != DN_PREC_FP32_X6)
+    return fail(DN_ERR_ARG, "backward precision must be DN_PREC_FP32 or DN_PREC_FP32_X6");
+  if (!cfg) return fail(DN_ERR_ARG, "null argument");
+  Plan p;
+  std::string err;
+  if (!build_plan(*cfg, N, H, W, true, p, err)) return fail(DN_ERR_ARG, err);
+  if (tail_begin_out) *tail_begin_out = tail_begin(p);
+  if (!params || !dy || !dparams || !ws) {
+    if (!params && !dy && !dparams && !ws && !tail_ready) return DN_OK;  // a tail_begin query
+    return fail(DN_ERR_ARG, "null argument");
+  }
+  if (ws_bytes < (size_t)p.total_floats * sizeof(float))
+    return fail(DN_ERR_WORKSPACE,
+                "workspace smaller than dn_unet_workspace_size(with_backward=1)");
+  return unet_backward(p, params, dy, dparams, dx, static_cast<float*>(ws), (hipStream_t)stream,
+                       precision, static_cast<hipEvent_t>(tail_ready));
   DN_GUARD_END
 }
 

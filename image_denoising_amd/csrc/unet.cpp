@@ -696,9 +696,25 @@ struct SideStream {
 // One side stream (and its fork / join events) per host thread and device: keyed on the
 // device of the caller's stream (not hipGetDevice(), which a caller need not have set to it) and
 // created under a guard for that device; thread-local, so two host threads running backwards on
-// one device never share the events between a record and its wait.
+// one device never share the events between a record and its wait.  The owner destroys them when
+// its thread exits (executors called from short-lived threads do not leak streams).
+struct SideStreams {
+  std::map<int, SideStream> per_device;
+  ~SideStreams() {
+    for (auto& kv : per_device) {
+      SideStream& ss = kv.second;
+      if (!ss.st) continue;
+      // (HIP releases a stream / event with work still pending once that work completes)
+      (void)hipEventDestroy(ss.fork);
+      (void)hipEventDestroy(ss.join);
+      (void)hipStreamDestroy(ss.st);
+    }
+  }
+};
+
 static SideStream* side_stream(hipStream_t s) {
-  thread_local std::map<int, SideStream> per_device;
+  thread_local SideStreams owner;
+  std::map<int, SideStream>& per_device = owner.per_device;
   hipDevice_t dev = 0;
   if (hipStreamGetDevice(s, &dev) != hipSuccess) return nullptr;
   SideStream& ss = per_device[dev];
@@ -716,8 +732,10 @@ static SideStream* side_stream(hipStream_t s) {
   return &ss;
 }
 
+long tail_begin(const Plan& p) { return p.P.L[D5A].woff; }
+
 dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* dx,
-                        float* ws, hipStream_t s, int prec) {
+                        float* ws, hipStream_t s, int prec, hipEvent_t tail_ready) {
   const StreamDeviceGuard device_guard(s);
   const bool x6 = prec == DN_PREC_FP32_X6;
   // bf16x6 3x3 weight gradients (k_wgrad3s, split at the operand read); DN_X6_WGRAD=0 keeps the
@@ -919,7 +937,12 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   // the head's and the decoder's reductions on the side stream now, behind their weight
   // gradients, overlapping the encoder's data gradients (DN_RED_EARLY=0: all at the end)
   static const bool red_early = !getenv("DN_RED_EARLY") || atoi(getenv("DN_RED_EARLY")) != 0;
-  if (side && red_early) DN_TIMED(s2, "reduce", 0, 0, 0, 0, 0, 0, red_flush(rb, s2));
+  if (side && red_early) {
+    DN_TIMED(s2, "reduce", 0, 0, 0, 0, 0, 0, red_flush(rb, s2));
+    // dprm[tail_begin ..] (dec_conv5a .. nin_c) is final behind this flush on s2
+    if (tail_ready) DN_TRY(hipEventRecord(tail_ready, s2));
+    tail_ready = nullptr;
+  }
   // up5: x = a6 (level 5), dU = g_c5[0:nf]
   DN_TRY(fork());
   DN_TRY(wgrad(W_UP2, V(p.g_c[4], p.cs[4], 0), V(p.a6, nf), N, H(5), Wd(5), nf, nf, G(UP5), SL(UP5),
@@ -967,6 +990,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     DN_TRY(hipStreamWaitEvent(s, side->join, 0));
   }
   DN_TIMED(s, "reduce", 0, 0, 0, 0, 0, 0, red_flush(rb, s));
+  if (tail_ready) DN_TRY(hipEventRecord(tail_ready, s));  // one stream: everything is final here
   // dL/dx: the network input feeds enc_conv0 and (as pool0) dec_conv1a's last C channels
   if (dx)
     DN_TIMED(s, "dgrad_input", 0, 0, 0, 0, 0, 0, launch_dgrad_input(ws + p.g_a0, prm + p.P.L[ENC0].woff, ws + p.g_d1a,

@@ -74,8 +74,12 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
 dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
                        hipStream_t s, int prec = DN_PREC_FP32, const uint8_t* sel_rd = nullptr);
 // dx (nullable): dL/dx of the network input, NCHW [N, in_nc, H, W]
+// tail_ready (nullable): recorded once dprm[tail_begin(p) ..] is final (dn_unet_backward_split)
 dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* dx,
-                        float* ws, hipStream_t s, int prec = DN_PREC_FP32);
+                        float* ws, hipStream_t s, int prec = DN_PREC_FP32,
+                        hipEvent_t tail_ready = nullptr);
+// first float of the parameter range the backward finishes early (dec_conv5a .. nin_c)
+long tail_begin(const Plan& p);
 // zc of the bf16x6 data gradient of a 3x3 layer producing nout channels (0: one block)
 int x6_dgrad_zc(int nout);
 

@@ -100,6 +100,38 @@ def allreduce_grads(flat_grad: torch.Tensor) -> float:
     return 1.0 / dist.get_world_size()
 
 
+def allreduce_grads_split(flat_grad: torch.Tensor, tail_begin: int, run_backward,
+                          comm_stream=None) -> float:
+    """The gradient all-reduce overlapped with the backward (two buckets; train.py:324-326
+    reduces during its backward too).  run_backward(event) enqueues the backward and has the
+    library record `event` once flat_grad[tail_begin:] (the decoder and the head, finished
+    first) is final; that bucket's all-reduce is enqueued on `comm_stream` behind the event,
+    so it runs while the encoder's gradients are still being computed, and the encoder bucket
+    flat_grad[:tail_begin] follows on the current stream behind the whole backward.  The
+    current stream then waits for both.  Sums are elementwise, so the result equals
+    allreduce_grads' bit for bit.  CPU tensors (the gloo tests): run_backward(None), then the
+    same two buckets in the same order.  Returns 1/world like allreduce_grads."""
+    if not is_initialized():
+        run_backward(None)
+        return 1.0
+    tail, head = flat_grad[tail_begin:], flat_grad[:tail_begin]
+    if flat_grad.device.type != "cuda" or comm_stream is None:
+        run_backward(None)
+        dist.all_reduce(tail, op=dist.ReduceOp.SUM)
+        dist.all_reduce(head, op=dist.ReduceOp.SUM)
+        return 1.0 / dist.get_world_size()
+    ev = torch.cuda.Event()
+    ev.record()  # materialise the event; the library re-records it mid-backward
+    run_backward(ev)
+    comm_stream.wait_event(ev)
+    with torch.cuda.stream(comm_stream):
+        w_tail = dist.all_reduce(tail, op=dist.ReduceOp.SUM, async_op=True)
+    w_head = dist.all_reduce(head, op=dist.ReduceOp.SUM, async_op=True)
+    w_tail.wait()
+    w_head.wait()
+    return 1.0 / dist.get_world_size()
+
+
 def allreduce_mean_(t: torch.Tensor) -> torch.Tensor:
     """mean of a (small) tensor over ranks, e.g. the logged loss (no host sync involved)"""
     if is_initialized():

@@ -26,7 +26,7 @@ from . import dist as dp
 from .arch_unet import UNet
 from .n2n import AugmentNoise, n2n_loss, n2n_subsample
 from .optim import FlatAdam, lr_at_epoch
-from .util import structure_loss
+from .util import structure_loss_into
 
 
 class N2NTrainer:
@@ -53,8 +53,27 @@ class N2NTrainer:
         self.grad = torch.zeros_like(net.flat_params)
         self.global_step = 0
         self._bufs = {}
+        self._overlap = os.environ.get("DN_AR_OVERLAP", "1") != "0"
+        self._tail_begin = net.tail_begin() if self.distributed and self._overlap else 0
 
     _side = {}
+    _comm = {}
+
+    @classmethod
+    def _comm_stream(cls, device):
+        """the stream the early gradient bucket's all-reduce is enqueued on"""
+        if torch.device(device).type != "cuda":
+            return None
+        st = cls._comm.get(device)
+        if st is None:
+            st = cls._comm[device] = torch.cuda.Stream(device=device)
+        return st
+
+    def _backward(self, dout, ws, N, h, w, ev):
+        if ev is None:
+            self.net._run_backward(dout, self.grad, ws, N, h, w)
+        else:
+            self.net._run_backward_split(dout, self.grad, ws, N, h, w, ev)
 
     @classmethod
     def _side_stream(cls, device):
@@ -133,9 +152,17 @@ class N2NTrainer:
         if side is not None:
             main.wait_stream(side)
         loss3, dout = n2n_loss(b["out"], sub2, b["den"], rd, self.lambda_for(epoch))
-        self.net._run_backward(dout, self.grad, b["ws_grad"], N, H // 2, W // 2)
-        # RCCL all-reduce(sum) over xGMI, one per step; 1/world folded into Adam
-        scale = dp.allreduce_grads(self.grad) if self.distributed else 1.0
+        # RCCL all-reduce(sum) over xGMI; 1/world folded into Adam.  Data-parallel: two buckets,
+        # the decoder + head one overlapping the encoder's backward (DN_AR_OVERLAP=0: one
+        # all-reduce after the whole backward)
+        if self.distributed and self._overlap:
+            scale = dp.allreduce_grads_split(
+                self.grad, self._tail_begin,
+                lambda ev: self._backward(dout, b["ws_grad"], N, H // 2, W // 2, ev),
+                self._comm_stream(clean.device))
+        else:
+            self.net._run_backward(dout, self.grad, b["ws_grad"], N, H // 2, W // 2)
+            scale = dp.allreduce_grads(self.grad) if self.distributed else 1.0
         self.opt.lr = lr_at_epoch(epoch, self.base_lr, self.n_epoch, self.gamma)
         self.opt.step(self.grad, grad_scale=scale)
         self.global_step += 1
@@ -145,13 +172,17 @@ class N2NTrainer:
 class StructureTrainer:
     """The step of the reference's own train.py loop (train.py:355-368), fused:
 
-        pred  = UNet(noisy)   [saved]                 dn_unet_forward   (train.py:361)
-        pred2 = UNet(clean)   [saved]                 dn_unet_forward
+        pred, pred2 = UNet([noisy; clean])  [saved]   dn_unet_forward   (train.py:361-362)
         loss5, dpred, dpred2 = Structure_loss(pred, pred2, clean)
                                                       dn_structure_loss (util.py:56-70)
-        dW = backward(dpred) + backward(dpred2)       dn_unet_backward x2 + dn_accumulate
+        dW = backward([dpred; dpred2])                dn_unet_backward
         [data parallel: one RCCL all-reduce(sum) of dW]
         Adam(W, dW / world)                           dn_adam_step      (train.py:368)
+
+    `network(noisy)` and `network(clean)` share the weights, so they run as ONE forward and ONE
+    backward over the 2N batch [noisy; clean]: the weight gradient of a batch is the sum over its
+    images, i.e. dW(pred) + dW(pred2) exactly as autograd forms it in the reference, with half
+    the launches and every small-level launch at twice the occupancy.
 
     Inputs are device tensors already scaled to [0, 1] (train.py:357 divides by 255).
     Returns loss5 = [pixel L1 (= F.l1_loss(pred, clean), train.py:365), tv1, tv2, cst, total].
@@ -167,18 +198,18 @@ class StructureTrainer:
             dp.broadcast_params(net.flat_params)
         self.opt = FlatAdam(net.flat_params, lr=lr)
         self.grad = torch.zeros_like(net.flat_params)
-        self.grad2 = torch.zeros_like(net.flat_params)
         self._bufs = {}
 
-    def _buffers(self, N, H, W, device):
-        key = (N, H, W, device)
+    def _buffers(self, N, C, H, W, device):
+        key = (N, C, H, W, device)
         if key not in self._bufs:
             f = dict(dtype=torch.float32, device=device)
             self._bufs = {key: dict(
-                pred=torch.empty((N, self.net.out_nc, H, W), **f),
-                pred2=torch.empty((N, self.net.out_nc, H, W), **f),
-                ws1=self.net._workspace(N, H, W, with_backward=True, fresh=True),
-                ws2=self.net._workspace(N, H, W, with_backward=True, fresh=True))}
+                inp=torch.empty((2 * N, C, H, W), **f),
+                pred=torch.empty((2 * N, self.net.out_nc, H, W), **f),
+                dpred=torch.empty((2 * N, self.net.out_nc, H, W), **f),
+                loss5=torch.empty(5, **f),
+                ws=self.net._workspace(2 * N, H, W, with_backward=True, fresh=True))}
         return self._bufs[key]
 
     def train_step(self, clean: torch.Tensor, noisy: torch.Tensor, epoch: int = 1) -> torch.Tensor:
@@ -187,17 +218,16 @@ class StructureTrainer:
             raise ValueError("clean and noisy must share one [N, in_nc, H, W] shape")
         if self.net.in_nc != self.net.out_nc:
             raise ValueError("Structure_loss compares the output with the input: in_nc == out_nc")
-        N, _, H, W = clean.shape
-        b = self._buffers(N, H, W, clean.device)
-        self.net._run_forward(noisy, b["pred"], b["ws1"])
-        self.net._run_forward(clean, b["pred2"], b["ws2"])
+        N, C, H, W = clean.shape
+        b = self._buffers(N, C, H, W, clean.device)
+        b["inp"][:N].copy_(noisy)
+        b["inp"][N:].copy_(clean)
+        self.net._run_forward(b["inp"], b["pred"], b["ws"])
         a, be, g = self.weights
-        loss5, dpred, dpred2 = structure_loss(b["pred"], b["pred2"], clean, a, be, g)
-        self.net._run_backward(dpred, self.grad, b["ws1"], N, H, W)
-        self.net._run_backward(dpred2, self.grad2, b["ws2"], N, H, W)
-        _lib.call("dn_accumulate", _lib.ptr(self.grad), _lib.ptr(self.grad2), self.grad.numel(),
-                  _lib.stream_of(self.grad))
+        pred, pred2 = b["pred"][:N], b["pred"][N:]
+        structure_loss_into(pred, pred2, clean, a, be, g, b["dpred"][:N], b["dpred"][N:], b["loss5"])
+        self.net._run_backward(b["dpred"], self.grad, b["ws"], 2 * N, H, W)
         scale = dp.allreduce_grads(self.grad) if self.distributed else 1.0
         self.opt.lr = lr_at_epoch(epoch, self.base_lr, self.n_epoch, self.gamma)
         self.opt.step(self.grad, grad_scale=scale)
-        return loss5
+        return b["loss5"].clone()

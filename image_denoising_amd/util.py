@@ -12,18 +12,30 @@ from . import _lib
 from .n2n import _partials_for
 
 
+def structure_loss_into(pred, pred2, target, alpha, beta, gamma, dpred, dpred2, loss5):
+    """dn_structure_loss into given contiguous buffers: loss5 = [pixel, tv1, tv2, cst, total],
+    dpred = dL/dpred, dpred2 = dL/dpred2 (all on pred's device and stream)"""
+    for t in (pred, pred2, target, dpred, dpred2, loss5):
+        if not t.is_contiguous():
+            raise ValueError("structure_loss_into needs contiguous tensors")
+    if (pred.shape != pred2.shape or pred.shape != target.shape or pred.dim() != 4
+            or dpred.shape != pred.shape or dpred2.shape != pred.shape or loss5.numel() != 5):
+        raise ValueError("pred, pred2, target, dpred and dpred2 must share one [N,C,H,W] shape")
+    N, C, H, W = pred.shape
+    _lib.call("dn_structure_loss", _lib.ptr(pred), _lib.ptr(pred2), _lib.ptr(target), N, C, H, W,
+              float(alpha), float(beta), float(gamma), _lib.ptr(dpred), _lib.ptr(dpred2),
+              _lib.ptr(loss5), _partials_for(pred.device).data_ptr(), _lib.stream_of(pred))
+
+
 def structure_loss(pred, pred2, target, alpha=1.0, beta=0.5, gamma=0.5):
     """returns (loss5 = [pixel, tv1, tv2, cst, total] device tensor, dpred, dpred2)"""
     pred, pred2, target = pred.contiguous(), pred2.contiguous(), target.contiguous()
     if pred.shape != pred2.shape or pred.shape != target.shape or pred.dim() != 4:
         raise ValueError("pred, pred2 and target must share one [N,C,H,W] shape")
-    N, C, H, W = pred.shape
     dpred = torch.empty_like(pred)
     dpred2 = torch.empty_like(pred2)
     loss5 = torch.empty(5, dtype=torch.float32, device=pred.device)
-    _lib.call("dn_structure_loss", _lib.ptr(pred), _lib.ptr(pred2), _lib.ptr(target), N, C, H, W,
-              float(alpha), float(beta), float(gamma), _lib.ptr(dpred), _lib.ptr(dpred2),
-              _lib.ptr(loss5), _partials_for(pred.device).data_ptr(), _lib.stream_of(pred))
+    structure_loss_into(pred, pred2, target, alpha, beta, gamma, dpred, dpred2, loss5)
     return loss5, dpred, dpred2
 
 

@@ -62,8 +62,9 @@ const char* dn_version(void);
 /* The ABI revision of this header; a caller compiled against another revision must not bind.
    Revision 3 (library 0.3.x): dn_unet_backward / dn_unet_backward_prec gained the nullable
    `float* dx` argument after `dparams` (revision 2 had no dx: an old caller's arguments would
-   be shifted, so check dn_abi_version() == DN_ABI_VERSION before binding). */
-#define DN_ABI_VERSION 3
+   be shifted, so check dn_abi_version() == DN_ABI_VERSION before binding).  Revision 4
+   (library 0.4.x): dn_unet_backward_split added (existing signatures unchanged). */
+#define DN_ABI_VERSION 4
 int dn_abi_version(void);
 /* copies the last error message of this thread into buf (NUL-terminated); returns its length */
 int dn_last_error(char* buf, size_t len);
@@ -144,6 +145,20 @@ dn_status dn_unet_forward_prec(const dn_unet_cfg* cfg, const float* params, cons
 dn_status dn_unet_backward_prec(const dn_unet_cfg* cfg, const float* params, const float* dy,
                                 float* dparams, float* dx, int N, int H, int W, void* ws,
                                 size_t ws_bytes, int precision, void* stream);
+/* dn_unet_backward_prec for a data-parallel step that overlaps the gradient all-reduce with
+   the backward (train.py:324-326 reduces inside the backward too).  The backward finishes the
+   head's and the decoder's parameter gradients first: dparams[*tail_begin ..] (the state_dict
+   tail from dec_conv5a on: every decoder layer except upsample5, the head) is final once
+   tail_ready (a hipEvent_t the caller created on the device of stream, passed as void*) fires;
+   the library records it on the stream that finishes that range.  dparams[0 .. *tail_begin)
+   (the encoder and upsample5) is final when the work queued on `stream` completes, as for
+   dn_unet_backward_prec.  A caller then all-reduces the tail on a stream that waits on
+   tail_ready while the encoder's gradients are still being computed.  tail_ready may be NULL
+   (then only *tail_begin is set); tail_begin may be NULL. */
+dn_status dn_unet_backward_split(const dn_unet_cfg* cfg, const float* params, const float* dy,
+                                 float* dparams, float* dx, int N, int H, int W, void* ws,
+                                 size_t ws_bytes, int precision, void* stream, void* tail_ready,
+                                 int64_t* tail_begin);
 
 /* Debug/introspection: (offset_floats, channel_stride, level) of every NHWC buffer of the
    workspace plan, in the order c1 a0 a1 c2..c5 a2..a5 p5 a6 d{2..5}a d{2..5}b d1a d1b nin_a nin_b

@@ -10,6 +10,7 @@ a fixed global batch, then rank 0 writes what the test compares.
     python tests/dp_worker.py OUT.npz PRECISION nccl       (one rank, RCCL)
     python tests/dp_worker.py OUT.npz PRECISION local      (no group; env-selected streams)
     python tests/dp_worker.py OUT.npz PRECISION grad       (one UNet forward + backward)
+    python tests/dp_worker.py OUT.npz PRECISION igrad      (one ImprovedUNet forward + backward)
 
 The `nccl` form is a ONE-rank RCCL group on the box's one GPU (RCCL does not put two ranks on
 one device): the product trainer's broadcast and per-step all-reduce run through RCCL for real,
@@ -110,8 +111,27 @@ def main_grad(out, prec):
     np.savez(out, y=y.detach().cpu().numpy(), g=g.cpu().numpy(), dx=x.grad.cpu().numpy())
 
 
+def main_igrad(out, prec):
+    """one forward + backward of the product ImprovedUNet (DPW_SHAPE B,H,W; C = 1) under the
+    env's kernel routing (DN_W6_MIN_TILES, DN_X6_W6)"""
+    from image_denoising_amd.improved_unet import ImprovedUNet
+
+    torch.manual_seed(0)
+    net = ImprovedUNet(in_nc=1, out_nc=1, n_feature=48).to("cuda").set_precision(prec)
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(B, 1, H, W, generator=g).cuda()
+    y = net(x)
+    (y ** 2).mean().backward()
+    names = [n for n, _ in net.named_parameters()]
+    grads = [p.grad.detach().reshape(-1).cpu().numpy() for _, p in net.named_parameters()]
+    np.savez(out, y=y.detach().cpu().numpy(), names=np.array(names),
+             **{f"g{i}": v for i, v in enumerate(grads)})
+
+
 def main():
     out, prec = sys.argv[1], sys.argv[2]
+    if len(sys.argv) > 3 and sys.argv[3] == "igrad":
+        return main_igrad(out, prec)
     if len(sys.argv) > 3 and sys.argv[3] == "grad":
         return main_grad(out, prec)
     if len(sys.argv) > 3 and sys.argv[3] == "nccl":

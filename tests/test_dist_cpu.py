@@ -166,9 +166,11 @@ def _cpu_stand_ins(net, tr):
         l1, l2, l, dout = n2n_ref.n2n_loss(out, sub2, den.numpy(), rd_idx.numpy(), lam)
         return torch.tensor([l1, l2, l]), torch.from_numpy(dout)
 
-    def sloss(pred, pred2, target, a, b, g):
+    def sloss_into(pred, pred2, target, a, b, g, dpred, dpred2, loss5):
         l, dp_, dp2, parts = n2n_ref.structure_loss(pred, pred2, target, a, b, g)
-        return torch.tensor(parts), torch.from_numpy(dp_), torch.from_numpy(dp2)
+        loss5.copy_(torch.tensor(parts))
+        dpred.copy_(torch.from_numpy(dp_))
+        dpred2.copy_(torch.from_numpy(dp2))
 
     def adam(opt, grad, grad_scale):  # dn_adam_step's formula (torch _single_tensor_adam)
         b1, b2 = opt.betas
@@ -180,12 +182,10 @@ def _cpu_stand_ins(net, tr):
         opt.params.addcdiv_(opt.exp_avg, denom, value=-opt.lr / bc1)
 
     trainer_mod.n2n_subsample, trainer_mod.n2n_loss = subsample, loss
-    trainer_mod.structure_loss = sloss
-    by_ptr = {t.data_ptr(): t for t in (tr.grad, getattr(tr, "grad2", tr.grad))}
+    trainer_mod.structure_loss_into = sloss_into
 
-    def call(name, *a):  # the one raw launch left in the trainers: StructureTrainer's sum
-        assert name == "dn_accumulate", name
-        by_ptr[a[0]].add_(by_ptr[a[1]])
+    def call(name, *a):  # the trainers launch nothing raw besides the stand-ins above
+        raise AssertionError(name)
 
     trainer_mod._lib.call = call
     optim_mod.adam_launch = adam
@@ -279,9 +279,9 @@ def _run_trainer(kind, rank, world, steps=2):
     return torch.stack(losses), tr.grad / world, net.flat_params.clone()
 
 
-def _trainer_worker(rank, world, port, kind, out_q):
+def _trainer_worker(rank, world, port, kind, out_q, overlap="1"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DN_AR_OVERLAP=overlap)
     from image_denoising_amd import dist as dp
 
     dp.init_from_env("gloo")
@@ -301,14 +301,16 @@ def _single_worker(kind, out_q):
     out_q.put((losses.numpy(), grad.numpy(), flat.numpy()))
 
 
-def _spawn(target, args, nproc):
-    """run target(rank?, *args, q) in fresh spawned processes; rank 0's one queue item"""
+def _spawn(target, args, nproc, nargs=None):
+    """run target(rank?, *args[:nargs], q, *args[nargs:]) in fresh spawned processes; rank 0's
+    one queue item"""
+    nargs = len(args) if nargs is None else nargs
     import queue as _queue
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=target, args=((r,) if nproc > 1 else ()) + args + (q,))
-             for r in range(nproc)]
+    procs = [ctx.Process(target=target, args=((r,) if nproc > 1 else ()) + args[:nargs] + (q,)
+                         + args[nargs:]) for r in range(nproc)]
     for p_ in procs:
         p_.start()
     got = None
@@ -344,3 +346,29 @@ def test_two_rank_product_trainer_equals_full_batch(kind):
     d = np.abs(flats[0] - flat)
     assert (d > 1e-6).mean() < 2e-3, (d > 1e-6).mean()
     assert d.max() <= 2 * 2 * 3e-4 + 1e-6
+
+
+def test_two_rank_bucketed_allreduce_equals_one_allreduce():
+    """N2NTrainer's overlapped all-reduce (two buckets: the decoder + head range the backward
+    finishes first, then the encoder; DN_AR_OVERLAP=1, the default) gives the single
+    all-reduce's step bit for bit (DN_AR_OVERLAP=0): sums are elementwise"""
+    port = _free_port()
+    bucketed = _spawn(_trainer_worker, (2, port, "n2n", "1"), 2, nargs=3)
+    one = _spawn(_trainer_worker, (2, _free_port(), "n2n", "0"), 2, nargs=3)
+    assert np.array_equal(bucketed[0], one[0])
+    assert np.array_equal(bucketed[1], one[1])
+    assert np.array_equal(bucketed[2][0], one[2][0]) and np.array_equal(bucketed[2][1], one[2][1])
+
+
+def test_tail_bucket_is_the_decoder_and_head():
+    """the early bucket starts at dec_conv5a's weight (state_dict order): everything after it is
+    a decoder layer below upsample5 or the head"""
+    from image_denoising_amd import UNet
+
+    net = UNet(1, 1, 48)
+    off = 0
+    for name, p in net.named_parameters():
+        if name.startswith("dec_conv5a"):
+            break
+        off += p.numel()
+    assert net.tail_begin() == off

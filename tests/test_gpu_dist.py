@@ -74,6 +74,37 @@ def test_two_rank_n2n_trainer_equals_full_batch(tmp_path, prec):
     assert d.max() <= 2 * 2 * 3e-4 + 1e-6
 
 
+def _two_rank_gloo(tmp_path, tag, prec, extra):
+    out = str(tmp_path / f"{tag}.npz")
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONUNBUFFERED="1", **extra)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), out,
+                                       prec], env=env, cwd=ROOT))
+    try:
+        codes = [p.wait(timeout=240) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert codes == [0, 0], codes
+    return np.load(out)
+
+
+def test_two_rank_bucketed_allreduce_equals_one_allreduce(tmp_path):
+    """The overlapped gradient all-reduce (default: the decoder + head bucket all-reduced on a
+    comm stream behind the library's tail-ready event, while the encoder's gradients are still
+    computed; then the encoder bucket) against one all-reduce after the backward
+    (DN_AR_OVERLAP=0), two ranks on the GPU over gloo: bit-identical losses, gradient and
+    weights (the sums are elementwise, only their issue order moves)."""
+    a = _two_rank_gloo(tmp_path, "bucketed", "fp32_x6", {"DN_AR_OVERLAP": "1"})
+    b = _two_rank_gloo(tmp_path, "one", "fp32_x6", {"DN_AR_OVERLAP": "0"})
+    for k in ("losses", "grad", "flat0", "flat1"):
+        assert np.array_equal(a[k], b[k]), k
+
+
 def test_one_rank_rccl_n2n_trainer_bit_exact(tmp_path):
     """The RCCL path itself (BASELINE configs[2]'s collective, train.py:324-326): a ONE-rank
     "nccl" process group on the box's GPU, started in a fresh process before any GPU call.
@@ -133,12 +164,12 @@ def test_backward_with_padded_concat_strides(tmp_path, prec):
         assert np.abs(a - b).max() <= 1e-5 * np.abs(a).max(), (k, np.abs(a - b).max())
 
 
-def _worker_env_run(tmp_path, tag, extra, mode, prec="fp32_x6"):
+def _worker_env_run(tmp_path, tag, extra, mode, prec="fp32_x6", shape="8,128,128"):
     """dp_worker.py on 8 x 128^2 (the 96-output convs at 128^2 take k_c3w6, the 48-channel
     encoder the pipelined kernels with the fused pool)"""
     out = str(tmp_path / f"{tag}.npz")
-    env = dict(os.environ, PYTHONUNBUFFERED="1", DPW_SHAPE="8,128,128", **extra)
-    for k in ("DN_POOL_FUSE", "DN_X6_W6", "DN_X6_RING3"):
+    env = dict(os.environ, PYTHONUNBUFFERED="1", DPW_SHAPE=shape, **extra)
+    for k in ("DN_POOL_FUSE", "DN_X6_W6", "DN_X6_RING3", "DN_W6_MIN_TILES"):
         if k not in extra:
             env.pop(k, None)
     p = subprocess.run([sys.executable, os.path.join(HERE, "dp_worker.py"), out, prec, mode],
@@ -180,3 +211,20 @@ def test_winograd_step_matches_direct_kernels(tmp_path):
     for k, tol in (("y", 2e-5), ("g", 2e-5), ("dx", 5e-2)):
         a, b = w6[k], d[k]
         assert np.abs(a - b).max() <= tol * np.abs(a).max(), (k, np.abs(a - b).max())
+
+
+def test_improved_unet_winograd_blocks_match_direct_kernels(tmp_path):
+    """ImprovedUNet's 96 / 192 / 384-channel 3x3 forwards and data gradients on k_c3w6 in
+    96-channel output blocks (blockIdx.z: the per-block image stride wp_z, the channel offset of
+    the epilogue) against the direct bf16x6 kernels (DN_X6_W6=0).  DN_W6_MIN_TILES=1 routes every
+    96-block launch to the Winograd kernel at this test size (the default takes it from one
+    round of 512 tiles, i.e. at the bench's 64 x 256^2).  Same arithmetic class, so the output
+    and every parameter gradient agree to fp32 rounding: 2e-5 of the max magnitude, as the UNet
+    test above."""
+    w6 = _worker_env_run(tmp_path, "iw6", {"DN_W6_MIN_TILES": "1"}, "igrad", shape="2,64,64")
+    d = _worker_env_run(tmp_path, "idirect", {"DN_X6_W6": "0"}, "igrad", shape="2,64,64")
+    a, b = w6["y"], d["y"]
+    assert np.abs(a - b).max() <= 2e-5 * np.abs(a).max(), np.abs(a - b).max()
+    ga = np.concatenate([w6[f"g{i}"] for i in range(len(w6["names"]))])
+    gb = np.concatenate([d[f"g{i}"] for i in range(len(d["names"]))])
+    assert np.abs(ga - gb).max() <= 2e-5 * np.abs(ga).max(), np.abs(ga - gb).max()

@@ -70,6 +70,9 @@ def _forward(x, w, b, act, x6):
     (100, 96, 2, 256, 256), (36, 48, 4, 128, 128), (80, 96, 8, 128, 128), (16, 48, 8, 128, 128),
     # 32 outputs (ImprovedUNet RDB growth convs): 4-wave and pipelined (+ tail)
     (48, 32, 2, 32, 32), (144, 32, 1, 24, 40), (80, 32, 8, 128, 128), (112, 32, 8, 128, 128),
+    # ImprovedUNet routes on large grids: K 48..79 at 32 outputs, zero-padded 32-wide K (88,
+    # 120), and 72 -> 24 (the pipelined / half kernels, not only the 4-wave small-grid ones)
+    (48, 32, 8, 128, 128), (88, 32, 8, 128, 128), (120, 32, 8, 128, 128), (72, 24, 8, 128, 128),
 ])
 @pytest.mark.parametrize("act", [0, 1])
 def test_x6_forward_vs_fp64(cin, cout, N, H, W, act):
@@ -119,6 +122,9 @@ def _dgrad(dz, w, cin, mode, mask, base, x6):
     # ImprovedUNet shapes: final conv (K = out_nc), RDB growth convs (K = 32, wide outputs)
     (24, 3, 1, 32, 32), (24, 1, 2, 32, 32), (144, 32, 1, 16, 16), (112, 32, 1, 16, 16),
     (80, 32, 2, 16, 16), (120, 32, 1, 32, 32), (72, 24, 1, 32, 32),
+    # ... on large grids: K = 32 data gradients into 80 / 112 / 144 channels (48-channel blocks,
+    # a partial last one) and 72 -> 24
+    (80, 32, 8, 128, 128), (112, 32, 8, 128, 128), (144, 32, 8, 128, 128), (72, 24, 8, 128, 128),
 ])
 @pytest.mark.parametrize("mode", ["plain", "mask", "accum"])
 def test_x6_backward_data_vs_fp64(cin, cout, N, H, W, mode):
