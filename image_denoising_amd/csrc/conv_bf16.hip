@@ -11,12 +11,16 @@
 //   [w*MT, w*MT+MT).  K is staged 32 input channels at a time (one MFMA K): the x tile (with
 //   halo) once per chunk, the weights one kernel row (3 taps; 1x1: the single tap) per stage,
 //   double-buffered by global_load_lds.  Per stage a wave issues 3*MT*NT MFMAs of 16x16x32.
-//   LDS rows are 40 bf16 (80 B: 32 + 8 pad) per pixel / per (tap, output channel): a lane's
-//   8-element operand (k = 8*(lane>>4) .. +7) is one ds_read_b128.
+//   LDS rows are 32 bf16 (64 B) per pixel / per (tap, output channel), the 16-B quad q of row r
+//   stored at quad x6_swz(r, q) = q ^ ((r >> 1) & 3) (the bf16x6 kernels' layout): a lane's
+//   8-element operand (k = 8*(lane>>4) .. +7) is one ds_read_b128, conflict-free over gfx950's
+//   ds_read_b128 lane groups for every tap offset.  (The unswizzled 80-B rows of round 2 were
+//   2-way on a third of those groups: SQ_LDS_BANK_CONFLICT 47 % of the LDS-active cycles.)
 #include <cstdlib>
 
 #include "conv_epi.h"
 #include "dn_internal.h"
+#include "x6_core.h"
 
 namespace dn {
 
@@ -29,9 +33,9 @@ struct BCfg {
   static constexpr int SPC = K3 ? 3 : 1;                     // weight stages per K chunk
   static constexpr int TW = 16, TH = 4 * MT, IH = TH + HALO, IW = TW + HALO;
   static constexpr int KC = 32;                       // input channels per chunk
-  static constexpr int XS = 40;                       // bf16 per pixel row of the x tile
+  static constexpr int XS = 32;                       // bf16 per pixel row of the x tile
   static constexpr int NP = 16 * NT;
-  static constexpr int WS = 40;                       // bf16 per (tap, n) row of a weight stage
+  static constexpr int WS = 32;                       // bf16 per (tap, n) row of a weight stage
   static constexpr int WST = (TPS * NP * WS + 511) / 512 * 512;  // bf16 per stage, whole KiBs
   static constexpr int LXB = (IH * IW * XS + 511) / 512 * 512;  // bf16 of the x tile
   static constexpr int XQ = IH * IW * (KC / 4);       // float4 items of the x tile
@@ -59,7 +63,7 @@ __device__ __forceinline__ void blds16b(__amdgpu_buffer_rsrc_t rs, void* l, int 
 #endif
 }
 
-template <int NT, int MT, bool K3>
+template <int NT, int MT, bool K3, bool IB = false>
 __global__ __launch_bounds__(256, 2) void k_fwd_bf16(FwdArgs a) {
   using C = BCfg<NT, MT, K3>;
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
@@ -88,10 +92,26 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16(FwdArgs a) {
     for (int q = 0; q < NT; ++q) acc[m][q] = f32x4b{0.f, 0.f, 0.f, 0.f};
 
   float4 xr[C::XITEMS];
+  typedef unsigned u32x2b __attribute__((ext_vector_type(2)));
+  u32x2b xh[IB ? C::XITEMS : 1];  // (IB) bf16 input: 4 channels = 8 bytes, stored as loaded
   auto load_x = [&](int k0) {
 #pragma unroll
     for (int it = 0; it < C::XITEMS; ++it) {
       const int e = tid + it * 256;
+      if constexpr (IB) {  // channel quads whole (K % 4 == 0, aligned views: the launcher)
+        u32x2b v = {0u, 0u};
+        if (e < C::XQ) {
+          const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+          const int iy = pix / C::IW, ix = pix - iy * C::IW;
+          const int gy = iy0 + iy, gx = ix0 + ix, k = k0 + 4 * q;
+          if (gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt && k < a.K)
+            v = *reinterpret_cast<const u32x2b*>(reinterpret_cast<const __bf16*>(a.in) +
+                                                 ((long)n * a.IHt * a.IWt + (long)gy * a.IWt + gx) *
+                                                     a.in_stride + a.in_off + k);
+        }
+        xh[it] = v;
+        continue;
+      }
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (e < C::XQ) {
         const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
@@ -118,11 +138,16 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16(FwdArgs a) {
       const int e = tid + it * 256;
       if (e < C::XQ) {
         const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
+        __bf16* dst = lx + pix * C::XS + x6_swz(pix, q >> 1) * 8 + (q & 1) * 4;
+        if constexpr (IB) {
+          *reinterpret_cast<u32x2b*>(dst) = xh[it];
+          continue;
+        }
         typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
         bf16x4 h;
         h[0] = (__bf16)xr[it].x; h[1] = (__bf16)xr[it].y;
         h[2] = (__bf16)xr[it].z; h[3] = (__bf16)xr[it].w;
-        *reinterpret_cast<bf16x4*>(lx + pix * C::XS + 4 * q) = h;
+        *reinterpret_cast<bf16x4*>(dst) = h;
       }
     }
   };
@@ -149,11 +174,13 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16(FwdArgs a) {
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const int r = wave * MT + m;
-        av[m] = *reinterpret_cast<const bf16x8*>(lx + ((r + ky) * C::IW + li + kx) * C::XS + 8 * lg);
+        const int pix = (r + ky) * C::IW + li + kx;
+        av[m] = *reinterpret_cast<const bf16x8*>(lx + pix * C::XS + x6_swz(pix, lg) * 8);
       }
 #pragma unroll
       for (int q = 0; q < NT; ++q)
-        bv[q] = *reinterpret_cast<const bf16x8*>(lw + (kx * C::NP + q * 16 + li) * C::WS + 8 * lg);
+        bv[q] = *reinterpret_cast<const bf16x8*>(lw + (kx * C::NP + q * 16 + li) * C::WS +
+                                                 x6_swz(kx * C::NP + q * 16 + li, lg) * 8);
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -194,7 +221,7 @@ __device__ __forceinline__ void bf_barrier() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-template <int NT, int MT>
+template <int NT, int MT, bool IB = false>
 __global__ __launch_bounds__(256, 2) void k_fwd_bf16p(FwdArgs a) {
   using C = BCfg<NT, MT, true>;
   constexpr int PIECES = C::WST / 512, PPW = (PIECES + 3) / 4;
@@ -212,7 +239,9 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16p(FwdArgs a) {
   const int tx0 = (bxr % tiles_x) * C::TW;
   const int n = byr;
   const int iy0 = ty0 - 1, ix0 = tx0 - 1;
-  const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
+  constexpr int EB = IB ? 2 : 4;  // bytes per stored activation
+  const unsigned char* inb = reinterpret_cast<const unsigned char*>(a.in) +
+                             ((long)n * a.IHt * a.IWt * a.in_stride + a.in_off) * EB;
   const __bf16* wimg = reinterpret_cast<const __bf16*>(a.wp);
   const int nch = (a.K + C::KC - 1) / C::KC;
   const int nst = 3 * nch;
@@ -225,11 +254,13 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16p(FwdArgs a) {
 
   // this tile's input rows through a 32-bit buffer resource (host: < 2 GiB per tile's rows)
   const int ry0 = iy0 > 0 ? iy0 : 0, ry1 = iy0 + C::IH < a.IHt ? iy0 + C::IH : a.IHt;
-  const long row_floats = (long)a.IWt * a.in_stride;
+  const long row_elems = (long)a.IWt * a.in_stride;
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(inb + ry0 * row_floats), (short)0, (int)((ry1 - ry0) * row_floats * 4),
-      0x00020000);
-  f32x4b xr[C::XITEMS];
+      const_cast<unsigned char*>(inb + ry0 * row_elems * EB), (short)0,
+      (int)((ry1 - ry0) * row_elems * EB), 0x00020000);
+  typedef unsigned u32x2b __attribute__((ext_vector_type(2)));
+  f32x4b xr[IB ? 1 : C::XITEMS];
+  u32x2b xh[IB ? C::XITEMS : 1];  // (IB) bf16 input: 4 channels = 8 bytes, stored as loaded
   auto load_x = [&](int k0) {
 #pragma unroll
     for (int it = 0; it < C::XITEMS; ++it) {
@@ -238,8 +269,11 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16p(FwdArgs a) {
       const int iy = pix / C::IW, ix = pix - iy * C::IW;
       const int gy = iy0 + iy, gx = ix0 + ix, k = k0 + 4 * q;
       const bool ok = e < C::XQ && gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt && k < a.K;
-      const int off = ok ? (((gy - ry0) * a.IWt + gx) * a.in_stride + k) * 4 : 0x7fffffff;
-      xr[it] = __builtin_bit_cast(f32x4b, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      const int off = ok ? (((gy - ry0) * a.IWt + gx) * a.in_stride + k) * EB : 0x7fffffff;
+      if constexpr (IB)
+        xh[it] = __builtin_bit_cast(u32x2b, __builtin_amdgcn_raw_buffer_load_b64(xrs, off, 0, 0));
+      else
+        xr[it] = __builtin_bit_cast(f32x4b, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
   };
   auto store_x = [&]() {
@@ -248,11 +282,16 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16p(FwdArgs a) {
       const int e = tid + it * 256;
       if (e < C::XQ) {
         const int q = e % (C::KC / 4), pix = e / (C::KC / 4);
-        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-        bf16x4 h;
-        h[0] = (__bf16)xr[it][0]; h[1] = (__bf16)xr[it][1];
-        h[2] = (__bf16)xr[it][2]; h[3] = (__bf16)xr[it][3];
-        *reinterpret_cast<bf16x4*>(lx + pix * C::XS + 4 * q) = h;
+        __bf16* dst = lx + pix * C::XS + x6_swz(pix, q >> 1) * 8 + (q & 1) * 4;
+        if constexpr (IB) {
+          *reinterpret_cast<u32x2b*>(dst) = xh[it];
+        } else {
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          bf16x4 h;
+          h[0] = (__bf16)xr[it][0]; h[1] = (__bf16)xr[it][1];
+          h[2] = (__bf16)xr[it][2]; h[3] = (__bf16)xr[it][3];
+          *reinterpret_cast<bf16x4*>(dst) = h;
+        }
       }
     }
   };
@@ -287,11 +326,13 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16p(FwdArgs a) {
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const int r = wave * MT + m;
-        av[m] = *reinterpret_cast<const bf16x8*>(lx + ((r + ky) * C::IW + li + kx) * C::XS + 8 * lg);
+        const int pix = (r + ky) * C::IW + li + kx;
+        av[m] = *reinterpret_cast<const bf16x8*>(lx + pix * C::XS + x6_swz(pix, lg) * 8);
       }
 #pragma unroll
       for (int q = 0; q < NT; ++q)
-        bv[q] = *reinterpret_cast<const bf16x8*>(lw + (kx * C::NP + q * 16 + li) * C::WS + 8 * lg);
+        bv[q] = *reinterpret_cast<const bf16x8*>(lw + (kx * C::NP + q * 16 + li) * C::WS +
+                                                 x6_swz(kx * C::NP + q * 16 + li, lg) * 8);
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -317,8 +358,8 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16p(FwdArgs a) {
   fwd_epilogue<NT, MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
 }
 
-// bf16 weight image: [chunk][ky][kx][n][WS] (k = chunk*32 + kk for kk < 32; zero padded), each
-// (chunk, ky) stage rounded up to whole KiB
+// bf16 weight image: [chunk][ky][kx][n][32] (k = chunk*32 + kk; zero padded), the quads of row
+// kx*NP + n swizzled as the LDS image (x6_swz), each (chunk, ky) stage rounded up to whole KiB
 __global__ __launch_bounds__(256) void k_pack_bf16(WView wv, int K, int NOUT, int NP, int WST,
                                                    int k3, long total, __bf16* __restrict__ out) {
   const int spc = k3 ? 3 : 1;
@@ -327,10 +368,11 @@ __global__ __launch_bounds__(256) void k_pack_bf16(WView wv, int K, int NOUT, in
     const int r = (int)(e - st * WST);
     const int c = (int)(st / spc), ky = (int)(st % spc);
     float v = 0.f;
-    if (r < spc * NP * 40) {
-      const int kx = r / (NP * 40), nn = (r / 40) % NP, kk = r % 40;
+    if (r < spc * NP * 32) {
+      const int row = r / 32, kx = row / NP, nn = row % NP;
+      const int kk = x6_swz(row, (r % 32) / 8) * 8 + r % 8;  // the swizzle is an involution
       const int k = c * 32 + kk;
-      if (kk < 32 && k < K && nn < NOUT) {
+      if (k < K && nn < NOUT) {
         const int t = k3 ? ky * 3 + kx : 0;
         const int tm = wv.flip ? wv.taps - 1 - t : t;
         v = wv.w[wv.off + (long)k * wv.sK + (long)nn * wv.sN + (long)tm * wv.sT];
@@ -345,7 +387,10 @@ static hipError_t run_bf16(const FwdArgs& a, hipStream_t s) {
   using C = BCfg<NT, MT, K3>;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
   const int nz = a.out_layout == OUT_UP2 ? 4 : 1;
-  hipLaunchKernelGGL((k_fwd_bf16<NT, MT, K3>), dim3(tx * ty, a.N, nz), dim3(256), 0, s, a);
+  if (a.in_bf16)
+    hipLaunchKernelGGL((k_fwd_bf16<NT, MT, K3, true>), dim3(tx * ty, a.N, nz), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_fwd_bf16<NT, MT, K3>), dim3(tx * ty, a.N, nz), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -403,6 +448,9 @@ hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize) {
       (a.out_layout != OUT_NHWC && !(a.out_layout == OUT_UP2 && ksize == 1)) ||
       (a.epi != EPI_BIAS && a.epi != EPI_BIAS_ACT) || !a.bias || (ksize != 1 && ksize != 3))
     return hipErrorInvalidValue;
+  // bf16 activation storage: whole channel quads (8-byte loads / stores), the float4 epilogue
+  if ((a.in_bf16 && ((a.K | a.in_stride | a.in_off) & 3)) || (a.out_bf16 && a.out_layout != OUT_NHWC))
+    return hipErrorInvalidValue;
   const long tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16) *
                      (a.out_layout == OUT_UP2 ? 4 : 1);
   const bool small = tiles < 1024;
@@ -417,12 +465,15 @@ hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize) {
                     (long)BCfg<6, 4, true>::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL;
   if (pipe) {
     const int tx = (a.OW + 15) / 16, ty = (a.OH + 15) / 16;
+    const dim3 grid(tx * ty, a.N, 1);
     if (nt == 3) {
-      prof_kernel("k_fwd_bf16p<3,4>");
-      hipLaunchKernelGGL((k_fwd_bf16p<3, 4>), dim3(tx * ty, a.N, 1), dim3(256), 0, s, a);
+      prof_kernel(a.in_bf16 ? "k_fwd_bf16p<3,4,bf16in>" : "k_fwd_bf16p<3,4>");
+      if (a.in_bf16) hipLaunchKernelGGL((k_fwd_bf16p<3, 4, true>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((k_fwd_bf16p<3, 4>), grid, dim3(256), 0, s, a);
     } else {
-      prof_kernel("k_fwd_bf16p<6,4>");
-      hipLaunchKernelGGL((k_fwd_bf16p<6, 4>), dim3(tx * ty, a.N, 1), dim3(256), 0, s, a);
+      prof_kernel(a.in_bf16 ? "k_fwd_bf16p<6,4,bf16in>" : "k_fwd_bf16p<6,4>");
+      if (a.in_bf16) hipLaunchKernelGGL((k_fwd_bf16p<6, 4, true>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((k_fwd_bf16p<6, 4>), grid, dim3(256), 0, s, a);
     }
     return hipGetLastError();
   }

@@ -290,7 +290,13 @@ __device__ __forceinline__ void fwd_epilogue_vec_at(const FwdArgs& a, const f32x
       } else if (EPI == EPI_ACCUM) {
         v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
       }
-      *reinterpret_cast<float4*>(a.out + oi[m][k]) = v;
+      if (a.out_bf16) {  // (uniform) bf16 activation storage: RNE, 8 bytes per 4 channels
+        typedef __bf16 bf16x4e __attribute__((ext_vector_type(4)));
+        const bf16x4e h = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+        *reinterpret_cast<bf16x4e*>(reinterpret_cast<__bf16*>(a.out) + oi[m][k]) = h;
+      } else {
+        *reinterpret_cast<float4*>(a.out + oi[m][k]) = v;
+      }
     }
 }
 

@@ -1356,10 +1356,11 @@ __device__ __forceinline__ void pk_bf16(const PackJob& j, long e) {
   const int r = (int)(e - st * WST);
   const int c = (int)(st / spc), ky = (int)(st % spc);
   float v = 0.f;
-  if (r < spc * NP * 40) {
-    const int kx = r / (NP * 40), nn = (r / 40) % NP, kk = r % 40;
+  if (r < spc * NP * 32) {  // conv_bf16.hip's image: 32-bf16 rows, quads swizzled (x6_swz)
+    const int row = r / 32, kx = row / NP, nn = row % NP;
+    const int kk = x6_swz(row, (r % 32) / 8) * 8 + r % 8;
     const int k = c * 32 + kk;
-    if (kk < 32 && k < j.K && nn < j.NOUT) {
+    if (k < j.K && nn < j.NOUT) {
       const int t = j.g2 ? ky * 3 + kx : 0;
       const int tm = j.flip ? j.taps - 1 - t : t;
       v = j.w[(long)k * j.sK + (long)nn * j.sN + (long)tm * j.sT];
@@ -1998,8 +1999,19 @@ static hipError_t run_wgrad3s(const WgradArgs& a, int splits, hipStream_t s, int
   return hipGetLastError();
 }
 
+// DN_WG_P=1/0: the 96-output weight gradients on k_wgrad3p (operands split once per stage into
+// LDS planes, wgrad_x6p.hip) or k_wgrad3s (split at the operand read); default DN_WG_P_DEFAULT
+#ifndef DN_WG_P_DEFAULT
+#define DN_WG_P_DEFAULT 1
+#endif
+static bool wg_p() {
+  static const bool on = getenv("DN_WG_P") ? atoi(getenv("DN_WG_P")) != 0 : DN_WG_P_DEFAULT != 0;
+  return on;
+}
+
 hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s) {
   if (!wgrad3_x6_ok(a)) return hipErrorInvalidValue;
+  if (a.Cout == 96 && wg_p() && !wg_planes() && wgrad3p_ok(a)) return launch_wgrad3p(a, splits, s, 1);
   return a.Cout == 96 ? run_wgrad3s<6, 2, 2>(a, splits, s) : run_wgrad3s<3, 1, 3>(a, splits, s);
 }
 
@@ -2042,6 +2054,7 @@ hipError_t launch_gwgrad_x6(const WgradArgs& a0, int splits, hipStream_t s) {
   a.zc = cb;
   a.cout_total = a0.Cout;
   a.co_base = 0;
+  if (cb == 96 && wg_p() && !wg_planes() && wgrad3p_ok(a)) return launch_wgrad3p(a, splits, s, nz);
   if (cb == 96) return run_wgrad3s<6, 2, 2>(a, splits, s, nz);
   if (cb == 48) return run_wgrad3s<3, 1, 3>(a, splits, s, nz);
   const int ct = gw6_cib(cb, a.Cin);
@@ -2067,9 +2080,12 @@ hipError_t launch_gwgrad_x6(const WgradArgs& a0, int splits, hipStream_t s) {
 // SAVE: na / nb written for the backward; PAIR: the input is a pair image (hd.rd); B1: plain
 // bf16 products (the bf16 base's autocast arithmetic): the input rounded to bf16, the images'
 // leading planes (the weights rounded to bf16), one MFMA per block chained in fp32
-template <bool SAVE, bool PAIR, bool B1 = false>
+// IBF (with B1): the input activation is stored as bf16 (FwdArgs::in_bf16), 8 bytes per lane and
+// 4 channels, taken as the operand without conversion
+template <bool SAVE, bool PAIR, bool B1 = false, bool IBF = false>
 __global__ __launch_bounds__(512, 1) void k_nin_head_x6(FwdArgs a, HeadArgs hd, const __bf16* wimg,
                                                       int nwt) {
+  static_assert(!IBF || B1, "bf16 input only in the plain-bf16 head");
   __shared__ __attribute__((aligned(16))) __bf16 lw[2 * X6_HEAD_BF];
   __shared__ __attribute__((aligned(16))) float lb[2 * 96 + X6_HEAD_OCMAX * 97];  // ba|bb|wc|bc
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2095,13 +2111,22 @@ __global__ __launch_bounds__(512, 1) void k_nin_head_x6(FwdArgs a, HeadArgs hd, 
     const int n = wt / (a.OH * tiles_x), r = wt - n * a.OH * tiles_x;
     const int gy = r / tiles_x, gx = (r - gy * tiles_x) * 16 + li;
     const bool ok = wt < nwt && gx < a.OW;
+    constexpr int EB = IBF ? 2 : 4;  // bytes per stored activation
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.in + ((long)n * a.IHt + gy) * in_row + a.in_off), (short)0,
-        (int)(in_row * 4), 0x00020000);
-    const int off = ok ? (gx * a.in_stride + 4 * lg) * 4 : 0x7fffffff;
+        const_cast<unsigned char*>(reinterpret_cast<const unsigned char*>(a.in) +
+                                   (((long)n * a.IHt + gy) * in_row + a.in_off) * EB),
+        (short)0, (int)(in_row * EB), 0x00020000);
+    const int off = ok ? (gx * a.in_stride + 4 * lg) * EB : 0x7fffffff;
 #pragma unroll
-    for (int q = 0; q < 6; ++q)
-      v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 64 * q, 0, 0));
+    for (int q = 0; q < 6; ++q) {
+      if constexpr (IBF) {  // bf16 bits of channels 16q + 4lg .. +3 in v[q][0..1]
+        typedef unsigned u32x2h __attribute__((ext_vector_type(2)));
+        const u32x2h d = __builtin_bit_cast(u32x2h, __builtin_amdgcn_raw_buffer_load_b64(rs, off + 32 * q, 0, 0));
+        v[q] = f32x4{__uint_as_float(d[0]), __uint_as_float(d[1]), 0.f, 0.f};
+      } else {
+        v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 64 * q, 0, 0));
+      }
+    }
     if constexpr (PAIR) {  // the cell's pair choice, loaded with the row (no wait of its own later)
       const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
           const_cast<unsigned char*>(hd.rd + ((long)n * a.OH + gy) * (a.OW / 2)), (short)0,
@@ -2120,7 +2145,9 @@ __global__ __launch_bounds__(512, 1) void k_nin_head_x6(FwdArgs a, HeadArgs hd, 
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rs, off + 64 * q, 0, 0);
   };
   // out = W (LDS image at `img`) x in, three 32-channel K blocks of six split products each
-  auto gemm96 = [&](const __bf16* img, const f32x4 (&in)[6], f32x4 (&out)[6][1]) {
+  // (INB: `in` holds bf16 bits as loaded by load() under IBF)
+  auto gemm96 = [&](auto inb_tag, const __bf16* img, const f32x4 (&in)[6], f32x4 (&out)[6][1]) {
+    constexpr bool INB = decltype(inb_tag)::value;
 #pragma unroll
     for (int f = 0; f < 6; ++f) out[f][0] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -2129,8 +2156,14 @@ __global__ __launch_bounds__(512, 1) void k_nin_head_x6(FwdArgs a, HeadArgs hd, 
       const float v8[8] = {in[2 * b][0], in[2 * b][1], in[2 * b][2], in[2 * b][3],
                            in[2 * b + 1][0], in[2 * b + 1][1], in[2 * b + 1][2], in[2 * b + 1][3]};
       if constexpr (B1) {
+        if constexpr (INB) {
+          const u32x4_t d = {__float_as_uint(in[2 * b][0]), __float_as_uint(in[2 * b][1]),
+                             __float_as_uint(in[2 * b + 1][0]), __float_as_uint(in[2 * b + 1][1])};
+          xv[0][0] = __builtin_bit_cast(bf16x8, d);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xv[0][0][j] = (__bf16)v8[j];
+          for (int j = 0; j < 8; ++j) xv[0][0][j] = (__bf16)v8[j];
+        }
 #pragma unroll
         for (int f = 0; f < 6; ++f) {
           const int row = b * 96 + f * 16 + li;
@@ -2161,7 +2194,7 @@ __global__ __launch_bounds__(512, 1) void k_nin_head_x6(FwdArgs a, HeadArgs hd, 
     const long row = (long)n * a.OH + gy;
     const int soff = ok ? (gx * 96 + 4 * lg) * 4 : 0x7fffffff;
     f32x4 u[6][1], h[6];
-    gemm96(lw, xin, u);  // nin_a
+    gemm96(std::integral_constant<bool, IBF>{}, lw, xin, u);  // nin_a
 #pragma unroll
     for (int f = 0; f < 6; ++f) {
       bias_act(u[f][0], *reinterpret_cast<const float4*>(lb + f * 16 + 4 * lg));
@@ -2170,7 +2203,7 @@ __global__ __launch_bounds__(512, 1) void k_nin_head_x6(FwdArgs a, HeadArgs hd, 
     if constexpr (SAVE)
 #pragma unroll
       for (int f = 0; f < 6; ++f) save(hd.na, row, soff, h[f], f);
-    gemm96(lw + X6_HEAD_BF, h, u);  // nin_b
+    gemm96(std::false_type{}, lw + X6_HEAD_BF, h, u);  // nin_b
 #pragma unroll
     for (int f = 0; f < 6; ++f) {
       bias_act(u[f][0], *reinterpret_cast<const float4*>(lb + 96 + f * 16 + 4 * lg));
@@ -2231,7 +2264,8 @@ hipError_t launch_pack_head_x6(const float* wa, const float* wb, void* out, hipS
 
 hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* wimg, hipStream_t s,
                               bool bf16) {
-  if ((bf16 && (h.rd || (h.na && h.nb))) || a.K != 96 || h.oc < 1 || h.oc > X6_HEAD_OCMAX || ((a.in_stride | a.in_off) & 3) ||
+  if ((bf16 && (h.rd || (h.na && h.nb))) || (a.in_bf16 && !bf16) || a.K != 96 || h.oc < 1 ||
+      h.oc > X6_HEAD_OCMAX || ((a.in_stride | a.in_off) & 3) ||
       (long)a.IWt * a.in_stride * 4 >= 0x7fffffffL || (long)a.OW * 96 * 4 * 2 >= 0x7fffffffL)
     return hipErrorInvalidValue;
   const long nwt = (long)a.N * a.OH * ((a.OW + 15) / 16);  // one 16-pixel row per wave-tile
@@ -2244,6 +2278,8 @@ hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* w
   if (save && h.rd) return hipErrorInvalidValue;  // the pair pass saves nothing
   if (h.rd) hipLaunchKernelGGL((k_nin_head_x6<false, true>), grid, block, 0, s, a, h, w, (int)nwt);
   else if (save) hipLaunchKernelGGL((k_nin_head_x6<true, false>), grid, block, 0, s, a, h, w, (int)nwt);
+  else if (bf16 && a.in_bf16)
+    hipLaunchKernelGGL((k_nin_head_x6<false, false, true, true>), grid, block, 0, s, a, h, w, (int)nwt);
   else if (bf16) hipLaunchKernelGGL((k_nin_head_x6<false, false, true>), grid, block, 0, s, a, h, w, (int)nwt);
   else hipLaunchKernelGGL((k_nin_head_x6<false, false>), grid, block, 0, s, a, h, w, (int)nwt);
   return hipGetLastError();

@@ -104,6 +104,9 @@ struct FwdArgs {
   // split-bf16 3x3 forward, "selected pixels" mode (launch_fwd_x6_sel): per 2x2 output cell the
   // N2N pair choice rd (0..7, [N][OH/2][OW/2]); only the cell's two pair pixels are computed
   const unsigned char* sel_rd;
+  // mixed-precision bf16 forward (conv_bf16.hip): the input / output activations are stored as
+  // bf16 (RNE of the fp32 value; strides and offsets in elements) instead of fp32
+  int in_bf16, out_bf16;
 };
 
 // Fused output head (arch_unet.py:186-190, 253-257): the dec_conv1b kernel keeps its
@@ -301,6 +304,10 @@ hipError_t launch_wgrad(int mode, const WgradArgs& a, int splits, hipStream_t s,
 bool wgrad3_x6_ok(const WgradArgs& a);
 int wgrad_splits_x6(const WgradArgs& a, int splits);  // split count when the x6 kernel is taken
 hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s);
+// ... its 96-output form with the operands split once per stage into LDS planes (wgrad_x6p.hip,
+// k_wgrad3p; nz = output-channel blocks of a.zc == 96 over blockIdx.z, else 1)
+bool wgrad3p_ok(const WgradArgs& a);
+hipError_t launch_wgrad3p(const WgradArgs& a, int splits, hipStream_t s, int nz);
 bool wgrad1_ok(int mode, const WgradArgs& a);
 long wgrad_slab_floats(int mode, int N, int KH, int KW, int cin, int cout);
 hipError_t launch_wgrad1(int mode, const WgradArgs& a, float* dwb, hipStream_t s,

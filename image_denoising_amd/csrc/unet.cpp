@@ -422,6 +422,23 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     const int m = x6_image_mode(N, H(l), Wd(l), i == D1A ? p.c1kp : L.cin, L.cout, 0, true);
     return (i == D1B && !p.with_bwd) ? (m & ~X6_W6) : m;
   };
+  // bf16 base (forward-only plans): bf16 storage of the decoder's a-conv outputs, whose only
+  // reader is the matching b-conv (DN_BF16_STORE=0: fp32 storage, A/B)
+  static const bool bf16_store_env = !getenv("DN_BF16_STORE") || atoi(getenv("DN_BF16_STORE")) != 0;
+  const bool bf16_store = bf16 && bf16_store_env && !p.with_bwd;
+  // (bf16 base: the fused head kernel in plain bf16 products, see below; it reads d1b as bf16)
+  static const bool bf16_head_env = !getenv("DN_BF16_HEAD_X6") || atoi(getenv("DN_BF16_HEAD_X6")) != 0;
+  const bool bf16_head_x6 = bf16 && bf16_head_env && !p.with_bwd && p.OC <= X6_HEAD_OCMAX;
+  auto bf16_store_out = [&](int i) {
+    if (i == D1B) return bf16_store && bf16_head_x6 && p.packBF[i] >= 0;
+    return bf16_store && (i == D1A || i == D2A || i == D3A || i == D4A || i == D5A) &&
+           p.packBF[i] >= 0 && p.packBF[i + 1] >= 0;
+  };
+  auto bf16_store_in = [&](int i) {
+    return bf16_store && (i == D1B || i == D2B || i == D3B || i == D4B || i == D5B) &&
+           bf16_store_out(i - 1);
+  };
+  // (dec_conv1b -> the bf16 head: bf16_store_out(D1B))
   // pool (x6 path, EPI_BIAS_ACT): the 2x2 max-pool of `out` fused into the conv's epilogue into
   // that view (*pooled set); otherwise the caller pools
   auto conv_forward = [&](const View& in, int Nn, int h, int w, int K, const float* wp,
@@ -457,6 +474,11 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     if (i == D1A) a.K = p.c1kp;  // the zero pad channel as in the x6 path: K % 4 == 0 (pipelined)
     a.wp = ws + p.packBF[i]; a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
     a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = layout;
+    // the activations that only a bf16 3x3 conv reads (d_l a -> d_l b, d1a -> d1b) stored as
+    // bf16: the consumer rounds its staged operands to bf16 anyway, so the result is
+    // bit-identical and those tensors move half the bytes
+    a.out_bf16 = bf16_store_out(i);
+    a.in_bf16 = bf16_store_in(i);
     return launch_fwd_bf16(a, st, ksize);
   };
 
@@ -466,9 +488,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   const bool head_x6 = x6 && (head_x6_env || sel) && p.OC <= X6_HEAD_OCMAX;
   // bf16 base (inference only): the fused head kernel in plain bf16 products instead of nin_a /
   // nin_b as two bf16 1x1 launches + an fp32 nin_c (two 96-channel round trips through HBM
-  // saved; DN_BF16_HEAD_X6=0 keeps the three launches)
-  static const bool bf16_head_env = !getenv("DN_BF16_HEAD_X6") || atoi(getenv("DN_BF16_HEAD_X6")) != 0;
-  const bool bf16_head_x6 = bf16 && bf16_head_env && !p.with_bwd && p.OC <= X6_HEAD_OCMAX;
+  // saved; DN_BF16_HEAD_X6=0 keeps the three launches; bf16_head_x6 above)
   // the 96-channel deconvs on the persistent bf16x6 kernel, also in the bf16 base (one pass over
   // the input instead of a bf16 1x1 launch per output parity; DN_BF16_DECONV_X6=0 keeps those)
   static const bool bf16_dx6_env = !getenv("DN_BF16_DECONV_X6") || atoi(getenv("DN_BF16_DECONV_X6")) != 0;
@@ -606,6 +626,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
       h.ba = Bs(NINA); h.bb = Bs(NINB);
       h.wc = prm + p.P.L[NINC].woff; h.bc = Bs(NINC); h.oc = p.OC;
       h.y = y;
+      a.in_bf16 = bf16_store_out(D1B);  // d1b stored as bf16 by dec_conv1b
       DN_TIMED(s, "head", 2.0 * N * H(0) * Wd(0) * 96 * (2 * 96 + p.OC), 96, p.OC, H(0), Wd(0), N,
                launch_nin_head_x6(a, h, ws + p.packH, s, /*bf16=*/true));
       return DN_OK;

@@ -1,0 +1,352 @@
+// 3x3 weight gradient at fp32 accuracy on the bf16 matrix cores, operands split ONCE per stage
+// into bf16 planes (k_wgrad3p: 96 output channels).
+//
+// GEMM M = output channels, N = input channels x 9 taps, K = pixels (as k_wgrad3s,
+// conv_x6.hip).  k_wgrad3s splits each fp32 operand at the read, so every value is split by
+// each of the two waves that share it, and the three horizontal taps need funnel shifts of the
+// split window: its stage loop is vector-issue bound (SQ counters: every issue slot of a SIMD
+// taken, MFMA busy 0.46).  Here the next stage's fp32 operands are loaded into registers (buffer
+// loads, out-of-range offsets read zeros) while the current stage computes, split once by the
+// workgroup's threads and written into three bf16 planes of the other LDS buffer; the MFMA
+// operands are read from the planes with ds_read_b64_tr_b16, the hardware transpose that turns
+// pixel-major (NHWC) bf16 rows into the K-contiguous fragment a lane needs.  A tap offset is
+// then only a different starting row of the X plane.  One barrier per stage.
+//
+//   Workgroup = 4 waves (two workgroups per CU), wave (wm, wn): output channels 48wm .. +47
+//   (three 16-row fragments) x input channels ci0 + 16wn .. +15 x 9 taps; acc[9][3] fp32.
+//   K stage = 32 pixels: 32 >> SWL rows of sw = 1 << SWL pixels (sw >= 8).
+//   LDS: two buffers of three bf16 planes, each [G: 32 px x 96 co | X: (sh+2)(sw+2) px x 32 ci].
+//   The 16 channels (32 B) of block b of pixel row r sit in block b ^ ((r >> 3) & 1) of the row: the two 16-lane groups of a 32-lane half read rows 8 apart,
+//   which the flip puts on the other 32 banks (conflict-free transposed reads).
+//   Each 32-pixel block of the six products is summed from zero and added to the running fp32
+//   sum with a round-to-nearest add (x6_block), as in k_wgrad3s.
+#include <cstdlib>
+
+#include "conv_epi.h"
+#include "x6_core.h"
+
+#ifndef DN_WGP_FOLD
+#define DN_WGP_FOLD 1
+#endif
+
+namespace dn {
+
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ i16x4 lds_tr16(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) i16x4*)(p));
+}
+
+// eight K-consecutive bf16 of a lane (two transposed 4-row reads)
+__device__ __forceinline__ bf16x8 tr_frag(const __bf16* p0, const __bf16* p1) {
+  const i16x4 a = lds_tr16(p0), b = lds_tr16(p1);
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int SWL>
+struct Wp3Cfg {
+  static constexpr int COUT = 96, MFW = 3, CIB = 32, NW = 4, NTHR = 256;
+  static constexpr int SW = 1 << SWL, SH = 32 >> SWL, XW = SW + 2, XPIX = (SH + 2) * XW;
+  static constexpr int GQ = 32 * COUT / 4, XQ = XPIX * CIB / 4, NQ = GQ + XQ;  // float4 items
+  static constexpr int NIT = (NQ + NTHR - 1) / NTHR;
+  static constexpr int GPL = 32 * COUT, XPL = XPIX * CIB;  // bf16 of G / X per plane
+  static constexpr int PL = GPL + XPL;                     // plane stride: [G | X]
+  static constexpr int BUF = 3 * PL;                       // bf16 per stage buffer
+  static_assert(GQ % NTHR == 0, "items 0 .. GQ/NTHR - 1 of every thread are G items");
+  static_assert(2 * BUF * 2 <= 81920, "two workgroups per CU");
+};
+
+// plane index of channel block `blk` (16 channels) of row r (row width `rw` channels)
+__device__ __forceinline__ int wp_idx(int r, int rw, int blk) {
+  return r * rw + ((blk ^ ((r >> 3) & 1)) << 4);
+}
+
+template <int SWL>
+__global__ __launch_bounds__(256, 2) void k_wgrad3p(WgradArgs a0) {
+  using C = Wp3Cfg<SWL>;
+  constexpr int MFW = C::MFW, SW = C::SW, SH = C::SH, XW = C::XW;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * C::BUF];
+  const WgradArgs a = wg_block(a0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 15, lg = lane >> 4;
+  const int ci0 = blockIdx.y * C::CIB;
+  const int ux = (a.KW + SW - 1) / SW, uy = (a.KH + SH - 1) / SH;
+  const long U = (long)a.N * uy * ux;
+  const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
+  const bool do_bias = a.bias && blockIdx.y == 0 && wn == 0;
+
+  f32x4 acc[9][MFW][1];
+  f32x4 accb[MFW][1];
+#pragma unroll
+  for (int i = 0; i < MFW; ++i) {
+    accb[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t][i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // ---- the split pass: item q (a float4 of 4 channels of one pixel) of this thread ----------
+  // Items 0 .. NG-1 of a thread are G items, NG .. NIT-1 X items.  Stage-invariant parts: the
+  // offset relative to the stage origin, the LDS plane index of the 4 channels (low 16 bits) and
+  // the halo-edge class (bits 16..: 0 top row, 1 bottom row, 2 left column, 3 right column,
+  // 5 no data)
+  constexpr int NG = C::GQ / C::NTHR, NX = C::NIT - NG;
+  int ioff[C::NIT], ilde[C::NIT];
+#pragma unroll
+  for (int it = 0; it < C::NIT; ++it) {
+    const int q = tid + it * C::NTHR;
+    ioff[it] = 0; ilde[it] = 32 << 16;
+    if (it < NG) {
+      const int px = q / (C::COUT / 4), c = 4 * (q % (C::COUT / 4));
+      ioff[it] = ((px >> SWL) * a.KW + (px & (SW - 1))) * a.g_stride + c;
+      ilde[it] = (wp_idx(px, C::COUT, c >> 4) + (c & 15)) | ((c < a.Cout ? 0 : 32) << 16);
+    } else if (q < C::NQ) {
+      const int r = q - C::GQ, xp = r / (C::CIB / 4), c = 4 * (r % (C::CIB / 4));
+      const int yy = xp / XW, xx = xp - yy * XW;
+      ioff[it] = ((yy - 1) * a.KW + xx - 1) * a.x_stride + ci0 + c;
+      const int e = (yy == 0) | ((yy == SH + 1) << 1) | ((xx == 0) << 2) | ((xx == SW + 1) << 3) |
+                    ((ci0 + c < a.Cin ? 0 : 1) << 5);
+      ilde[it] = (C::GPL + wp_idx(xp, C::CIB, c >> 4) + (c & 15)) | (e << 16);
+    }
+  }
+  const bool exact = a.KW % SW == 0 && a.KH % SH == 0;
+  f32x4 pg[NG], px_[NX];  // the next stage's G / X operands in flight
+  // stage u = (image n, row block iy, column block ix), decoded incrementally
+  struct Pos { int n, iy, ix; };
+  auto pos_of = [&](long u) {
+    Pos p;
+    p.n = (int)(u / ((long)uy * ux));
+    const int rem = (int)(u - (long)p.n * uy * ux);
+    p.iy = rem / ux; p.ix = rem - p.iy * ux;
+    return p;
+  };
+  auto next = [&](Pos p) {
+    if (++p.ix == ux) { p.ix = 0; if (++p.iy == uy) { p.iy = 0; ++p.n; } }
+    return p;
+  };
+  auto emask_of = [&](Pos p) {
+    const int py0 = p.iy * SH, px0 = p.ix * SW;
+    return (py0 == 0) | ((py0 + SH >= a.KH) << 1) | ((px0 == 0) << 2) | ((px0 + SW >= a.KW) << 3) |
+           (1 << 5);
+  };
+  // item it's byte offset in its operand image (0x7fffffff: zeros)
+  auto item_off = [&](Pos p, int it, bool isg, int base) {
+    const int q = tid + it * C::NTHR;
+    const int py0 = p.iy * SH, px0 = p.ix * SW;
+    bool ok = !((ilde[it] >> 16) & emask_of(p));
+    if (!exact && q < C::NQ) {  // sides that are not whole stage blocks: per-item bounds
+      if (isg) {
+        const int pxl = q / (C::COUT / 4);
+        ok = ok && py0 + (pxl >> SWL) < a.KH && px0 + (pxl & (SW - 1)) < a.KW;
+      } else {
+        const int xp = (q - C::GQ) / (C::CIB / 4), yy = xp / XW, xx = xp - yy * XW;
+        ok = ok && py0 - 1 + yy < a.KH && px0 - 1 + xx < a.KW;
+      }
+    }
+    return ok ? (base + ioff[it]) * 4 : 0x7fffffff;
+  };
+  auto load_g = [&](Pos p) {
+    const long img = (long)p.n * a.KH * a.KW;
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.g + img * a.g_stride + a.g_off), (short)0,
+        (int)((long)a.KH * a.KW * a.g_stride * 4), 0x00020000);
+    const int base = (p.iy * SH * a.KW + p.ix * SW) * a.g_stride;
+#pragma unroll
+    for (int it = 0; it < NG; ++it)
+      pg[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             gr, item_off(p, it, true, base), 0, 0));
+  };
+  auto load_x = [&](Pos p) {
+    const long img = (long)p.n * a.KH * a.KW;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x + img * a.x_stride + a.x_off), (short)0,
+        (int)((long)a.KH * a.KW * a.x_stride * 4), 0x00020000);
+    const int base = (p.iy * SH * a.KW + p.ix * SW) * a.x_stride;
+#pragma unroll
+    for (int it = 0; it < NX; ++it)
+      px_[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              xr, item_off(p, NG + it, false, base), 0, 0));
+  };
+  auto store4 = [&](__bf16* buf, int it, const f32x4& v) {
+    const int o = ilde[it] & 0xffff;
+    unsigned h0, m0, l0, h1, m1, l1;
+    split3x2(v[0], v[1], h0, m0, l0);
+    split3x2(v[2], v[3], h1, m1, l1);
+    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+    *reinterpret_cast<u32x2_t*>(buf + o) = u32x2_t{h0, h1};
+    *reinterpret_cast<u32x2_t*>(buf + o + C::PL) = u32x2_t{m0, m1};
+    *reinterpret_cast<u32x2_t*>(buf + o + 2 * C::PL) = u32x2_t{l0, l1};
+  };
+  auto store_g = [&](__bf16* buf) {
+#pragma unroll
+    for (int it = 0; it < NG; ++it) store4(buf, it, pg[it]);
+  };
+  auto store_x = [&](__bf16* buf) {
+#pragma unroll
+    for (int it = 0; it < NX; ++it)
+      if (tid + (NG + it) * C::NTHR < C::NQ) store4(buf, NG + it, px_[it]);
+  };
+
+  // ---- MFMA operand addresses (stage-invariant) ----------------------------------------------
+  // A (G planes [px][96]): lane 4q+p of group lg supplies row 8lg + 4t + q, columns 4p..4p+3
+  // of block 3wm + i, i.e. block (3wm + i) ^ (lg & 1) of the row
+  const int abase = (8 * lg + (li >> 2)) * C::COUT + 4 * (li & 3);
+  const int aflip = lg & 1;
+  // B (X planes [xp][32]): stage pixel 8lg + j = (row pr0, column pc0 + j); tap (ky, kx), read t
+  // -> X row r0 + d, d = ky*XW + kx + 4t, r0 = pr0*XW + pc0 + (li >> 2), in block wn ^ bit 3 of
+  // the row.  Bit k of bmask: that flip for the k-th (ky, kx, t)
+  const int pr0 = (8 * lg) >> SWL, pc0 = (8 * lg) & (SW - 1);
+  const int r0 = pr0 * XW + pc0 + (li >> 2);
+  const int bbase = C::GPL + r0 * C::CIB + 16 * wn + 4 * (li & 3);
+  const int bsgn = wn ? -16 : 16;
+  unsigned bmask0 = 0;
+#pragma unroll
+  for (int k = 0; k < 18; ++k) {
+    const int d = (k >> 1) / 3 * XW + (k >> 1) % 3 + 4 * (k & 1);
+    bmask0 |= (unsigned)(((r0 + d) >> 3) & 1) << k;
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+
+  Pos pn = pos_of(u_beg);
+  if (u_beg < u_end) {
+    load_g(pn);
+    load_x(pn);
+    store_g(lds);
+    store_x(lds);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own plane writes done
+  __syncthreads();
+#pragma unroll 1
+  for (long u = u_beg; u < u_end; ++u) {
+    const int cb = (int)((u - u_beg) & 1);
+    const __bf16* buf = lds + cb * C::BUF;
+    __bf16* nbuf = lds + (cb ^ 1) * C::BUF;
+    pn = next(pn);
+    const bool more = u + 1 < u_end;
+    if (more) load_g(pn);  // in flight during the first kernel row's MFMAs
+    int aoff = abase;
+    unsigned bmask = bmask0;
+    asm volatile("" : "+v"(aoff), "+v"(bmask));  // (addresses formed here, not held across stages)
+    bf16x8 av[3][MFW];
+#pragma unroll
+    for (int i = 0; i < MFW; ++i) {
+      const int o = aoff + (((3 * wm + i) ^ aflip) << 4);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const __bf16* p = buf + pl * C::PL + o;
+        av[pl][i] = tr_frag(p, p + 4 * C::COUT);
+      }
+    }
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      if (ky == 1 && more) {  // G of the next stage into the other buffer, then its X loads
+        store_g(nbuf);
+        load_x(pn);
+      }
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int k = 2 * (3 * ky + kx);
+        const int d = ky * XW + kx;
+        const int oa = bbase + d * C::CIB + (int)((bmask >> k) & 1) * bsgn;
+        const int ob = bbase + (d + 4) * C::CIB + (int)((bmask >> (k + 1)) & 1) * bsgn;
+        bf16x8 bv[3][1];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) bv[pl][0] = tr_frag(buf + pl * C::PL + oa, buf + pl * C::PL + ob);
+        const int t = 3 * ky + kx;
+        // the six products of a fragment, one fragment at a time (a dependent 16x16x32 chain
+        // issues back-to-back, MI355X_MICROARCH.md): the five corrections chained from zero,
+        // the leading product a0 b0 last on top of them, so the 32-pixel block reaches the
+        // running sum through ONE round-to-nearest add (4 VALU per fragment instead of 8).  The
+        // block sum is still fresh per stage: the chain's accumulator is at most the block's
+        // own magnitude, as for a leading product summed from zero (DN_WGP_FOLD=0: x6_block's
+        // separate hi / lo sums and two adds, for A/B).
+#pragma unroll
+        for (int i = 0; i < MFW; ++i) {
+          const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+          f32x4 lo = mfma_bf16(av[0][i], bv[1][0], z);
+          lo = mfma_bf16(av[1][i], bv[0][0], lo);
+          lo = mfma_bf16(av[0][i], bv[2][0], lo);
+          lo = mfma_bf16(av[1][i], bv[1][0], lo);
+          lo = mfma_bf16(av[2][i], bv[0][0], lo);
+#if DN_WGP_FOLD
+          const f32x4 blk = mfma_bf16(av[0][i], bv[0][0], lo);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[t][i][0][r] = acc[t][i][0][r] + blk[r];
+#else
+          const f32x4 hi = mfma_bf16(av[0][i], bv[0][0], z);
+          x6_acc_add(acc[t][i][0], hi, lo);
+#endif
+          asm volatile("" : "+v"(acc[t][i][0]));
+        }
+      }
+    }
+    if (do_bias) {
+#pragma unroll
+      for (int i = 0; i < MFW; ++i) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 hi = mfma_bf16(av[0][i], ones, z);
+        f32x4 lo = mfma_bf16(av[1][i], ones, z);
+        lo = mfma_bf16(av[2][i], ones, lo);
+        x6_acc_add(accb[i][0], hi, lo);
+      }
+    }
+    if (more) store_x(nbuf);  // (waits for its loads itself)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own plane writes done
+    __syncthreads();                     // next buffer complete; everyone done with this one
+  }
+
+  float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
+  const int ci = ci0 + 16 * wn + li;
+  const int cot = a.cout_total ? a.cout_total : a.Cout;
+#pragma unroll
+  for (int i = 0; i < MFW; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = (3 * wm + i) * 16 + 4 * lg + r;
+        if (co < a.Cout && ci < a.Cin)
+          slab[((long)(a.co_base + co) * a.cin_total + a.ci_base + ci) * 9 + t] = acc[t][i][0][r];
+      }
+  if (do_bias && li == 0) {
+#pragma unroll
+    for (int i = 0; i < MFW; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = (3 * wm + i) * 16 + 4 * lg + r;
+        if (co < a.Cout) slab[(long)cot * a.cin_total * 9 + a.co_base + co] = accb[i][0][r];
+      }
+  }
+}
+
+// 96 output channels (or 96-channel blocks, a.zc == 96), 32 input channels per workgroup,
+// 16-byte aligned NHWC views, images under 2 GiB per operand (32-bit buffer offsets)
+bool wgrad3p_ok(const WgradArgs& a) {
+  if ((a.zc ? a.zc != 96 : a.Cout != 96) || a.Cin < 32 || a.KW < 8) return false;
+  if ((a.g_stride | a.g_off | a.x_stride | a.x_off) & 3) return false;
+  if (a.x_off + ((a.Cin + 3) & ~3) > a.x_stride) return false;
+  return (long)a.KH * a.KW * a.g_stride * 4 < 0x7fffffffL &&
+         (long)a.KH * a.KW * a.x_stride * 4 < 0x7fffffffL;
+}
+
+hipError_t launch_wgrad3p(const WgradArgs& a, int splits, hipStream_t s, int nz) {
+  if (!wgrad3p_ok(a)) return hipErrorInvalidValue;
+  const dim3 grid(splits, (a.Cin + 31) / 32, nz), block(256);
+  if (a.KW >= 32) {
+    prof_kernel("k_wgrad3p<5>");
+    hipLaunchKernelGGL(k_wgrad3p<5>, grid, block, 0, s, a);
+  } else if (a.KW >= 16) {
+    prof_kernel("k_wgrad3p<4>");
+    hipLaunchKernelGGL(k_wgrad3p<4>, grid, block, 0, s, a);
+  } else {
+    prof_kernel("k_wgrad3p<3>");
+    hipLaunchKernelGGL(k_wgrad3p<3>, grid, block, 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace dn
