@@ -461,6 +461,333 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// The N2N no-grad pass's dec_conv1b at the pair pixels only, on the Winograd transform
+// (k_c3w6s).  train.py:151-154's pair table makes every cell's two pixels an aligned F(2,3)
+// tile: horizontal neighbours (rd 0, 3, 4, 7: row 2ci + r, columns 2cj, 2cj + 1) are a tile along
+// x, vertical ones (rd 1, 2, 5, 6: rows 2ci, 2ci + 1 of column 2cj + c) a tile along y.  The cells
+// are listed per orientation (k_w6s_lists, raster order), and a workgroup takes 64 consecutive
+// cells of one list: M = those cells, N = 96 output channels, K = 32 input channels x the three
+// rows (x tiles) or columns (y tiles) of the kernel, four positions p: 12 instead of 18 products
+// per cell and input chunk.  Each cell's V (its four input pixels along the tile, for one kernel
+// row k3) is gathered straight from global memory (no halo sharing: cells are not adjacent in a
+// list), transformed, split into three bf16 planes in LDS, between two barriers per (chunk, k3)
+// phase; the other workgroup on the CU keeps the matrix cores busy meanwhile.  Weights: the
+// layer's PK_W6 image (u along kx for each ky) for x tiles, the same with the taps transposed
+// (u along ky for each kx; WView flip = 2) for y tiles, straight into registers as in k_c3w6.
+// Output: the pair image [N][OH/2][OW][96] (column 2cj + s = pixel pair[rd][s] of cell (ci, cj)),
+// bias + LeakyReLU, as k_c3x6s writes it for the head.
+// ------------------------------------------------------------------------------------
+struct SCfgW {
+  static constexpr int WAVES = 4, MT = 4, NTW = 3, NP = 96, CELLS = 64, KC = 32;
+  static constexpr int VPL = 4 * CELLS * KC;        // bf16 per plane of V: [p][cell][32 ch]
+  static constexpr int VBYTES = 3 * VPL * 2;        // 48 KiB
+  static constexpr int WSTP = x6_wst(NP);
+  static constexpr int XCH = WAVES * 2 * NTW * 2 * 4 * 64;  // floats of the exchange area
+  static constexpr int LBYTES = VBYTES > XCH * 4 ? VBYTES : XCH * 4;
+  static_assert(2 * (LBYTES + CELLS * 4) <= 163840, "two workgroups per CU");
+};
+
+// list entry: cj | ci << 15 | (r or c) << 30 | swap << 31
+__device__ __forceinline__ unsigned w6s_entry(int ci, int cj, int rd) {
+  const unsigned rc = (rd == 2 || rd == 3 || rd == 6 || rd == 7) ? 1u : 0u;
+  return (unsigned)cj | ((unsigned)ci << 15) | (rc << 30) | ((rd >= 4 ? 1u : 0u) << 31);
+}
+
+// per image n: the cells of orientation o (0: x tiles, rd 0/3/4/7; 1: y tiles, rd 1/2/5/6) in
+// raster order -> list[(n * 2 + o) * cells + i], their number -> cnt[n * 2 + o]
+__global__ __launch_bounds__(1024) void k_w6s_lists(const unsigned char* __restrict__ rd, int ch,
+                                                     int cw, unsigned* __restrict__ list,
+                                                     int* __restrict__ cnt) {
+  __shared__ int part[2][1024];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const long cells = (long)ch * cw;
+  const unsigned char* r = rd + (long)n * cells;
+  unsigned* lo[2] = {list + (long)(2 * n) * cells, list + (long)(2 * n + 1) * cells};
+  int base[2] = {0, 0};
+  for (long c0 = 0; c0 < cells; c0 += 16L * 1024) {
+    // 16 consecutive cells per thread
+    int k[2] = {0, 0};
+    const long e0 = c0 + 16L * tid;
+    for (int j = 0; j < 16; ++j) {
+      const long e = e0 + j;
+      if (e < cells) {
+        const int v = r[e] & 7;
+        ++k[(v == 1 || v == 2 || v == 5 || v == 6) ? 1 : 0];
+      }
+    }
+    part[0][tid] = k[0];
+    part[1][tid] = k[1];
+    __syncthreads();
+    // inclusive scan of the two count arrays (Hillis-Steele over 1024 threads)
+    for (int d = 1; d < 1024; d <<= 1) {
+      const int a0 = tid >= d ? part[0][tid - d] : 0, a1 = tid >= d ? part[1][tid - d] : 0;
+      __syncthreads();
+      part[0][tid] += a0;
+      part[1][tid] += a1;
+      __syncthreads();
+    }
+    int o0 = base[0] + part[0][tid] - k[0], o1 = base[1] + part[1][tid] - k[1];
+    for (int j = 0; j < 16; ++j) {
+      const long e = e0 + j;
+      if (e < cells) {
+        const int v = r[e] & 7;
+        const int ci = (int)(e / cw), cj = (int)(e - (long)ci * cw);
+        const unsigned en = w6s_entry(ci, cj, v);
+        if (v == 1 || v == 2 || v == 5 || v == 6) lo[1][o1++] = en;
+        else lo[0][o0++] = en;
+      }
+    }
+    base[0] += part[0][1023];
+    base[1] += part[1][1023];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    cnt[2 * n] = base[0];
+    cnt[2 * n + 1] = base[1];
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void k_c3w6s(FwdArgs a, const unsigned* __restrict__ list,
+                                                  const int* __restrict__ cnt,
+                                                  const __bf16* __restrict__ wpv) {
+  using C = SCfgW;
+  constexpr int MT = C::MT, NTW = C::NTW;
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
+  __shared__ unsigned lent[C::CELLS];
+  __bf16* lv = reinterpret_cast<__bf16*>(lds_raw);
+  const int o = blockIdx.z, n = blockIdx.y, cbase = blockIdx.x * C::CELLS;
+  const int ncell = cnt[2 * n + o];
+  if (cbase >= ncell) return;  // (uniform: the list is shorter than the grid allows)
+  const long cells = (long)(a.OH / 2) * (a.OW / 2);
+  const unsigned* lst = list + (long)(2 * n + o) * cells;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lg = lane >> 4;
+  const int nh = wave & 1, ph = wave >> 1;
+  if (tid < C::CELLS) lent[tid] = cbase + tid < ncell ? lst[cbase + tid] : 0xffffffffu;
+  __syncthreads();
+
+  f32x4 acc[2][MT][NTW];
+#pragma unroll
+  for (int pi = 0; pi < 2; ++pi)
+#pragma unroll
+    for (int f = 0; f < MT; ++f)
+#pragma unroll
+      for (int q = 0; q < NTW; ++q) acc[pi][f][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // the image through a 32-bit buffer resource (host: < 2 GiB), out-of-range offsets read zeros
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off), (short)0,
+      (int)((long)a.IHt * a.IWt * a.in_stride * 4), 0x00020000);
+  // transform items: (cell, channel quad c4) = tid + 256 it -> cells tid >> 3 and +32, quad tid & 7
+  const int c4 = tid & 7;
+  unsigned ent[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) ent[it] = lent[(tid >> 3) + 32 * it];
+  auto transform = [&](int k0, int k3) {
+    f32x4 d[2][4];
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const unsigned e = ent[it];
+      const bool live = e != 0xffffffffu;
+      const int cj = e & 0x7fff, ci = (e >> 15) & 0x7fff, rc = (e >> 30) & 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        // x tiles: row 2ci + r + k3 - 1, column 2cj - 1 + i; y tiles: row 2ci - 1 + i, column
+        // 2cj + c + k3 - 1
+        const int gy = o == 0 ? 2 * ci + rc + k3 - 1 : 2 * ci - 1 + i;
+        const int gx = o == 0 ? 2 * cj - 1 + i : 2 * cj + rc + k3 - 1;
+        const bool ok = live && gy >= 0 && gy < a.IHt && gx >= 0 && gx < a.IWt;
+        const int off = ok ? (((gy * a.IWt + gx) * a.in_stride) + k0 + 4 * c4) * 4 : 0x7fffffff;
+        d[it][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int cell = (tid >> 3) + 32 * it;
+      f32x4 v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        v[0][c] = d[it][0][c] - d[it][2][c];
+        v[1][c] = d[it][1][c] + d[it][2][c];
+        v[2][c] = d[it][2][c] - d[it][1][c];
+        v[3][c] = d[it][1][c] - d[it][3][c];
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        unsigned h0, m0, l0, h1, m1, l1;
+        split3x2(v[p][0], v[p][1], h0, m0, l0);
+        split3x2(v[p][2], v[p][3], h1, m1, l1);
+        const int row = p * C::CELLS + cell;
+        const int off = row * C::KC + x6_swz(row, c4 >> 1) * 8 + (c4 & 1) * 4;  // bf16 index
+        typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<u32x2_t*>(lv + off) = u32x2_t{h0, h1};
+        *reinterpret_cast<u32x2_t*>(lv + C::VPL + off) = u32x2_t{m0, m1};
+        *reinterpret_cast<u32x2_t*>(lv + 2 * C::VPL + off) = u32x2_t{l0, l1};
+      }
+    }
+  };
+
+  // weights: fragment q = output channels 48nh + 16q .. +15 of stage st (= c*12 + k3*4 + p)
+  const int nch = a.K / C::KC;
+  const __bf16* wimg = o == 0 ? reinterpret_cast<const __bf16*>(a.wp) : wpv;
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__bf16*>(wimg), (short)0, nch * 12 * C::WSTP * 2, 0x00020000);
+  int woff[NTW];
+#pragma unroll
+  for (int q = 0; q < NTW; ++q) {
+    const int row = (NTW * nh + q) * 16 + li;
+    woff[q] = (row * C::KC + x6_swz(row, lg) * 8) * 2;
+  }
+  bf16x8 w[3][NTW];
+  auto load_wq = [&](int st, int q) {
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      w[pl][q] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, (st * C::WSTP + pl * 96 * 32) * 2 + woff[q], 0, 0));
+  };
+  // one stage: position p = 2ph + pi of this phase, its A fragments from V
+  auto stage = [&](auto pic, int nxt, int liv, int lgv) {
+    constexpr int PI = decltype(pic)::value;
+    const int p = 2 * ph + PI;
+    bf16x8 av[3][MT];
+#pragma unroll
+    for (int f = 0; f < MT; ++f) {
+      const int row = p * C::CELLS + 16 * f + liv;
+      const int off = row * C::KC + x6_swz(row, lgv) * 8;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) av[pl][f] = *reinterpret_cast<const bf16x8*>(lv + pl * C::VPL + off);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < NTW; ++q) {
+#pragma unroll
+      for (int f = 0; f < MT; ++f) {
+        f32x4(&ah)[1][NTW] = *reinterpret_cast<f32x4(*)[1][NTW]>(&acc[PI][f]);
+        bf16x8 a2[3][1];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a2[pl][0] = av[pl][f];
+        x6_group<1, NTW, 1>(ah, a2, w, q);
+        asm volatile("" : "+v"(ah[0][q]));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (nxt >= 0) load_wq(nxt, q);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < NTW; ++q) load_wq(2 * ph, q);
+  const int nph = nch * 3;
+#pragma unroll 1
+  for (int ph3 = 0; ph3 < nph; ++ph3) {
+    const int c = ph3 / 3, k3 = ph3 - 3 * c;
+    int liv = li, lgv = lg;
+    asm volatile("" : "+v"(liv), "+v"(lgv));
+    if (ph3 > 0) w6_barrier();  // every wave is done with the previous phase's V
+    transform(c * C::KC, k3);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own V stores done
+    w6_barrier();
+    const int st0 = ph3 * 4 + 2 * ph;  // c*12 + k3*4 + 2ph
+    stage(std::integral_constant<int, 0>{}, st0 + 1, liv, lgv);
+    stage(std::integral_constant<int, 1>{}, ph3 + 1 < nph ? st0 + 4 : -1, liv, lgv);
+  }
+
+  // output transform (as k_c3w6): ph 0 holds m0, m1, ph 1 holds m2, m3;
+  //   ph 0: (y0, y1) += (m0 + m1, m1);   ph 1: (y0, y1) += (m2, -m2 - m3)
+  // wave ph keeps M fragments 2ph, 2ph+1 and hands the other two's partials to its partner
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  w6_barrier();  // every wave is done with V: it becomes the exchange area
+  f32x4 y[2][2][NTW];
+  {
+    float* xo = reinterpret_cast<float*>(lds_raw) + (wave * 2 * NTW * 2) * 4 * 64;
+    const int pw = wave ^ 2;
+    const float* xi = reinterpret_cast<const float*>(lds_raw) + (pw * 2 * NTW * 2) * 4 * 64;
+    auto part = [&](auto phc) {
+      constexpr int PH = decltype(phc)::value;
+#pragma unroll
+      for (int ff = 0; ff < 2; ++ff)
+#pragma unroll
+        for (int q = 0; q < NTW; ++q) {
+          constexpr int FO = 2 * (1 - PH), FK = 2 * PH;
+          f32x4 o0, o1, k0, k1;
+          if constexpr (PH == 0) {
+            o0 = acc[0][FO + ff][q] + acc[1][FO + ff][q]; o1 = acc[1][FO + ff][q];
+            k0 = acc[0][FK + ff][q] + acc[1][FK + ff][q]; k1 = acc[1][FK + ff][q];
+          } else {
+            o0 = acc[0][FO + ff][q]; o1 = -acc[0][FO + ff][q] - acc[1][FO + ff][q];
+            k0 = acc[0][FK + ff][q]; k1 = -acc[0][FK + ff][q] - acc[1][FK + ff][q];
+          }
+          *reinterpret_cast<f32x4*>(xo + ((ff * NTW + q) * 2 + 0) * 256 + lane * 4) = o0;
+          *reinterpret_cast<f32x4*>(xo + ((ff * NTW + q) * 2 + 1) * 256 + lane * 4) = o1;
+          y[ff][0][q] = k0;
+          y[ff][1][q] = k1;
+        }
+    };
+    if (ph == 0) part(std::integral_constant<int, 0>{});
+    else part(std::integral_constant<int, 1>{});
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    w6_barrier();
+#pragma unroll
+    for (int ff = 0; ff < 2; ++ff)
+#pragma unroll
+      for (int q = 0; q < NTW; ++q) {
+        const f32x4 i0 = *reinterpret_cast<const f32x4*>(xi + ((ff * NTW + q) * 2 + 0) * 256 + lane * 4);
+        const f32x4 i1 = *reinterpret_cast<const f32x4*>(xi + ((ff * NTW + q) * 2 + 1) * 256 + lane * 4);
+        if (ph == 0) { y[ff][0][q] = y[ff][0][q] + i0; y[ff][1][q] = y[ff][1][q] + i1; }
+        else { y[ff][0][q] = i0 + y[ff][0][q]; y[ff][1][q] = i1 + y[ff][1][q]; }
+      }
+  }
+  // epilogue: lane (li, lg) of fragment 2ph + ff holds cells 16(2ph + ff) + 4lg + e (e < 4),
+  // output channel 48nh + 16q + li; bias + LeakyReLU, then the two pixels of the cell to the pair
+  // image row ci, columns 2cj + s (s = 0 takes pair[rd][0]: y0 unless the entry's swap bit)
+#pragma unroll
+  for (int q = 0; q < NTW; ++q) {
+    const int ch = 48 * nh + 16 * q + li;
+    const float b = a.bias[ch];
+#pragma unroll
+    for (int ff = 0; ff < 2; ++ff)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const unsigned en = lent[16 * (2 * ph + ff) + 4 * lg + e];
+        if (en == 0xffffffffu) continue;
+        const int cj = en & 0x7fff, ci = (en >> 15) & 0x7fff, sw = en >> 31;
+        float v0 = y[ff][0][q][e] + b, v1 = y[ff][1][q][e] + b;
+        v0 = v0 > 0.f ? v0 : v0 * 0.2f;
+        v1 = v1 > 0.f ? v1 : v1 * 0.2f;
+        float* dst = a.out + (((long)n * (a.OH / 2) + ci) * a.OW + 2 * cj) * a.out_stride + a.out_off + ch;
+        dst[0] = sw ? v1 : v0;
+        dst[a.out_stride] = sw ? v0 : v1;
+      }
+  }
+}
+
+// the cell lists of k_c3w6s for rd [N][OH/2][OW/2]: list (2 * N * cells uint32), cnt (2 * N int)
+hipError_t launch_w6s_lists(const unsigned char* rd, int N, int OH, int OW, unsigned* list, int* cnt,
+                            hipStream_t s) {
+  if (N < 1 || (OH | OW) & 1 || OH / 2 >= 32768 || OW / 2 >= 32768) return hipErrorInvalidValue;
+  prof_kernel("k_w6s_lists");
+  hipLaunchKernelGGL(k_w6s_lists, dim3(N), dim3(1024), 0, s, rd, OH / 2, OW / 2, list, cnt);
+  return hipGetLastError();
+}
+
+// dec_conv1b at the pair pixels on the Winograd kernel: a.wp = the layer's PK_W6 image (x tiles),
+// wpv = the tap-transposed one (y tiles), list / cnt from launch_w6s_lists on the same rd
+hipError_t launch_fwd_w6s(const FwdArgs& a, const unsigned* list, const int* cnt, const void* wpv,
+                          hipStream_t s) {
+  if (a.NOUT != 96 || a.K % 32 || a.K <= 0 || a.zc || a.epi != EPI_BIAS_ACT || !a.bias ||
+      a.out_layout != OUT_NHWC || ((a.in_stride | a.in_off) & 3) || (a.OH | a.OW) & 1 ||
+      a.IHt != a.OH || a.IWt != a.OW || (long)a.IHt * a.IWt * a.in_stride * 4 >= 0x7fffffffL ||
+      (a.x6_tail & 7) != 0)
+    return hipErrorInvalidValue;
+  const long cells = (long)(a.OH / 2) * (a.OW / 2);
+  const dim3 grid((unsigned)((cells + SCfgW::CELLS - 1) / SCfgW::CELLS), a.N, 2);
+  prof_kernel("k_c3w6s");
+  hipLaunchKernelGGL(k_c3w6s, grid, dim3(SCfgW::WAVES * 64), 0, s, a, list, cnt,
+                     static_cast<const __bf16*>(wpv));
+  return hipGetLastError();
+}
+
 int w6_stages_per_chunk() { return WCfg::SPC; }
 
 // k_c3w6 for a 96-output-channel forward / data gradient on a PK_W6 image (a.x6_tail & X6_W6)

@@ -1276,7 +1276,8 @@ __device__ __forceinline__ void pk_w6(const PackJob& j, long e0) {
   if (live && k < j.K && nn < j.NOUT && (j.zc == 0 || z * j.zc + nn < j.ntot)) {
     double g[3];
     for (int kx = 0; kx < 3; ++kx) {
-      const int t = 3 * ky + kx, tm = j.flip ? j.taps - 1 - t : t;
+      // flip 2: the transposed taps (u along ky for each kx: the y-tile image of k_c3w6s)
+      const int t = 3 * ky + kx, tm = j.flip == 2 ? 3 * kx + ky : (j.flip ? j.taps - 1 - t : t);
       g[kx] = j.w[(long)z * j.sZ + (long)k * j.sK + (long)nn * j.sN + (long)tm * j.sT];
     }
     const double u = p == 0 ? g[0] : (p == 1 ? (g[0] + g[1] + g[2]) * 0.5

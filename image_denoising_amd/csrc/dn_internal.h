@@ -83,7 +83,7 @@ struct WView {
   const float* w;
   long off, sK, sN, sT, sZ;  // idx = off + k*sK + n*sN + tap(t)*sT + blockIdx.z*sZ
   int taps;
-  int flip;                  // tap(t) = flip ? taps-1-t : t
+  int flip;                  // tap(t) = flip ? taps-1-t : t; 2 (PK_W6 only): 3x3 taps transposed
 };
 
 struct FwdArgs {
@@ -378,6 +378,13 @@ bool x6r_enabled();
 // image; FwdArgs::x6_tail carries X6_W6 | x6_tail_mode(K) for it (see x6_image_mode)
 constexpr int X6_W6 = 8;
 hipError_t launch_fwd_w6(const FwdArgs& a, hipStream_t s);
+// the N2N pair-pixel dec_conv1b on the Winograd kernel (conv_w6.hip k_c3w6s): the cells of rd
+// listed per tile orientation (list: 2 N (OH/2)(OW/2) uint32, cnt: 2 N int), then the pass over
+// them; a.wp = PK_W6 image, wpv = the tap-transposed PK_W6 image (WView flip = 2)
+hipError_t launch_w6s_lists(const unsigned char* rd, int N, int OH, int OW, unsigned* list, int* cnt,
+                            hipStream_t s);
+hipError_t launch_fwd_w6s(const FwdArgs& a, const unsigned* list, const int* cnt, const void* wpv,
+                          hipStream_t s);
 // the weight-image mode of a split-bf16 3x3 launch (pack and launch agree on it): the tail
 // packing of the last chunk on large grids with aligned views, | X6_W6 for the Winograd kernel
 int x6_image_mode(int N, int H, int W, int K, int nout, int zc, bool aligned);

@@ -168,6 +168,12 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
     }
     p.packX[i] = alloc_f((e + 1) / 2);
   }
+  p.packXV = p.w6s_list = p.w6s_cnt = -1;
+  if (!bwd) {
+    p.packXV = alloc_f((x6_pack_elems(96, 96, 0) + 1) / 2);
+    p.w6s_list = alloc_f(2L * N * (H / 2) * (W / 2));
+    p.w6s_cnt = alloc_f(2L * N);
+  }
   p.fwd_floats = off;
   if (bwd) {
     p.g_nb = alloc(0, 96);
@@ -416,11 +422,14 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // the encoder's 2x2 max-pools fused into the x6 convs' epilogues (DN_POOL_FUSE=0: separate
   // k_pool_fwd launches, A/B)
   static const bool pool_fuse = !getenv("DN_POOL_FUSE") || atoi(getenv("DN_POOL_FUSE")) != 0;
+  // the N2N pair-pixel pass's dec_conv1b: on the Winograd kernel k_c3w6s (default), or on the
+  // direct k_c3x6s (DN_W6_SEL=0, A/B), whose forward-only plans keep dec_conv1b's direct image
+  static const bool w6_sel_env = !getenv("DN_W6_SEL") || atoi(getenv("DN_W6_SEL")) != 0;
   auto x6_tail_f = [&](int i) -> int {
     const Layer& L = p.P.L[i];
     const int l = layer_level(i);
     const int m = x6_image_mode(N, H(l), Wd(l), i == D1A ? p.c1kp : L.cin, L.cout, 0, true);
-    return (i == D1B && !p.with_bwd) ? (m & ~X6_W6) : m;
+    return (i == D1B && !p.with_bwd && !w6_sel_env) ? (m & ~X6_W6) : m;
   };
   // bf16 base (forward-only plans): bf16 storage of the decoder's a-conv outputs, whose only
   // reader is the matching b-conv (DN_BF16_STORE=0: fp32 storage, A/B)
@@ -485,6 +494,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // DN_X6_HEAD=0: the fp32 nin head (A/B); the pair-pixel pass always takes the bf16x6 head
   static const bool head_x6_env = !getenv("DN_X6_HEAD") || atoi(getenv("DN_X6_HEAD")) != 0;
   const bool sel = x6 && sel_rd && !p.with_bwd && p.OC <= X6_HEAD_OCMAX;
+  const bool w6_sel = sel && w6_sel_env && p.packXV >= 0 && (x6_tail_f(D1B) & X6_W6);
   const bool head_x6 = x6 && (head_x6_env || sel) && p.OC <= X6_HEAD_OCMAX;
   // bf16 base (inference only): the fused head kernel in plain bf16 products instead of nin_a /
   // nin_b as two bf16 1x1 launches + an fp32 nin_c (two 96-channel round trips through HBM
@@ -544,6 +554,12 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
                                             ws + p.packBF[i], j), j));
     else if (x6) DN_TRY(add(pack_job_x6(conv_fwd_view(w, L.cin, 3), L.cin, L.cout, 0,
                                         ws + p.packX[i], x6_tail_f(i), j), j));
+    // dec_conv1b's y-tile image for the Winograd pair pass: PK_W6 over the transposed taps
+    if (x6 && i == D1B && w6_sel && (x6_tail_f(i) & X6_W6)) {
+      WView v = conv_fwd_view(w, L.cin, 3);
+      v.flip = 2;
+      DN_TRY(add(pack_job_x6(v, L.cin, L.cout, 0, ws + p.packXV, X6_W6, j), j));
+    }
     else DN_TRY(add(pack_job(L.k == 3 ? G_C3 : G_C1, conv_fwd_view(w, L.cin, L.k), L.cin, L.cout, 1,
                              ws + p.packF[i], 0, 0, j), j));
   }
@@ -647,9 +663,17 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     a.N = N; a.OH = H(0); a.OW = Wd(0); a.K = 96; a.NOUT = 96;
     a.wp = ws + p.packX[D1B]; a.bias = Bs(D1B); a.epi = EPI_BIAS_ACT;
     a.out = ws + p.d1b; a.out_stride = 96; a.out_off = 0; a.out_layout = OUT_NHWC;
-    a.sel_rd = sel_rd;
-    DN_TIMED(s, "fwd3sel", 2.0 * N * (H(0) / 2) * Wd(0) * 96 * 96 * 9, 96, 96, H(0) / 2, Wd(0), N,
-             launch_fwd_x6_sel(a, s));
+    if (w6_sel) {  // the cells listed per tile orientation, then the Winograd pass over them
+      unsigned* list = reinterpret_cast<unsigned*>(ws + p.w6s_list);
+      int* cnt = reinterpret_cast<int*>(ws + p.w6s_cnt);
+      DN_TIMED(s, "sel_lists", 0, 0, 0, 0, 0, 0, launch_w6s_lists(sel_rd, N, H(0), Wd(0), list, cnt, s));
+      DN_TIMED(s, "fwd3sel", 2.0 * N * (H(0) / 2) * Wd(0) * 96 * 96 * 9, 96, 96, H(0) / 2, Wd(0), N,
+               launch_fwd_w6s(a, list, cnt, ws + p.packXV, s));
+    } else {
+      a.sel_rd = sel_rd;
+      DN_TIMED(s, "fwd3sel", 2.0 * N * (H(0) / 2) * Wd(0) * 96 * 96 * 9, 96, 96, H(0) / 2, Wd(0), N,
+               launch_fwd_x6_sel(a, s));
+    }
     FwdArgs ah{};
     ah.in = ws + p.d1b; ah.in_stride = 96; ah.in_off = 0; ah.IHt = H(0) / 2; ah.IWt = Wd(0);
     ah.N = N; ah.OH = H(0) / 2; ah.OW = Wd(0); ah.K = 96; ah.NOUT = 96;

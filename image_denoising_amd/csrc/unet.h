@@ -43,6 +43,10 @@ struct Plan {
   long packUX[NL];              // bf16x6 parity images of the 96-channel deconvs (-1: none)
   long packBF[NL];              // bf16 images of the 3x3 layers (mixed-precision forward)
   long packX[NL];               // pre-split bf16x6 images of the 3x3 layers (forward)
+  // forward-only plans, the N2N pair-pixel pass on the Winograd kernel (k_c3w6s): dec_conv1b's
+  // tap-transposed PK_W6 image (y tiles) and the per-orientation cell lists (2 N cells uint32)
+  // with their counts (2 N int); -1 in plans with a backward
+  long packXV, w6s_list, w6s_cnt;
   long fwd_floats;
   // gradients
   long g_nb, g_na, g_d1b, g_d1a, g_c1;

@@ -390,26 +390,71 @@ def _pair_mask(rd, N, H, W):
     return cells.transpose(0, 1, 3, 2, 4).reshape(N, 1, H, W)
 
 
+def _rd_set(kind, n, g):
+    """per-cell pair choices: all eight (mixed), only horizontal pairs (rd 0/3/4/7: F(2,3) tiles
+    along x in the Winograd pass) or only vertical ones (1/2/5/6: tiles along y)"""
+    r = torch.randint(0, 8, (n,), generator=g, dtype=torch.uint8)
+    if kind == "h":
+        r = torch.tensor([0, 3, 4, 7], dtype=torch.uint8)[r % 4]
+    elif kind == "v":
+        r = torch.tensor([1, 2, 5, 6], dtype=torch.uint8)[r % 4]
+    return r
+
+
 @pytest.mark.parametrize("prec", PRECS)
-@pytest.mark.parametrize("C,N,H,W", [(1, 2, 64, 64), (3, 1, 64, 96), (1, 8, 128, 128)])
-def test_unet_forward_n2n_pair_pixels_bit_identical(C, N, H, W, prec):
-    """dn_unet_forward_n2n (the N2N step's no-grad pass) = the full forward at the pair pixels,
-    bit for bit; with fp32_x6 nothing else is written (dec_conv1b and the head run on the pair
-    pixels only)."""
+@pytest.mark.parametrize("rdk", ["mixed", "h", "v"])
+@pytest.mark.parametrize("C,N,H,W", [(1, 2, 64, 64), (3, 1, 64, 96), (1, 8, 128, 128),
+                                     (3, 4, 128, 160)])
+def test_unet_forward_n2n_pair_pixels(C, N, H, W, prec, rdk):
+    """dn_unet_forward_n2n (the N2N step's no-grad pass) = the full forward at the pair pixels;
+    with fp32_x6 nothing else is written (dec_conv1b and the head run on the pair pixels only).
+    From one round of 8 x 16 tiles (8 x 128^2 and up) the pair pass's dec_conv1b runs the
+    Winograd kernel k_c3w6s (F(2,3) along x for horizontal pairs, along y for vertical ones)
+    while the full forward runs k_c3w6 along x: the same fp32-accurate arithmetic class, so
+    they agree to 2e-5 of max |y| (unit-gain weights: every level contributes); below that both
+    run direct kernels with the same per-pixel arithmetic and agree bit for bit."""
     net = _net(C, prec)
     _unit_gain(net)
     g = torch.Generator().manual_seed(3)
     x = torch.rand(N, C, H, W, generator=g).to(DEV)
-    rd = torch.randint(0, 8, (N * (H // 2) * (W // 2),), generator=g, dtype=torch.uint8).to(DEV)
+    rd = _rd_set(rdk, N * (H // 2) * (W // 2), g).to(DEV)
     ws = net._workspace(N, H, W, with_backward=False, fresh=True)
     full = torch.empty(N, C, H, W, device=DEV)
     net._run_forward(x, full, ws)
     den = torch.full((N, C, H, W), float("nan"), device=DEV)
     net._run_forward_n2n(x, den, ws, rd)
     sel = torch.from_numpy(_pair_mask(rd.cpu(), N, H, W)).to(DEV).expand(N, C, H, W)
-    assert torch.equal(den[sel], full[sel])
+    assert bool(torch.isfinite(den[sel]).all())
+    winograd = prec == "fp32_x6" and N * (H // 8) * (W // 16) >= 512
+    if winograd:
+        err = (den[sel] - full[sel]).abs().max().item()
+        assert err <= 2e-5 * full.abs().max().item(), err
+    else:
+        assert torch.equal(den[sel], full[sel])
     if prec == "fp32_x6":
         assert bool(torch.isnan(den[~sel]).all())
+
+
+@pytest.mark.parametrize("rdk", ["h", "v", "mixed"])
+def test_unet_forward_n2n_pair_pixels_vs_oracle(rdk):
+    """The Winograd pair pass (8 x 128^2: k_c3w6s for both tile orientations) against the CPU
+    oracle of arch_unet.UNet.forward in fp64 at the pair pixels, reference initialisation:
+    1e-4 of max |y| (north_star's fp32 tolerance on the denoised image)."""
+    from oracle import unet_ref
+
+    C, N, H, W = 1, 8, 128, 128
+    net = _net(C, "fp32_x6")
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(N, C, H, W, generator=g)
+    rd = _rd_set(rdk, N * (H // 2) * (W // 2), g)
+    ws = net._workspace(N, H, W, with_backward=False, fresh=True)
+    den = torch.full((N, C, H, W), float("nan"), device=DEV)
+    net._run_forward_n2n(x.to(DEV), den, ws, rd.to(DEV))
+    with torch.no_grad():
+        ref = unet_ref.forward(net.flat_params.detach().cpu().double(), x.double(), C, C)
+    sel = torch.from_numpy(_pair_mask(rd, N, H, W))
+    d, r = den.cpu().double()[sel], ref[sel]
+    assert (d - r).abs().max().item() <= 1e-4 * r.abs().max().item()
 
 
 def _unit_gain(net, seed=0):
