@@ -554,14 +554,14 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
                                             ws + p.packBF[i], j), j));
     else if (x6) DN_TRY(add(pack_job_x6(conv_fwd_view(w, L.cin, 3), L.cin, L.cout, 0,
                                         ws + p.packX[i], x6_tail_f(i), j), j));
+    else DN_TRY(add(pack_job(L.k == 3 ? G_C3 : G_C1, conv_fwd_view(w, L.cin, L.k), L.cin, L.cout, 1,
+                             ws + p.packF[i], 0, 0, j), j));
     // dec_conv1b's y-tile image for the Winograd pair pass: PK_W6 over the transposed taps
-    if (x6 && i == D1B && w6_sel && (x6_tail_f(i) & X6_W6)) {
+    if (i == D1B && w6_sel) {
       WView v = conv_fwd_view(w, L.cin, 3);
       v.flip = 2;
       DN_TRY(add(pack_job_x6(v, L.cin, L.cout, 0, ws + p.packXV, X6_W6, j), j));
     }
-    else DN_TRY(add(pack_job(L.k == 3 ? G_C3 : G_C1, conv_fwd_view(w, L.cin, L.k), L.cin, L.cout, 1,
-                             ws + p.packF[i], 0, 0, j), j));
   }
   if (bf16_head_x6) {
     DN_TRY(add(true, pack_job_head_x6(prm + p.P.L[NINA].woff, prm + p.P.L[NINB].woff, ws + p.packH)));

@@ -62,7 +62,10 @@ __device__ __forceinline__ int wp_idx(int r, int rw, int blk) {
   return r * rw + ((blk ^ ((r >> 3) & 1)) << 4);
 }
 
-template <int SWL>
+// GL: the next stage's G operands are split into the other buffer at the end of the stage, with
+// X (a whole stage of load latency for both), instead of after the first kernel row (which then
+// issues the X loads into the same registers)
+template <int SWL, bool GL = false>
 __global__ __launch_bounds__(256, 2) void k_wgrad3p(WgradArgs a0) {
   using C = Wp3Cfg<SWL>;
   constexpr int MFW = C::MFW, SW = C::SW, SH = C::SH, XW = C::XW;
@@ -227,7 +230,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3p(WgradArgs a0) {
     __bf16* nbuf = lds + (cb ^ 1) * C::BUF;
     pn = next(pn);
     const bool more = u + 1 < u_end;
-    if (more) load_g(pn);  // in flight during the first kernel row's MFMAs
+    if (more) load_g(pn);  // in flight during the first kernel row's MFMAs (GL: the whole stage)
+    if (GL && more) load_x(pn);
     int aoff = abase;
     unsigned bmask = bmask0;
     asm volatile("" : "+v"(aoff), "+v"(bmask));  // (addresses formed here, not held across stages)
@@ -243,7 +247,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3p(WgradArgs a0) {
     }
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
-      if (ky == 1 && more) {  // G of the next stage into the other buffer, then its X loads
+      if (!GL && ky == 1 && more) {  // G of the next stage into the other buffer, then its X loads
         store_g(nbuf);
         load_x(pn);
       }
@@ -294,6 +298,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3p(WgradArgs a0) {
         x6_acc_add(accb[i][0], hi, lo);
       }
     }
+    if (GL && more) store_g(nbuf);
     if (more) store_x(nbuf);  // (waits for its loads itself)
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own plane writes done
     __syncthreads();                     // next buffer complete; everyone done with this one
@@ -333,18 +338,26 @@ bool wgrad3p_ok(const WgradArgs& a) {
          (long)a.KH * a.KW * a.x_stride * 4 < 0x7fffffffL;
 }
 
+// DN_WGP_SWL: the widest stage row (log2 pixels, 3..5; default 5) and DN_WGP_GL=1: the late G
+// split (A/B switches)
 hipError_t launch_wgrad3p(const WgradArgs& a, int splits, hipStream_t s, int nz) {
   if (!wgrad3p_ok(a)) return hipErrorInvalidValue;
+  static const int swl_max = getenv("DN_WGP_SWL") ? atoi(getenv("DN_WGP_SWL")) : 5;
+  static const bool gl = getenv("DN_WGP_GL") && atoi(getenv("DN_WGP_GL")) != 0;
   const dim3 grid(splits, (a.Cin + 31) / 32, nz), block(256);
-  if (a.KW >= 32) {
-    prof_kernel("k_wgrad3p<5>");
-    hipLaunchKernelGGL(k_wgrad3p<5>, grid, block, 0, s, a);
-  } else if (a.KW >= 16) {
-    prof_kernel("k_wgrad3p<4>");
-    hipLaunchKernelGGL(k_wgrad3p<4>, grid, block, 0, s, a);
+  const int swl = a.KW >= 32 && swl_max >= 5 ? 5 : (a.KW >= 16 && swl_max >= 4 ? 4 : 3);
+  static const char* kn[2][3] = {{"k_wgrad3p<3>", "k_wgrad3p<4>", "k_wgrad3p<5>"},
+                                 {"k_wgrad3p<3,gl>", "k_wgrad3p<4,gl>", "k_wgrad3p<5,gl>"}};
+  prof_kernel(kn[gl][swl - 3]);
+  if (swl == 5) {
+    if (gl) hipLaunchKernelGGL((k_wgrad3p<5, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_wgrad3p<5>), grid, block, 0, s, a);
+  } else if (swl == 4) {
+    if (gl) hipLaunchKernelGGL((k_wgrad3p<4, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_wgrad3p<4>), grid, block, 0, s, a);
   } else {
-    prof_kernel("k_wgrad3p<3>");
-    hipLaunchKernelGGL(k_wgrad3p<3>, grid, block, 0, s, a);
+    if (gl) hipLaunchKernelGGL((k_wgrad3p<3, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_wgrad3p<3>), grid, block, 0, s, a);
   }
   return hipGetLastError();
 }
