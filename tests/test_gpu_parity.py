@@ -395,9 +395,9 @@ def _rd_set(kind, n, g):
     along x in the Winograd pass) or only vertical ones (1/2/5/6: tiles along y)"""
     r = torch.randint(0, 8, (n,), generator=g, dtype=torch.uint8)
     if kind == "h":
-        r = torch.tensor([0, 3, 4, 7], dtype=torch.uint8)[r % 4]
+        r = torch.tensor([0, 3, 4, 7], dtype=torch.uint8)[(r % 4).long()]
     elif kind == "v":
-        r = torch.tensor([1, 2, 5, 6], dtype=torch.uint8)[r % 4]
+        r = torch.tensor([1, 2, 5, 6], dtype=torch.uint8)[(r % 4).long()]
     return r
 
 
