@@ -338,12 +338,13 @@ bool wgrad3p_ok(const WgradArgs& a) {
          (long)a.KH * a.KW * a.x_stride * 4 < 0x7fffffffL;
 }
 
-// DN_WGP_SWL: the widest stage row (log2 pixels, 3..5; default 5) and DN_WGP_GL=1: the late G
-// split (A/B switches)
+// DN_WGP_SWL: the widest stage row (log2 pixels, 3..5; default 4: 2 rows of 16 pixels, 72 X pixels
+// per stage instead of 102 for one row of 32) and DN_WGP_GL (default 1: the late G split); A/B on
+// one box (profiles/r4_wgp2_ab.log): 96->96 @64 x 128^2 1.04-1.06 (GL 0, SWL 5) -> 1.01-1.03 ms
 hipError_t launch_wgrad3p(const WgradArgs& a, int splits, hipStream_t s, int nz) {
   if (!wgrad3p_ok(a)) return hipErrorInvalidValue;
-  static const int swl_max = getenv("DN_WGP_SWL") ? atoi(getenv("DN_WGP_SWL")) : 5;
-  static const bool gl = getenv("DN_WGP_GL") && atoi(getenv("DN_WGP_GL")) != 0;
+  static const int swl_max = getenv("DN_WGP_SWL") ? atoi(getenv("DN_WGP_SWL")) : 4;
+  static const bool gl = !getenv("DN_WGP_GL") || atoi(getenv("DN_WGP_GL")) != 0;
   const dim3 grid(splits, (a.Cin + 31) / 32, nz), block(256);
   const int swl = a.KW >= 32 && swl_max >= 5 ? 5 : (a.KW >= 16 && swl_max >= 4 ? 4 : 3);
   static const char* kn[2][3] = {{"k_wgrad3p<3>", "k_wgrad3p<4>", "k_wgrad3p<5>"},

@@ -219,12 +219,14 @@ def test_improved_unet_winograd_blocks_match_direct_kernels(tmp_path):
     the epilogue) against the direct bf16x6 kernels (DN_X6_W6=0).  DN_W6_MIN_TILES=1 routes every
     96-block launch to the Winograd kernel at this test size (the default takes it from one
     round of 512 tiles, i.e. at the bench's 64 x 256^2).  Same arithmetic class, so the output
-    and every parameter gradient agree to fp32 rounding: 2e-5 of the max magnitude, as the UNet
-    test above."""
+    agrees to 2e-5 of its max magnitude, as the UNet test above.  The parameter gradients go
+    through ImprovedUNet's GroupNorm backward, which amplifies fp32 rounding differences
+    (test_gpu_iunet compares them per tensor at 1e-3 against the oracle); measured here 2.0e-5 of
+    the max gradient, bound 1e-4 (an indexing or block-offset error is O(1))."""
     w6 = _worker_env_run(tmp_path, "iw6", {"DN_W6_MIN_TILES": "1"}, "igrad", shape="2,64,64")
     d = _worker_env_run(tmp_path, "idirect", {"DN_X6_W6": "0"}, "igrad", shape="2,64,64")
     a, b = w6["y"], d["y"]
     assert np.abs(a - b).max() <= 2e-5 * np.abs(a).max(), np.abs(a - b).max()
     ga = np.concatenate([w6[f"g{i}"] for i in range(len(w6["names"]))])
     gb = np.concatenate([d[f"g{i}"] for i in range(len(d["names"]))])
-    assert np.abs(ga - gb).max() <= 2e-5 * np.abs(ga).max(), np.abs(ga - gb).max()
+    assert np.abs(ga - gb).max() <= 1e-4 * np.abs(ga).max(), np.abs(ga - gb).max()
