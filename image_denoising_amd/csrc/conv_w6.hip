@@ -51,13 +51,23 @@ struct WCfg {
   static_assert(2 * LBYTES <= 163840, "two workgroups per CU");
 };
 
-// 16-B quad index of V element (row, kq, j, p): p is XOR-swizzled by j >> 2, row & 1 and kq, so
-// the 16 tiles (two rows x 8) that lanes li = 0..15 read at one (p, kq) fall on 16 distinct quads
-// of a 256-B window (conflict-free ds_read_b128), and so do the (kq, j & 3) pairs of the transform's
-// 8-B writes (without kq in the swizzle those were 4-way bank conflicts: SQ_LDS_BANK_CONFLICT 41 %
-// of the LDS-active cycles)
+// 16-B quad index of V element (row, kq, j, p): p is XOR-swizzled by row & 1 and the bit-reversed
+// kq, so that every ds_read_b128 lane group of the stage reads (lanes {0-3, 12-15, 20-27}, ...:
+// two tile rows, two kq, four tiles each) and every 16-lane group of the transform's 8-B writes
+// (one row, two tiles, four kq x two halves) falls on distinct banks.  Found by a brute-force search
+// over XOR swizzles in the bits of j, row and a permutation of kq against gfx950's LDS lane groups
+// (MI355X_MICROARCH.md); the round-3 swizzle p ^ (j >> 2) ^ ((row & 1) << 1) ^ kq left the reads
+// 2-way (SQ_LDS_BANK_CONFLICT 37 % of the LDS-active cycles of k_c3w6<1>, profiles/r4_pmc_sq_n2n.txt).
+// DN_W6_SWZ=0 builds the round-3 swizzle (A/B).
+#ifndef DN_W6_SWZ
+#define DN_W6_SWZ 1
+#endif
 __device__ __forceinline__ int w6_vq(int row, int kq, int j, int p) {
+#if DN_W6_SWZ
+  return ((row * 4 + kq) * 8 + j) * 4 + (p ^ (row & 1) ^ (((kq & 1) << 1) | (kq >> 1)));
+#else
   return ((row * 4 + kq) * 8 + j) * 4 + (p ^ (j >> 2) ^ ((row & 1) << 1) ^ kq);
+#endif
 }
 
 __device__ __forceinline__ void w6_barrier() {
@@ -478,6 +488,9 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
 // Output: the pair image [N][OH/2][OW][96] (column 2cj + s = pixel pair[rd][s] of cell (ci, cj)),
 // bias + LeakyReLU, as k_c3x6s writes it for the head.
 // ------------------------------------------------------------------------------------
+#ifndef DN_W6S_PF
+#define DN_W6S_PF 1
+#endif
 struct SCfgW {
   static constexpr int WAVES = 4, MT = 4, NTW = 3, NP = 96, CELLS = 64, KC = 32;
   static constexpr int VPL = 4 * CELLS * KC;        // bf16 per plane of V: [p][cell][32 ch]
@@ -585,8 +598,9 @@ __global__ __launch_bounds__(256, 2) void k_c3w6s(FwdArgs a, const unsigned* __r
   unsigned ent[2];
 #pragma unroll
   for (int it = 0; it < 2; ++it) ent[it] = lent[(tid >> 3) + 32 * it];
-  auto transform = [&](int k0, int k3) {
-    f32x4 d[2][4];
+  // tload: the phase's input pixels into d (tload_phase), twrite: V from them
+  f32x4 d[2][4];
+  auto tload = [&](int k0, int k3) {
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const unsigned e = ent[it];
@@ -603,6 +617,8 @@ __global__ __launch_bounds__(256, 2) void k_c3w6s(FwdArgs a, const unsigned* __r
         d[it][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
       }
     }
+  };
+  auto twrite = [&]() {
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int cell = (tid >> 3) + 32 * it;
@@ -678,16 +694,26 @@ __global__ __launch_bounds__(256, 2) void k_c3w6s(FwdArgs a, const unsigned* __r
   };
 #pragma unroll
   for (int q = 0; q < NTW; ++q) load_wq(2 * ph, q);
+  // DN_W6S_PF (default 1): the next phase's input pixels are requested right after this phase's
+  // V is written, so their latency runs under this phase's MFMAs instead of between the two
+  // barriers of the next transform (a tile has three phases per input chunk, each with its own
+  // gather from L2); 0: loaded inside the transform (A/B)
   const int nph = nch * 3;
+  if (DN_W6S_PF) tload(0, 0);
 #pragma unroll 1
   for (int ph3 = 0; ph3 < nph; ++ph3) {
     const int c = ph3 / 3, k3 = ph3 - 3 * c;
     int liv = li, lgv = lg;
     asm volatile("" : "+v"(liv), "+v"(lgv));
     if (ph3 > 0) w6_barrier();  // every wave is done with the previous phase's V
-    transform(c * C::KC, k3);
+    if (!DN_W6S_PF) tload(c * C::KC, k3);
+    twrite();
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own V stores done
     w6_barrier();
+    if (DN_W6S_PF && ph3 + 1 < nph) {
+      const int c1 = (ph3 + 1) / 3;
+      tload(c1 * C::KC, ph3 + 1 - 3 * c1);
+    }
     const int st0 = ph3 * 4 + 2 * ph;  // c*12 + k3*4 + 2ph
     stage(std::integral_constant<int, 0>{}, st0 + 1, liv, lgv);
     stage(std::integral_constant<int, 1>{}, ph3 + 1 < nph ? st0 + 4 : -1, liv, lgv);
