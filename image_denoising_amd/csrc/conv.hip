@@ -1279,7 +1279,10 @@ int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
   // per-workgroup slab (up to 110 KB written, then re-read by the reduction) outweighs the work
   // of a 2-chunk split
   static const int mu_env = getenv("DN_WG_MIN_UNITS") ? atoi(getenv("DN_WG_MIN_UNITS")) : 2;
-  const int mu = mu_env < 1 ? 1 : mu_env;
+  // (DN_WG_MIN_UNITS96: the same for the 96-output 3x3 layers, whose per-split slab is twice a
+  // 48-output one's; default = DN_WG_MIN_UNITS)
+  static const int mu96_env = getenv("DN_WG_MIN_UNITS96") ? atoi(getenv("DN_WG_MIN_UNITS96")) : mu_env;
+  const int mu = (mode == W_C3 && Cout == 96 ? mu96_env : mu_env) < 1 ? 1 : (mode == W_C3 && Cout == 96 ? mu96_env : mu_env);
   if (want > units / mu) want = units / mu;
   if (want < 1) want = 1;
   return (int)want;

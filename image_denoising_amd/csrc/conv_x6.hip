@@ -1240,8 +1240,10 @@ static hipError_t run_x6h(const FwdArgs& a, int nz, hipStream_t s) {
 
 // small grids (below one round of 16 x 16 tiles), plain image: the 3-slot ring, and where the
 // caller gave split-K space (a.ks_part / a.ks_cnt) the stages split over ks workgroups so that
-// tiles x ks fills one round of two workgroups per CU, at least 3 stages per split, ks <= 8
-// (DN_X6_SPLITK=0: no split; =k: at most k)
+// 8-row tiles x ks fill one round of two workgroups per CU, at least 3 stages per split, ks <= 8
+// (DN_X6_SPLITK=0: no split; =k: at most k).  ks follows from the shape alone, not from MT: the
+// MT = 1 and MT = 2 launches of one shape (a fused pool takes MT = 2) split the stages alike and
+// so stay bit-identical, as without the split.
 template <int NT, int MT>
 static hipError_t run_x6h3(const FwdArgs& a0, int nz, hipStream_t s) {
   using C = HCfg<NT, MT, 3>;
@@ -1249,14 +1251,15 @@ static hipError_t run_x6h3(const FwdArgs& a0, int nz, hipStream_t s) {
   static const int ks_env = getenv("DN_X6_SPLITK") ? atoi(getenv("DN_X6_SPLITK")) : 8;
   const int tx = (a0.OW + C::TW - 1) / C::TW, ty = (a0.OH + C::TH - 1) / C::TH;
   const long tiles = (long)tx * ty * a0.N * nz;
+  const long tiles8 = (long)((a0.OW + 15) / 16) * ((a0.OH + 7) / 8) * a0.N * nz;
   const int nst = 9 * ((a0.K + C::KC - 1) / C::KC);
   FwdArgs a = a0;
   a.ks = 1;
-  if (a.ks_part && a.ks_cnt && tiles <= kSplitSlots / 2) {
-    int ks = (int)(kSplitSlots / tiles);
+  if (a.ks_part && a.ks_cnt && tiles8 <= 256) {
+    int ks = (int)(512 / tiles8);
     if (ks > nst / 3) ks = nst / 3;
     if (ks > ks_env) ks = ks_env;
-    a.ks = ks < 1 ? 1 : ks;
+    if (ks > 1 && tiles * ks <= kSplitSlots) a.ks = ks;
   }
   static const std::string kn = x6_kmore(x6_kname("k_c3x6h", NT, 0, MT), "3");
   static const std::string knk = x6_kmore(kn, "ks");

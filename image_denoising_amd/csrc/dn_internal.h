@@ -112,7 +112,7 @@ struct FwdArgs {
   // ks_cnt[tile], reset by it) adds them in split order and runs the epilogue.  ks <= 1: off
   float* ks_part; unsigned* ks_cnt; int ks;
 };
-constexpr int kSplitSlots = 512;           // tiles x splits of one split-K launch, at most
+constexpr int kSplitSlots = 1024;          // tiles x splits of one split-K launch, at most
 constexpr int kSplitFloats = 256 * 6 * 4;  // fp32 partial of one workgroup (256 lanes x 6 f32x4)
 
 // Fused output head (arch_unet.py:186-190, 253-257): the dec_conv1b kernel keeps its
