@@ -475,7 +475,9 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
         a.pool_out = pool->p; a.pool_stride = pool->stride; a.pool_off = pool->off;
         if (pooled) *pooled = true;
       }
-      a.ks_part = ws + p.ks_part; a.ks_cnt = reinterpret_cast<unsigned*>(ws + p.ks_cnt);
+      // (not dec_conv1b: the pair pass computes it per pixel pair with the unsplit sums, and
+      // small test grids compare the two bit for bit)
+      if (i != D1B) { a.ks_part = ws + p.ks_part; a.ks_cnt = reinterpret_cast<unsigned*>(ws + p.ks_cnt); }
       return launch_fwd_x6(a, st);
     }
     if (!bf16 || i == NL || p.packBF[i] < 0)
