@@ -1373,14 +1373,15 @@ __device__ __forceinline__ void pk_f32(const PackJob& j, long e) {
 }
 
 // nin_a / nin_b (OIHW 96x96x1x1) -> the two pre-split head images: [plane][b][out][32] in the
-// head kernel's permuted K order (see k_nin_head_x6)
+// head kernel's permuted K order (see k_nin_head_x6); j.flip: the transposed matrices (row o of
+// the image = column o of the weight), the backward's Wb^T | Wa^T (k_head_bwd_x6)
 __device__ __forceinline__ void pk_head_x6(const PackJob& j, long e) {
   const int layer = (int)(e / X6_HEAD_BF), r0 = (int)(e % X6_HEAD_BF);
   const int p = r0 / (3 * 96 * 32), row = (r0 / 32) % (3 * 96), k = r0 % 32;  // row = b*96 + o
   const int b = row / 96, o = row % 96, g = k >> 3, jj = k & 7;
   const int ch = 32 * b + (jj < 4 ? 4 * g + jj : 16 + 4 * g + (jj - 4));
   __bf16 h, m, l;
-  split3((layer ? j.w2 : j.w)[o * 96 + ch], h, m, l);
+  split3((layer ? j.w2 : j.w)[j.flip ? ch * 96 + o : o * 96 + ch], h, m, l);
   static_cast<__bf16*>(j.out)[layer * X6_HEAD_BF + (p * 3 * 96 + row) * 32 + x6_swz(row, g) * 8 + jj] =
       p == 0 ? h : (p == 1 ? m : l);
 }
@@ -1478,6 +1479,12 @@ static bool pack_view(const WView& wv, PackJob& j) {
 PackJob pack_job_head_x6(const float* wa, const float* wb, void* out) {
   PackJob j{};
   j.kind = PK_HEAD_X6; j.w = wa; j.w2 = wb; j.out = out;
+  return j;
+}
+
+PackJob pack_job_head_bwd_x6(const float* wa, const float* wb, void* out) {
+  PackJob j{};
+  j.kind = PK_HEAD_X6; j.w = wb; j.w2 = wa; j.out = out; j.flip = 1;  // Wb^T | Wa^T
   return j;
 }
 
@@ -2314,6 +2321,141 @@ __global__ __launch_bounds__(512, 1) void k_nin_head_x6(FwdArgs a, HeadArgs hd, 
   }
 }
 
+
+// ------------------------------------------------------------------------------------
+// Backward of the fused head in the bf16x6 arithmetic (k_head_bwd's products on the fp32
+// matrix cores, arch_unet.py:186-190 differentiated):
+//   g_nb = leaky'(nb) * (Wc^T dy)      (fp32 VALU, K = oc, nin_c's weights in LDS)
+//   g_na = leaky'(na) * (Wb^T g_nb)    (bf16x6 GEMM, image Wb^T)
+//   g_d1b = leaky'(d1b) * (Wa^T g_na)  (bf16x6 GEMM, image Wa^T)
+// The tile stays in the MFMA C/D map (rows = channels, columns = 16 pixels), which is the B
+// operand of the next GEMM as in k_nin_head_x6; the transposed images (pk_head_x6 with flip) are
+// DMA'd into LDS once per workgroup.  One 8-wave workgroup per CU walks 16-pixel wave-tiles of
+// the flattened pixel range; a tile's nb / dy / na / d1b loads are issued together at its start
+// (the other wave on the SIMD computes meanwhile).  Every 16-pixel tile addresses its rows
+// through its own buffer resource (pixel ranges beyond 2 GiB, out-of-range lanes read zeros and
+// drop their stores).
+// ------------------------------------------------------------------------------------
+template <int OCM>  // nin_c outputs at most (registers of dy)
+__global__ __launch_bounds__(512, 1) void k_head_bwd_x6(HeadBwdArgs h, const __bf16* wimg, long nwt) {
+  __shared__ __attribute__((aligned(16))) __bf16 lw[2 * X6_HEAD_BF];
+  __shared__ __attribute__((aligned(16))) float lc[X6_HEAD_OCMAX * 96];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, lg = lane >> 4;
+  for (int q = wave; q < 2 * X6_HEAD_BF * 2 / 1024; q += 8)
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(wimg + q * 512 + lane * 8),
+        (__attribute__((address_space(3))) void*)(lw + q * 512), 16, 0, 0);
+  for (int e = threadIdx.x; e < h.oc * 96; e += 512) lc[e] = h.wc[e];
+  __syncthreads();
+  auto rsrc = [&](const float* base, long px0, int npx_t) {  // 16 pixels x 96 channels
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base + px0 * 96), (short)0,
+                                             npx_t * 96 * 4, 0x00020000);
+  };
+  auto mask = [](f32x4& v, const f32x4& m) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = m[r] > 0.f ? v[r] : v[r] * 0.2f;
+  };
+  // out = W (LDS image at `img`) x in: three 32-channel K blocks of six split products each
+  // (k_nin_head_x6's gemm96)
+  auto gemm96 = [&](const __bf16* img, const f32x4 (&in)[6], f32x4 (&out)[6][1]) {
+#pragma unroll
+    for (int f = 0; f < 6; ++f) out[f][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      bf16x8 xv[3][1];
+      const float v8[8] = {in[2 * b][0], in[2 * b][1], in[2 * b][2], in[2 * b][3],
+                           in[2 * b + 1][0], in[2 * b + 1][1], in[2 * b + 1][2], in[2 * b + 1][3]};
+      split3x8(v8, xv[0][0], xv[1][0], xv[2][0]);
+      bf16x8 wv[3][6];
+#pragma unroll
+      for (int f = 0; f < 6; ++f) {
+        const int row = b * 96 + f * 16 + li;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          wv[pl][f] = *reinterpret_cast<const bf16x8*>(img + (pl * 3 * 96 + row) * 32 + x6_swz(row, lg) * 8);
+      }
+      x6_block<6, 1, 1>(out, wv, xv);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  const int loff = (li * 96 + 4 * lg) * 4;  // lane's bytes within a tile row set
+  for (long wt = (long)blockIdx.x * 8 + wave; wt < nwt; wt += (long)gridDim.x * 8) {
+    const long px0 = wt * 16;
+    const int npx_t = h.npx - px0 < 16 ? (int)(h.npx - px0) : 16;
+    const bool ok = li < npx_t;
+    const int off = ok ? loff : 0x7fffffff;
+    const __amdgpu_buffer_rsrc_t rnb = rsrc(h.nb, px0, npx_t), rna = rsrc(h.na, px0, npx_t),
+                                 rd1 = rsrc(h.d1b, px0, npx_t);
+    f32x4 nb[6], na[6], d1[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+      nb[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rnb, off + 64 * q, 0, 0));
+    float dy[OCM];
+    const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(h.dy + px0 * h.dy_stride), (short)0, npx_t * h.dy_stride * 4, 0x00020000);
+#pragma unroll
+    for (int o = 0; o < OCM; ++o)
+      if (o < h.oc)
+        dy[o] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                              rdy, ok ? (li * h.dy_stride + o) * 4 : 0x7fffffff, 0, 0));
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+      na[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rna, off + 64 * q, 0, 0));
+    // g_nb (K = oc, k_head_bwd's order)
+    f32x4 t[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) t[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int o = 0; o < OCM; ++o) {
+      if (o >= h.oc) break;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const float4 w = *reinterpret_cast<const float4*>(lc + o * 96 + q * 16 + 4 * lg);
+        t[q][0] = fmaf(w.x, dy[o], t[q][0]); t[q][1] = fmaf(w.y, dy[o], t[q][1]);
+        t[q][2] = fmaf(w.z, dy[o], t[q][2]); t[q][3] = fmaf(w.w, dy[o], t[q][3]);
+      }
+    }
+    const __amdgpu_buffer_rsrc_t wnb = rsrc(h.g_nb, px0, npx_t);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      mask(t[q], nb[q]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, t[q]), wnb, off + 64 * q, 0, 0);
+    }
+    f32x4 u[6][1];
+    gemm96(lw, t, u);  // Wb^T g_nb
+    // d1b's loads behind the first GEMM (registers), in flight during the second
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+      d1[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rd1, off + 64 * q, 0, 0));
+    const __amdgpu_buffer_rsrc_t wna = rsrc(h.g_na, px0, npx_t);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      mask(u[q][0], na[q]);
+      t[q] = u[q][0];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, t[q]), wna, off + 64 * q, 0, 0);
+    }
+    gemm96(lw + X6_HEAD_BF, t, u);  // Wa^T g_na
+    const __amdgpu_buffer_rsrc_t wd1 = rsrc(h.g_d1b, px0, npx_t);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      mask(u[q][0], d1[q]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u[q][0]), wd1, off + 64 * q, 0, 0);
+    }
+  }
+}
+
+// wimg = pack_job_head_bwd_x6's images; every tensor NHWC stride 96 (dy: dy_stride, oc <=
+// X6_HEAD_BWD_OCMAX: dy in registers; more outputs spill, k_head_bwd takes them)
+hipError_t launch_head_bwd_x6(const HeadBwdArgs& h, const void* wimg, hipStream_t s) {
+  if (h.oc < 1 || h.oc > X6_HEAD_BWD_OCMAX || h.npx < 1 || h.dy_stride < h.oc) return hipErrorInvalidValue;
+  const long nwt = (h.npx + 15) / 16;
+  const long blocks = (nwt + 7) / 8 < 256 ? (nwt + 7) / 8 : 256;  // one workgroup per CU
+  prof_kernel("k_head_bwd_x6<4>");
+  hipLaunchKernelGGL(k_head_bwd_x6<4>, dim3((unsigned)blocks), dim3(512), 0, s, h,
+                     static_cast<const __bf16*>(wimg), nwt);
+  return hipGetLastError();
+}
 
 // nin_a / nin_b weights (OIHW 96x96x1x1, contiguous) -> the two pre-split head images
 hipError_t launch_pack_head_x6(const float* wa, const float* wb, void* out, hipStream_t s) {

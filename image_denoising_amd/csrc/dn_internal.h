@@ -142,6 +142,7 @@ constexpr int HEAD_WS = 100;   // k-row stride of a head weight image (conflict-
 constexpr int HEAD_LW = 9728;  // 96 * HEAD_WS rounded up to 256 floats
 constexpr int X6_HEAD_BF = 3 * 3 * 96 * 32;  // bf16 per layer of the bf16x6 head image (54 KiB)
 constexpr int X6_HEAD_OCMAX = 16;  // most nin_c outputs of the bf16x6 head (kept in its LDS)
+constexpr int X6_HEAD_BWD_OCMAX = 4;  // most nin_c outputs of its backward (k_head_bwd_x6)
 
 struct WgradArgs {
   const float* g; int g_stride, g_off;  // gradient operand (rows = co), NHWC
@@ -207,6 +208,8 @@ hipError_t pack_flush(PackBatch& b, hipStream_t s);  // one launch; empties b
 hipError_t pack_add(PackBatch& b, const PackJob& j, hipStream_t s);  // flushes a full batch first
 bool pack_job_x6(const WView& wv, int K, int nout, int zc, void* out, int tail, PackJob& j);
 PackJob pack_job_head_x6(const float* wa, const float* wb, void* out);
+PackJob pack_job_head_bwd_x6(const float* wa, const float* wb, void* out);  // Wb^T | Wa^T
+hipError_t launch_head_bwd_x6(const HeadBwdArgs& h, const void* wimg, hipStream_t s);
 PackJob pack_job_deconv_x6(const float* w, void* out);
 PackJob pack_job_deconv_dgrad_x6(const float* w, void* out);
 PackJob pack_job_zero(float* out, int n);

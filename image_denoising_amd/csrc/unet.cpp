@@ -818,6 +818,10 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     a.out = dx.p; a.out_stride = dx.stride; a.out_off = dx.off;
     return launch_deconv_dgrad_x6(a, ws + p.packUXB[i], st);
   };
+  // the head's data gradients in the bf16x6 arithmetic (k_head_bwd_x6; DN_X6_HEAD_BWD=0: the
+  // fp32-MFMA k_head_bwd)
+  static const bool hbx6_env = !getenv("DN_X6_HEAD_BWD") || atoi(getenv("DN_X6_HEAD_BWD")) != 0;
+  const bool head_bwd_x6 = x6 && hbx6_env && p.OC <= X6_HEAD_BWD_OCMAX;
   // flipped/transposed weight images for the data gradients, the head's images and the
   // weight gradients' zero padding: one launch
   {
@@ -841,8 +845,11 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                             dgrad_nout(p, i), 1, ws + p.packB[i], 0, 0, j), j));
       }
     }
-    DN_TRY(launch_pack_head(conv_dgrad_view(prm + p.P.L[NINB].woff, 96, 1),
-                            conv_dgrad_view(prm + p.P.L[NINA].woff, 96, 1), ws + p.packHB, s, &pb));
+    if (head_bwd_x6)
+      DN_TRY(add(true, pack_job_head_bwd_x6(prm + p.P.L[NINA].woff, prm + p.P.L[NINB].woff, ws + p.packHB)));
+    else
+      DN_TRY(launch_pack_head(conv_dgrad_view(prm + p.P.L[NINB].woff, 96, 1),
+                              conv_dgrad_view(prm + p.P.L[NINA].woff, 96, 1), ws + p.packHB, s, &pb));
     DN_TRY(add(true, pack_job_zero(ws + p.zeros, 64)));
     DN_TIMED(s, "pack", 0, 0, 0, 0, 0, 0, pack_flush(pb, s));
   }
@@ -902,7 +909,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     h.g_nb = ws + p.g_nb; h.g_na = ws + p.g_na; h.g_d1b = ws + p.g_d1b;
     h.npx = (long)N * H(0) * Wd(0);
     DN_TIMED(s, "head_bwd", 2.0 * h.npx * 96 * (2 * 96 + OC), OC, 96, H(0), Wd(0), N,
-             launch_head_bwd(h, s));
+             head_bwd_x6 ? launch_head_bwd_x6(h, ws + p.packHB, s) : launch_head_bwd(h, s));
   }
   DN_TRY(fork());
   if (OC <= 4)
