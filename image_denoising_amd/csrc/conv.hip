@@ -1418,9 +1418,10 @@ long wgrad_slab_floats(int mode, int N, int KH, int KW, int cin, int cout) {
   return f;
 }
 
-// k_wgrad1 + its reductions straight into dwb (PyTorch layout, bias after the weight)
+// k_wgrad1 + its reductions straight into dwb (PyTorch layout, bias after the weight); x6: the
+// 96 x 96 1x1 on k_wgrad1p (bf16x6), the same splits and slab rows
 hipError_t launch_wgrad1(int mode, const WgradArgs& a0, float* dwb, hipStream_t s,
-                         RedBatch* rb) {
+                         RedBatch* rb, bool x6) {
   const bool up2 = mode == W_UP2;
   const int sp = wgrad1_splits(mode, a0.N, a0.KH, a0.KW), z = up2 ? 4 : 1;
   const long W = (long)a0.Cout * a0.Cin, row = W + a0.Cout;
@@ -1428,6 +1429,10 @@ hipError_t launch_wgrad1(int mode, const WgradArgs& a0, float* dwb, hipStream_t 
   a.slab_stride = row;
   a.wlayout = up2 ? 1 : 0;  // deconv weight (in, out, 2, 2): [ci][co] per parity
   const dim3 grid(sp, 1, z);
+  if (x6 && !up2 && wgrad1p_ok(a)) {
+    const hipError_t e = launch_wgrad1p(a, sp, s);
+    return e != hipSuccess ? e : launch_reduce(a.slab, row, sp, row, dwb, s, rb);
+  }
   if (a.Cout == 96)
     hipLaunchKernelGGL((k_wgrad1<6, 6, 2, 2>), grid, dim3(256), 0, s, a, (int)up2);
   else

@@ -317,10 +317,12 @@ hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s);
 // k_wgrad3p; nz = output-channel blocks of a.zc == 96 over blockIdx.z, else 1)
 bool wgrad3p_ok(const WgradArgs& a);
 hipError_t launch_wgrad3p(const WgradArgs& a, int splits, hipStream_t s, int nz);
+bool wgrad1p_ok(const WgradArgs& a);  // 96 -> 96 1x1 on k_wgrad1p (bf16x6)
+hipError_t launch_wgrad1p(const WgradArgs& a, int splits, hipStream_t s);
 bool wgrad1_ok(int mode, const WgradArgs& a);
 long wgrad_slab_floats(int mode, int N, int KH, int KW, int cin, int cout);
 hipError_t launch_wgrad1(int mode, const WgradArgs& a, float* dwb, hipStream_t s,
-                         RedBatch* rb = nullptr);
+                         RedBatch* rb = nullptr, bool x6 = false);
 hipError_t launch_reduce_scatter(const float* slab, long slab_stride, int splits, long n,
                                  float* out, long grp, long ostride, long ooff, hipStream_t s,
                                  RedBatch* rb = nullptr);

@@ -390,7 +390,9 @@ hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, 
     hipError_t e = hipMemsetAsync(slab, 0, 64 * sizeof(float), s);
     if (e != hipSuccess) return e;
   }
-  if (wgrad1_ok(mode, a)) return launch_wgrad1(mode, a, dwb, s, rb);  // 1x1 / deconv, own splits
+  // 1x1 / deconv, own splits (x6: the 96 x 96 1x1 layers on k_wgrad1p; DN_X6_WGRAD1=0: k_wgrad1)
+  static const bool wg1_x6 = !getenv("DN_X6_WGRAD1") || atoi(getenv("DN_X6_WGRAD1")) != 0;
+  if (wgrad1_ok(mode, a)) return launch_wgrad1(mode, a, dwb, s, rb, x6 && wg1_x6);
   if (x6 && mode == W_C3) splits = wgrad_splits_x6(a, splits);
   hipError_t e = launch_wgrad(mode, a, splits, s, x6);
   if (e != hipSuccess) return e;
@@ -921,10 +923,10 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                  p.splits[NINC], s2, false, Z, &rb));
   DN_TRY(fork());
   DN_TRY(wgrad(W_C1, V(p.g_nb, 96), V(p.na, 96), N, H(0), Wd(0), 96, 96, G(NINB), SL(NINB),
-               p.splits[NINB], s2, false, Z, &rb));
+               p.splits[NINB], s2, x6, Z, &rb));
   DN_TRY(fork());
   DN_TRY(wgrad(W_C1, V(p.g_na, 96), V(p.d1b, 96), N, H(0), Wd(0), 96, 96, G(NINA), SL(NINA),
-               p.splits[NINA], s2, false, Z, &rb));
+               p.splits[NINA], s2, x6, Z, &rb));
   DN_TRY(fork());
   DN_TRY(wgrad(W_C3, V(p.g_d1b, 96), V(p.d1a, 96), N, H(0), Wd(0), 96, 96, G(D1B), SL(D1B),
                p.splits[D1B], s2, x6w, Z, &rb));

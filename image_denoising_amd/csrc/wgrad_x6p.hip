@@ -363,4 +363,177 @@ hipError_t launch_wgrad3p(const WgradArgs& a, int splits, hipStream_t s, int nz)
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------
+// 1x1 weight gradient of the 96 x 96 head layers (nin_a, nin_b: arch_unet.py:186-189) in the
+// same arithmetic (k_wgrad1p; k_wgrad1 does them on the fp32 matrix cores).  K = pixels of the
+// flattened N x H x W range (a 1x1 conv has no halo), 32 per stage: G [32 px][96 co] and X
+// [32 px][96 ci] split once into three bf16 planes of the stage buffer, the next stage's fp32
+// operands in registers meanwhile, one barrier per stage.  Wave (wm, wn): output channels
+// 48wm .. +47 x input channels 48wn .. +47 (3 x 3 fragments, six products each, the fold of
+// k_wgrad3p); both operands are read with ds_read_b64_tr_b16 in the same pattern (pixel-major
+// rows, 16-channel blocks flipped by bit 3 of the row).  The bias gradient is G against a ones
+// fragment in the wn = 0 waves.  Each workgroup writes its partial [W | b] to a slab row.
+// ------------------------------------------------------------------------------------
+struct Wp1Cfg {
+  static constexpr int C = 96, NTHR = 256, PX = 32;
+  static constexpr int GQ = PX * C / 4, NQ = 2 * GQ, NIT = NQ / NTHR;  // float4 items
+  static constexpr int GPL = PX * C, PL = 2 * GPL, BUF = 3 * PL;     // bf16
+  static_assert(NQ % NTHR == 0 && GQ % NTHR == 0, "whole items per thread");
+  static_assert(2 * BUF * 2 <= 81920, "two workgroups per CU");
+};
+
+__global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
+  using C = Wp1Cfg;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * C::BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 15, lg = lane >> 4;
+  const long U = (npx + C::PX - 1) / C::PX;
+  const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
+  const bool do_bias = wn == 0;
+
+  f32x4 acc[3][3], accb[3][1];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    accb[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // item it of this thread: operand (G for it < NIT/2), pixel, 4 channels; its LDS index
+  constexpr int NG = C::GQ / C::NTHR;
+  int ioff[C::NIT], ipx[C::NIT], ilds[C::NIT];
+#pragma unroll
+  for (int it = 0; it < C::NIT; ++it) {
+    const int q = tid + it * C::NTHR, r = it < NG ? q : q - C::GQ;
+    const int px = r / (C::C / 4), c = 4 * (r % (C::C / 4));
+    ipx[it] = px;
+    ioff[it] = px * (it < NG ? a.g_stride : a.x_stride) + c;
+    ilds[it] = (it < NG ? 0 : C::GPL) + wp_idx(px, C::C, c >> 4) + (c & 15);
+  }
+  f32x4 pv[C::NIT];
+  auto load = [&](long u) {
+    const long p0 = u * C::PX;
+    const int np = npx - p0 < C::PX ? (int)(npx - p0) : C::PX;
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.g + p0 * a.g_stride + a.g_off), (short)0, np * a.g_stride * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x + p0 * a.x_stride + a.x_off), (short)0, np * a.x_stride * 4, 0x00020000);
+#pragma unroll
+    for (int it = 0; it < C::NIT; ++it) {
+      const int off = ipx[it] < np ? ioff[it] * 4 : 0x7fffffff;
+      pv[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(it < NG ? gr : xr, off, 0, 0));
+    }
+  };
+  auto store = [&](__bf16* buf) {
+#pragma unroll
+    for (int it = 0; it < C::NIT; ++it) {
+      const int o = ilds[it];
+      unsigned h0, m0, l0, h1, m1, l1;
+      split3x2(pv[it][0], pv[it][1], h0, m0, l0);
+      split3x2(pv[it][2], pv[it][3], h1, m1, l1);
+      typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2_t*>(buf + o) = u32x2_t{h0, h1};
+      *reinterpret_cast<u32x2_t*>(buf + o + C::PL) = u32x2_t{m0, m1};
+      *reinterpret_cast<u32x2_t*>(buf + o + 2 * C::PL) = u32x2_t{l0, l1};
+    }
+  };
+  // lane 4q+p of group lg: row 8lg + 4t + q, columns 4p .. 4p+3 of its block (see k_wgrad3p)
+  const int abase = (8 * lg + (li >> 2)) * C::C + 4 * (li & 3);
+  const int aflip = lg & 1;
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+
+  if (u_beg < u_end) {
+    load(u_beg);
+    store(lds);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own plane writes done
+  __syncthreads();
+#pragma unroll 1
+  for (long u = u_beg; u < u_end; ++u) {
+    const int cb = (int)((u - u_beg) & 1);
+    const __bf16* buf = lds + cb * C::BUF;
+    const bool more = u + 1 < u_end;
+    if (more) load(u + 1);  // in flight during this stage's MFMAs
+    int aoff = abase;
+    asm volatile("" : "+v"(aoff));
+    bf16x8 av[3][3], bv[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int oa = aoff + (((3 * wm + i) ^ aflip) << 4);
+      const int ob = C::GPL + aoff + (((3 * wn + i) ^ aflip) << 4);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const __bf16* pa = buf + pl * C::PL + oa;
+        const __bf16* pb = buf + pl * C::PL + ob;
+        av[pl][i] = tr_frag(pa, pa + 4 * C::C);
+        bv[pl][i] = tr_frag(pb, pb + 4 * C::C);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        // the five corrections chained from zero, the leading product last (k_wgrad3p's fold)
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        f32x4 lo = mfma_bf16(av[0][i], bv[1][j], z);
+        lo = mfma_bf16(av[1][i], bv[0][j], lo);
+        lo = mfma_bf16(av[0][i], bv[2][j], lo);
+        lo = mfma_bf16(av[1][i], bv[1][j], lo);
+        lo = mfma_bf16(av[2][i], bv[0][j], lo);
+        const f32x4 blk = mfma_bf16(av[0][i], bv[0][j], lo);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] + blk[r];
+        asm volatile("" : "+v"(acc[i][j]));
+      }
+    if (do_bias) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 hi = mfma_bf16(av[0][i], ones, z);
+        f32x4 lo = mfma_bf16(av[1][i], ones, z);
+        lo = mfma_bf16(av[2][i], ones, lo);
+        x6_acc_add(accb[i][0], hi, lo);
+      }
+    }
+    if (more) store(lds + (cb ^ 1) * C::BUF);  // (waits for its loads itself)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __syncthreads();  // next buffer complete; everyone done with this one
+  }
+  float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = (3 * wm + i) * 16 + 4 * lg + r, ci = (3 * wn + j) * 16 + li;
+        slab[co * C::C + ci] = acc[i][j][r];
+      }
+  if (do_bias && li == 0) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) slab[C::C * C::C + (3 * wm + i) * 16 + 4 * lg + r] = accb[i][0][r];
+  }
+}
+
+// 96 -> 96 1x1, NHWC views with 16-byte aligned pixels (g / x stride and offset % 4 == 0)
+bool wgrad1p_ok(const WgradArgs& a) {
+  if (a.Cout != 96 || a.Cin != 96 || a.zc > 0) return false;
+  if ((a.g_stride | a.g_off | a.x_stride | a.x_off) & 3) return false;
+  return a.g_off + 96 <= a.g_stride && a.x_off + 96 <= a.x_stride &&
+         32L * a.g_stride * 4 < 0x7fffffffL && 32L * a.x_stride * 4 < 0x7fffffffL;
+}
+
+// k_wgrad1p over `splits` slab rows of [W (co, ci) | b] (a.slab, a.slab_stride >= 96*96 + 96)
+hipError_t launch_wgrad1p(const WgradArgs& a, int splits, hipStream_t s) {
+  if (!wgrad1p_ok(a) || splits < 1 || a.slab_stride < 96 * 96 + 96) return hipErrorInvalidValue;
+  prof_kernel("k_wgrad1p");
+  hipLaunchKernelGGL(k_wgrad1p, dim3(splits), dim3(256), 0, s, a, (long)a.N * a.KH * a.KW);
+  return hipGetLastError();
+}
+
 }  // namespace dn
