@@ -1429,15 +1429,16 @@ hipError_t launch_wgrad1(int mode, const WgradArgs& a0, float* dwb, hipStream_t 
   a.slab_stride = row;
   a.wlayout = up2 ? 1 : 0;  // deconv weight (in, out, 2, 2): [ci][co] per parity
   const dim3 grid(sp, 1, z);
-  if (x6 && !up2 && wgrad1p_ok(a)) {
-    const hipError_t e = launch_wgrad1p(a, sp, s);
-    return e != hipSuccess ? e : launch_reduce(a.slab, row, sp, row, dwb, s, rb);
+  hipError_t e;
+  if (x6 && wgrad1p_ok(a)) {
+    e = launch_wgrad1p(a, sp, s, up2);
+  } else {
+    if (a.Cout == 96)
+      hipLaunchKernelGGL((k_wgrad1<6, 6, 2, 2>), grid, dim3(256), 0, s, a, (int)up2);
+    else
+      hipLaunchKernelGGL((k_wgrad1<3, 3, 1, 3>), grid, dim3(192), 0, s, a, (int)up2);
+    e = hipGetLastError();
   }
-  if (a.Cout == 96)
-    hipLaunchKernelGGL((k_wgrad1<6, 6, 2, 2>), grid, dim3(256), 0, s, a, (int)up2);
-  else
-    hipLaunchKernelGGL((k_wgrad1<3, 3, 1, 3>), grid, dim3(192), 0, s, a, (int)up2);
-  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (!up2) return launch_reduce(a.slab, row, sp, row, dwb, s, rb);
   // W[ci][co][a][b] in output order: element e = 4 (ci*Cout + co) + ab lives in parity ab's

@@ -318,7 +318,7 @@ hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s);
 bool wgrad3p_ok(const WgradArgs& a);
 hipError_t launch_wgrad3p(const WgradArgs& a, int splits, hipStream_t s, int nz);
 bool wgrad1p_ok(const WgradArgs& a);  // 96 -> 96 1x1 on k_wgrad1p (bf16x6)
-hipError_t launch_wgrad1p(const WgradArgs& a, int splits, hipStream_t s);
+hipError_t launch_wgrad1p(const WgradArgs& a, int splits, hipStream_t s, bool up2 = false);
 bool wgrad1_ok(int mode, const WgradArgs& a);
 long wgrad_slab_floats(int mode, int N, int KH, int KW, int cin, int cout);
 hipError_t launch_wgrad1(int mode, const WgradArgs& a, float* dwb, hipStream_t s,

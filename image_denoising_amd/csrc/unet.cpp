@@ -977,7 +977,7 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     // deconv wgrad: x = d_l b (level l), dU at level l-1
     DN_TRY(fork());
     DN_TRY(wgrad(W_UP2, dU, V(p.db[l], 2 * nf), N, H(l), Wd(l), 2 * nf, 2 * nf, G(iu), SL(iu),
-                 p.splits[iu], s2, false, Z, &rb));
+                 p.splits[iu], s2, x6, Z, &rb));
     DN_TRY(deconv_dgrad(dU, N, H(l), Wd(l), 2 * nf, iu, 2 * nf, V(p.db[l], 2 * nf), EPI_MASK,
                         V(p.g_db[l], 2 * nf), s));
     const int ia = da_idx[l], ib = ia + 1;

@@ -364,8 +364,11 @@ hipError_t launch_wgrad3p(const WgradArgs& a, int splits, hipStream_t s, int nz)
 }
 
 // ------------------------------------------------------------------------------------
-// 1x1 weight gradient of the 96 x 96 head layers (nin_a, nin_b: arch_unet.py:186-189) in the
-// same arithmetic (k_wgrad1p; k_wgrad1 does them on the fp32 matrix cores).  K = pixels of the
+// 1x1 weight gradient of the 96 x 96 head layers (nin_a, nin_b: arch_unet.py:186-189) and of
+// the 96-channel deconvs (UP2: UpsampleCat's ConvTranspose2d(2, 2), arch_unet.py:57) in the
+// same arithmetic (k_wgrad1p; k_wgrad1 does them on the fp32 matrix cores).  UP2: blockIdx.z =
+// parity (a, b); the gradient operand of low-res pixel (y, x) is g at (2y + a, 2x + b), so its
+// rows are gathered per pixel (64-bit addresses, plain loads) while x stays a flat range.  K = pixels of the
 // flattened N x H x W range (a 1x1 conv has no halo), 32 per stage: G [32 px][96 co] and X
 // [32 px][96 ci] split once into three bf16 planes of the stage buffer, the next stage's fp32
 // operands in registers meanwhile, one barrier per stage.  Wave (wm, wn): output channels
@@ -382,6 +385,7 @@ struct Wp1Cfg {
   static_assert(2 * BUF * 2 <= 81920, "two workgroups per CU");
 };
 
+template <bool UP2>
 __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
   using C = Wp1Cfg;
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * C::BUF];
@@ -412,6 +416,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
     ilds[it] = (it < NG ? 0 : C::GPL) + wp_idx(px, C::C, c >> 4) + (c & 15);
   }
   f32x4 pv[C::NIT];
+  const int pa = UP2 ? (int)(blockIdx.z >> 1) : 0, pb = UP2 ? (int)(blockIdx.z & 1) : 0;
   auto load = [&](long u) {
     const long p0 = u * C::PX;
     const int np = npx - p0 < C::PX ? (int)(npx - p0) : C::PX;
@@ -421,6 +426,14 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
         const_cast<float*>(a.x + p0 * a.x_stride + a.x_off), (short)0, np * a.x_stride * 4, 0x00020000);
 #pragma unroll
     for (int it = 0; it < C::NIT; ++it) {
+      if (UP2 && it < NG) {  // low-res pixel p -> g pixel (2y + a, 2x + b) of its image
+        const long p = p0 + ipx[it], r = p / a.KW;  // r = n KH + y
+        const int xx = (int)(p - r * a.KW);
+        const float* src = a.g + ((2 * r + pa) * 2 * a.KW + 2 * xx + pb) * a.g_stride + a.g_off +
+                           (ioff[it] - ipx[it] * a.g_stride);
+        pv[it] = ipx[it] < np ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
+        continue;
+      }
       const int off = ipx[it] < np ? ioff[it] * 4 : 0x7fffffff;
       pv[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(it < NG ? gr : xr, off, 0, 0));
     }
@@ -502,7 +515,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __syncthreads();  // next buffer complete; everyone done with this one
   }
-  float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
+  // slab row (UP2: parity z's block of gridDim.x rows, the deconv layout [ci][co])
+  float* slab = a.slab + ((long)blockIdx.z * gridDim.x + blockIdx.x) * a.slab_stride;
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -510,7 +524,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = (3 * wm + i) * 16 + 4 * lg + r, ci = (3 * wn + j) * 16 + li;
-        slab[co * C::C + ci] = acc[i][j][r];
+        slab[UP2 ? ci * C::C + co : co * C::C + ci] = acc[i][j][r];
       }
   if (do_bias && li == 0) {
 #pragma unroll
@@ -528,11 +542,18 @@ bool wgrad1p_ok(const WgradArgs& a) {
          32L * a.g_stride * 4 < 0x7fffffffL && 32L * a.x_stride * 4 < 0x7fffffffL;
 }
 
-// k_wgrad1p over `splits` slab rows of [W (co, ci) | b] (a.slab, a.slab_stride >= 96*96 + 96)
-hipError_t launch_wgrad1p(const WgradArgs& a, int splits, hipStream_t s) {
+// k_wgrad1p over `splits` slab rows of [W (co, ci) | b] (a.slab, a.slab_stride >= 96*96 + 96);
+// up2: 4 x splits rows of [W (ci, co) | b], parity-major (a.KH x a.KW = the low-res input)
+hipError_t launch_wgrad1p(const WgradArgs& a, int splits, hipStream_t s, bool up2) {
   if (!wgrad1p_ok(a) || splits < 1 || a.slab_stride < 96 * 96 + 96) return hipErrorInvalidValue;
-  prof_kernel("k_wgrad1p");
-  hipLaunchKernelGGL(k_wgrad1p, dim3(splits), dim3(256), 0, s, a, (long)a.N * a.KH * a.KW);
+  const long npx = (long)a.N * a.KH * a.KW;
+  if (up2) {
+    prof_kernel("k_wgrad1p<up2>");
+    hipLaunchKernelGGL(k_wgrad1p<true>, dim3(splits, 1, 4), dim3(256), 0, s, a, npx);
+  } else {
+    prof_kernel("k_wgrad1p");
+    hipLaunchKernelGGL(k_wgrad1p<false>, dim3(splits), dim3(256), 0, s, a, npx);
+  }
   return hipGetLastError();
 }
 
