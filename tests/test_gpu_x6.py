@@ -125,6 +125,9 @@ def _dgrad(dz, w, cin, mode, mask, base, x6):
     # ... on large grids: K = 32 data gradients into 80 / 112 / 144 channels (48-channel blocks,
     # a partial last one) and 72 -> 24
     (80, 32, 8, 128, 128), (112, 32, 8, 128, 128), (144, 32, 8, 128, 128), (72, 24, 8, 128, 128),
+    # ImprovedUNet's wide levels on grids over the Winograd threshold: data gradients into 192 /
+    # 384 channels in 96-channel output blocks (blockIdx.z, the per-block image stride)
+    (192, 96, 8, 64, 64), (384, 96, 4, 64, 64), (192, 192, 8, 64, 64),
 ])
 @pytest.mark.parametrize("mode", ["plain", "mask", "accum"])
 def test_x6_backward_data_vs_fp64(cin, cout, N, H, W, mode):
