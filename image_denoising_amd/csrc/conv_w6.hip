@@ -70,6 +70,15 @@ __device__ __forceinline__ int w6_vq(int row, int kq, int j, int p) {
 #endif
 }
 
+// 8-B slot of V element (row, j, p) of a tail-mode-1 chunk (<= 4 channels: one bf16x4 per
+// plane): p XOR-swizzled by row & 3, so the transform's 16-lane writes (two rows x 8 tiles) and
+// the stage's 8-B reads (a half-wave: four rows x 8 tiles) fall on distinct banks.  (In the
+// quad layout above these were 2- and 4-way conflicts: k_c3w6<1> 24 % of its LDS-active cycles
+// against 7 % for the kernels without this chunk.)
+__device__ __forceinline__ int w6_vt(int row, int j, int p) {
+  return (row * 8 + j) * 4 + (p ^ (row & 3));
+}
+
 __device__ __forceinline__ void w6_barrier() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   __builtin_amdgcn_s_barrier();
@@ -182,7 +191,8 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
           unsigned h0, m0, l0, h1, m1, l1;
           split3x2(v[p][0], v[p][1], h0, m0, l0);
           split3x2(v[p][2], v[p][3], h1, m1, l1);
-          const int o = w6_vq(row, c4 >> 1, j, p) * 8 + (c4 & 1) * 4;  // bf16 index in a plane
+          // bf16 index in a plane (tail mode 1: the 8-B slot layout w6_vt)
+          const int o = C4 == 1 ? w6_vt(row, j, p) * 4 : w6_vq(row, c4 >> 1, j, p) * 8 + (c4 & 1) * 4;
           typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
           *reinterpret_cast<u32x2_t*>(lv + o) = u32x2_t{h0, h1};
           *reinterpret_cast<u32x2_t*>(lv + C::VPL + o) = u32x2_t{m0, m1};
@@ -289,8 +299,8 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
       } else if constexpr (MODE == 1) {
         // lane group 0: channels 0..3 of ky 0 and 1; group 1: ky 2 and zeros; 2, 3: zeros
         const int ka = 2 * lgv, kb = ka + 1;
-        const int oa = w6_vq(row0 + (ka < 3 ? ka : 0), 0, j, p) * 8;
-        const int ob = w6_vq(row0 + (kb < 3 ? kb : 0), 0, j, p) * 8;
+        const int oa = w6_vt(row0 + (ka < 3 ? ka : 0), j, p) * 4;
+        const int ob = w6_vt(row0 + (kb < 3 ? kb : 0), j, p) * 4;
         const bf16x4 z4 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) {
