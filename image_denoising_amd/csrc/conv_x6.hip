@@ -1202,9 +1202,9 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
       for (int q = 0; q < NT; ++q)
         *reinterpret_cast<f32x4*>(part + ((long)kk * NF + m * NT + q) * 1024 + tid * 4) = acc[m][q];
     __threadfence();  // this thread's partials visible device-wide before the ticket
-    x6_barrier();
+    __syncthreads();
     if (tid == 0) ks_last = atomicAdd(a.ks_cnt + tl, 1u) == (unsigned)(ks - 1);
-    x6_barrier();
+    __syncthreads();  // (a full barrier: waits for wave 0's LDS write, unlike x6_barrier)
     if (!ks_last) return;  // (uniform) another split finishes the tile
     __threadfence();       // acquire: every split's partials
 #pragma unroll
