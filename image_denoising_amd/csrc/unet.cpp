@@ -206,7 +206,7 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
       }
       p.packB[i] = alloc_f(n);
     }
-    p.packHB = alloc_f(2 * HEAD_LW);
+    p.packHB = alloc_f(2 * HEAD_LW > X6_HEAD_BF ? 2 * HEAD_LW : X6_HEAD_BF);  // fp32 | bf16x6 (Wb^T | Wa^T)
     for (int i = 0; i < NL; ++i)  // 4 x X6_HEAD_BF bf16 per 96-channel deconv
       p.packUXB[i] = p.packUX[i] >= 0 ? alloc_f(2 * X6_HEAD_BF) : -1;
     for (int i = 0; i < NL; ++i) {  // bf16x6 data-gradient images of the 3x3 layers
