@@ -1192,28 +1192,33 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
   }
   x6_fold(acc, accl);
   if (ks > 1) {
-    // partial sums of split kk: [tile][split][fragment][lane] f32x4, coalesced per fragment
-    constexpr int NF = MT * NT;
+    // partial sums of split kk: [tile][split][fragment][lane] f32x4, coalesced per fragment.
+    // Stored and loaded with sc0 sc1 (system-coherent: through the L2s to memory), so the
+    // ticket needs only the stores' completion, not an agent-scope fence -- whose L2 write-back
+    // and invalidate made every split launch 3-6x slower (profiles/r4_splitk_ab.log).
+    constexpr int NF = MT * NT, SC = 1 | 16;  // cache policy: sc0 | sc1
     const long tl = ((long)blockIdx.z * gridDim.y + n) * (gridDim.x / ks) + tile;
-    float* part = a.ks_part + tl * ks * (NF * 1024L);
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        a.ks_part + tl * ks * (NF * 1024L), (short)0, ks * NF * 1024 * 4, 0x00020000);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int q = 0; q < NT; ++q)
-        *reinterpret_cast<f32x4*>(part + ((long)kk * NF + m * NT + q) * 1024 + tid * 4) = acc[m][q];
-    __threadfence();  // this thread's partials visible device-wide before the ticket
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[m][q]), prs,
+                                               ((kk * NF + m * NT + q) * 1024 + tid * 4) * 4, 0, SC);
+    X6_WAITCNT_VM(0);  // this thread's partials written through before the ticket
     __syncthreads();
     if (tid == 0) ks_last = atomicAdd(a.ks_cnt + tl, 1u) == (unsigned)(ks - 1);
     __syncthreads();  // (a full barrier: waits for wave 0's LDS write, unlike x6_barrier)
     if (!ks_last) return;  // (uniform) another split finishes the tile
-    __threadfence();       // acquire: every split's partials
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
-        const float* pq = part + (m * NT + q) * 1024 + tid * 4;
-        f32x4 v = *reinterpret_cast<const f32x4*>(pq);
-        for (int k = 1; k < ks; ++k) v += *reinterpret_cast<const f32x4*>(pq + (long)k * NF * 1024);
+        const int o = ((m * NT + q) * 1024 + tid * 4) * 4;
+        f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, o, 0, SC));
+        for (int k = 1; k < ks; ++k)
+          v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, o + k * NF * 4096, 0, SC));
         acc[m][q] = v;
       }
     if (tid == 0) atomicExch(a.ks_cnt + tl, 0u);  // the ticket for the next launch
@@ -1240,15 +1245,18 @@ static hipError_t run_x6h(const FwdArgs& a, int nz, hipStream_t s) {
 
 // small grids (below one round of 16 x 16 tiles), plain image: the 3-slot ring, and where the
 // caller gave split-K space (a.ks_part / a.ks_cnt) the stages split over ks workgroups so that
-// 8-row tiles x ks fill one round of two workgroups per CU, at least 3 stages per split, ks <= 8
-// (DN_X6_SPLITK=0: no split; =k: at most k).  ks follows from the shape alone, not from MT: the
+// 8-row tiles x ks fill one round of two workgroups per CU, at least 3 stages per split, ks <= k
+// for DN_X6_SPLITK=k (default 0: no split, measured faster).  ks follows from the shape alone, not from MT: the
 // MT = 1 and MT = 2 launches of one shape (a fused pool takes MT = 2) split the stages alike and
 // so stay bit-identical, as without the split.
+#ifndef DN_X6_SPLITK_DEFAULT
+#define DN_X6_SPLITK_DEFAULT 0  // off until a split measures faster (profiles/r4_splitk_ab.log)
+#endif
 template <int NT, int MT>
 static hipError_t run_x6h3(const FwdArgs& a0, int nz, hipStream_t s) {
   using C = HCfg<NT, MT, 3>;
   static_assert(MT * NT * 1024 <= kSplitFloats, "split-K partial size");
-  static const int ks_env = getenv("DN_X6_SPLITK") ? atoi(getenv("DN_X6_SPLITK")) : 8;
+  static const int ks_env = getenv("DN_X6_SPLITK") ? atoi(getenv("DN_X6_SPLITK")) : DN_X6_SPLITK_DEFAULT;
   const int tx = (a0.OW + C::TW - 1) / C::TW, ty = (a0.OH + C::TH - 1) / C::TH;
   const long tiles = (long)tx * ty * a0.N * nz;
   const long tiles8 = (long)((a0.OW + 15) / 16) * ((a0.OH + 7) / 8) * a0.N * nz;

@@ -200,20 +200,20 @@ def test_small_grid_ring_step_equals_single_stage_prefetch(tmp_path):
 
 
 def test_small_grid_split_k_matches_unsplit(tmp_path):
-    """The small-grid 3x3 launches with their stages split over up to 8 workgroups (default:
-    partial sums added by the last split in split order) against one workgroup per tile
-    (DN_X6_SPLITK=0), 8 x 128^2 (levels 4^2-32^2 split): the same products summed in a different
-    association, so outputs and parameter gradients agree to fp32 rounding (2e-5 of the max
-    magnitude, as the Winograd test below; dL/dx by scale only, see there).  The split is
-    deterministic: a second run of the N2N step is bit-identical whatever order the splits
-    arrive in."""
-    sk = _worker_env_run(tmp_path, "splitk", {}, "grad")
-    one = _worker_env_run(tmp_path, "nosplit", {"DN_X6_SPLITK": "0"}, "grad")
+    """The small-grid 3x3 launches with their stages split over up to 8 workgroups
+    (DN_X6_SPLITK=8; off by default: slower) against one workgroup per tile
+    (default), 8 x 128^2 (levels 4^2-32^2 split): the same products summed in a different
+    association (partial sums added by the last split in split order), so outputs and
+    parameter gradients agree to fp32 rounding (2e-5 of the max magnitude, as the Winograd test
+    below; dL/dx by scale only, see there).  The split is deterministic: a second run of the
+    N2N step is bit-identical whatever order the splits arrive in."""
+    sk = _worker_env_run(tmp_path, "splitk", {"DN_X6_SPLITK": "8"}, "grad")
+    one = _worker_env_run(tmp_path, "nosplit", {}, "grad")
     for k, tol in (("y", 2e-5), ("g", 2e-5), ("dx", 5e-2)):
         a, b = sk[k], one[k]
         assert np.abs(a - b).max() <= tol * np.abs(a).max(), (k, np.abs(a - b).max())
-    r1 = _worker_env_run(tmp_path, "splitk_a", {}, "local")
-    r2 = _worker_env_run(tmp_path, "splitk_b", {}, "local")
+    r1 = _worker_env_run(tmp_path, "splitk_a", {"DN_X6_SPLITK": "8"}, "local")
+    r2 = _worker_env_run(tmp_path, "splitk_b", {"DN_X6_SPLITK": "8"}, "local")
     for k in ("losses", "grad", "flat"):
         assert np.array_equal(r1[k], r2[k]), k
 
