@@ -954,18 +954,12 @@ struct HCfg {
 #define DN_X6H_PIN 0  // A/B switch: 1 = MT = 2's hi adds pinned per group (100->96 @256^2: 1-2 % slower)
 #endif
 // S_ = 3 (small grids, MT = 1): a 3-slot weight ring, stage st + 2 requested at the start of st,
-// so a stage waits on neither the L2 latency of its weights nor that of the next stage's.
-// With a.ks > 1 (S_ = 3 only) a tile's stages are split over ks workgroups (grid.x = tiles x
-// ks): below one round of tiles the serial chain of 18-45 stages per workgroup, not the
-// arithmetic, is the launch's time.  Each split writes its fp32 partial sums to a.ks_part; the
-// last to arrive (a ticket in a.ks_cnt) adds the ks partials in split order -- the same sums
-// whatever the arrival order -- and runs the epilogue.
+// so a stage waits on neither the L2 latency of its weights nor that of the next stage's
 template <int NT, int TAIL, int MT_ = 2, int S_ = 2>
 __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
   using C = HCfg<NT, MT_, S_>;
   constexpr int MT = C::MT;
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
-  __shared__ unsigned ks_last;
   __bf16* lx = reinterpret_cast<__bf16*>(lds_raw);
   __bf16* ring = lx + 3 * C::XPL;
 
@@ -975,10 +969,8 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
   int bxr, byr;  // XCD-aware tile order (conv_epi.h xcd_tile)
   xcd_tile(bxr, byr);
-  const int ks = C::S == 3 && a.ks > 1 ? a.ks : 1;
-  const int kk = bxr % ks, tile = bxr / ks;  // split kk of tile `tile`
-  const int ty0 = (tile / tiles_x) * C::TH;
-  const int tx0 = (tile % tiles_x) * C::TW;
+  const int ty0 = (bxr / tiles_x) * C::TH;
+  const int tx0 = (bxr % tiles_x) * C::TW;
   const int n = byr;
   const int iy0 = ty0 - 1, ix0 = tx0 - 1;
   const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
@@ -987,8 +979,6 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
   constexpr int tail = TAIL;
   constexpr int tail_st = tail == 1 ? 2 : 5;
   const int nst = 9 * nch - (tail ? 9 - tail_st : 0);
-  // this workgroup's stages [st_lo, st_hi) (all of them without a split)
-  const int st_lo = kk * nst / ks, st_hi = (kk + 1) * nst / ks, c_lo = st_lo / 9;
 
   f32x4 acc[MT][NT], accl[MT][NT];
 #pragma unroll
@@ -1058,24 +1048,22 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
     }
   };
 
-  // prologue: the first S - 1 stages' weights (L2) and the first chunk's x tile (HBM) in flight
-  // together
+  // prologue: the first S - 1 stages' weights (L2) and chunk 0's x tile (HBM) in flight together
 #pragma unroll
-  for (int j = 0; j + 1 < C::S; ++j) load_w(st_lo + j < st_hi ? st_lo + j : st_hi - 1, (st_lo + j) % C::S);
-  load_x(c_lo * C::KC);
+  for (int j = 0; j + 1 < C::S; ++j) load_w(j < nst ? j : nst - 1, j);
+  load_x(0);
   store_x();                           // waits for the x loads (and the older DMA)
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
   x6_barrier();
 
   auto stage = [&](int c, int t) {
-    const bool more = 9 * (c + 1) < st_hi;     // the next chunk has stages of this workgroup
-    const int tf = c == c_lo ? st_lo - 9 * c : 0;  // this chunk's first stage here
+    const bool more = c + 1 < nch;
     const int st = 9 * c + t;
     const __bf16* lw = ring + (st % C::S) * C::WST;
     // stage st+S-1's weights into the slot of stage st-1 (every wave left it at the last
     // barrier); past the end a re-load of the last stage
-    load_w(st + C::S - 1 < st_hi ? st + C::S - 1 : st_hi - 1, (st + C::S - 1) % C::S);
-    if (t == tf && more) load_x((c + 1) * C::KC);  // the next chunk, after this stage's DMA
+    load_w(st + C::S - 1 < nst ? st + C::S - 1 : nst - 1, (st + C::S - 1) % C::S);
+    if (t == 0 && more) load_x((c + 1) * C::KC);  // the next chunk, after this stage's DMA
     const int mode = (tail && c + 1 == nch) ? tail : 0;
     // MT = 4: the A pieces of two rows at a time (registers), the B fragments read once for all
     constexpr int MH = MT >= 4 ? 2 : MT;
@@ -1174,55 +1162,22 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
     // loads while they were issued after it (t <= S-2); after the last stage none in flight
     // (the epilogue reuses the ring)
     if constexpr (C::S == 2) {
-      if (t == tf && more) X6_WAITCNT_VM(C::XITEMS);
+      if (t == 0 && more) X6_WAITCNT_VM(C::XITEMS);
       else X6_WAITCNT_VM(0);
     } else {
-      if (st + 1 == st_hi) X6_WAITCNT_VM(0);
-      else if (t - tf <= C::S - 2 && more) X6_WAITCNT_VM((C::S - 2) * C::PPW + C::XITEMS);
+      if (st + 1 == nst) X6_WAITCNT_VM(0);
+      else if (t <= C::S - 2 && more) X6_WAITCNT_VM((C::S - 2) * C::PPW + C::XITEMS);
       else X6_WAITCNT_VM((C::S - 2) * C::PPW);
     }
     if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
     x6_barrier();
   };
-  for (int c = c_lo; 9 * c < st_hi; ++c) {
+  for (int c = 0; c < nch; ++c) {
     const int ns = (tail && c + 1 == nch) ? tail_st : 9;
-    const int t1 = st_hi - 9 * c < ns ? st_hi - 9 * c : ns;
 #pragma unroll 1
-    for (int t = c == c_lo ? st_lo - 9 * c : 0; t < t1; ++t) stage(c, t);
+    for (int t = 0; t < ns; ++t) stage(c, t);
   }
   x6_fold(acc, accl);
-  if (ks > 1) {
-    // partial sums of split kk: [tile][split][fragment][lane] f32x4, coalesced per fragment.
-    // Stored and loaded with sc0 sc1 (system-coherent: through the L2s to memory), so the
-    // ticket needs only the stores' completion, not an agent-scope fence -- whose L2 write-back
-    // and invalidate made every split launch 3-6x slower (profiles/r4_splitk_ab.log).
-    constexpr int NF = MT * NT, SC = 1 | 16;  // cache policy: sc0 | sc1
-    const long tl = ((long)blockIdx.z * gridDim.y + n) * (gridDim.x / ks) + tile;
-    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-        a.ks_part + tl * ks * (NF * 1024L), (short)0, ks * NF * 1024 * 4, 0x00020000);
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int q = 0; q < NT; ++q)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[m][q]), prs,
-                                               ((kk * NF + m * NT + q) * 1024 + tid * 4) * 4, 0, SC);
-    X6_WAITCNT_VM(0);  // this thread's partials written through before the ticket
-    __syncthreads();
-    if (tid == 0) ks_last = atomicAdd(a.ks_cnt + tl, 1u) == (unsigned)(ks - 1);
-    __syncthreads();  // (a full barrier: waits for wave 0's LDS write, unlike x6_barrier)
-    if (!ks_last) return;  // (uniform) another split finishes the tile
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int q = 0; q < NT; ++q) {
-        const int o = ((m * NT + q) * 1024 + tid * 4) * 4;
-        f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, o, 0, SC));
-        for (int k = 1; k < ks; ++k)
-          v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, o + k * NF * 4096, 0, SC));
-        acc[m][q] = v;
-      }
-    if (tid == 0) atomicExch(a.ks_cnt + tl, 0u);  // the ticket for the next launch
-  }
   fwd_epilogue<NT, MT, C::PS, false>(a, acc, reinterpret_cast<float*>(lds_raw), ty0, tx0, n);
 }
 
@@ -1243,36 +1198,14 @@ static hipError_t run_x6h(const FwdArgs& a, int nz, hipStream_t s) {
   return hipGetLastError();
 }
 
-// small grids (below one round of 16 x 16 tiles), plain image: the 3-slot ring, and where the
-// caller gave split-K space (a.ks_part / a.ks_cnt) the stages split over ks workgroups so that
-// 8-row tiles x ks fill one round of two workgroups per CU, at least 3 stages per split, ks <= k
-// for DN_X6_SPLITK=k (default 0: no split, measured faster).  ks follows from the shape alone, not from MT: the
-// MT = 1 and MT = 2 launches of one shape (a fused pool takes MT = 2) split the stages alike and
-// so stay bit-identical, as without the split.
-#ifndef DN_X6_SPLITK_DEFAULT
-#define DN_X6_SPLITK_DEFAULT 0  // off until a split measures faster (profiles/r4_splitk_ab.log)
-#endif
+// small grids (below one round of 16 x 16 tiles), plain image: the 3-slot ring
 template <int NT, int MT>
-static hipError_t run_x6h3(const FwdArgs& a0, int nz, hipStream_t s) {
+static hipError_t run_x6h3(const FwdArgs& a, int nz, hipStream_t s) {
   using C = HCfg<NT, MT, 3>;
-  static_assert(MT * NT * 1024 <= kSplitFloats, "split-K partial size");
-  static const int ks_env = getenv("DN_X6_SPLITK") ? atoi(getenv("DN_X6_SPLITK")) : DN_X6_SPLITK_DEFAULT;
-  const int tx = (a0.OW + C::TW - 1) / C::TW, ty = (a0.OH + C::TH - 1) / C::TH;
-  const long tiles = (long)tx * ty * a0.N * nz;
-  const long tiles8 = (long)((a0.OW + 15) / 16) * ((a0.OH + 7) / 8) * a0.N * nz;
-  const int nst = 9 * ((a0.K + C::KC - 1) / C::KC);
-  FwdArgs a = a0;
-  a.ks = 1;
-  if (a.ks_part && a.ks_cnt && tiles8 <= 256) {
-    int ks = (int)(512 / tiles8);
-    if (ks > nst / 3) ks = nst / 3;
-    if (ks > ks_env) ks = ks_env;
-    if (ks > 1 && tiles * ks <= kSplitSlots) a.ks = ks;
-  }
+  const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
   static const std::string kn = x6_kmore(x6_kname("k_c3x6h", NT, 0, MT), "3");
-  static const std::string knk = x6_kmore(kn, "ks");
-  prof_kernel(a.ks > 1 ? knk.c_str() : kn.c_str());
-  hipLaunchKernelGGL((k_c3x6h<NT, 0, MT, 3>), dim3(tx * ty * a.ks, a.N, nz), dim3(C::WAVES * 64), 0, s, a);
+  prof_kernel(kn.c_str());
+  hipLaunchKernelGGL((k_c3x6h<NT, 0, MT, 3>), dim3(tx * ty, a.N, nz), dim3(C::WAVES * 64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -107,13 +107,7 @@ struct FwdArgs {
   // mixed-precision bf16 forward (conv_bf16.hip): the input / output activations are stored as
   // bf16 (RNE of the fp32 value; strides and offsets in elements) instead of fp32
   int in_bf16, out_bf16;
-  // small-grid split-K (k_c3x6h with the 3-slot ring): the stages of a tile split over ks
-  // workgroups; each writes its fp32 partial sums to ks_part, the last to arrive (ticket in
-  // ks_cnt[tile], reset by it) adds them in split order and runs the epilogue.  ks <= 1: off
-  float* ks_part; unsigned* ks_cnt; int ks;
 };
-constexpr int kSplitSlots = 1024;          // tiles x splits of one split-K launch, at most
-constexpr int kSplitFloats = 256 * 6 * 4;  // fp32 partial of one workgroup (256 lanes x 6 f32x4)
 
 // Fused output head (arch_unet.py:186-190, 253-257): the dec_conv1b kernel keeps its
 // 96-channel tile in registers and runs nin_a -> nin_b -> nin_c on it.

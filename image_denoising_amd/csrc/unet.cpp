@@ -174,8 +174,6 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
     p.w6s_list = alloc_f(2L * N * (H / 2) * (W / 2));
     p.w6s_cnt = alloc_f(2L * N);
   }
-  p.ks_part = alloc_f((long)kSplitSlots * kSplitFloats);
-  p.ks_cnt = alloc_f(kSplitSlots);
   p.fwd_floats = off;
   if (bwd) {
     p.g_nb = alloc(0, 96);
@@ -477,9 +475,6 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
         a.pool_out = pool->p; a.pool_stride = pool->stride; a.pool_off = pool->off;
         if (pooled) *pooled = true;
       }
-      // (not dec_conv1b: the pair pass computes it per pixel pair with the unsplit sums, and
-      // small test grids compare the two bit for bit)
-      if (i != D1B) { a.ks_part = ws + p.ks_part; a.ks_cnt = reinterpret_cast<unsigned*>(ws + p.ks_cnt); }
       return launch_fwd_x6(a, st);
     }
     if (!bf16 || i == NL || p.packBF[i] < 0)
@@ -585,7 +580,6 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     DN_TRY(launch_pack_head(conv_fwd_view(prm + p.P.L[NINA].woff, 96, 1),
                             conv_fwd_view(prm + p.P.L[NINB].woff, 96, 1), ws + p.packH, s, &pb));
   }
-  if (x6) DN_TRY(add(true, pack_job_zero(ws + p.ks_cnt, kSplitSlots)));  // split-K tickets
   {
     const OpTimer timer(s, "pack", 0);
     DN_TRY(pack_flush(pb, s));
@@ -887,7 +881,6 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     a.out = dx.p; a.out_stride = dx.stride; a.out_off = dx.off; a.out_layout = OUT_NHWC;
     a.mask = mask.p; a.mask_stride = mask.stride; a.mask_off = mask.off;
     a.x6_tail = x6_tail_b(i);
-    a.ks_part = ws + p.ks_part; a.ks_cnt = reinterpret_cast<unsigned*>(ws + p.ks_cnt);
     return launch_fwd_x6(a, st);
   };
   const View none{nullptr, 0, 0};

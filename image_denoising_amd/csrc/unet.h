@@ -47,9 +47,6 @@ struct Plan {
   // tap-transposed PK_W6 image (y tiles) and the per-orientation cell lists (2 N cells uint32)
   // with their counts (2 N int); -1 in plans with a backward
   long packXV, w6s_list, w6s_cnt;
-  // split-K space of the small-grid 3x3 launches (forward and data gradients, one stream):
-  // kSplitSlots partials of kSplitFloats, and kSplitSlots tickets zeroed by every forward's pack
-  long ks_part, ks_cnt;
   long fwd_floats;
   // gradients
   long g_nb, g_na, g_d1b, g_d1a, g_c1;

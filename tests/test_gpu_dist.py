@@ -169,7 +169,7 @@ def _worker_env_run(tmp_path, tag, extra, mode, prec="fp32_x6", shape="8,128,128
     encoder the pipelined kernels with the fused pool)"""
     out = str(tmp_path / f"{tag}.npz")
     env = dict(os.environ, PYTHONUNBUFFERED="1", DPW_SHAPE=shape, **extra)
-    for k in ("DN_POOL_FUSE", "DN_X6_W6", "DN_X6_RING3", "DN_W6_MIN_TILES", "DN_X6_SPLITK"):
+    for k in ("DN_POOL_FUSE", "DN_X6_W6", "DN_X6_RING3", "DN_W6_MIN_TILES"):
         if k not in extra:
             env.pop(k, None)
     p = subprocess.run([sys.executable, os.path.join(HERE, "dp_worker.py"), out, prec, mode],
@@ -191,31 +191,11 @@ def test_fused_pool_step_equals_separate_pool(tmp_path):
 def test_small_grid_ring_step_equals_single_stage_prefetch(tmp_path):
     """Below one round of 16 x 16 tiles (here every level under 64^2 of the 8 x 128^2 step) the
     3x3 convs run on k_c3x6h with a 3-slot weight ring (default) instead of k_c3x6
-    (DN_X6_RING3=0): the same products in the same order, so the N2N step is bit-identical
-    (without the split-K of those launches, tested below)."""
-    ring = _worker_env_run(tmp_path, "ring3", {"DN_X6_SPLITK": "0"}, "local")
+    (DN_X6_RING3=0): the same products in the same order, so the N2N step is bit-identical."""
+    ring = _worker_env_run(tmp_path, "ring3", {}, "local")
     old = _worker_env_run(tmp_path, "noring", {"DN_X6_RING3": "0"}, "local")
     for k in ("losses", "grad", "flat"):
         assert np.array_equal(ring[k], old[k]), k
-
-
-def test_small_grid_split_k_matches_unsplit(tmp_path):
-    """The small-grid 3x3 launches with their stages split over up to 8 workgroups
-    (DN_X6_SPLITK=8; off by default: slower) against one workgroup per tile
-    (default), 8 x 128^2 (levels 4^2-32^2 split): the same products summed in a different
-    association (partial sums added by the last split in split order), so outputs and
-    parameter gradients agree to fp32 rounding (2e-5 of the max magnitude, as the Winograd test
-    below; dL/dx by scale only, see there).  The split is deterministic: a second run of the
-    N2N step is bit-identical whatever order the splits arrive in."""
-    sk = _worker_env_run(tmp_path, "splitk", {"DN_X6_SPLITK": "8"}, "grad")
-    one = _worker_env_run(tmp_path, "nosplit", {}, "grad")
-    for k, tol in (("y", 2e-5), ("g", 2e-5), ("dx", 5e-2)):
-        a, b = sk[k], one[k]
-        assert np.abs(a - b).max() <= tol * np.abs(a).max(), (k, np.abs(a - b).max())
-    r1 = _worker_env_run(tmp_path, "splitk_a", {"DN_X6_SPLITK": "8"}, "local")
-    r2 = _worker_env_run(tmp_path, "splitk_b", {"DN_X6_SPLITK": "8"}, "local")
-    for k in ("losses", "grad", "flat"):
-        assert np.array_equal(r1[k], r2[k]), k
 
 
 def test_winograd_step_matches_direct_kernels(tmp_path):
