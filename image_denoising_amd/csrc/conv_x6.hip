@@ -2017,9 +2017,16 @@ static bool wg_p() {
   return on;
 }
 
+// DN_WG_P48=1/0: the 48-output ones (the encoder) on k_wgrad3p<.., 48> or k_wgrad3s
+static bool wg_p48() {
+  static const bool on = !getenv("DN_WG_P48") || atoi(getenv("DN_WG_P48")) != 0;
+  return on;
+}
+
 hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s) {
   if (!wgrad3_x6_ok(a)) return hipErrorInvalidValue;
   if (a.Cout == 96 && wg_p() && !wg_planes() && wgrad3p_ok(a)) return launch_wgrad3p(a, splits, s, 1);
+  if (a.Cout == 48 && wg_p48() && !wg_planes() && wgrad3p_ok(a)) return launch_wgrad3p(a, splits, s, 1);
   return a.Cout == 96 ? run_wgrad3s<6, 2, 2>(a, splits, s) : run_wgrad3s<3, 1, 3>(a, splits, s);
 }
 

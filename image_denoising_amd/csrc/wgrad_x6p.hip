@@ -44,15 +44,21 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* p0, const __bf16* p1) {
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-template <int SWL>
+// CO = 96: 4 waves (wm, wn) = 48 output channels x 16 of 32 input channels each.  CO = 48 (the
+// encoder's 48 -> 48 layers): 3 waves, wn = 16 of 48 input channels, all 48 outputs; the G and X
+// plane rows are padded to 64 channels (the block flip pairs blocks 2 and 3).
+template <int SWL, int CO = 96>
 struct Wp3Cfg {
-  static constexpr int COUT = 96, MFW = 3, CIB = 32, NW = 4, NTHR = 256;
+  static constexpr int COUT = CO, MFW = 3, CIB = CO == 96 ? 32 : 48, NW = CO == 96 ? 4 : 3;
+  static constexpr int NTHR = 64 * NW;
+  static constexpr int GRW = CO == 96 ? 96 : 64, XRW = CO == 96 ? 32 : 64;  // plane row widths
   static constexpr int SW = 1 << SWL, SH = 32 >> SWL, XW = SW + 2, XPIX = (SH + 2) * XW;
   static constexpr int GQ = 32 * COUT / 4, XQ = XPIX * CIB / 4, NQ = GQ + XQ;  // float4 items
   static constexpr int NIT = (NQ + NTHR - 1) / NTHR;
-  static constexpr int GPL = 32 * COUT, XPL = XPIX * CIB;  // bf16 of G / X per plane
+  static constexpr int GPL = 32 * GRW, XPL = XPIX * XRW;   // bf16 of G / X per plane
   static constexpr int PL = GPL + XPL;                     // plane stride: [G | X]
   static constexpr int BUF = 3 * PL;                       // bf16 per stage buffer
+  static_assert(CO == 96 || CO == 48, "96 or 48 output channels");
   static_assert(GQ % NTHR == 0, "items 0 .. GQ/NTHR - 1 of every thread are G items");
   static_assert(2 * BUF * 2 <= 81920, "two workgroups per CU");
 };
@@ -65,15 +71,15 @@ __device__ __forceinline__ int wp_idx(int r, int rw, int blk) {
 // GL: the next stage's G operands are split into the other buffer at the end of the stage, with
 // X (a whole stage of load latency for both), instead of after the first kernel row (which then
 // issues the X loads into the same registers)
-template <int SWL, bool GL = false>
-__global__ __launch_bounds__(256, 2) void k_wgrad3p(WgradArgs a0) {
-  using C = Wp3Cfg<SWL>;
+template <int SWL, bool GL = false, int CO = 96>
+__global__ __launch_bounds__(CO == 96 ? 256 : 192, 2) void k_wgrad3p(WgradArgs a0) {
+  using C = Wp3Cfg<SWL, CO>;
   constexpr int MFW = C::MFW, SW = C::SW, SH = C::SH, XW = C::XW;
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * C::BUF];
   const WgradArgs a = wg_block(a0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = CO == 96 ? wave >> 1 : 0, wn = CO == 96 ? wave & 1 : wave;
   const int li = lane & 15, lg = lane >> 4;
   const int ci0 = blockIdx.y * C::CIB;
   const int ux = (a.KW + SW - 1) / SW, uy = (a.KH + SH - 1) / SH;
@@ -104,14 +110,14 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3p(WgradArgs a0) {
     if (it < NG) {
       const int px = q / (C::COUT / 4), c = 4 * (q % (C::COUT / 4));
       ioff[it] = ((px >> SWL) * a.KW + (px & (SW - 1))) * a.g_stride + c;
-      ilde[it] = (wp_idx(px, C::COUT, c >> 4) + (c & 15)) | ((c < a.Cout ? 0 : 32) << 16);
+      ilde[it] = (wp_idx(px, C::GRW, c >> 4) + (c & 15)) | ((c < a.Cout ? 0 : 32) << 16);
     } else if (q < C::NQ) {
       const int r = q - C::GQ, xp = r / (C::CIB / 4), c = 4 * (r % (C::CIB / 4));
       const int yy = xp / XW, xx = xp - yy * XW;
       ioff[it] = ((yy - 1) * a.KW + xx - 1) * a.x_stride + ci0 + c;
       const int e = (yy == 0) | ((yy == SH + 1) << 1) | ((xx == 0) << 2) | ((xx == SW + 1) << 3) |
                     ((ci0 + c < a.Cin ? 0 : 1) << 5);
-      ilde[it] = (C::GPL + wp_idx(xp, C::CIB, c >> 4) + (c & 15)) | (e << 16);
+      ilde[it] = (C::GPL + wp_idx(xp, C::XRW, c >> 4) + (c & 15)) | (e << 16);
     }
   }
   const bool exact = a.KW % SW == 0 && a.KH % SH == 0;
@@ -195,15 +201,15 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3p(WgradArgs a0) {
   // ---- MFMA operand addresses (stage-invariant) ----------------------------------------------
   // A (G planes [px][96]): lane 4q+p of group lg supplies row 8lg + 4t + q, columns 4p..4p+3
   // of block 3wm + i, i.e. block (3wm + i) ^ (lg & 1) of the row
-  const int abase = (8 * lg + (li >> 2)) * C::COUT + 4 * (li & 3);
+  const int abase = (8 * lg + (li >> 2)) * C::GRW + 4 * (li & 3);
   const int aflip = lg & 1;
   // B (X planes [xp][32]): stage pixel 8lg + j = (row pr0, column pc0 + j); tap (ky, kx), read t
   // -> X row r0 + d, d = ky*XW + kx + 4t, r0 = pr0*XW + pc0 + (li >> 2), in block wn ^ bit 3 of
   // the row.  Bit k of bmask: that flip for the k-th (ky, kx, t)
   const int pr0 = (8 * lg) >> SWL, pc0 = (8 * lg) & (SW - 1);
   const int r0 = pr0 * XW + pc0 + (li >> 2);
-  const int bbase = C::GPL + r0 * C::CIB + 16 * wn + 4 * (li & 3);
-  const int bsgn = wn ? -16 : 16;
+  const int bbase = C::GPL + r0 * C::XRW + 16 * wn + 4 * (li & 3);
+  const int bsgn = (wn & 1) ? -16 : 16;
   unsigned bmask0 = 0;
 #pragma unroll
   for (int k = 0; k < 18; ++k) {
@@ -242,7 +248,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3p(WgradArgs a0) {
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl) {
         const __bf16* p = buf + pl * C::PL + o;
-        av[pl][i] = tr_frag(p, p + 4 * C::COUT);
+        av[pl][i] = tr_frag(p, p + 4 * C::GRW);
       }
     }
 #pragma unroll
@@ -255,8 +261,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3p(WgradArgs a0) {
       for (int kx = 0; kx < 3; ++kx) {
         const int k = 2 * (3 * ky + kx);
         const int d = ky * XW + kx;
-        const int oa = bbase + d * C::CIB + (int)((bmask >> k) & 1) * bsgn;
-        const int ob = bbase + (d + 4) * C::CIB + (int)((bmask >> (k + 1)) & 1) * bsgn;
+        const int oa = bbase + d * C::XRW + (int)((bmask >> k) & 1) * bsgn;
+        const int ob = bbase + (d + 4) * C::XRW + (int)((bmask >> (k + 1)) & 1) * bsgn;
         bf16x8 bv[3][1];
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) bv[pl][0] = tr_frag(buf + pl * C::PL + oa, buf + pl * C::PL + ob);
@@ -331,7 +337,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3p(WgradArgs a0) {
 // 96 output channels (or 96-channel blocks, a.zc == 96), 32 input channels per workgroup,
 // 16-byte aligned NHWC views, images under 2 GiB per operand (32-bit buffer offsets)
 bool wgrad3p_ok(const WgradArgs& a) {
-  if ((a.zc ? a.zc != 96 : a.Cout != 96) || a.Cin < 32 || a.KW < 8) return false;
+  if ((a.zc ? a.zc != 96 : (a.Cout != 96 && a.Cout != 48)) || a.Cin < 32 || a.KW < 8) return false;
   if ((a.g_stride | a.g_off | a.x_stride | a.x_off) & 3) return false;
   if (a.x_off + ((a.Cin + 3) & ~3) > a.x_stride) return false;
   return (long)a.KH * a.KW * a.g_stride * 4 < 0x7fffffffL &&
@@ -345,6 +351,17 @@ hipError_t launch_wgrad3p(const WgradArgs& a, int splits, hipStream_t s, int nz)
   if (!wgrad3p_ok(a)) return hipErrorInvalidValue;
   static const int swl_max = getenv("DN_WGP_SWL") ? atoi(getenv("DN_WGP_SWL")) : 4;
   static const bool gl = !getenv("DN_WGP_GL") || atoi(getenv("DN_WGP_GL")) != 0;
+  if (!a.zc && a.Cout == 48) {  // the encoder's 48 -> 48 layers: 3 waves, rows of <= 16 pixels
+    const dim3 grid(splits, (a.Cin + 47) / 48, nz), block(192);
+    if (a.KW >= 16 && swl_max >= 4) {
+      prof_kernel("k_wgrad3p<4,gl,48>");
+      hipLaunchKernelGGL((k_wgrad3p<4, true, 48>), grid, block, 0, s, a);
+    } else {
+      prof_kernel("k_wgrad3p<3,gl,48>");
+      hipLaunchKernelGGL((k_wgrad3p<3, true, 48>), grid, block, 0, s, a);
+    }
+    return hipGetLastError();
+  }
   const dim3 grid(splits, (a.Cin + 31) / 32, nz), block(256);
   const int swl = a.KW >= 32 && swl_max >= 5 ? 5 : (a.KW >= 16 && swl_max >= 4 ? 4 : 3);
   static const char* kn[2][3] = {{"k_wgrad3p<3>", "k_wgrad3p<4>", "k_wgrad3p<5>"},

@@ -185,13 +185,14 @@ def _wgrad(dz, x, x6):
     return dwb.cpu().numpy()
 
 
-# k_wgrad3s (split at the operand read): 96 / 48 outputs; 32-wide rows and the 16/8/4-wide
+# k_wgrad3p (96 / 48 outputs; operands split once per stage into LDS planes): 32-wide rows and the 16/8/4-wide
 # multi-row K stages;
 # Cin 96 / 144 (concat) / 48 / 97 (a partial 32-channel block); long pixel sums (64 x 128^2)
 @pytest.mark.parametrize("cin,cout,N,H,W", [
     (96, 96, 2, 32, 32), (144, 96, 2, 16, 32), (48, 96, 2, 64, 64), (97, 96, 1, 32, 32),
     (96, 96, 4, 16, 16), (96, 96, 8, 8, 8), (96, 96, 16, 4, 4), (96, 96, 64, 128, 128),
     (48, 48, 2, 32, 32), (144, 48, 4, 16, 16), (48, 48, 64, 128, 128),  # 48 outputs
+    (48, 48, 8, 8, 8), (100, 48, 2, 16, 16),  # (k_wgrad3p<.., 48>: 8-wide rows, a partial block)
     # sides that are not whole stage blocks (the generic DMA addressing) and an exact 8-wide one
     (96, 96, 2, 20, 36), (48, 48, 3, 24, 40), (96, 96, 2, 13, 16), (96, 96, 2, 12, 8),
 ])
