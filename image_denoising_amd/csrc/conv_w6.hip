@@ -571,15 +571,39 @@ __global__ __launch_bounds__(1024) void k_w6s_lists(const unsigned char* __restr
   }
 }
 
+// Block order (remap, DN_W6S_XCD=1): workgroup b runs on XCD b % 8; XCD x gets a contiguous run of
+// the logical order (image, 64-cell chunk, orientation), so the x-tile and y-tile workgroups of
+// the same cell rows, and the neighbouring chunks that share their input rows, run on one L2 at
+// about the same time (otherwise each input row is fetched from HBM by up to four workgroups
+// on different XCDs: 5.25 GB per launch for 1.6 GB of input, profiles/r4_n2n_pmc_step.json).
+__device__ __forceinline__ void w6s_block(int remap, int nchunk, int& o, int& n, int& chunk) {
+  const unsigned b = blockIdx.x, tot = gridDim.x;
+  unsigned l = b;
+  if (remap && tot >= 8) {
+    const unsigned x = b % 8, base = tot / 8, extra = tot % 8;
+    l = x * base + (x < extra ? x : extra) + b / 8;  // XCD x: (tot - x + 7) / 8 blocks
+    o = (int)(l & 1);
+    l >>= 1;
+  } else {  // round 4's first order: chunk fastest, then image, then orientation
+    o = (int)(l / (tot / 2));
+    l -= (unsigned)o * (tot / 2);
+  }
+  chunk = (int)(l % (unsigned)nchunk);
+  n = (int)(l / (unsigned)nchunk);
+}
+
 __global__ __launch_bounds__(256, 2) void k_c3w6s(FwdArgs a, const unsigned* __restrict__ list,
                                                   const int* __restrict__ cnt,
-                                                  const __bf16* __restrict__ wpv) {
+                                                  const __bf16* __restrict__ wpv, int nchunk,
+                                                  int remap) {
   using C = SCfgW;
   constexpr int MT = C::MT, NTW = C::NTW;
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
   __shared__ unsigned lent[C::CELLS];
   __bf16* lv = reinterpret_cast<__bf16*>(lds_raw);
-  const int o = blockIdx.z, n = blockIdx.y, cbase = blockIdx.x * C::CELLS;
+  int o, n, chunk;
+  w6s_block(remap, nchunk, o, n, chunk);
+  const int cbase = chunk * C::CELLS;
   const int ncell = cnt[2 * n + o];
   if (cbase >= ncell) return;  // (uniform: the list is shorter than the grid allows)
   const long cells = (long)(a.OH / 2) * (a.OW / 2);
@@ -817,10 +841,13 @@ hipError_t launch_fwd_w6s(const FwdArgs& a, const unsigned* list, const int* cnt
       (a.x6_tail & 7) != 0)
     return hipErrorInvalidValue;
   const long cells = (long)(a.OH / 2) * (a.OW / 2);
-  const dim3 grid((unsigned)((cells + SCfgW::CELLS - 1) / SCfgW::CELLS), a.N, 2);
+  const long nchunk = (cells + SCfgW::CELLS - 1) / SCfgW::CELLS;
+  if (nchunk * a.N * 2 >= (1L << 31)) return hipErrorInvalidValue;
+  static const int remap = !getenv("DN_W6S_XCD") || atoi(getenv("DN_W6S_XCD")) != 0;
+  const dim3 grid((unsigned)(nchunk * a.N * 2));
   prof_kernel("k_c3w6s");
   hipLaunchKernelGGL(k_c3w6s, grid, dim3(SCfgW::WAVES * 64), 0, s, a, list, cnt,
-                     static_cast<const __bf16*>(wpv));
+                     static_cast<const __bf16*>(wpv), (int)nchunk, remap);
   return hipGetLastError();
 }
 
