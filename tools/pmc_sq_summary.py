@@ -17,7 +17,7 @@ for r in csv.DictReader(open(f[0])):
     acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     dur[k][r["Dispatch_Id"]] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
 rows = sorted(acc.items(), key=lambda kv: -sum(kv[1].get("SQ_WAVE_CYCLES", [0])))
-for k, cs in rows[:10]:
+for k, cs in rows[:24]:
     m = {c: sum(v) / len(v) for c, v in cs.items()}
     line = f"{k[:44]:44s} n={len(next(iter(cs.values()))):3d}"
     wc = m.get("SQ_WAVE_CYCLES")
