@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DN_LIB_PATH", os.path.join(_HERE, "libdenoise_hip.so"))
 
 
-ABI_VERSION = 4  # include/denoise_hip.h DN_ABI_VERSION
+ABI_VERSION = 5  # include/denoise_hip.h DN_ABI_VERSION
 
 
 class DnOpRecord(ctypes.Structure):  # include/denoise_hip.h dn_op_record
@@ -54,6 +54,10 @@ SIGNATURES = {
                                     c_void_p, c_size_t, c_int, c_void_p]),
     "dn_unet_forward_prec": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int, c_void_p,
                                      c_size_t, c_int, c_void_p]),
+    "dn_unet_pack_weights": (c_int, [POINTER(DnCfg), _F, c_int, c_int, c_int, c_void_p, c_size_t,
+                                     c_int, c_void_p]),
+    "dn_unet_forward_prepacked": (c_int, [POINTER(DnCfg), _F, _F, _F, c_int, c_int, c_int,
+                                          c_void_p, c_size_t, c_int, c_void_p]),
     "dn_unet_backward_prec": (c_int, [POINTER(DnCfg), _F, _F, _F, _F, c_int, c_int, c_int,
                                       c_void_p, c_size_t, c_int, c_void_p]),
     "dn_unet_backward_split": (c_int, [POINTER(DnCfg), _F, _F, _F, _F, c_int, c_int, c_int,
@@ -156,7 +160,7 @@ def lib() -> ctypes.CDLL:
                 "`python -m image_denoising_amd._build` (hipcc --offload-arch=gfx950)")
         L = ctypes.CDLL(LIB_PATH)
         L.dn_abi_version.restype = c_int
-        if L.dn_abi_version() != ABI_VERSION:  # the argument lists below are revision 4's
+        if L.dn_abi_version() != ABI_VERSION:  # the argument lists below are revision 5's
             raise RuntimeError(f"{LIB_PATH}: ABI revision {L.dn_abi_version()}, the binding "
                                f"expects {ABI_VERSION} (include/denoise_hip.h DN_ABI_VERSION)")
         for name, (res, args) in SIGNATURES.items():

@@ -250,6 +250,24 @@ class UNet(nn.Module):
                   _lib.ptr(x), _lib.ptr(y), N, H, W, ws.data_ptr(), ws.numel(), self._prec(),
                   _lib.stream_of(x))
 
+    def _infer_prec(self) -> int:
+        """the precision code of a no-grad forward (bf16 for the configs[4] frozen base)"""
+        return 1 if getattr(self, "inference_precision", "fp32") == "bf16" else self._prec()
+
+    def _pack_weights(self, ws, N, H, W):
+        """dn_unet_pack_weights: the forward's weight images for (N, H, W) into ws, once, for
+        _run_forward_prepacked calls with these parameters (SURVEY §8b persistent packing)"""
+        _lib.call("dn_unet_pack_weights", ctypes.byref(self._cfg), _lib.ptr(self._flat), N, H, W,
+                  ws.data_ptr(), ws.numel(), self._infer_prec(), _lib.stream_of(self._flat))
+
+    def _run_forward_prepacked(self, x, y, ws):
+        """the no-grad forward on the images _pack_weights left in ws (no re-pack): bit-identical
+        to _run_forward_inference while the parameters are unchanged"""
+        N, _, H, W = x.shape
+        _lib.call("dn_unet_forward_prepacked", ctypes.byref(self._cfg), _lib.ptr(self._flat),
+                  _lib.ptr(x), _lib.ptr(y), N, H, W, ws.data_ptr(), ws.numel(), self._infer_prec(),
+                  _lib.stream_of(x))
+
     def _run_forward_n2n(self, x, den, ws, rd_idx):
         """the N2N no-grad pass: den = UNet(x) at the pair pixels of rd_idx only
         (dn_unet_forward_n2n; training_script.md:141-144 reads nothing else)"""

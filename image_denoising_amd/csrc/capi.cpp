@@ -35,7 +35,7 @@ extern "C" {
 #define DN_SRC_HASH "unknown"
 #endif
 // src= the sha256 prefix of the sources this library was compiled from (_build.source_hash)
-const char* dn_version(void) { return "denoise_hip 0.4.0 gfx950 src=" DN_SRC_HASH; }
+const char* dn_version(void) { return "denoise_hip 0.5.0 gfx950 src=" DN_SRC_HASH; }
 
 int dn_abi_version(void) { return DN_ABI_VERSION; }
 
@@ -114,6 +114,48 @@ dn_status dn_unet_forward_prec(const dn_unet_cfg* cfg, const float* params, cons
   if (ws_bytes < (size_t)p.total_floats * sizeof(float))
     return fail(DN_ERR_WORKSPACE, "workspace smaller than dn_unet_workspace_size()");
   return unet_forward(p, params, x, y, static_cast<float*>(ws), (hipStream_t)stream, precision);
+  DN_GUARD_END
+}
+
+// the plan a forward entry point runs on this workspace (dn_unet_forward_prec's rule; bf16:
+// the forward-only plan)
+static dn_status forward_plan(const dn_unet_cfg* cfg, int N, int H, int W, size_t ws_bytes,
+                              int precision, Plan& p) {
+  std::string err;
+  if (precision != DN_PREC_FP32 && precision != DN_PREC_FP32_X6 && precision != DN_PREC_BF16)
+    return fail(DN_ERR_ARG, "unknown precision");
+  const bool bwd_ok = precision != DN_PREC_BF16;
+  if (!bwd_ok || !build_plan(*cfg, N, H, W, true, p, err) ||
+      ws_bytes < (size_t)p.total_floats * sizeof(float))
+    if (!build_plan(*cfg, N, H, W, false, p, err)) return fail(DN_ERR_ARG, err);
+  if (ws_bytes < (size_t)p.total_floats * sizeof(float))
+    return fail(DN_ERR_WORKSPACE, "workspace smaller than dn_unet_workspace_size()");
+  if (!bwd_ok) p.with_bwd = false;
+  return DN_OK;
+}
+
+dn_status dn_unet_pack_weights(const dn_unet_cfg* cfg, const float* params, int N, int H, int W,
+                               void* ws, size_t ws_bytes, int precision, void* stream) {
+  DN_GUARD_BEGIN
+  if (!cfg || !params || !ws) return fail(DN_ERR_ARG, "null argument");
+  Plan p;
+  const dn_status st = forward_plan(cfg, N, H, W, ws_bytes, precision, p);
+  if (st != DN_OK) return st;
+  return unet_forward(p, params, nullptr, nullptr, static_cast<float*>(ws), (hipStream_t)stream,
+                      precision, nullptr, PACK_ONLY);
+  DN_GUARD_END
+}
+
+dn_status dn_unet_forward_prepacked(const dn_unet_cfg* cfg, const float* params, const float* x,
+                                    float* y, int N, int H, int W, void* ws, size_t ws_bytes,
+                                    int precision, void* stream) {
+  DN_GUARD_BEGIN
+  if (!cfg || !params || !x || !y || !ws) return fail(DN_ERR_ARG, "null argument");
+  Plan p;
+  const dn_status st = forward_plan(cfg, N, H, W, ws_bytes, precision, p);
+  if (st != DN_OK) return st;
+  return unet_forward(p, params, x, y, static_cast<float*>(ws), (hipStream_t)stream, precision,
+                      nullptr, RUN_ONLY);
   DN_GUARD_END
 }
 

@@ -401,7 +401,7 @@ hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, 
 // forward: arch_unet.py:194-260 (non-blind-spot branch)
 // ------------------------------------------------------------------------------------
 dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
-                       hipStream_t s, int prec, const uint8_t* sel_rd) {
+                       hipStream_t s, int prec, const uint8_t* sel_rd, int pack) {
   const StreamDeviceGuard device_guard(s);
   const bool bf16 = prec == DN_PREC_BF16, x6 = prec == DN_PREC_FP32_X6;
   // bf16x6 96-channel deconvs (k_deconv_x6); DN_X6_DECONV=0 keeps the fp32 kernel (A/B)
@@ -532,58 +532,62 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     return launch_fwd_bf16(a, st, 1);
   };
 
-  // every weight image of the pass (fp32, bf16x6 and bf16 alike) in one pack launch
-  PackBatch pb;
-  auto add = [&](bool ok, const PackJob& j) { return ok ? pack_add(pb, j, s) : hipErrorInvalidValue; };
-  for (int i = ENC1; i < NINA; ++i) {
-    const Layer& L = p.P.L[i];
-    const float* w = prm + L.woff;
-    PackJob j;
-    if (L.deconv && deconv_x6_layer(i)) {
-      DN_TRY(add(true, pack_job_deconv_x6(w, ws + p.packUX[i])));
-    } else if (L.deconv && bf16) {  // ConvTranspose2d [cin][cout][2][2]: a 1x1 image per parity
-      const long img = bf16_pack_elems(L.cin, L.cout, 1);
-      for (int ab = 0; ab < 4; ++ab) {
-        WView v{};
-        v.w = w; v.off = ab; v.sK = (long)L.cout * 4; v.sN = 4; v.taps = 1;
-        DN_TRY(add(pack_job_bf16(v, L.cin, L.cout, 1,
-                                 reinterpret_cast<unsigned short*>(ws + p.packBF[i]) + ab * img, j), j));
+  // every weight image of the pass (fp32, bf16x6 and bf16 alike) in one pack launch (not for a
+  // prepacked forward: dn_unet_pack_weights left them in ws)
+  if (pack != RUN_ONLY) {
+    PackBatch pb;
+    auto add = [&](bool ok, const PackJob& j) { return ok ? pack_add(pb, j, s) : hipErrorInvalidValue; };
+    for (int i = ENC1; i < NINA; ++i) {
+      const Layer& L = p.P.L[i];
+      const float* w = prm + L.woff;
+      PackJob j;
+      if (L.deconv && deconv_x6_layer(i)) {
+        DN_TRY(add(true, pack_job_deconv_x6(w, ws + p.packUX[i])));
+      } else if (L.deconv && bf16) {  // ConvTranspose2d [cin][cout][2][2]: a 1x1 image per parity
+        const long img = bf16_pack_elems(L.cin, L.cout, 1);
+        for (int ab = 0; ab < 4; ++ab) {
+          WView v{};
+          v.w = w; v.off = ab; v.sK = (long)L.cout * 4; v.sN = 4; v.taps = 1;
+          DN_TRY(add(pack_job_bf16(v, L.cin, L.cout, 1,
+                                   reinterpret_cast<unsigned short*>(ws + p.packBF[i]) + ab * img, j), j));
+        }
+      } else if (L.deconv) {
+        DN_TRY(add(pack_job(G_UP, deconv_fwd_view(w, L.cout), L.cin, L.cout, 4, ws + p.packF[i], 0, 0, j),
+                   j));
+      } else if (bf16) DN_TRY(add(pack_job_bf16(conv_fwd_view(w, L.cin, 3), L.cin, L.cout, 3,
+                                              ws + p.packBF[i], j), j));
+      else if (x6) DN_TRY(add(pack_job_x6(conv_fwd_view(w, L.cin, 3), L.cin, L.cout, 0,
+                                          ws + p.packX[i], x6_tail_f(i), j), j));
+      else DN_TRY(add(pack_job(L.k == 3 ? G_C3 : G_C1, conv_fwd_view(w, L.cin, L.k), L.cin, L.cout, 1,
+                               ws + p.packF[i], 0, 0, j), j));
+      // dec_conv1b's y-tile image for the Winograd pair pass: PK_W6 over the transposed taps
+      if (i == D1B && w6_sel) {
+        WView v = conv_fwd_view(w, L.cin, 3);
+        v.flip = 2;
+        DN_TRY(add(pack_job_x6(v, L.cin, L.cout, 0, ws + p.packXV, X6_W6, j), j));
       }
-    } else if (L.deconv) {
-      DN_TRY(add(pack_job(G_UP, deconv_fwd_view(w, L.cout), L.cin, L.cout, 4, ws + p.packF[i], 0, 0, j),
-                 j));
-    } else if (bf16) DN_TRY(add(pack_job_bf16(conv_fwd_view(w, L.cin, 3), L.cin, L.cout, 3,
-                                            ws + p.packBF[i], j), j));
-    else if (x6) DN_TRY(add(pack_job_x6(conv_fwd_view(w, L.cin, 3), L.cin, L.cout, 0,
-                                        ws + p.packX[i], x6_tail_f(i), j), j));
-    else DN_TRY(add(pack_job(L.k == 3 ? G_C3 : G_C1, conv_fwd_view(w, L.cin, L.k), L.cin, L.cout, 1,
-                             ws + p.packF[i], 0, 0, j), j));
-    // dec_conv1b's y-tile image for the Winograd pair pass: PK_W6 over the transposed taps
-    if (i == D1B && w6_sel) {
-      WView v = conv_fwd_view(w, L.cin, 3);
-      v.flip = 2;
-      DN_TRY(add(pack_job_x6(v, L.cin, L.cout, 0, ws + p.packXV, X6_W6, j), j));
+    }
+    if (bf16_head_x6) {
+      DN_TRY(add(true, pack_job_head_x6(prm + p.P.L[NINA].woff, prm + p.P.L[NINB].woff, ws + p.packH)));
+    } else if (bf16) {  // nin_a, nin_b on the bf16 kernel, nin_c (96 -> out_nc) on the fp32 one
+      for (int i = NINA; i <= NINB; ++i)
+        DN_TRY(launch_pack_bf16(conv_fwd_view(prm + p.P.L[i].woff, 96, 1), 96, 96,
+                                ws + p.packBF[i], s, 1));
+      PackJob j;
+      DN_TRY(add(pack_job(G_C1, conv_fwd_view(prm + p.P.L[NINC].woff, 96, 1), 96, p.OC, 1,
+                          ws + p.packF[NINC], 0, 0, j), j));
+    } else if (head_x6) {
+      DN_TRY(add(true, pack_job_head_x6(prm + p.P.L[NINA].woff, prm + p.P.L[NINB].woff, ws + p.packH)));
+    } else {
+      DN_TRY(launch_pack_head(conv_fwd_view(prm + p.P.L[NINA].woff, 96, 1),
+                              conv_fwd_view(prm + p.P.L[NINB].woff, 96, 1), ws + p.packH, s, &pb));
+    }
+    {
+      const OpTimer timer(s, "pack", 0);
+      DN_TRY(pack_flush(pb, s));
     }
   }
-  if (bf16_head_x6) {
-    DN_TRY(add(true, pack_job_head_x6(prm + p.P.L[NINA].woff, prm + p.P.L[NINB].woff, ws + p.packH)));
-  } else if (bf16) {  // nin_a, nin_b on the bf16 kernel, nin_c (96 -> out_nc) on the fp32 one
-    for (int i = NINA; i <= NINB; ++i)
-      DN_TRY(launch_pack_bf16(conv_fwd_view(prm + p.P.L[i].woff, 96, 1), 96, 96,
-                              ws + p.packBF[i], s, 1));
-    PackJob j;
-    DN_TRY(add(pack_job(G_C1, conv_fwd_view(prm + p.P.L[NINC].woff, 96, 1), 96, p.OC, 1,
-                        ws + p.packF[NINC], 0, 0, j), j));
-  } else if (head_x6) {
-    DN_TRY(add(true, pack_job_head_x6(prm + p.P.L[NINA].woff, prm + p.P.L[NINB].woff, ws + p.packH)));
-  } else {
-    DN_TRY(launch_pack_head(conv_fwd_view(prm + p.P.L[NINA].woff, 96, 1),
-                            conv_fwd_view(prm + p.P.L[NINB].woff, 96, 1), ws + p.packH, s, &pb));
-  }
-  {
-    const OpTimer timer(s, "pack", 0);
-    DN_TRY(pack_flush(pb, s));
-  }
+  if (pack == PACK_ONLY) return DN_OK;
   // enc_conv0, fused with pool0 = x -> channels [2nf, 2nf+C) of the up1 concat buffer
   DN_TIMED(s, "enc0", 2.0 * N * p.H * p.W * C * nf * 9, C, nf, p.H, p.W, N,
            launch_enc0_fwd(x, N, C, p.H, p.W, prm + p.P.L[ENC0].woff, Bs(ENC0), ws + p.a0,

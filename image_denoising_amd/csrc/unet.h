@@ -75,8 +75,14 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
 // by three-way operand splitting, fp32-accurate), DN_PREC_BF16 (forward only, bf16 operands)
 // sel_rd (nullable, DN_PREC_FP32_X6 and no backward only): dec_conv1b and the head run on the
 // two N2N pair pixels of every 2x2 cell only; y is written at those pixels and nowhere else
+// pack: PACK_RUN packs the weight images into ws and runs; PACK_ONLY packs and returns (x, y
+// unused; dn_unet_pack_weights); RUN_ONLY runs on the images a PACK_ONLY call left in ws
+// (dn_unet_forward_prepacked: the same params, shape and precision; biases and the thin layers
+// are still read from prm)
+enum { PACK_RUN = 0, PACK_ONLY = 1, RUN_ONLY = 2 };
 dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y, float* ws,
-                       hipStream_t s, int prec = DN_PREC_FP32, const uint8_t* sel_rd = nullptr);
+                       hipStream_t s, int prec = DN_PREC_FP32, const uint8_t* sel_rd = nullptr,
+                       int pack = PACK_RUN);
 // dx (nullable): dL/dx of the network input, NCHW [N, in_nc, H, W]
 // tail_ready (nullable): recorded once dprm[tail_begin(p) ..] is final (dn_unet_backward_split)
 dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float* dprm, float* dx,

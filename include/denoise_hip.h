@@ -63,8 +63,9 @@ const char* dn_version(void);
    Revision 3 (library 0.3.x): dn_unet_backward / dn_unet_backward_prec gained the nullable
    `float* dx` argument after `dparams` (revision 2 had no dx: an old caller's arguments would
    be shifted, so check dn_abi_version() == DN_ABI_VERSION before binding).  Revision 4
-   (library 0.4.x): dn_unet_backward_split added (existing signatures unchanged). */
-#define DN_ABI_VERSION 4
+   (library 0.4.x): dn_unet_backward_split added.  Revision 5 (library 0.5.x):
+   dn_unet_pack_weights / dn_unet_forward_prepacked added (existing signatures unchanged). */
+#define DN_ABI_VERSION 5
 int dn_abi_version(void);
 /* copies the last error message of this thread into buf (NUL-terminated); returns its length */
 int dn_last_error(char* buf, size_t len);
@@ -145,6 +146,19 @@ dn_status dn_unet_forward_prec(const dn_unet_cfg* cfg, const float* params, cons
 dn_status dn_unet_backward_prec(const dn_unet_cfg* cfg, const float* params, const float* dy,
                                 float* dparams, float* dx, int N, int H, int W, void* ws,
                                 size_t ws_bytes, int precision, void* stream);
+/* Persistent packed weights (SURVEY §8b dn_unet_pack_weights; replaces the per-call weight
+   relayout that arch_unet.UNet's nn.Conv2d modules never need, arch_unet.py:115-192): packs the
+   forward's weight images for (N, H, W, precision) into ws -- the plan is chosen by ws_bytes as
+   in dn_unet_forward_prec -- and dn_unet_forward_prepacked then runs the forward on them without
+   re-packing (inference over many batches with fixed weights: evaluation.py:66-108).  The
+   prepacked forward still reads the biases and the thin layers (enc_conv0, nin_c) from params,
+   which must be the buffer that was packed; its output equals dn_unet_forward_prec's bit for
+   bit.  Any forward or backward with packing (every other entry point) overwrites the images. */
+dn_status dn_unet_pack_weights(const dn_unet_cfg* cfg, const float* params, int N, int H, int W,
+                               void* ws, size_t ws_bytes, int precision, void* stream);
+dn_status dn_unet_forward_prepacked(const dn_unet_cfg* cfg, const float* params, const float* x,
+                                    float* y, int N, int H, int W, void* ws, size_t ws_bytes,
+                                    int precision, void* stream);
 /* dn_unet_backward_prec for a data-parallel step that overlaps the gradient all-reduce with
    the backward (train.py:324-326 reduces inside the backward too).  The backward finishes the
    head's and the decoder's parameter gradients first: dparams[*tail_begin ..] (the state_dict

@@ -435,6 +435,40 @@ def test_unet_forward_n2n_pair_pixels(C, N, H, W, prec, rdk):
         assert bool(torch.isnan(den[~sel]).all())
 
 
+@pytest.mark.parametrize("prec", ["fp32", "fp32_x6", "bf16"])
+def test_unet_forward_prepacked_equals_forward(prec):
+    """dn_unet_pack_weights once, then dn_unet_forward_prepacked on several batches: bit for bit
+    the forward that packs per call (SURVEY §8b persistent packed weights), for each arithmetic;
+    and the images really persist: after the parameters change, a prepacked forward still gives
+    the old weights' result while a packing forward gives the new one."""
+    net = _net(1, "fp32" if prec == "bf16" else prec)
+    if prec == "bf16":
+        net.set_inference_precision("bf16")
+    g = torch.Generator().manual_seed(11)
+    N, H, W = 2, 64, 96
+    ws = net._workspace(N, H, W, with_backward=False, fresh=True)
+    ws2 = net._workspace(N, H, W, with_backward=False, fresh=True).clone()
+    xs = [torch.rand(N, 1, H, W, generator=g).to(DEV) for _ in range(2)]
+    net._pack_weights(ws, N, H, W)
+    for x in xs:
+        ref, pre = torch.empty_like(x), torch.empty_like(x)
+        net._run_forward_inference(x, ref, ws2)
+        net._run_forward_prepacked(x, pre, ws)
+        assert torch.equal(pre, ref)
+    old = torch.empty_like(xs[0])
+    net._run_forward_inference(xs[0], old, ws2)
+    with torch.no_grad():
+        net.flat_params.mul_(1.5)
+    pre, new = torch.empty_like(old), torch.empty_like(old)
+    net._run_forward_inference(xs[0], new, ws2)
+    assert not torch.equal(new, old)
+    net._run_forward_prepacked(xs[0], pre, ws)  # images of the old weights, new biases
+    assert not torch.equal(pre, new)
+    net._pack_weights(ws, N, H, W)
+    net._run_forward_prepacked(xs[0], pre, ws)
+    assert torch.equal(pre, new)
+
+
 @pytest.mark.parametrize("rdk", ["h", "v", "mixed"])
 def test_unet_forward_n2n_pair_pixels_vs_oracle(rdk):
     """The Winograd pair pass (8 x 128^2: k_c3w6s for both tile orientations) against the CPU

@@ -29,14 +29,15 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_revision_matches_header_and_binding():
-    """DN_ABI_VERSION (revision 4: dn_unet_backward_split; 3: dn_unet_backward's dx argument) ==
+    """DN_ABI_VERSION (revision 5: dn_unet_pack_weights / dn_unet_forward_prepacked; 4:
+    dn_unet_backward_split; 3: dn_unet_backward's dx argument) ==
     the library's == the binding's, so a caller built against an older argument list is refused,
     not mis-bound"""
     from image_denoising_amd import _lib
 
     src = open(os.path.join(ROOT, "include", "denoise_hip.h")).read()
     rev = int(re.search(r"#define DN_ABI_VERSION (\d+)", src).group(1))
-    assert rev == _lib.lib().dn_abi_version() == _lib.ABI_VERSION == 4
+    assert rev == _lib.lib().dn_abi_version() == _lib.ABI_VERSION == 5
 
 
 def test_library_built_from_these_sources():
