@@ -467,11 +467,11 @@ hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize) {
     const int tx = (a.OW + 15) / 16, ty = (a.OH + 15) / 16;
     const dim3 grid(tx * ty, a.N, 1);
     if (nt == 3) {
-      prof_kernel(a.in_bf16 ? "k_fwd_bf16p<3,4,bf16in>" : "k_fwd_bf16p<3,4>");
+      prof_kernel(a.in_bf16 ? "k_fwd_bf16p<3,4,true>" : "k_fwd_bf16p<3,4,false>");  // (rocprofv3 names)
       if (a.in_bf16) hipLaunchKernelGGL((k_fwd_bf16p<3, 4, true>), grid, dim3(256), 0, s, a);
       else hipLaunchKernelGGL((k_fwd_bf16p<3, 4>), grid, dim3(256), 0, s, a);
     } else {
-      prof_kernel(a.in_bf16 ? "k_fwd_bf16p<6,4,bf16in>" : "k_fwd_bf16p<6,4>");
+      prof_kernel(a.in_bf16 ? "k_fwd_bf16p<6,4,true>" : "k_fwd_bf16p<6,4,false>");  // (rocprofv3 names)
       if (a.in_bf16) hipLaunchKernelGGL((k_fwd_bf16p<6, 4, true>), grid, dim3(256), 0, s, a);
       else hipLaunchKernelGGL((k_fwd_bf16p<6, 4>), grid, dim3(256), 0, s, a);
     }
