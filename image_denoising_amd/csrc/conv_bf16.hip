@@ -451,9 +451,14 @@ hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize) {
   // bf16 activation storage: whole channel quads (8-byte loads / stores), the float4 epilogue
   if ((a.in_bf16 && ((a.K | a.in_stride | a.in_off) & 3)) || (a.out_bf16 && a.out_layout != OUT_NHWC))
     return hipErrorInvalidValue;
+  // a fused 2x2 max-pool (the float4 epilogue's, as the x6 kernels): 3x3, activated, NHWC
+  // fp32 output, even sides, an even number of rows per wave (MT = 4 even on small grids)
+  if (a.pool_out && (ksize != 3 || a.epi != EPI_BIAS_ACT || a.out_layout != OUT_NHWC || a.out_bf16 ||
+                     ((a.pool_stride | a.pool_off) & 3) || ((a.OH | a.OW) & 1)))
+    return hipErrorInvalidValue;
   const long tiles = (long)a.N * ((a.OH + 15) / 16) * ((a.OW + 15) / 16) *
                      (a.out_layout == OUT_UP2 ? 4 : 1);
-  const bool small = tiles < 1024;
+  const bool small = tiles < 1024 && !a.pool_out;
   if (ksize == 1) {
     if (nt == 3) return small ? run_bf16<3, 1, false>(a, s) : run_bf16<3, 4, false>(a, s);
     return small ? run_bf16<6, 1, false>(a, s) : run_bf16<6, 4, false>(a, s);

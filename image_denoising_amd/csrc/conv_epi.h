@@ -233,6 +233,7 @@ __device__ __forceinline__ void fwd_epilogue_vec_at(const FwdArgs& a, const f32x
                          a.pool_off + cz + c] = mx;
           }
       }
+      if (a.pool_only) return;  // nothing reads the full-resolution activation
     }
   }
   const bool has_bias = BIAS && a.bias != nullptr;

@@ -99,6 +99,7 @@ struct FwdArgs {
   // number of tile rows per wave): pooled NHWC pixel (OH/2, OW/2) at pool_out[pix * pool_stride +
   // pool_off + channel], in the window order of k_pool_fwd (bit-identical to pooling `out`)
   float* pool_out; int pool_stride, pool_off;
+  int pool_only;  // with pool_out: the full-resolution output is not stored (forward-only plans)
   int zc;        // > 0: blockIdx.z selects output channels [z*zc, z*zc+zc) (wide layers)
   int x6_tail;   // split-bf16 kernels: packing of the last K chunk, x6_tail_mode(K) (0: plain)
   // split-bf16 3x3 forward, "selected pixels" mode (launch_fwd_x6_sel): per 2x2 output cell the

@@ -452,6 +452,11 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // (dec_conv1b -> the bf16 head: bf16_store_out(D1B))
   // pool (x6 path, EPI_BIAS_ACT): the 2x2 max-pool of `out` fused into the conv's epilogue into
   // that view (*pooled set); otherwise the caller pools
+  // forward-only plans: an encoder conv whose pool is fused stores only the pooled output
+  // (its full-resolution activation is read by nothing but that pool; the backward's pool
+  // routing reads it in plans with a backward).  DN_POOL_ONLY=0 stores it anyway.
+  static const bool pool_only_env = !getenv("DN_POOL_ONLY") || atoi(getenv("DN_POOL_ONLY")) != 0;
+  const int pool_only = !p.with_bwd && pool_only_env ? 1 : 0;
   auto conv_forward = [&](const View& in, int Nn, int h, int w, int K, const float* wp,
                           const float* b, int cout, int ksize, int act, const View& out,
                           int layout, hipStream_t st, const View* pool = nullptr,
@@ -473,6 +478,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
       a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = layout;
       if (pool && pool_fuse && act && layout == OUT_NHWC && !(a.x6_tail & X6_W6)) {
         a.pool_out = pool->p; a.pool_stride = pool->stride; a.pool_off = pool->off;
+        a.pool_only = pool_only;
         if (pooled) *pooled = true;
       }
       return launch_fwd_x6(a, st);
@@ -490,6 +496,13 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     // bit-identical and those tensors move half the bytes
     a.out_bf16 = bf16_store_out(i);
     a.in_bf16 = bf16_store_in(i);
+    // the encoder's pools fused as in the x6 path (DN_BF16_POOL_FUSE=0: separate k_pool_fwd)
+    static const bool bf16_pool_env = !getenv("DN_BF16_POOL_FUSE") || atoi(getenv("DN_BF16_POOL_FUSE")) != 0;
+    if (pool && pool_fuse && bf16_pool_env && act && ksize == 3 && layout == OUT_NHWC && !a.out_bf16) {
+      a.pool_out = pool->p; a.pool_stride = pool->stride; a.pool_off = pool->off;
+      a.pool_only = pool_only;
+      if (pooled) *pooled = true;
+    }
     return launch_fwd_bf16(a, st, ksize);
   };
 
