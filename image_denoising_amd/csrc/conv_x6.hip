@@ -2453,6 +2453,10 @@ hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* w
 #ifndef DN_DECONV_CPOL
 #define DN_DECONV_CPOL 0  // A/B: cache policy bits of the output stores (2 = nt, streaming)
 #endif
+// B1: plain bf16 products (the bf16 base's autocast arithmetic, as k_nin_head_x6's B1): the input
+// rounded to bf16, the images' leading planes (the weights rounded to bf16), one MFMA per block
+// chained in fp32 -- a sixth of the MFMAs, so the launch is bound by its output stores
+template <bool B1 = false>
 __global__ __launch_bounds__(512, 1) void k_deconv_x6(FwdArgs a, const __bf16* wimg, int nwt) {
   __shared__ __attribute__((aligned(16))) __bf16 lw[2 * X6_HEAD_BF];
   __shared__ __attribute__((aligned(16))) float lbias[96];
@@ -2501,6 +2505,18 @@ __global__ __launch_bounds__(512, 1) void k_deconv_x6(FwdArgs a, const __bf16* w
     for (int b = 0; b < 3; ++b) {
       const float4 u0 = xin[2 * b], u1 = xin[2 * b + 1];
       const float v8[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+      if constexpr (B1) {
+        bf16x8 x0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x0[j] = (__bf16)v8[j];
+#pragma unroll
+        for (int f = 0; f < 6; ++f) {
+          const int row = b * 96 + f * 16 + li;
+          const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(img + row * 32 + x6_swz(row, lg) * 8);
+          out[f][0] = mfma_bf16(w0, x0, out[f][0]);
+        }
+        continue;
+      }
       bf16x8 xv[3][1];
       split3x8(v8, xv[0][0], xv[1][0], xv[2][0]);
       // one output fragment at a time, its three weight planes read one fragment ahead: 24
@@ -2575,8 +2591,9 @@ hipError_t launch_pack_deconv_x6(const float* w, void* out, hipStream_t s) {
   return pack_flush(b, s);
 }
 
-// a: in = x (IHt = OH = h, IWt = OW = w), out = the 2h x 2w view, bias; K = NOUT = 96
-hipError_t launch_deconv_x6(const FwdArgs& a, const void* wimg, hipStream_t s) {
+// a: in = x (IHt = OH = h, IWt = OW = w), out = the 2h x 2w view, bias; K = NOUT = 96; b1: plain
+// bf16 products (the bf16 base)
+hipError_t launch_deconv_x6(const FwdArgs& a, const void* wimg, hipStream_t s, bool b1) {
   if (!deconv_x6_ok(a)) return hipErrorInvalidValue;
   const long nwt = (long)a.N * a.OH * ((a.OW + 15) / 16);  // one low-res 16-pixel row per wave-tile
   if (nwt >= (1L << 31) - (1L << 20)) return hipErrorInvalidValue;
@@ -2584,8 +2601,15 @@ hipError_t launch_deconv_x6(const FwdArgs& a, const void* wimg, hipStream_t s) {
   long groups = (nwt + 3) / 4;
   if (groups > 128) groups = 128;
   groups = (groups + 7) / 8 * 8;
-  hipLaunchKernelGGL(k_deconv_x6, dim3((unsigned)(2 * groups)), dim3(512), 0, s, a,
-                     static_cast<const __bf16*>(wimg), (int)nwt);
+  if (b1) {
+    prof_kernel("k_deconv_x6<true>");
+    hipLaunchKernelGGL(k_deconv_x6<true>, dim3((unsigned)(2 * groups)), dim3(512), 0, s, a,
+                       static_cast<const __bf16*>(wimg), (int)nwt);
+  } else {
+    prof_kernel("k_deconv_x6<false>");
+    hipLaunchKernelGGL(k_deconv_x6<false>, dim3((unsigned)(2 * groups)), dim3(512), 0, s, a,
+                       static_cast<const __bf16*>(wimg), (int)nwt);
+  }
   return hipGetLastError();
 }
 

@@ -296,7 +296,7 @@ hipError_t launch_fwd_x6_sel(const FwdArgs& a, hipStream_t s);
 // bf16x6 ConvTranspose2d(96, 96, 2, 2) forward: four pre-split parity images (4 x X6_HEAD_BF bf16)
 bool deconv_x6_ok(const FwdArgs& a);
 hipError_t launch_pack_deconv_x6(const float* w, void* out, hipStream_t s);
-hipError_t launch_deconv_x6(const FwdArgs& a, const void* wimg, hipStream_t s);
+hipError_t launch_deconv_x6(const FwdArgs& a, const void* wimg, hipStream_t s, bool b1 = false);
 // its data gradient: a.in = dy (IHt x IWt = 2 OH x 2 OW, stride in_stride), a.out = dx (OH x OW,
 // stride out_stride), a.mask (EPI_MASK) / EPI_PLAIN; K = NOUT = 96; wimg = the pre-split images
 // (pack_job_deconv_dgrad_x6, 4 x X6_HEAD_BF bf16)

@@ -532,7 +532,9 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
       a.N = Nn; a.OH = h; a.OW = w; a.K = cin; a.NOUT = cout; a.bias = b;
       a.out = out.p; a.out_stride = out.stride; a.out_off = out.off;
       if (!deconv_x6_ok(a)) return hipErrorInvalidValue;
-      return launch_deconv_x6(a, ws + p.packUX[i], st);
+      // (the bf16 base: plain bf16 products, as its convs; DN_BF16_DECONV_B1=0: bf16x6)
+      static const bool b1_env = !getenv("DN_BF16_DECONV_B1") || atoi(getenv("DN_BF16_DECONV_B1")) != 0;
+      return launch_deconv_x6(a, ws + p.packUX[i], st, bf16 && b1_env);
     }
     if (!bf16 || i == NL || p.packBF[i] < 0)
       return dn::deconv_forward(xin, Nn, h, w, cin, wp, b, cout, out, st);
