@@ -244,7 +244,7 @@ hipError_t launch_fwd_nt(int gather, int nt, const FwdArgs& a, hipStream_t s);
 hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s);
 hipError_t launch_enc0_fwd(const float* x, int N, int C, int H, int W, const float* w,
                            const float* b, float* out, float* cat, int cat_stride, int cat_off,
-                           int cat_zero_to, float* xcopy, hipStream_t s);
+                           int cat_zero_to, float* xcopy, hipStream_t s, bool out_bf16 = false);
 int enc0_wgrad_splits(int N, int H, int W);
 hipError_t launch_enc0_wgrad(const float* g, int g_stride, const float* x, int N, int C, int H,
                              int W, float* slab, int splits, float* dwb, hipStream_t s,

@@ -24,7 +24,7 @@ __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, i
                                                   const float* __restrict__ b,
                                                   float* __restrict__ out, float* __restrict__ cat,
                                                   int cat_stride, int cat_off, int cat_zero_to,
-                                                  float* __restrict__ xcopy) {
+                                                  float* __restrict__ xcopy, int obf) {
   constexpr int KT = 9 * C;
   __shared__ __attribute__((aligned(16))) float wl[(KT + 1) * E0_CO];  // [tap*C+ci | bias][co]
   __shared__ __attribute__((aligned(16))) float st[256 * E0_CO];
@@ -82,6 +82,17 @@ __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, i
   __syncthreads();
   const long npx = total - p0 < 256 ? total - p0 : 256;
   const float4* s4 = reinterpret_cast<const float4*>(st);
+  if (obf) {  // bf16 storage (RNE, the value the bf16 base's enc_conv1 stages anyway)
+    typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+    u16x4* o2 = reinterpret_cast<u16x4*>(reinterpret_cast<unsigned short*>(out) + p0 * E0_CO);
+    for (int e = tid; e < npx * (E0_CO / 4); e += 256) {
+      const float4 v = s4[e];
+      const __bf16 q[4] = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+      o2[e] = u16x4{__builtin_bit_cast(unsigned short, q[0]), __builtin_bit_cast(unsigned short, q[1]),
+                    __builtin_bit_cast(unsigned short, q[2]), __builtin_bit_cast(unsigned short, q[3])};
+    }
+    return;
+  }
   float4* o4 = reinterpret_cast<float4*>(out + p0 * E0_CO);
   for (int e = tid; e < npx * (E0_CO / 4); e += 256) o4[e] = s4[e];
 }
@@ -166,22 +177,22 @@ __global__ __launch_bounds__(256) void k_wgrad_c3_thin(const float* __restrict__
 
 hipError_t launch_enc0_fwd(const float* x, int N, int C, int H, int W, const float* w,
                            const float* b, float* out, float* cat, int cat_stride, int cat_off,
-                           int cat_zero_to, float* xcopy, hipStream_t s) {
+                           int cat_zero_to, float* xcopy, hipStream_t s, bool out_bf16) {
   if (C < 1 || C > 4) return hipErrorInvalidValue;
   const long total = (long)N * H * W;
   const dim3 grid((unsigned)((total + 255) / 256));
   if (C == 1)
     hipLaunchKernelGGL(k_enc0_fwd<1>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
-                       cat_off, cat_zero_to, xcopy);
+                       cat_off, cat_zero_to, xcopy, (int)out_bf16);
   else if (C == 2)
     hipLaunchKernelGGL(k_enc0_fwd<2>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
-                       cat_off, cat_zero_to, xcopy);
+                       cat_off, cat_zero_to, xcopy, (int)out_bf16);
   else if (C == 3)
     hipLaunchKernelGGL(k_enc0_fwd<3>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
-                       cat_off, cat_zero_to, xcopy);
+                       cat_off, cat_zero_to, xcopy, (int)out_bf16);
   else
     hipLaunchKernelGGL(k_enc0_fwd<4>, grid, dim3(256), 0, s, x, N, H, W, w, b, out, cat, cat_stride,
-                       cat_off, cat_zero_to, xcopy);
+                       cat_off, cat_zero_to, xcopy, (int)out_bf16);
   return hipGetLastError();
 }
 

@@ -445,7 +445,12 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     return bf16_store && (i == D1A || i == D2A || i == D3A || i == D4A || i == D5A) &&
            p.packBF[i] >= 0 && p.packBF[i + 1] >= 0;
   };
+  // enc_conv0's output too: only enc_conv1 reads it in a forward-only plan (DN_BF16_ENC0_STORE=0:
+  // fp32)
+  static const bool enc0_env = !getenv("DN_BF16_ENC0_STORE") || atoi(getenv("DN_BF16_ENC0_STORE")) != 0;
+  const bool enc0_bf16 = bf16_store && enc0_env && p.packBF[ENC1] >= 0;
   auto bf16_store_in = [&](int i) {
+    if (i == ENC1) return enc0_bf16;
     return bf16_store && (i == D1B || i == D2B || i == D3B || i == D4B || i == D5B) &&
            bf16_store_out(i - 1);
   };
@@ -606,7 +611,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // enc_conv0, fused with pool0 = x -> channels [2nf, 2nf+C) of the up1 concat buffer
   DN_TIMED(s, "enc0", 2.0 * N * p.H * p.W * C * nf * 9, C, nf, p.H, p.W, N,
            launch_enc0_fwd(x, N, C, p.H, p.W, prm + p.P.L[ENC0].woff, Bs(ENC0), ws + p.a0,
-                           ws + p.c1, p.c1s, 2 * nf, p.c1kp, p.with_bwd ? ws + p.xin : nullptr, s));
+                           ws + p.c1, p.c1s, 2 * nf, p.c1kp, p.with_bwd ? ws + p.xin : nullptr, s,
+                           enc0_bf16));
   {  // enc_conv1 + pool1 -> skip slice of c2
     const View pv = V(p.c[1], p.cs[1], 2 * nf);
     bool pooled = false;
