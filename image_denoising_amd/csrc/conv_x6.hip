@@ -938,8 +938,7 @@ struct HCfg {
   static constexpr int LBYTES_MAIN = 2 * 3 * XPL + 2 * S * WST;
   static constexpr int LEPI = 4 * WAVES * 16 * PS;
   static constexpr int LBYTES = LBYTES_MAIN > LEPI ? LBYTES_MAIN : LEPI;
-  // (S_ >= 4, the small grids' deep ring: one workgroup per CU is enough below one round of tiles)
-  static_assert(2 * LBYTES <= 163840 || (S_ >= 4 && LBYTES <= 163840), "two workgroups per CU");
+  static_assert(2 * LBYTES <= 163840, "two workgroups per CU");
 };
 
 #ifndef DN_X6H_LOOK
@@ -1200,18 +1199,10 @@ static hipError_t run_x6h(const FwdArgs& a, int nz, hipStream_t s) {
 }
 
 // small grids (below one round of 16 x 16 tiles), plain image: the 3-slot ring
-// (DN_X6_RING=4: a 4-slot ring, stage st + 3 requested at the start of st; A/B)
 template <int NT, int MT>
 static hipError_t run_x6h3(const FwdArgs& a, int nz, hipStream_t s) {
   using C = HCfg<NT, MT, 3>;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
-  static const int ring = getenv("DN_X6_RING") ? atoi(getenv("DN_X6_RING")) : 3;
-  if (ring == 4) {
-    static const std::string kn4 = x6_kmore(x6_kname("k_c3x6h", NT, 0, MT), "4");
-    prof_kernel(kn4.c_str());
-    hipLaunchKernelGGL((k_c3x6h<NT, 0, MT, 4>), dim3(tx * ty, a.N, nz), dim3(C::WAVES * 64), 0, s, a);
-    return hipGetLastError();
-  }
   static const std::string kn = x6_kmore(x6_kname("k_c3x6h", NT, 0, MT), "3");
   prof_kernel(kn.c_str());
   hipLaunchKernelGGL((k_c3x6h<NT, 0, MT, 3>), dim3(tx * ty, a.N, nz), dim3(C::WAVES * 64), 0, s, a);
