@@ -221,8 +221,10 @@ __device__ __forceinline__ void bf_barrier() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
+// (MT = 6 with NT = 6: the larger wave tile -- fewer LDS fragment reads per MFMA -- needs the
+// whole register file, one workgroup per CU; DN_BF16_MT / DN_BF16_MT3 select it)
 template <int NT, int MT, bool IB = false>
-__global__ __launch_bounds__(256, 2) void k_fwd_bf16p(FwdArgs a) {
+__global__ __launch_bounds__(256, (NT * MT > 24) ? 1 : 2) void k_fwd_bf16p(FwdArgs a) {
   using C = BCfg<NT, MT, true>;
   constexpr int PIECES = C::WST / 512, PPW = (PIECES + 3) / 4;
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
@@ -465,21 +467,36 @@ hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize) {
   }
   // pipelined kernel: aligned views, whole channel quads, < 2 GiB of input rows per tile
   static const bool pipe_env = !getenv("DN_BF16_PIPE") || atoi(getenv("DN_BF16_PIPE")) != 0;
+  // rows per wave: 96-output convs 4 (DN_BF16_MT=6: one workgroup per CU, slower); 48-output
+  // convs 8 -- fewer LDS fragment reads per MFMA at the same occupancy -- where the grid still
+  // has >= 4096 such tiles (8 rounds of 512 resident workgroups), else 4 (DN_BF16_MT3: 4 / 8
+  // forces it).  The accumulation order does not depend on MT: bit-identical results.
+  static const int mt6 = getenv("DN_BF16_MT") && atoi(getenv("DN_BF16_MT")) == 6 ? 6 : 4;
+  static const int mt3e = getenv("DN_BF16_MT3") ? atoi(getenv("DN_BF16_MT3")) : 0;
+  const long tiles8 = (long)a.N * ((a.OH + 31) / 32) * ((a.OW + 15) / 16);
+  const int mt3 = mt3e == 4 || mt3e == 8 ? mt3e : (tiles8 >= 4096 ? 8 : 4);
+  const int mt = nt == 3 ? mt3 : mt6;
   const bool pipe = pipe_env && !small && a.out_layout == OUT_NHWC && a.K % 4 == 0 &&
                     ((a.in_stride | a.in_off) & 3) == 0 &&
-                    (long)BCfg<6, 4, true>::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL;
+                    (long)BCfg<6, 8, true>::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL;
   if (pipe) {
-    const int tx = (a.OW + 15) / 16, ty = (a.OH + 15) / 16;
+    const int tx = (a.OW + 15) / 16, ty = (a.OH + 4 * mt - 1) / (4 * mt);
     const dim3 grid(tx * ty, a.N, 1);
+#define DN_BF16P_LAUNCH(NT_, MT_)                                                              \
+  do {                                                                                         \
+    prof_kernel(a.in_bf16 ? "k_fwd_bf16p<" #NT_ "," #MT_ ",true>"                              \
+                          : "k_fwd_bf16p<" #NT_ "," #MT_ ",false>");  /* (rocprofv3 names) */  \
+    if (a.in_bf16) hipLaunchKernelGGL((k_fwd_bf16p<NT_, MT_, true>), grid, dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((k_fwd_bf16p<NT_, MT_, false>), grid, dim3(256), 0, s, a);          \
+  } while (0)
     if (nt == 3) {
-      prof_kernel(a.in_bf16 ? "k_fwd_bf16p<3,4,true>" : "k_fwd_bf16p<3,4,false>");  // (rocprofv3 names)
-      if (a.in_bf16) hipLaunchKernelGGL((k_fwd_bf16p<3, 4, true>), grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((k_fwd_bf16p<3, 4>), grid, dim3(256), 0, s, a);
+      if (mt == 8) DN_BF16P_LAUNCH(3, 8);
+      else DN_BF16P_LAUNCH(3, 4);
     } else {
-      prof_kernel(a.in_bf16 ? "k_fwd_bf16p<6,4,true>" : "k_fwd_bf16p<6,4,false>");  // (rocprofv3 names)
-      if (a.in_bf16) hipLaunchKernelGGL((k_fwd_bf16p<6, 4, true>), grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((k_fwd_bf16p<6, 4>), grid, dim3(256), 0, s, a);
+      if (mt == 6) DN_BF16P_LAUNCH(6, 6);
+      else DN_BF16P_LAUNCH(6, 4);
     }
+#undef DN_BF16P_LAUNCH
     return hipGetLastError();
   }
   if (nt == 3) return small ? run_bf16<3, 1, true>(a, s) : run_bf16<3, 4, true>(a, s);

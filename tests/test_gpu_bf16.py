@@ -167,3 +167,17 @@ def test_conv_bf16_vs_fp64_of_rounded_operands(cin, cout, N, H, W, xs):
     ref = torch.nn.functional.leaky_relu(
         torch.nn.functional.conv2d(xr, wr, b.double(), padding=1), 0.2)
     assert rel_err(y.numpy(), ref.numpy()) < 1e-5
+
+
+def test_conv_bf16_48_rows8_tile():
+    """48 -> 48 at 8 x 512^2 (>= 4096 tiles of 32 rows): the 8-rows-per-wave pipelined tile.
+    Image 0 against an fp32 conv of the bf16-rounded operands (products exact, only the
+    accumulation order differs)."""
+    g = torch.Generator().manual_seed(48)
+    x = torch.randn(8, 48, 512, 512, generator=g)
+    w = torch.randn(48, 48, 3, 3, generator=g) * 0.05
+    b = torch.randn(48, generator=g) * 0.1
+    y = _conv_bf16(x, w, b, 1)
+    xr, wr = x[:1].bfloat16().float(), w.bfloat16().float()
+    ref = torch.nn.functional.leaky_relu(torch.nn.functional.conv2d(xr, wr, b, padding=1), 0.2)
+    assert rel_err(y[:1].numpy(), ref.numpy()) < 1e-5
