@@ -63,8 +63,17 @@ struct Wp3Cfg {
   static_assert(2 * BUF * 2 <= 81920, "two workgroups per CU");
 };
 
-// plane index of channel block `blk` (16 channels) of row r (row width `rw` channels)
+// the swizzle of a 64-channel (128-B) plane row: a 16-lane group of ds_read_b64_tr_b16 reads
+// rows s .. s+3 and the other group of its half-wave rows s+8 .. s+11, but a 128-B row covers
+// only half of the 64 banks, so rows two apart collide; block b of row r sits in block
+// b ^ (bit 1 of r | bit 3 of r << 1), which puts those eight rows on eight distinct 8-bank sets
+// for any s (adding 8 toggles bit 3 only, adding 2 to an even row toggles bit 1)
+__device__ __forceinline__ int wp_flip64(int r) { return ((r >> 1) & 1) | ((r >> 2) & 2); }
+
+// plane index of channel block `blk` (16 channels) of row r (row width `rw` channels: 96 and
+// 32 keep the bit-3 flip of two 32-B blocks, 64 the two-bit flip above)
 __device__ __forceinline__ int wp_idx(int r, int rw, int blk) {
+  if (rw == 64) return r * 64 + ((blk ^ wp_flip64(r)) << 4);
   return r * rw + ((blk ^ ((r >> 3) & 1)) << 4);
 }
 
@@ -202,7 +211,7 @@ __global__ __launch_bounds__(CO == 96 ? 256 : 192, 2) void k_wgrad3p(WgradArgs a
   // A (G planes [px][96]): lane 4q+p of group lg supplies row 8lg + 4t + q, columns 4p..4p+3
   // of block 3wm + i, i.e. block (3wm + i) ^ (lg & 1) of the row
   const int abase = (8 * lg + (li >> 2)) * C::GRW + 4 * (li & 3);
-  const int aflip = lg & 1;
+  const int aflip = C::GRW == 64 ? wp_flip64(8 * lg + (li >> 2)) : lg & 1;  // (+4t: same flip)
   // B (X planes [xp][32]): stage pixel 8lg + j = (row pr0, column pc0 + j); tap (ky, kx), read t
   // -> X row r0 + d, d = ky*XW + kx + 4t, r0 = pr0*XW + pc0 + (li >> 2), in block wn ^ bit 3 of
   // the row.  Bit k of bmask: that flip for the k-th (ky, kx, t)
@@ -211,10 +220,14 @@ __global__ __launch_bounds__(CO == 96 ? 256 : 192, 2) void k_wgrad3p(WgradArgs a
   const int bbase = C::GPL + r0 * C::XRW + 16 * wn + 4 * (li & 3);
   const int bsgn = (wn & 1) ? -16 : 16;
   unsigned bmask0 = 0;
+  // 64-channel rows (CO = 48): the block wn ^ flip of the k-th read, two bits per read
+  const int bbase64 = C::GPL + r0 * C::XRW + 4 * (li & 3);
+  unsigned bm64[2] = {0u, 0u};
 #pragma unroll
   for (int k = 0; k < 18; ++k) {
     const int d = (k >> 1) / 3 * XW + (k >> 1) % 3 + 4 * (k & 1);
     bmask0 |= (unsigned)(((r0 + d) >> 3) & 1) << k;
+    bm64[k >> 4] |= (unsigned)(wn ^ wp_flip64(r0 + d)) << (2 * (k & 15));
   }
   bf16x8 ones;
 #pragma unroll
@@ -239,8 +252,9 @@ __global__ __launch_bounds__(CO == 96 ? 256 : 192, 2) void k_wgrad3p(WgradArgs a
     if (more) load_g(pn);  // in flight during the first kernel row's MFMAs (GL: the whole stage)
     if (GL && more) load_x(pn);
     int aoff = abase;
-    unsigned bmask = bmask0;
+    unsigned bmask = bmask0, bml = bm64[0], bmh = bm64[1];
     asm volatile("" : "+v"(aoff), "+v"(bmask));  // (addresses formed here, not held across stages)
+    if (C::XRW == 64) asm volatile("" : "+v"(bml), "+v"(bmh));
     bf16x8 av[3][MFW];
 #pragma unroll
     for (int i = 0; i < MFW; ++i) {
@@ -261,8 +275,15 @@ __global__ __launch_bounds__(CO == 96 ? 256 : 192, 2) void k_wgrad3p(WgradArgs a
       for (int kx = 0; kx < 3; ++kx) {
         const int k = 2 * (3 * ky + kx);
         const int d = ky * XW + kx;
-        const int oa = bbase + d * C::XRW + (int)((bmask >> k) & 1) * bsgn;
-        const int ob = bbase + (d + 4) * C::XRW + (int)((bmask >> (k + 1)) & 1) * bsgn;
+        int oa, ob;
+        if (C::XRW == 64) {
+          const unsigned m = k < 16 ? bml : bmh;
+          oa = bbase64 + d * 64 + (int)(((m >> (2 * (k & 15))) & 3) << 4);
+          ob = bbase64 + (d + 4) * 64 + (int)(((m >> (2 * ((k + 1) & 15))) & 3) << 4);
+        } else {
+          oa = bbase + d * C::XRW + (int)((bmask >> k) & 1) * bsgn;
+          ob = bbase + (d + 4) * C::XRW + (int)((bmask >> (k + 1)) & 1) * bsgn;
+        }
         bf16x8 bv[3][1];
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) bv[pl][0] = tr_frag(buf + pl * C::PL + oa, buf + pl * C::PL + ob);

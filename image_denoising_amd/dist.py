@@ -108,8 +108,10 @@ def allreduce_grads_split(flat_grad: torch.Tensor, tail_begin: int, run_backward
     first) is final; that bucket's all-reduce is enqueued on `comm_stream` behind the event,
     so it runs while the encoder's gradients are still being computed, and the encoder bucket
     flat_grad[:tail_begin] follows on the current stream behind the whole backward.  The
-    current stream then waits for both.  Sums are elementwise, so the result equals
-    allreduce_grads' bit for bit.  CPU tensors (the gloo tests): run_backward(None), then the
+    current stream then waits for both.  At world 2 every element is one a + b, so the result
+    equals allreduce_grads' bit for bit; from 3 ranks on, a ring all-reduce's per-element
+    summation order follows the chunk the element falls in, and moving the chunk boundaries
+    (two buckets) may change the last bits: equal up to fp32 summation order.  CPU tensors (the gloo tests): run_backward(None), then the
     same two buckets in the same order.  Returns 1/world like allreduce_grads."""
     if not is_initialized():
         run_backward(None)

@@ -53,7 +53,10 @@ class N2NTrainer:
         self.grad = torch.zeros_like(net.flat_params)
         self.global_step = 0
         self._bufs = {}
-        self._overlap = os.environ.get("DN_AR_OVERLAP", "1") != "0"
+        # the overlapped all-reduce needs the split backward (arch_unet.UNet); other nets
+        # (ImprovedUNet) take the one all-reduce after the whole backward
+        self._overlap = (os.environ.get("DN_AR_OVERLAP", "1") != "0"
+                         and hasattr(net, "_run_backward_split") and hasattr(net, "tail_begin"))
         self._tail_begin = net.tail_begin() if self.distributed and self._overlap else 0
 
     _side = {}

@@ -139,15 +139,25 @@ def _cpu_stand_ins(net, tr):
     from image_denoising_amd import _lib
     from oracle import n2n_ref, unet_ref
 
+    from image_denoising_amd import ImprovedUNet
+    from oracle import iunet_ref
+
     _lib.stream_of = lambda t: None
     saved = {}
+    iunet = isinstance(net, ImprovedUNet)
 
     def run_forward(x, y, ws):
         saved[ws.data_ptr()] = x.detach().clone()
+        ref = iunet_ref if iunet else unet_ref
         with torch.no_grad():
-            y.copy_(unet_ref.forward(net.flat_params, x, net.in_nc, net.out_nc))
+            y.copy_(ref.forward(net.flat_params, x, net.in_nc, net.out_nc))
 
     def run_backward(dy, dflat, ws, N, H, W, dx=None):
+        if iunet:  # autograd through the ImprovedUNet restatement
+            p = net.flat_params.detach().clone().requires_grad_(True)
+            iunet_ref.forward(p, saved[ws.data_ptr()], net.in_nc, net.out_nc).backward(dy)
+            dflat.copy_(p.grad)
+            return
         _, g = unet_ref.forward_backward(net.flat_params, saved[ws.data_ptr()], dy, net.in_nc,
                                          net.out_nc)
         dflat.copy_(g)
@@ -236,7 +246,12 @@ def _run_trainer(kind, rank, world, steps=2):
     from image_denoising_amd.trainer import N2NTrainer, StructureTrainer
 
     torch.manual_seed(0)
-    net = UNet(1, 1, 48)
+    if kind == "n2n_iunet":  # N2NTrainer(ImprovedUNet): no split backward, one all-reduce
+        from image_denoising_amd import ImprovedUNet
+
+        net = ImprovedUNet(1, 1, 48)
+    else:
+        net = UNet(1, 1, 48)
     if rank == 1:  # replicas differ before the trainer's broadcast
         with torch.no_grad():
             net.flat_params.add_(0.5)
@@ -261,7 +276,7 @@ def _run_trainer(kind, rank, world, steps=2):
         losses = [tr.train_step(clean[sl], noisy[sl]).clone() for _ in range(steps)]
         flat = torch.cat([model.adapter.flat_params, net.flat_params]).clone()
         return torch.stack(losses), tr.grad / world, flat
-    tr = (N2NTrainer(net, distributed=dist_on) if kind == "n2n"
+    tr = (N2NTrainer(net, distributed=dist_on) if kind in ("n2n", "n2n_iunet")
           else StructureTrainer(net, distributed=dist_on))
     _cpu_stand_ins(net, tr)
     clean, noisy, rd = _trainer_inputs()
@@ -270,7 +285,7 @@ def _run_trainer(kind, rank, world, steps=2):
     cells = (TH // 2) * (TW // 2)
     losses = []
     for _ in range(steps):
-        if kind == "n2n":
+        if kind in ("n2n", "n2n_iunet"):
             l = tr.train_step(clean[sl], epoch=1, rd_idx=rd[rank * b * cells:(rank + 1) * b * cells],
                               noisy=noisy[sl])
         else:
@@ -330,9 +345,10 @@ def _spawn(target, args, nproc, nargs=None):
     return got
 
 
-@pytest.mark.parametrize("kind", ["n2n", "structure", "finetune"])
+@pytest.mark.parametrize("kind", ["n2n", "structure", "finetune", "n2n_iunet"])
 def test_two_rank_product_trainer_equals_full_batch(kind):
-    """N2NTrainer / StructureTrainer / FinetuneTrainer(distributed=True) on 2 gloo ranks == the
+    """N2NTrainer (UNet and ImprovedUNet) / StructureTrainer / FinetuneTrainer(distributed=True)
+    on 2 gloo ranks == the
     single-process
     trainer on the concatenated batch: broadcast (rank 1 starts perturbed), gradient all-reduce
     and the 1/world grad_scale into Adam, over two steps (Adam state carried)."""
@@ -340,7 +356,10 @@ def test_two_rank_product_trainer_equals_full_batch(kind):
     assert np.array_equal(flats[0], flats[1])  # replicas identical after two updates
     losses, g, flat = _spawn(_single_worker, (kind,), 1)
     assert np.abs(losses_dp - losses).max() <= 1e-5 * np.abs(losses).max()
-    assert np.abs(grad_dp - g).max() <= 1e-4 * np.abs(g).max()
+    # (ImprovedUNet: GroupNorm + sigmoids amplify the fp32 summation-order noise of the CPU
+    # convolutions' batch-dependent reductions to ~2e-4 of max |g|)
+    gtol = 1e-3 if kind == "n2n_iunet" else 1e-4
+    assert np.abs(grad_dp - g).max() <= gtol * np.abs(g).max()
     # Adam's first steps move each weight by ~lr*sign(g): a gradient within rounding of 0 may
     # take the other sign in either summation order; everything else agrees to rounding
     d = np.abs(flats[0] - flat)
@@ -351,7 +370,9 @@ def test_two_rank_product_trainer_equals_full_batch(kind):
 def test_two_rank_bucketed_allreduce_equals_one_allreduce():
     """N2NTrainer's overlapped all-reduce (two buckets: the decoder + head range the backward
     finishes first, then the encoder; DN_AR_OVERLAP=1, the default) gives the single
-    all-reduce's step bit for bit (DN_AR_OVERLAP=0): sums are elementwise"""
+    all-reduce's step bit for bit (DN_AR_OVERLAP=0).  That holds at world 2, where every element
+    is one a + b whatever the buckets; from 3 ranks on a ring all-reduce's summation order per
+    element depends on its chunk, so the two agree only to fp32 summation order."""
     port = _free_port()
     bucketed = _spawn(_trainer_worker, (2, port, "n2n", "1"), 2, nargs=3)
     one = _spawn(_trainer_worker, (2, _free_port(), "n2n", "0"), 2, nargs=3)

@@ -469,15 +469,20 @@ def test_unet_forward_prepacked_equals_forward(prec):
     assert torch.equal(pre, new)
 
 
+@pytest.mark.parametrize("unit_gain", [False, True])
 @pytest.mark.parametrize("rdk", ["h", "v", "mixed"])
-def test_unet_forward_n2n_pair_pixels_vs_oracle(rdk):
+def test_unet_forward_n2n_pair_pixels_vs_oracle(rdk, unit_gain):
     """The Winograd pair pass (8 x 128^2: k_c3w6s for both tile orientations) against the CPU
-    oracle of arch_unet.UNet.forward in fp64 at the pair pixels, reference initialisation:
-    1e-4 of max |y| (north_star's fp32 tolerance on the denoised image)."""
+    oracle of arch_unet.UNet.forward in fp64 at the pair pixels: 1e-4 of max |y| (north_star's
+    fp32 tolerance on the denoised image).  At the reference initialisation the deep paths are
+    ~1e-10 of y, so the unit-gain variant (every level O(1), _unit_gain) is the one that checks
+    the encoder and the bottleneck through the pair pass too."""
     from oracle import unet_ref
 
     C, N, H, W = 1, 8, 128, 128
     net = _net(C, "fp32_x6")
+    if unit_gain:
+        _unit_gain(net)
     g = torch.Generator().manual_seed(5)
     x = torch.rand(N, C, H, W, generator=g)
     rd = _rd_set(rdk, N * (H // 2) * (W // 2), g)
@@ -727,6 +732,55 @@ def test_config1_full_size_step_properties(prec):
     sel = _pair_mask(tr.last_rd[:2 * 128 * 128].cpu(), 2, 256, 256)
     assert rel_err(den0.numpy()[sel], ref.numpy()[sel]) < FP32_TOL
     assert torch.isfinite(tr.grad).all()
+
+
+def _layer_errs(got, want, C=1):
+    """per-layer max-norm relative error of two flat parameter-sized vectors"""
+    from oracle.unet_ref import layer_table
+
+    out, off = {}, 0
+    for name_, ws, bl, _ in layer_table(C, C):
+        n = int(np.prod(ws)) + bl
+        out[name_] = rel_err(got[off:off + n], want[off:off + n])
+        off += n
+    return out
+
+
+@pytest.mark.parametrize("prec", PRECS)
+def test_config1_full_size_step_vs_oracle(prec):
+    """The headline workload itself (BASELINE configs[1]: 64 x 1 x 256^2, reference init): one
+    N2N step on the device and on the CPU oracle (unet_ref.n2n_step: torch autograd of the
+    fp32 restatement, torch.optim.Adam; training_script.md:137-155, train.py:359-368) from the
+    same noisy batch and the same rd_idx.  loss1 and loss within 1e-4; the flat gradient per
+    layer within 1e-3 of the oracle's fp32 gradient (the per-layer bound of
+    test_unet_forward_backward_vs_reference: LeakyReLU slope flips at pre-activations within
+    rounding of 0); the Adam update as test_n2n_step_vs_reference checks it (first-step updates
+    are ~lr * sign(g), so only gradients within rounding of zero may differ, by <= 2 lr)."""
+    from image_denoising_amd import N2NTrainer
+    from oracle import unet_ref
+
+    N, H = 64, 256
+    net = _net(1, prec)
+    flat0 = net.flat_params.detach().cpu().clone()
+    g = torch.Generator(device="cpu").manual_seed(7)
+    clean = F.interpolate(torch.rand(N, 1, 32, 32, generator=g), size=(H, H), mode="bilinear",
+                          align_corners=False)
+    noisy = (clean + (25.0 / 255.0) * torch.randn(clean.shape, generator=g)).float()
+    rd = torch.randint(0, 8, (N * (H // 2) * (H // 2),), generator=g, dtype=torch.int64)
+    tr = N2NTrainer(net, lr=3e-4, n_epoch=100, increase_ratio=2.0)
+    loss3 = tr.train_step(noisy.to(DEV), epoch=1, rd_idx=rd.to(torch.uint8).to(DEV),
+                          noisy=noisy.to(DEV)).cpu().numpy()
+    grad = tr.grad.cpu().numpy()
+    post = net.flat_params.detach().cpu().numpy()
+    r = unet_ref.n2n_step(flat0, noisy, rd.numpy().astype(np.uint8), tr.lambda_for(1))
+    assert abs(loss3[0] - r["loss1"]) <= FP32_TOL * r["loss1"], (loss3, r["loss1"])
+    assert abs(loss3[2] - r["loss"]) <= FP32_TOL * r["loss"], (loss3, r["loss"])
+    errs = _layer_errs(grad, r["grad"].numpy())
+    assert max(errs.values()) < 1e-3, errs
+    upd, ref_upd = post - flat0.numpy(), r["params"].numpy() - flat0.numpy()
+    bad = np.abs(upd - ref_upd) > 1e-6
+    assert bad.mean() < 2e-3, bad.mean()
+    assert np.abs(upd - ref_upd).max() <= 6.1e-4  # never more than 2*lr apart
 
 
 @pytest.mark.parametrize("prec", PRECS)
