@@ -19,7 +19,7 @@ CSRC = os.path.join(PKG, "csrc")
 TAG = os.environ.get("DN_BUILD_TAG", "")
 BUILD = os.path.join(PKG, "_objs" + (f"_{TAG}" if TAG else ""))
 LIB = os.path.join(PKG, "libdenoise_hip" + (f"_{TAG}" if TAG else "") + ".so")
-SOURCES = ["conv.hip", "conv_bf16.hip", "conv_x6.hip", "conv_x6r.hip", "conv_w6.hip", "wgrad_x6p.hip", "elementwise.hip", "first_layer.hip", "eval.hip", "adapter.hip", "iunet_ops.hip", "unet.cpp",
+SOURCES = ["conv.hip", "conv_bf16.hip", "conv_x6.hip", "conv_w6.hip", "wgrad_x6p.hip", "elementwise.hip", "first_layer.hip", "eval.hip", "adapter.hip", "iunet_ops.hip", "unet.cpp",
            "iunet.cpp", "capi.cpp", "profile.cpp"]
 HEADERS = ["dn_internal.h", "conv_epi.h", "x6_core.h", "philox.h", "unet.h", "iunet.h", "iunet_ops.h"]
 ARCH = os.environ.get("DN_OFFLOAD_ARCH", "gfx950")
@@ -29,7 +29,7 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
             *os.environ.get("DN_EXTRA_CXXFLAGS", "").split()]
 # the bf16x6 kernels keep their fp32 adds scalar: the SLP vectorizer would pair them into
 # v_pk_add_f32, which costs more issue cycles beside MFMAs than the two adds (x6_core.h)
-FILE_FLAGS = {"conv_x6.hip": ["-fno-slp-vectorize"], "conv_x6r.hip": ["-fno-slp-vectorize"],
+FILE_FLAGS = {"conv_x6.hip": ["-fno-slp-vectorize"],
               "conv_w6.hip": ["-fno-slp-vectorize"], "wgrad_x6p.hip": ["-fno-slp-vectorize"]}
 
 

@@ -1172,14 +1172,9 @@ hipError_t launch_fwd(int gather, const FwdArgs& a, hipStream_t s) {
     if (nt == 6) return mt == 4 ? run_fwd<G_C3, 6, 4>(a, s) : mt == 2 ? run_fwd<G_C3, 6, 2>(a, s) : run_fwd<G_C3, 6, 1>(a, s);
     if (nt == 9) return mt == 2 ? run_fwd<G_C3, 9, 2>(a, s) : run_fwd<G_C3, 9, 1>(a, s);
   } else if (gather == G_C1) {
-    static const int c1_mt = getenv("DN_C1_MT") ? atoi(getenv("DN_C1_MT")) : 2;  // tuning probe
     if (nt == 1) return run_fwd<G_C1, 1, 4>(a, s);
     if (nt == 3) return small ? run_fwd<G_C1, 3, 1>(a, s) : run_fwd<G_C1, 3, 4>(a, s);
-    if (nt == 6) {
-      if (small || c1_mt == 1) return run_fwd<G_C1, 6, 1>(a, s);
-      if (c1_mt == 2) return run_fwd<G_C1, 6, 2>(a, s);
-      return run_fwd<G_C1, 6, 4>(a, s);
-    }
+    if (nt == 6) return small ? run_fwd<G_C1, 6, 1>(a, s) : run_fwd<G_C1, 6, 2>(a, s);
   } else if (gather == G_UP) {
     if (a.out_layout != OUT_UP2) return hipErrorInvalidValue;
     if (nt == 3) return run_fwd<G_UP, 3, 4>(a, s);
@@ -1275,15 +1270,9 @@ int wgrad_splits(int mode, int N, int KH, int KW, int Cin, int Cout) {
   long want = 768 / cib;
   const long slab_cap = (64L << 20) / ((long)Cout * Cin * taps + Cout);  // <= 256 MB of slab
   if (want > slab_cap) want = slab_cap;
-  // at least MU pixel chunks per split (DN_WG_MIN_UNITS, default 2): on the small levels the
-  // per-workgroup slab (up to 110 KB written, then re-read by the reduction) outweighs the work
-  // of a 2-chunk split
-  static const int mu_env = getenv("DN_WG_MIN_UNITS") ? atoi(getenv("DN_WG_MIN_UNITS")) : 2;
-  // (DN_WG_MIN_UNITS96: the same for the 96-output 3x3 layers, whose per-split slab is twice a
-  // 48-output one's; default = DN_WG_MIN_UNITS)
-  static const int mu96_env = getenv("DN_WG_MIN_UNITS96") ? atoi(getenv("DN_WG_MIN_UNITS96")) : mu_env;
-  const int mu = (mode == W_C3 && Cout == 96 ? mu96_env : mu_env) < 1 ? 1 : (mode == W_C3 && Cout == 96 ? mu96_env : mu_env);
-  if (want > units / mu) want = units / mu;
+  // at least 2 pixel chunks per split: on the small levels the per-workgroup slab (up to 110 KB
+  // written, then re-read by the reduction) outweighs the work of a 1-chunk split
+  if (want > units / 2) want = units / 2;
   if (want < 1) want = 1;
   return (int)want;
 }

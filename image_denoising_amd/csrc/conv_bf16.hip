@@ -209,9 +209,6 @@ __global__ __launch_bounds__(256, 2) void k_fwd_bf16(FwdArgs a) {
 // is hidden behind two weight stages instead of stalling the stage it was issued in (k_fwd_bf16
 // waits for it at that stage's barrier).
 // ------------------------------------------------------------------------------------
-#ifndef DN_BF_ABL_XWAIT
-#define DN_BF_ABL_XWAIT 0
-#endif
 #define BF_WAITCNT_VM(n) \
   __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
 
@@ -347,9 +344,7 @@ __global__ __launch_bounds__(256, (NT * MT > 24) ? 1 : 2) void k_fwd_bf16p(FwdAr
       store_x();
     }
     // own DMAs of stage st+1 landed; younger: the next chunk's x loads (issued at ky == 0)
-    // (DN_BF_ABL_XWAIT: diagnostic ablation, wrong results -- stage ky == 1 does not wait for the
-    // next chunk's x loads, so its weight DMA for ky == 2 may not have landed; timing only)
-    if ((ky == 0 || (DN_BF_ABL_XWAIT && ky == 1)) && more) BF_WAITCNT_VM(C::XITEMS);
+    if (ky == 0 && more) BF_WAITCNT_VM(C::XITEMS);
     else BF_WAITCNT_VM(0);
     if (xstep) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own x-tile stores done
     bf_barrier();
@@ -466,17 +461,13 @@ hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize) {
     return small ? run_bf16<6, 1, false>(a, s) : run_bf16<6, 4, false>(a, s);
   }
   // pipelined kernel: aligned views, whole channel quads, < 2 GiB of input rows per tile
-  static const bool pipe_env = !getenv("DN_BF16_PIPE") || atoi(getenv("DN_BF16_PIPE")) != 0;
-  // rows per wave: 96-output convs 4 (DN_BF16_MT=6: one workgroup per CU, slower); 48-output
-  // convs 8 -- fewer LDS fragment reads per MFMA at the same occupancy -- where the grid still
-  // has >= 4096 such tiles (8 rounds of 512 resident workgroups), else 4 (DN_BF16_MT3: 4 / 8
-  // forces it).  The accumulation order does not depend on MT: bit-identical results.
-  static const int mt6 = getenv("DN_BF16_MT") && atoi(getenv("DN_BF16_MT")) == 6 ? 6 : 4;
-  static const int mt3e = getenv("DN_BF16_MT3") ? atoi(getenv("DN_BF16_MT3")) : 0;
+  // rows per wave: 96-output convs 4 (6 needs the whole register file: one workgroup per CU,
+  // slower); 48-output convs 8 -- fewer LDS fragment reads per MFMA at the
+  // same occupancy -- where the grid still has >= 4096 such tiles (8 rounds of 512 resident
+  // workgroups), else 4.  The accumulation order does not depend on MT: bit-identical results.
   const long tiles8 = (long)a.N * ((a.OH + 31) / 32) * ((a.OW + 15) / 16);
-  const int mt3 = mt3e == 4 || mt3e == 8 ? mt3e : (tiles8 >= 4096 ? 8 : 4);
-  const int mt = nt == 3 ? mt3 : mt6;
-  const bool pipe = pipe_env && !small && a.out_layout == OUT_NHWC && a.K % 4 == 0 &&
+  const int mt = nt == 3 ? (tiles8 >= 4096 ? 8 : 4) : 4;
+  const bool pipe = !small && a.out_layout == OUT_NHWC && a.K % 4 == 0 &&
                     ((a.in_stride | a.in_off) & 3) == 0 &&
                     (long)BCfg<6, 8, true>::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL;
   if (pipe) {
@@ -493,8 +484,7 @@ hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize) {
       if (mt == 8) DN_BF16P_LAUNCH(3, 8);
       else DN_BF16P_LAUNCH(3, 4);
     } else {
-      if (mt == 6) DN_BF16P_LAUNCH(6, 6);
-      else DN_BF16P_LAUNCH(6, 4);
+      DN_BF16P_LAUNCH(6, 4);
     }
 #undef DN_BF16P_LAUNCH
     return hipGetLastError();

@@ -58,16 +58,8 @@ struct WCfg {
 // over XOR swizzles in the bits of j, row and a permutation of kq against gfx950's LDS lane groups
 // (MI355X_MICROARCH.md); the round-3 swizzle p ^ (j >> 2) ^ ((row & 1) << 1) ^ kq left the reads
 // 2-way (SQ_LDS_BANK_CONFLICT 37 % of the LDS-active cycles of k_c3w6<1>, profiles/r4_pmc_sq_n2n.txt).
-// DN_W6_SWZ=0 builds the round-3 swizzle (A/B).
-#ifndef DN_W6_SWZ
-#define DN_W6_SWZ 1
-#endif
 __device__ __forceinline__ int w6_vq(int row, int kq, int j, int p) {
-#if DN_W6_SWZ
   return ((row * 4 + kq) * 8 + j) * 4 + (p ^ (row & 1) ^ (((kq & 1) << 1) | (kq >> 1)));
-#else
-  return ((row * 4 + kq) * 8 + j) * 4 + (p ^ (j >> 2) ^ ((row & 1) << 1) ^ kq);
-#endif
 }
 
 // 8-B slot of V element (row, j, p) of a tail-mode-1 chunk (<= 4 channels: one bf16x4 per
@@ -85,23 +77,15 @@ __device__ __forceinline__ void w6_barrier() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-// diagnostic ablations (wrong results, timing only): NOT = V built for the first chunk only,
-// NOW = no weight loads in the stage loop
+// diagnostic ablations (wrong results, timing only; tools/probes/r5_w6abl.sh): NOT = V built for
+// the first chunk only, NOW = no weight loads in the stage loop
 #ifndef DN_W6_ABL_NOT
 #define DN_W6_ABL_NOT 0
 #endif
 #ifndef DN_W6_ABL_NOW
 #define DN_W6_ABL_NOW 0
 #endif
-#ifndef DN_W6_EARLY
-#define DN_W6_EARLY 0  // 1: the next chunk's x loads before the chunk-end barrier; 2: before its last stage
-#endif
-#ifndef DN_W6_TG
-#define DN_W6_TG 3  // transform items whose x loads are in flight together
-#endif
-#ifndef DN_W6_GM
-#define DN_W6_GM 1
-#endif
+constexpr int W6_TG = 3;  // transform items whose x loads are in flight together
 
 template <int I0, int N, class F>
 __device__ __forceinline__ void w6_for(F&& f) {
@@ -157,10 +141,10 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
     constexpr int C4 = decltype(c4tag)::value, NIT = C::IH * C::NJ * C4;
     constexpr int VIT = (NIT + C::WAVES * 64 - 1) / (C::WAVES * 64);
 #pragma unroll
-    for (int ig = 0; ig < VIT; ig += DN_W6_TG) {
+    for (int ig = 0; ig < VIT; ig += W6_TG) {
     f32x4 d[C::VITEMS][4];
 #pragma unroll
-    for (int it = ig; it < ig + DN_W6_TG && it < VIT; ++it) {
+    for (int it = ig; it < ig + W6_TG && it < VIT; ++it) {
       const int e = tid + it * C::WAVES * 64;
       const int c4 = e % C4, j = (e / C4) & 7, row = e / (8 * C4);
       const int gy = iy0 + row, k = k0 + 4 * c4;
@@ -174,7 +158,7 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
       }
     }
 #pragma unroll
-    for (int it = ig; it < ig + DN_W6_TG && it < VIT; ++it) {
+    for (int it = ig; it < ig + W6_TG && it < VIT; ++it) {
       const int e = tid + it * C::WAVES * 64;
       if (e < NIT) {
         const int c4 = e % C4, j = (e / C4) & 7, row = e / (8 * C4);
@@ -200,54 +184,6 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
         }
       }
     }
-    }
-  };
-
-  // the same for a full chunk in two halves: its x loads (tload, into d) and the V writes
-  // (twrite) -- the loads of chunk c+1 issued before the barrier that ends chunk c (DN_W6_EARLY)
-  constexpr int NIT8 = C::IH * C::NJ * 8;
-  auto tload = [&](int k0, int tid, f32x4 (&d)[C::VITEMS][4]) {
-#pragma unroll
-    for (int it = 0; it < C::VITEMS; ++it) {
-      const int e = tid + it * C::WAVES * 64;
-      const int c4 = e & 7, j = (e >> 3) & 7, row = e >> 6;
-      const int gy = iy0 + row, k = k0 + 4 * c4;
-      const bool rok = e < NIT8 && gy >= 0 && gy < a.IHt && k < a.K;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int gx = ix0 + 2 * j + i;
-        const bool ok = rok && gx >= 0 && gx < a.IWt;
-        const int off = ok ? (((gy - ry0) * a.IWt + gx) * a.in_stride + k) * 4 : 0x7fffffff;
-        d[it][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-      }
-    }
-  };
-  auto twrite = [&](int tid, const f32x4 (&d)[C::VITEMS][4]) {
-#pragma unroll
-    for (int it = 0; it < C::VITEMS; ++it) {
-      const int e = tid + it * C::WAVES * 64;
-      if (e < NIT8) {
-        const int c4 = e & 7, j = (e >> 3) & 7, row = e >> 6;
-        f32x4 v[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          v[0][c] = d[it][0][c] - d[it][2][c];
-          v[1][c] = d[it][1][c] + d[it][2][c];
-          v[2][c] = d[it][2][c] - d[it][1][c];
-          v[3][c] = d[it][1][c] - d[it][3][c];
-        }
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          unsigned h0, m0, l0, h1, m1, l1;
-          split3x2(v[p][0], v[p][1], h0, m0, l0);
-          split3x2(v[p][2], v[p][3], h1, m1, l1);
-          const int o = w6_vq(row, c4 >> 1, j, p) * 8 + (c4 & 1) * 4;
-          typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
-          *reinterpret_cast<u32x2_t*>(lv + o) = u32x2_t{h0, h1};
-          *reinterpret_cast<u32x2_t*>(lv + C::VPL + o) = u32x2_t{m0, m1};
-          *reinterpret_cast<u32x2_t*>(lv + 2 * C::VPL + o) = u32x2_t{l0, l1};
-        }
-      }
     }
   };
 
@@ -327,18 +263,14 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
       constexpr int PI = decltype(pic)::value;
 #pragma unroll
       for (int q = 0; q < NTW; ++q) {
-        constexpr int GM = DN_W6_GM;  // M fragments per MFMA group
 #pragma unroll
-        for (int mp = 0; mp < MT / GM; ++mp) {
-          f32x4(&ah)[GM][NTW] = *reinterpret_cast<f32x4(*)[GM][NTW]>(&acc[PI][GM * mp]);
-          bf16x8 a2[3][GM];
+        for (int mp = 0; mp < MT; ++mp) {  // one M fragment per MFMA group
+          f32x4(&ah)[1][NTW] = *reinterpret_cast<f32x4(*)[1][NTW]>(&acc[PI][mp]);
+          bf16x8 a2[3][1];
 #pragma unroll
-          for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-            for (int i = 0; i < GM; ++i) a2[pl][i] = av[pl][GM * mp + i];
-          x6_group<GM, NTW, 1>(ah, a2, w, q);
-#pragma unroll
-          for (int i = 0; i < GM; ++i) asm volatile("" : "+v"(ah[i][q]));
+          for (int pl = 0; pl < 3; ++pl) a2[pl][0] = av[pl][mp];
+          x6_group<1, NTW, 1>(ah, a2, w, q);
+          asm volatile("" : "+v"(ah[0][q]));
           __builtin_amdgcn_sched_barrier(0);
         }
         if (nxt >= 0 && !DN_W6_ABL_NOW) load_wq(nxt, q);
@@ -354,33 +286,21 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
 #pragma unroll
   for (int q = 0; q < NTW; ++q) load_wq(stage_of(0, 0, tail_only), q);
   const int nfull = TAIL ? nch - 1 : nch;  // full chunks; a tail-packed last one after the loop
-  f32x4 dx[C::VITEMS][4];  // (DN_W6_EARLY) the next full chunk's x, loaded before its barrier
 #pragma unroll 1
   for (int c = 0; c < nfull; ++c) {
     int liv = li, lgv = lg, tidv = tid;
     asm volatile("" : "+v"(liv), "+v"(lgv), "+v"(tidv));
     const bool more = c + 1 < nch;
     const bool next_tail = TAIL && c + 2 == nch;
-    if (!DN_W6_EARLY || c == 0) {
-      if (c > 0) w6_barrier();  // every wave is done with the previous chunk's V
-      if (!DN_W6_ABL_NOT || c == 0) transform(std::integral_constant<int, 8>{}, c * C::KC, tidv);
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own V stores done
-      w6_barrier();
-    }
+    if (c > 0) w6_barrier();  // every wave is done with the previous chunk's V
+    if (!DN_W6_ABL_NOT || c == 0) transform(std::integral_constant<int, 8>{}, c * C::KC, tidv);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own V stores done
+    w6_barrier();
     w6_for<0, 6>([&](auto si) {
       constexpr int s = decltype(si)::value;
       const int nxt = s + 1 < 6 ? stage_of(c, s + 1, false) : (more ? stage_of(c + 1, 0, next_tail) : -1);
-      if constexpr (DN_W6_EARLY == 2 && s == 5)
-        if (c + 1 < nfull) tload((c + 1) * C::KC, tidv, dx);
       stage(std::integral_constant<int, 0>{}, s, nxt, liv, lgv);
     });
-    if (DN_W6_EARLY && c + 1 < nfull) {
-      if (DN_W6_EARLY == 1) tload((c + 1) * C::KC, tidv, dx);
-      w6_barrier();  // every wave is done with this chunk's V
-      twrite(tidv, dx);
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      w6_barrier();
-    }
   }
   if constexpr (TAIL != 0) {
     const int c = nch - 1;
@@ -498,9 +418,6 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
 // Output: the pair image [N][OH/2][OW][96] (column 2cj + s = pixel pair[rd][s] of cell (ci, cj)),
 // bias + LeakyReLU, as k_c3x6s writes it for the head.
 // ------------------------------------------------------------------------------------
-#ifndef DN_W6S_PF
-#define DN_W6S_PF 1
-#endif
 struct SCfgW {
   static constexpr int WAVES = 4, MT = 4, NTW = 3, NP = 96, CELLS = 64, KC = 32;
   static constexpr int VPL = 4 * CELLS * KC;        // bf16 per plane of V: [p][cell][32 ch]
@@ -571,38 +488,34 @@ __global__ __launch_bounds__(1024) void k_w6s_lists(const unsigned char* __restr
   }
 }
 
-// Block order (remap, DN_W6S_XCD=1): workgroup b runs on XCD b % 8; XCD x gets a contiguous run of
+// Block order: workgroup b runs on XCD b % 8; XCD x gets a contiguous run of
 // the logical order (image, 64-cell chunk, orientation), so the x-tile and y-tile workgroups of
 // the same cell rows, and the neighbouring chunks that share their input rows, run on one L2 at
 // about the same time (otherwise each input row is fetched from HBM by up to four workgroups
 // on different XCDs: 5.25 GB per launch for 1.6 GB of input, profiles/r4_n2n_pmc_step.json).
-__device__ __forceinline__ void w6s_block(int remap, int nchunk, int& o, int& n, int& chunk) {
+__device__ __forceinline__ void w6s_block(int nchunk, int& o, int& n, int& chunk) {
   const unsigned b = blockIdx.x, tot = gridDim.x;
   unsigned l = b;
-  if (remap && tot >= 8) {
+  if (tot >= 8) {
     const unsigned x = b % 8, base = tot / 8, extra = tot % 8;
     l = x * base + (x < extra ? x : extra) + b / 8;  // XCD x: (tot - x + 7) / 8 blocks
-    o = (int)(l & 1);
-    l >>= 1;
-  } else {  // round 4's first order: chunk fastest, then image, then orientation
-    o = (int)(l / (tot / 2));
-    l -= (unsigned)o * (tot / 2);
   }
+  o = (int)(l & 1);
+  l >>= 1;
   chunk = (int)(l % (unsigned)nchunk);
   n = (int)(l / (unsigned)nchunk);
 }
 
 __global__ __launch_bounds__(256, 2) void k_c3w6s(FwdArgs a, const unsigned* __restrict__ list,
                                                   const int* __restrict__ cnt,
-                                                  const __bf16* __restrict__ wpv, int nchunk,
-                                                  int remap) {
+                                                  const __bf16* __restrict__ wpv, int nchunk) {
   using C = SCfgW;
   constexpr int MT = C::MT, NTW = C::NTW;
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
   __shared__ unsigned lent[C::CELLS];
   __bf16* lv = reinterpret_cast<__bf16*>(lds_raw);
   int o, n, chunk;
-  w6s_block(remap, nchunk, o, n, chunk);
+  w6s_block(nchunk, o, n, chunk);
   const int cbase = chunk * C::CELLS;
   const int ncell = cnt[2 * n + o];
   if (cbase >= ncell) return;  // (uniform: the list is shorter than the grid allows)
@@ -728,23 +641,21 @@ __global__ __launch_bounds__(256, 2) void k_c3w6s(FwdArgs a, const unsigned* __r
   };
 #pragma unroll
   for (int q = 0; q < NTW; ++q) load_wq(2 * ph, q);
-  // DN_W6S_PF (default 1): the next phase's input pixels are requested right after this phase's
-  // V is written, so their latency runs under this phase's MFMAs instead of between the two
-  // barriers of the next transform (a tile has three phases per input chunk, each with its own
-  // gather from L2); 0: loaded inside the transform (A/B)
+  // the next phase's input pixels are requested right after this phase's V is written, so their
+  // latency runs under this phase's MFMAs instead of between the two barriers of the next
+  // transform (a tile has three phases per input chunk, each with its own gather from L2)
   const int nph = nch * 3;
-  if (DN_W6S_PF) tload(0, 0);
+  tload(0, 0);
 #pragma unroll 1
   for (int ph3 = 0; ph3 < nph; ++ph3) {
     const int c = ph3 / 3, k3 = ph3 - 3 * c;
     int liv = li, lgv = lg;
     asm volatile("" : "+v"(liv), "+v"(lgv));
     if (ph3 > 0) w6_barrier();  // every wave is done with the previous phase's V
-    if (!DN_W6S_PF) tload(c * C::KC, k3);
     twrite();
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own V stores done
     w6_barrier();
-    if (DN_W6S_PF && ph3 + 1 < nph) {
+    if (ph3 + 1 < nph) {
       const int c1 = (ph3 + 1) / 3;
       tload(c1 * C::KC, ph3 + 1 - 3 * c1);
     }
@@ -843,11 +754,10 @@ hipError_t launch_fwd_w6s(const FwdArgs& a, const unsigned* list, const int* cnt
   const long cells = (long)(a.OH / 2) * (a.OW / 2);
   const long nchunk = (cells + SCfgW::CELLS - 1) / SCfgW::CELLS;
   if (nchunk * a.N * 2 >= (1L << 31)) return hipErrorInvalidValue;
-  static const int remap = !getenv("DN_W6S_XCD") || atoi(getenv("DN_W6S_XCD")) != 0;
   const dim3 grid((unsigned)(nchunk * a.N * 2));
   prof_kernel("k_c3w6s");
   hipLaunchKernelGGL(k_c3w6s, grid, dim3(SCfgW::WAVES * 64), 0, s, a, list, cnt,
-                     static_cast<const __bf16*>(wpv), (int)nchunk, remap);
+                     static_cast<const __bf16*>(wpv), (int)nchunk);
   return hipGetLastError();
 }
 

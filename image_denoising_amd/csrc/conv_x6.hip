@@ -276,9 +276,6 @@ __device__ __forceinline__ void x6_barrier() {
 #endif
 // A/B switch: static priority 1 for waves 4-7 (the second-dispatched half, the arbitration
 // loser of every stage) before the main loop (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-#ifndef DN_X6_PRIO
-#define DN_X6_PRIO 0
-#endif
 #if DN_X6_STAMPS
 constexpr int X6_STAMP_SLOTS = 128;
 __device__ unsigned long long g_x6_stamps[64 * 2 * X6_STAMP_SLOTS];
@@ -314,7 +311,6 @@ __global__ __launch_bounds__(64 * WV, 1) void k_c3x6p(FwdArgs a) {
   int bxr, byr;  // XCD-aware tile order (conv_epi.h xcd_tile)
   xcd_tile(bxr, byr);
   const int ty0 = (bxr / tiles_x) * C::TH;
-  if (DN_X6_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int tx0 = (bxr % tiles_x) * C::TW;
   const int n = byr;
   const int iy0 = ty0 - 1, ix0 = tx0 - 1;
@@ -457,7 +453,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_c3x6p(FwdArgs a) {
     // MFMAs that use them -- so the first MFMA waits for 3 reads, not for all 6 A + 6 B reads
     // of a stage that all 8 waves issue together after the barrier (384 LDS cycles); the MFMA
     // order per accumulator is that of x6_group_c (results unchanged bit for bit)
-    constexpr bool STAGED = MODE == 0 && DN_X6_CARRY && QG == 1 && NG >= 3 && DN_X6P_STAGED;
+    constexpr bool STAGED = MODE == 0 && QG == 1 && NG >= 3 && DN_X6P_STAGED;
     if constexpr (STAGED) {
     } else if (mode == 1) {
       // im2col stage t: lane group lg holds k = 8lg..8lg+7 = channels 0..3 of taps
@@ -575,7 +571,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_c3x6p(FwdArgs a) {
       f32x4 hi[MTC];
 #pragma unroll
       for (int m = 0; m < MTC; ++m)
-        hi[m] = mfma_bf16(av[0][m], bv[0][0], DN_X6_ABL_CHAIN ? acc[m][0] : z);
+        hi[m] = mfma_bf16(av[0][m], bv[0][0], z);
       lo(0, 1);
       __builtin_amdgcn_sched_barrier(0);
       read_a(2); read_b(1);
@@ -588,7 +584,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_c3x6p(FwdArgs a) {
 #pragma unroll
       for (int m = 0; m < MTC; ++m)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[m][0][r] = DN_X6_ABL_CHAIN ? hi[m][r] : acc[m][0][r] + hi[m][r];
+        for (int r = 0; r < 4; ++r) acc[m][0][r] = acc[m][0][r] + hi[m][r];
       pin_group(0);
       __builtin_amdgcn_sched_barrier(0);
       if (DN_X6P_DMAI) load_w_piece(wsrc, wslot, 0);
@@ -721,7 +717,6 @@ __global__ __launch_bounds__(512, 1) void k_c3x6s(FwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lg = lane >> 4;
-  if (DN_X6_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
   int bxr, byr;  // XCD-aware tile order (conv_epi.h xcd_tile)
   xcd_tile(bxr, byr);
@@ -944,9 +939,6 @@ struct HCfg {
 #ifndef DN_X6H_LOOK
 #define DN_X6H_LOOK 2  // B fragment groups read ahead of their MFMAs in k_c3x6h
 #endif
-#ifndef DN_X6H_CARRY
-#define DN_X6H_CARRY 1  // A/B switch: 0 = per-block sums in k_c3x6h
-#endif
 #ifndef DN_X6H_CARRY4
 #define DN_X6H_CARRY4 1  // A/B switch: 1 = MT = 4 with NT <= 3 carries the corrections too (96 acc VGPRs)
 #endif
@@ -1068,8 +1060,8 @@ __global__ __launch_bounds__(256, 2) void k_c3x6h(FwdArgs a) {
     // MT = 4: the A pieces of two rows at a time (registers), the B fragments read once for all
     constexpr int MH = MT >= 4 ? 2 : MT;
     // MT = 4 keeps the per-block form (its 2 x 48 accumulators at NT = 6 leave no room for accl)
-    constexpr bool BLK = !DN_X6H_CARRY || (MT >= 4 && !(DN_X6H_CARRY4 && NT <= 3));
-    constexpr int QG = MT >= 4 ? 1 : (DN_X6H_CARRY ? x6_qgc(MT, NT) : x6_qg(MT, NT)), NG = NT / QG,
+    constexpr bool BLK = MT >= 4 && !(DN_X6H_CARRY4 && NT <= 3);
+    constexpr int QG = MT >= 4 ? 1 : x6_qgc(MT, NT), NG = NT / QG,
                   LOOK = NG < DN_X6H_LOOK ? NG : DN_X6H_LOOK;
     bf16x8 bv[3][NT];
     auto read_b = [&](int g) {
@@ -1579,9 +1571,8 @@ hipError_t launch_fwd_x6_sel(const FwdArgs& a, hipStream_t s) {
       a.out_layout != OUT_NHWC || a.epi != EPI_BIAS_ACT || (a.OH | a.OW) & 1 ||
       ((a.in_stride | a.in_off) & 3) || (long)C::IH * a.IWt * a.in_stride * 4 >= 0x7fffffffL)
     return hipErrorInvalidValue;
-  // 32-row tiles (k_c3x6s) unless DN_X6_SEL32=0 (the 16-row k_c3x6p<6,0,true>, A/B)
-  static const bool sel32_env = !getenv("DN_X6_SEL32") || atoi(getenv("DN_X6_SEL32")) != 0;
-  if (sel32_env && (long)SCfg::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL) {
+  // 32-row tiles (k_c3x6s), else the 16-row k_c3x6p<6,0,true>
+  if ((long)SCfg::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL) {
     const int tx = (a.OW + SCfg::TW - 1) / SCfg::TW, ty = (a.OH + SCfg::TH - 1) / SCfg::TH;
     prof_kernel("k_c3x6s");
     hipLaunchKernelGGL(k_c3x6s, dim3(tx * ty, a.N, 1), dim3(SCfg::WAVES * 64), 0, s, a);
@@ -1609,13 +1600,7 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
     return hipErrorInvalidValue;
   const int nz = a.zc > 0 ? (a.NOUT + a.zc - 1) / a.zc : 1;
   if (a.x6_tail & X6_W6) return launch_fwd_w6(a, s);  // a Winograd image (x6_image_mode)
-  // DN_X6_REG=1: the 96-channel large-grid shapes on k_c3x6r (weights in registers, conv_x6r.hip)
-  if (x6r_enabled() && np == 96 && (a.x6_tail || x6_pipelined(a.N, a.OH, a.OW, a.NOUT, a.zc))) {
-    hipError_t e = hipSuccess;
-    if (launch_fwd_x6r(a, s, e)) return e;
-  }
   // large grids: the pipelined 16-row kernel (one workgroup per CU, >= 2 rounds of tiles)
-  static const bool no_pipe = getenv("DN_X6_NOPIPE") != nullptr;  // A/B probe
   // the pipelined kernel addresses one tile's 18 input rows through a 32-bit buffer resource
   const bool aligned = ((a.in_stride | a.in_off | a.K) & 3) == 0 &&
                        (long)PCfg<6>::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL;
@@ -1624,15 +1609,13 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
   };
   // large grids: the two-workgroups-per-CU kernel where it measured faster (48 / 32 output
   // channels: -6..-11 %; a 4-channel tail chunk: -3.6 %), else the one-per-CU kernel (equal
-  // within noise on the 96-channel shapes; tools/x6_micro.py); DN_X6_HALF=0/1 forces either
-  static const int half_env = getenv("DN_X6_HALF") ? atoi(getenv("DN_X6_HALF")) : -1;
+  // within noise on the 96-channel shapes; tools/x6_micro.py)
   const bool half_fits = (long)HCfg<6>::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL;
-  const bool half = half_fits && (half_env >= 0 ? half_env != 0 : (np <= 48 || a.x6_tail == 1));
+  const bool half = half_fits && (np <= 48 || a.x6_tail == 1);
   // 48 / 32 output channels: 16-row tiles (4 rows per wave, twice the MFMAs per operand read
-  // and per stage barrier) when they fill two rounds of resident workgroups; DN_X6_H4=0 keeps 8
-  static const bool h4_env = !getenv("DN_X6_H4") || atoi(getenv("DN_X6_H4")) != 0;
+  // and per stage barrier) when they fill two rounds of resident workgroups
   const long tiles16 = (long)a.N * nz * ((a.OH + 15) / 16) * ((a.OW + 15) / 16);
-  const bool h4 = h4_env && np <= 48 && tiles16 >= 1024 &&
+  const bool h4 = np <= 48 && tiles16 >= 1024 &&
                   (long)HCfg<3, 4>::IH * a.IWt * a.in_stride * 4 < 0x7fffffffL;
   auto run = [&]() {
     if (half && h4) return np == 32 ? run_x6h<2, 4>(a, nz, s) : run_x6h<3, 4>(a, nz, s);
@@ -1644,7 +1627,7 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
     if (!aligned || a.x6_tail != x6_tail_mode(a.K)) return hipErrorInvalidValue;
     return run();
   }
-  if (!no_pipe && x6_pipelined(a.N, a.OH, a.OW, a.NOUT, a.zc) && aligned) return run();
+  if (x6_pipelined(a.N, a.OH, a.OW, a.NOUT, a.zc) && aligned) return run();
   // (a fused pool needs an even number of tile rows per wave: MT = 2)
   const bool pool = a.pool_out != nullptr;
   // small grids: k_c3x6h with the 3-slot weight ring where the shape allows (float4 rows; two
@@ -1677,9 +1660,6 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
 // added to the fp32 accumulators.  Wave (wm, wn): MFW output-channel fragments x 16 input
 // channels x 9 taps; the bias gradient is the G pieces against a ones fragment.
 // ------------------------------------------------------------------------------------
-#ifndef DN_WG_ABL_NOSPLIT
-#define DN_WG_ABL_NOSPLIT 0
-#endif
 template <int CO_FR, int WM, int WN>
 struct Ws3Cfg {
   static constexpr int COUT = 16 * CO_FR, MFW = CO_FR / WM, CIB = 16 * WN;
@@ -1692,23 +1672,14 @@ struct Ws3Cfg {
   static constexpr int LBUF = LGF + LXF;
 };
 
-// PL (DN_WG_PLANES): the stage's operands split ONCE into bf16 planes in LDS between two
-// barriers (each was split once per reading wave pair at the operand read: 4.8 non-MFMA VALU per
-// MFMA), one fp32 DMA buffer (the next stage's DMA overlaps this stage's MFMAs); G planes
-// [piece][co][32 px] (swizzled quads), X planes [piece][stage row][ci][pixel pair]
-template <int CO_FR, int WM, int WN, int SWL, bool PL = false>
+// (the 96-output layers and the encoder's 48-output ones run k_wgrad3p / k_wgrad3q,
+// wgrad_x6p.hip; this kernel serves the output-channel-blocked launches of ImprovedUNet)
+template <int CO_FR, int WM, int WN, int SWL>
 __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
   using C = Ws3Cfg<CO_FR, WM, WN>;
   constexpr int MFW = C::MFW;
   const WgradArgs a = wg_block(a0);
-  constexpr int XPR = ((1 << SWL) + 2) / 2;                 // pixel pairs per X stage row
-  constexpr int XROWS = (C::PC >> SWL) + 2;
-  constexpr int GPLF = C::COUT * 16;                        // floats per G plane
-  constexpr int XPLF = XROWS * C::CIB * XPR;                // floats (dwords) per X plane
-  constexpr int LDSF = PL ? C::LBUF + 3 * (GPLF + XPLF) : 2 * C::LBUF;
-  __shared__ __attribute__((aligned(16))) float lds[LDSF];
-  __bf16* gpl = reinterpret_cast<__bf16*>(lds + C::LBUF);   // (PL) G planes
-  unsigned* xpl = reinterpret_cast<unsigned*>(lds + C::LBUF + 3 * GPLF);  // (PL) X planes
+  __shared__ __attribute__((aligned(16))) float lds[2 * C::LBUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
@@ -1818,62 +1789,21 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
 
   Pos pn = pos_of(u_beg);
   if (u_beg < u_end) issue(pn, lds);
-  if constexpr (!PL) __syncthreads();
+  __syncthreads();
   for (long u = u_beg; u < u_end; ++u) {
-    const int cb = PL ? 0 : (int)((u - u_beg) & 1);
+    const int cb = (int)((u - u_beg) & 1);
     const float* lgs = lds + cb * C::LBUF;
     const float* lxs = lgs + C::LGF;
     pn = next(pn);
-    if constexpr (PL) {
-      __syncthreads();  // this stage's DMA landed (vmcnt(0)); every wave done with the planes
-      // G: rows co, pixel octet g -> three 16-B plane quads (lanes = consecutive co)
-      for (int t = tid; t < C::COUT * 4; t += C::NTHR) {
-        const int c = t % C::COUT, g = t / C::COUT;
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = lgs[(8 * g + j) * C::GS + c];
-        bf16x8 p0, p1, p2;
-        split3x8(v, p0, p1, p2);
-        const int o = c * 32 + x6_swz(c, g) * 8;
-        *reinterpret_cast<bf16x8*>(gpl + o) = p0;
-        *reinterpret_cast<bf16x8*>(gpl + 2 * GPLF + o) = p1;
-        *reinterpret_cast<bf16x8*>(gpl + 4 * GPLF + o) = p2;
-      }
-      // X: (stage row, ci, pixel pair) -> one dword per plane (lanes = consecutive ci)
-      for (int t = tid; t < XROWS * C::CIB * XPR; t += C::NTHR) {
-        const int ci = t % C::CIB, r = t / C::CIB, d = r % XPR, yy = r / XPR;
-        const float* xp = lxs + (yy * (2 * XPR) + 2 * d) * C::XS + ci;
-        unsigned h, m, l;
-        split3x2(xp[0], xp[C::XS], h, m, l);
-        const int o = (yy * C::CIB + ci) * XPR + d;
-        xpl[o] = h; xpl[XPLF + o] = m; xpl[2 * XPLF + o] = l;
-      }
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own plane writes done
-      __syncthreads();                     // planes complete; the fp32 buffer is free
-      if (u + 1 < u_end) issue(pn, lds);
-    } else {
-      if (u + 1 < u_end) issue(pn, lds + (cb ^ 1) * C::LBUF);
-    }
+    if (u + 1 < u_end) issue(pn, lds + (cb ^ 1) * C::LBUF);
     // A: the wave's MFW gradient fragments
     bf16x8 av[3][MFW];
 #pragma unroll
     for (int i = 0; i < MFW; ++i) {
-      if constexpr (PL) {
-        const int row = (wm * MFW + i) * 16 + li;
-        const int o = row * 32 + x6_swz(row, lg) * 8;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) av[p][i] = *reinterpret_cast<const bf16x8*>(gpl + 2 * p * GPLF + o);
-        continue;
-      }
       float v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = lgs[(8 * lg + j) * C::GS + (wm * MFW + i) * 16 + li];
-#if DN_WG_ABL_NOSPLIT  // diagnostic ablation (wrong results): one bf16 plane, no split VALU
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { av[0][i][j] = (__bf16)v[j]; av[1][i][j] = av[0][i][j]; av[2][i][j] = av[0][i][j]; }
-#else
       split3x8(v, av[0][i], av[1][i], av[2][i]);
-#endif
 #pragma unroll
       for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(av[p][i]));  // kept, not re-split per tap
     }
@@ -1881,25 +1811,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
     for (int ky = 0; ky < 3; ++ky) {
       // the kernel row's 10-pixel window, split once: P[plane][d] = pieces of pixels 2d, 2d+1
       unsigned P[3][5];
-      if constexpr (PL) {
-        const unsigned* xq = xpl + ((pr0 + ky) * C::CIB + wn * 16 + li) * XPR + (pc0 >> 1);
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-          for (int d = 0; d < 5; ++d) P[pl][d] = xq[pl * XPLF + d];
-      } else {
+      {
       const float* xr = lxs + ((pr0 + ky) * xw + pc0) * C::XS + wn * 16 + li;
       float w[10];
 #pragma unroll
       for (int m = 0; m < 10; ++m) w[m] = xr[m * C::XS];
 #pragma unroll
       for (int d = 0; d < 5; ++d) {
-#if DN_WG_ABL_NOSPLIT
-        P[0][d] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t{w[2 * d], w[2 * d + 1]}), bf16x2_t));
-        P[1][d] = P[0][d]; P[2][d] = P[0][d];
-#else
         split3x2(w[2 * d], w[2 * d + 1], P[0][d], P[1][d], P[2][d]);
-#endif
       }
       }
 #pragma unroll
@@ -1931,9 +1850,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_wgrad3s(WgradArgs a0) {
         x6_acc_add(accb[i][0], hi, lo);
       }
     }
-    if constexpr (!PL) __syncthreads();  // next stage landed (vmcnt(0)); everyone done with this buffer
+    __syncthreads();  // next stage landed (vmcnt(0)); everyone done with this buffer
   }
-  if constexpr (PL) __syncthreads();  // the trailing DMA (none issued past the last stage)
 
   float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
   const int ci = ci0 + wn * 16 + li;
@@ -1975,28 +1893,10 @@ int wgrad_splits_x6(const WgradArgs& a, int splits) {
   return splits < cap ? splits : (cap < 1 ? 1 : cap);
 }
 
-#ifndef DN_WG_PLANES_DEFAULT
-#define DN_WG_PLANES_DEFAULT 0
-#endif
-static bool wg_planes() {  // DN_WG_PLANES=0/1: k_wgrad3s with the split at the operand read / in LDS planes
-  static const bool on = getenv("DN_WG_PLANES") ? atoi(getenv("DN_WG_PLANES")) != 0 : DN_WG_PLANES_DEFAULT != 0;
-  return on;
-}
-
 template <int CO_FR, int WM, int WN>
 static hipError_t run_wgrad3s(const WgradArgs& a, int splits, hipStream_t s, int nz = 1) {
   using C = Ws3Cfg<CO_FR, WM, WN>;
   const dim3 grid(splits, (a.Cin + C::CIB - 1) / C::CIB, nz), block(C::NTHR);
-  if (wg_planes()) {
-    static const std::string kp[3] = {x6_kmore(x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "3"), "true"),
-                                      x6_kmore(x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "4"), "true"),
-                                      x6_kmore(x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "5"), "true")};
-    prof_kernel(kp[a.KW >= 32 ? 2 : (a.KW >= 16 ? 1 : 0)].c_str());
-    if (a.KW >= 32) hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 5, true>), grid, block, 0, s, a);
-    else if (a.KW >= 16) hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 4, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_wgrad3s<CO_FR, WM, WN, 3, true>), grid, block, 0, s, a);
-    return hipGetLastError();
-  }
   static const std::string kn[3] = {x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "3"),
                                     x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "4"),
                                     x6_kmore(x6_kname("k_wgrad3s", CO_FR, WM, WN), "5")};
@@ -2007,26 +1907,9 @@ static hipError_t run_wgrad3s(const WgradArgs& a, int splits, hipStream_t s, int
   return hipGetLastError();
 }
 
-// DN_WG_P=1/0: the 96-output weight gradients on k_wgrad3p (operands split once per stage into
-// LDS planes, wgrad_x6p.hip) or k_wgrad3s (split at the operand read); default DN_WG_P_DEFAULT
-#ifndef DN_WG_P_DEFAULT
-#define DN_WG_P_DEFAULT 1
-#endif
-static bool wg_p() {
-  static const bool on = getenv("DN_WG_P") ? atoi(getenv("DN_WG_P")) != 0 : DN_WG_P_DEFAULT != 0;
-  return on;
-}
-
-// DN_WG_P48=1/0: the 48-output ones (the encoder) on k_wgrad3p<.., 48> or k_wgrad3s
-static bool wg_p48() {
-  static const bool on = !getenv("DN_WG_P48") || atoi(getenv("DN_WG_P48")) != 0;
-  return on;
-}
-
 hipError_t launch_wgrad3_x6(const WgradArgs& a, int splits, hipStream_t s) {
   if (!wgrad3_x6_ok(a)) return hipErrorInvalidValue;
-  if (a.Cout == 96 && wg_p() && !wg_planes() && wgrad3p_ok(a)) return launch_wgrad3p(a, splits, s, 1);
-  if (a.Cout == 48 && wg_p48() && !wg_planes() && wgrad3p_ok(a)) return launch_wgrad3p(a, splits, s, 1);
+  if (wgrad3p_ok(a)) return launch_wgrad3p(a, splits, s, 1);  // k_wgrad3p (96) / k_wgrad3q (48)
   return a.Cout == 96 ? run_wgrad3s<6, 2, 2>(a, splits, s) : run_wgrad3s<3, 1, 3>(a, splits, s);
 }
 
@@ -2069,7 +1952,7 @@ hipError_t launch_gwgrad_x6(const WgradArgs& a0, int splits, hipStream_t s) {
   a.zc = cb;
   a.cout_total = a0.Cout;
   a.co_base = 0;
-  if (cb == 96 && wg_p() && !wg_planes() && wgrad3p_ok(a)) return launch_wgrad3p(a, splits, s, nz);
+  if (cb == 96 && wgrad3p_ok(a)) return launch_wgrad3p(a, splits, s, nz);
   if (cb == 96) return run_wgrad3s<6, 2, 2>(a, splits, s, nz);
   if (cb == 48) return run_wgrad3s<3, 1, 3>(a, splits, s, nz);
   const int ct = gw6_cib(cb, a.Cin);
@@ -2450,9 +2333,6 @@ hipError_t launch_nin_head_x6(const FwdArgs& a, const HeadArgs& h, const void* w
 // 16 pixels -- so three of the four reads of an input row hit that XCD's L2.  The next row's
 // input is loaded into registers while the current one computes; the images are read from L2
 // once per workgroup.
-#ifndef DN_DECONV_CPOL
-#define DN_DECONV_CPOL 0  // A/B: cache policy bits of the output stores (2 = nt, streaming)
-#endif
 // B1: plain bf16 products (the bf16 base's autocast arithmetic, as k_nin_head_x6's B1): the input
 // rounded to bf16, the images' leading planes (the weights rounded to bf16), one MFMA per block
 // chained in fp32 -- a sixth of the MFMAs, so the launch is bound by its output stores
@@ -2556,7 +2436,7 @@ __global__ __launch_bounds__(512, 1) void k_deconv_x6(FwdArgs a, const __bf16* w
       const float4 o = make_float4(out[f][0][0] + bb.x, out[f][0][1] + bb.y, out[f][0][2] + bb.z,
                                    out[f][0][3] + bb.w);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rs, off + 64 * f, 0,
-                                             DN_DECONV_CPOL);
+                                             0);
     }
   };
   // three input register sets: a wave-tile's input is requested two tiles before it is used

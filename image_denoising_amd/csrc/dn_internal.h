@@ -377,9 +377,6 @@ int x6_tail_mode(int K);
 // the launch takes the pipelined kernel (large grid), so a tail-packed image may be used
 bool x6_pipelined(int N, int H, int W, int nout, int zc);
 hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s);
-// k_c3x6r (conv_x6r.hip): 96-output-channel forward / data gradient with the weights in
-// registers; false = the arguments are not its case (err untouched)
-bool x6r_enabled();
 // k_c3w6 (conv_w6.hip): the 1-D Winograd F(2,3) bf16x6 kernel for 96 output channels, on a PK_W6
 // image; FwdArgs::x6_tail carries X6_W6 | x6_tail_mode(K) for it (see x6_image_mode)
 constexpr int X6_W6 = 8;
@@ -394,7 +391,6 @@ hipError_t launch_fwd_w6s(const FwdArgs& a, const unsigned* list, const int* cnt
 // the weight-image mode of a split-bf16 3x3 launch (pack and launch agree on it): the tail
 // packing of the last chunk on large grids with aligned views, | X6_W6 for the Winograd kernel
 int x6_image_mode(int N, int H, int W, int K, int nout, int zc, bool aligned);
-bool launch_fwd_x6r(const FwdArgs& a, hipStream_t s, hipError_t& err);
 hipError_t launch_pack_bf16(const WView& wv, int K, int nout, void* out, hipStream_t s,
                             int ksize = 3);
 hipError_t launch_fwd_bf16(const FwdArgs& a, hipStream_t s, int ksize = 3);

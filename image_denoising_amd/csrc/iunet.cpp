@@ -79,20 +79,18 @@ bool x6_shape(int nout) { return nout == 32 || nout % 48 == 0; }
 bool x6_takes(int K, int nout, int tail) {
   // 32-wide tiles with K < 80 were staging-bound on round 2's 8-row kernels (no gain for 32x48,
   // 32x56); the 16-row ones take K >= 48 at 0.33-0.37 of the x6 peak against the fp32 kernel's
-  // 0.25-0.27 (48->32 @256^2: 1.05 -> 0.79 ms); DN_IU_X6_SMALL32=0 keeps them on fp32
-  static const bool small32 = !getenv("DN_IU_X6_SMALL32") || atoi(getenv("DN_IU_X6_SMALL32")) != 0;
-  if (nout == 32 && K < 80 && !(small32 && K % 4 == 0 && K >= 48)) return false;
+  // 0.25-0.27 (48->32 @256^2: 1.05 -> 0.79 ms)
+  if (nout == 32 && K < 80 && !(K % 4 == 0 && K >= 48)) return false;
   // 32-wide RDB growth convs with K >= 80 take a zero-padded last chunk when it cannot be
   // tail-packed (88, 120: 3 / 4 chunks, 9 / 7 % padding; on the fp32 kernel they ran at ~60 %
-  // of the x6 rate of their 80- / 112-channel neighbours); DN_IU_X6_PAD32=0 keeps them on fp32
-  static const bool pad32 = !getenv("DN_IU_X6_PAD32") || atoi(getenv("DN_IU_X6_PAD32")) != 0;
-  if (pad32 && nout == 32 && K % 4 == 0) return true;
+  // of the x6 rate of their 80- / 112-channel neighbours)
+  if (nout == 32 && K % 4 == 0) return true;
   // likewise the data gradients of those convs (K = 32 = the growth, nout = 80..144 of the dense
   // concatenation: 48-channel output blocks, the last one partial) and the 24-channel top
   // level's 72 -> 24 (a 32-wide tile, 8 outputs idle): the fp32 kernel ran them at 0.19-0.22 of
   // the x6 ceiling
-  if (pad32 && K == 32 && nout >= 80 && nout % 8 == 0) return true;
-  if (pad32 && nout == 24 && K >= 72 && K % 4 == 0) return true;
+  if (K == 32 && nout >= 80 && nout % 8 == 0) return true;
+  if (nout == 24 && K >= 72 && K % 4 == 0) return true;
   return x6_shape(nout) && (K % 32 == 0 || K >= 128 || tail) && (K > 32 || nout % 96 == 0);
 }
 // output-channel blocks of the wide layers: 96, or 48 where 96 would pad (144 = 3 x 48)
@@ -408,35 +406,50 @@ bool iunet_build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, IPlan
 namespace {
 
 // Optional per-op timing (DN_PROFILE_OPS=1): HIP events around every conv / weight gradient /
-// GroupNorm call, aggregated by shape and printed to stderr at the end of each pass.
+// GroupNorm call, aggregated by shape and printed to stderr at the end of each pass.  One record
+// list per host thread (thread_local g_prof below: no state shared between callers); a failing
+// HIP event call switches this thread's profiling off with a message, it never fails a pass.
 struct OpProf {
   struct Rec { std::string label; double flops; hipEvent_t a, b; };
   bool on = getenv("DN_PROFILE_OPS") != nullptr;
   std::vector<Rec> recs;
+  bool ok(hipError_t e, const char* what) {
+    if (e == hipSuccess) return true;
+    fprintf(stderr, "[dn ops] %s failed (%s): per-op timing off\n", what, hipGetErrorString(e));
+    on = false;
+    return false;
+  }
+  void drop() {
+    for (auto& r : recs) {
+      if (r.a) (void)hipEventDestroy(r.a);
+      if (r.b) (void)hipEventDestroy(r.b);
+    }
+    recs.clear();
+  }
   void flush(const char* pass) {
     if (!on || recs.empty()) return;
-    hipEventSynchronize(recs.back().b);
+    if (!ok(hipEventSynchronize(recs.back().b), "hipEventSynchronize")) return drop();
     struct Agg { double ms = 0, flops = 0; int n = 0; };
     std::vector<std::pair<std::string, Agg>> agg;
     double total = 0;
     for (auto& r : recs) {
       float ms = 0;
-      hipEventElapsedTime(&ms, r.a, r.b);
+      if (!ok(hipEventElapsedTime(&ms, r.a, r.b), "hipEventElapsedTime")) return drop();
       total += ms;
       auto it = std::find_if(agg.begin(), agg.end(), [&](auto& x) { return x.first == r.label; });
       if (it == agg.end()) { agg.push_back({r.label, Agg{}}); it = agg.end() - 1; }
       it->second.ms += ms; it->second.flops += r.flops; it->second.n += 1;
-      hipEventDestroy(r.a); hipEventDestroy(r.b);
     }
+    const size_t nrec = recs.size();
+    drop();
     std::sort(agg.begin(), agg.end(), [](auto& x, auto& y) { return x.second.ms > y.second.ms; });
-    fprintf(stderr, "[dn ops] %s: %.3f ms in %zu ops\n", pass, total, recs.size());
+    fprintf(stderr, "[dn ops] %s: %.3f ms in %zu ops\n", pass, total, nrec);
     for (auto& [l, a] : agg)
       fprintf(stderr, "  %8.3f ms  %7.1f TF/s  x%-3d %s\n", a.ms,
               a.flops > 0 ? a.flops / (a.ms * 1e-3) / 1e12 : 0.0, a.n, l.c_str());
-    recs.clear();
   }
 };
-OpProf g_prof;
+thread_local OpProf g_prof;
 
 // dn_profile_ops op name of an OpScope kind ("fwd" + k = 3 -> "fwd3", the bench's 3x3 ops)
 inline const char* prof_op(const char* kind, int k) {
@@ -460,11 +473,22 @@ struct OpScope {
     char b[128];
     snprintf(b, sizeof(b), "%-6s %dx%d k%d @%dx%d", kind, cout, cin, k, h, w);
     OpProf::Rec r{b, flop_mult * 2.0 * N * h * w * (double)cout * cin * k * k, nullptr, nullptr};
-    hipEventCreate(&r.a); hipEventCreate(&r.b);
-    hipEventRecord(r.a, s);
+    if (!g_prof.ok(hipEventCreate(&r.a), "hipEventCreate") ||
+        !g_prof.ok(hipEventCreate(&r.b), "hipEventCreate") ||
+        !g_prof.ok(hipEventRecord(r.a, s), "hipEventRecord")) {
+      if (r.a) (void)hipEventDestroy(r.a);
+      if (r.b) (void)hipEventDestroy(r.b);
+      on = false;
+      g_prof.drop();
+      return;
+    }
     g_prof.recs.push_back(r);
   }
-  ~OpScope() { if (on) hipEventRecord(g_prof.recs.back().b, s); }
+  ~OpScope() {
+    if (on && g_prof.on && !g_prof.recs.empty() &&
+        !g_prof.ok(hipEventRecord(g_prof.recs.back().b, s), "hipEventRecord"))
+      g_prof.drop();
+  }
 };
 
 struct Ctx {
@@ -629,9 +653,8 @@ dn_status wgrad_g(const Ctx& c, float* dprm, int mode, const IConv& L, const Vie
   a.wlayout = 0; a.cin_total = L.cin; a.ci_base = 0; a.bias = bias ? 1 : 0;
   int sp = gwgrad_splits(mode, c.p.N, h, w, L.cin, L.cout);
   IU_TRY(hipMemsetAsync(slab, 0, 64 * sizeof(float), c.s));
-  // fp32_x6: the 3x3 weight gradients on the bf16x6 kernel too (DN_IU_X6_WGRAD=0: fp32, A/B)
-  static const bool x6w_env = !getenv("DN_IU_X6_WGRAD") || atoi(getenv("DN_IU_X6_WGRAD")) != 0;
-  if (x6w_env && c.prec == DN_PREC_FP32_X6 && mode == W_C3 && gwgrad_x6_ok(a)) {
+  // fp32_x6: the 3x3 weight gradients on the bf16x6 kernel too
+  if (c.prec == DN_PREC_FP32_X6 && mode == W_C3 && gwgrad_x6_ok(a)) {
     sp = gwgrad_x6_splits(a, sp);
     IU_TRY(launch_gwgrad_x6(a, sp, c.s));
   } else {

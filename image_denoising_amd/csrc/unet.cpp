@@ -388,9 +388,8 @@ hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, 
     hipError_t e = hipMemsetAsync(slab, 0, 64 * sizeof(float), s);
     if (e != hipSuccess) return e;
   }
-  // 1x1 / deconv, own splits (x6: the 96 x 96 1x1 layers on k_wgrad1p; DN_X6_WGRAD1=0: k_wgrad1)
-  static const bool wg1_x6 = !getenv("DN_X6_WGRAD1") || atoi(getenv("DN_X6_WGRAD1")) != 0;
-  if (wgrad1_ok(mode, a)) return launch_wgrad1(mode, a, dwb, s, rb, x6 && wg1_x6);
+  // 1x1 / deconv, own splits (x6: the 96 x 96 1x1 layers on k_wgrad1p)
+  if (wgrad1_ok(mode, a)) return launch_wgrad1(mode, a, dwb, s, rb, x6);
   if (x6 && mode == W_C3) splits = wgrad_splits_x6(a, splits);
   hipError_t e = launch_wgrad(mode, a, splits, s, x6);
   if (e != hipSuccess) return e;
@@ -404,8 +403,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
                        hipStream_t s, int prec, const uint8_t* sel_rd, int pack) {
   const StreamDeviceGuard device_guard(s);
   const bool bf16 = prec == DN_PREC_BF16, x6 = prec == DN_PREC_FP32_X6;
-  // bf16x6 96-channel deconvs (k_deconv_x6); DN_X6_DECONV=0 keeps the fp32 kernel (A/B)
-  static const bool x6_deconv = !getenv("DN_X6_DECONV") || atoi(getenv("DN_X6_DECONV")) != 0;
+  // (bf16x6 96-channel deconvs: k_deconv_x6)
   const int N = p.N, nf = p.nf, C = p.C;
   auto H = [&](int l) { return p.H >> l; };
   auto Wd = [&](int l) { return p.W >> l; };
@@ -424,31 +422,25 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // the encoder's 2x2 max-pools fused into the x6 convs' epilogues (DN_POOL_FUSE=0: separate
   // k_pool_fwd launches, A/B)
   static const bool pool_fuse = !getenv("DN_POOL_FUSE") || atoi(getenv("DN_POOL_FUSE")) != 0;
-  // the N2N pair-pixel pass's dec_conv1b: on the Winograd kernel k_c3w6s (default), or on the
-  // direct k_c3x6s (DN_W6_SEL=0, A/B), whose forward-only plans keep dec_conv1b's direct image
-  static const bool w6_sel_env = !getenv("DN_W6_SEL") || atoi(getenv("DN_W6_SEL")) != 0;
+  // (the N2N pair-pixel pass's dec_conv1b runs the Winograd kernel k_c3w6s wherever the full
+  // forward's dec_conv1b has a Winograd image; the direct k_c3x6s below one round of tiles)
   auto x6_tail_f = [&](int i) -> int {
     const Layer& L = p.P.L[i];
     const int l = layer_level(i);
-    const int m = x6_image_mode(N, H(l), Wd(l), i == D1A ? p.c1kp : L.cin, L.cout, 0, true);
-    return (i == D1B && !p.with_bwd && !w6_sel_env) ? (m & ~X6_W6) : m;
+    return x6_image_mode(N, H(l), Wd(l), i == D1A ? p.c1kp : L.cin, L.cout, 0, true);
   };
   // bf16 base (forward-only plans): bf16 storage of the decoder's a-conv outputs, whose only
-  // reader is the matching b-conv (DN_BF16_STORE=0: fp32 storage, A/B)
-  static const bool bf16_store_env = !getenv("DN_BF16_STORE") || atoi(getenv("DN_BF16_STORE")) != 0;
-  const bool bf16_store = bf16 && bf16_store_env && !p.with_bwd;
+  // reader is the matching b-conv
+  const bool bf16_store = bf16 && !p.with_bwd;
   // (bf16 base: the fused head kernel in plain bf16 products, see below; it reads d1b as bf16)
-  static const bool bf16_head_env = !getenv("DN_BF16_HEAD_X6") || atoi(getenv("DN_BF16_HEAD_X6")) != 0;
-  const bool bf16_head_x6 = bf16 && bf16_head_env && !p.with_bwd && p.OC <= X6_HEAD_OCMAX;
+  const bool bf16_head_x6 = bf16 && !p.with_bwd && p.OC <= X6_HEAD_OCMAX;
   auto bf16_store_out = [&](int i) {
     if (i == D1B) return bf16_store && bf16_head_x6 && p.packBF[i] >= 0;
     return bf16_store && (i == D1A || i == D2A || i == D3A || i == D4A || i == D5A) &&
            p.packBF[i] >= 0 && p.packBF[i + 1] >= 0;
   };
-  // enc_conv0's output too: only enc_conv1 reads it in a forward-only plan (DN_BF16_ENC0_STORE=0:
-  // fp32)
-  static const bool enc0_env = !getenv("DN_BF16_ENC0_STORE") || atoi(getenv("DN_BF16_ENC0_STORE")) != 0;
-  const bool enc0_bf16 = bf16_store && enc0_env && p.packBF[ENC1] >= 0;
+  // enc_conv0's output too: only enc_conv1 reads it in a forward-only plan
+  const bool enc0_bf16 = bf16_store && p.packBF[ENC1] >= 0;
   auto bf16_store_in = [&](int i) {
     if (i == ENC1) return enc0_bf16;
     return bf16_store && (i == D1B || i == D2B || i == D3B || i == D4B || i == D5B) &&
@@ -459,9 +451,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // that view (*pooled set); otherwise the caller pools
   // forward-only plans: an encoder conv whose pool is fused stores only the pooled output
   // (its full-resolution activation is read by nothing but that pool; the backward's pool
-  // routing reads it in plans with a backward).  DN_POOL_ONLY=0 stores it anyway.
-  static const bool pool_only_env = !getenv("DN_POOL_ONLY") || atoi(getenv("DN_POOL_ONLY")) != 0;
-  const int pool_only = !p.with_bwd && pool_only_env ? 1 : 0;
+  // routing reads it in plans with a backward)
+  const int pool_only = !p.with_bwd ? 1 : 0;
   auto conv_forward = [&](const View& in, int Nn, int h, int w, int K, const float* wp,
                           const float* b, int cout, int ksize, int act, const View& out,
                           int layout, hipStream_t st, const View* pool = nullptr,
@@ -501,9 +492,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     // bit-identical and those tensors move half the bytes
     a.out_bf16 = bf16_store_out(i);
     a.in_bf16 = bf16_store_in(i);
-    // the encoder's pools fused as in the x6 path (DN_BF16_POOL_FUSE=0: separate k_pool_fwd)
-    static const bool bf16_pool_env = !getenv("DN_BF16_POOL_FUSE") || atoi(getenv("DN_BF16_POOL_FUSE")) != 0;
-    if (pool && pool_fuse && bf16_pool_env && act && ksize == 3 && layout == OUT_NHWC && !a.out_bf16) {
+    // the encoder's pools fused as in the x6 path
+    if (pool && pool_fuse && act && ksize == 3 && layout == OUT_NHWC && !a.out_bf16) {
       a.pool_out = pool->p; a.pool_stride = pool->stride; a.pool_off = pool->off;
       a.pool_only = pool_only;
       if (pooled) *pooled = true;
@@ -511,20 +501,16 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     return launch_fwd_bf16(a, st, ksize);
   };
 
-  // DN_X6_HEAD=0: the fp32 nin head (A/B); the pair-pixel pass always takes the bf16x6 head
-  static const bool head_x6_env = !getenv("DN_X6_HEAD") || atoi(getenv("DN_X6_HEAD")) != 0;
+  // the bf16x6 nin head (k_nin_head_x6), also at the pair pixels
   const bool sel = x6 && sel_rd && !p.with_bwd && p.OC <= X6_HEAD_OCMAX;
-  const bool w6_sel = sel && w6_sel_env && p.packXV >= 0 && (x6_tail_f(D1B) & X6_W6);
-  const bool head_x6 = x6 && (head_x6_env || sel) && p.OC <= X6_HEAD_OCMAX;
+  const bool w6_sel = sel && p.packXV >= 0 && (x6_tail_f(D1B) & X6_W6);
+  const bool head_x6 = x6 && p.OC <= X6_HEAD_OCMAX;
   // bf16 base (inference only): the fused head kernel in plain bf16 products instead of nin_a /
   // nin_b as two bf16 1x1 launches + an fp32 nin_c (two 96-channel round trips through HBM
-  // saved; DN_BF16_HEAD_X6=0 keeps the three launches; bf16_head_x6 above)
+  // saved; bf16_head_x6 above)
   // the 96-channel deconvs on the persistent bf16x6 kernel, also in the bf16 base (one pass over
-  // the input instead of a bf16 1x1 launch per output parity; DN_BF16_DECONV_X6=0 keeps those)
-  static const bool bf16_dx6_env = !getenv("DN_BF16_DECONV_X6") || atoi(getenv("DN_BF16_DECONV_X6")) != 0;
-  auto deconv_x6_layer = [&](int i) {
-    return (x6 || (bf16 && bf16_dx6_env)) && x6_deconv && p.packUX[i] >= 0;
-  };
+  // the input instead of a bf16 1x1 launch per output parity)
+  auto deconv_x6_layer = [&](int i) { return (x6 || bf16) && p.packUX[i] >= 0; };
   // ConvTranspose2d(2,2): fp32 kernel, or the bf16 1x1 kernel per output parity
   auto deconv_forward = [&](const View& xin, int Nn, int h, int w, int cin, const float* wp,
                             const float* b, int cout, const View& out, hipStream_t st) -> hipError_t {
@@ -537,9 +523,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
       a.N = Nn; a.OH = h; a.OW = w; a.K = cin; a.NOUT = cout; a.bias = b;
       a.out = out.p; a.out_stride = out.stride; a.out_off = out.off;
       if (!deconv_x6_ok(a)) return hipErrorInvalidValue;
-      // (the bf16 base: plain bf16 products, as its convs; DN_BF16_DECONV_B1=0: bf16x6)
-      static const bool b1_env = !getenv("DN_BF16_DECONV_B1") || atoi(getenv("DN_BF16_DECONV_B1")) != 0;
-      return launch_deconv_x6(a, ws + p.packUX[i], st, bf16 && b1_env);
+      // (the bf16 base: plain bf16 products, as its convs)
+      return launch_deconv_x6(a, ws + p.packUX[i], st, bf16);
     }
     if (!bf16 || i == NL || p.packBF[i] < 0)
       return dn::deconv_forward(xin, Nn, h, w, cin, wp, b, cout, out, st);
@@ -810,10 +795,8 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                         float* ws, hipStream_t s, int prec, hipEvent_t tail_ready) {
   const StreamDeviceGuard device_guard(s);
   const bool x6 = prec == DN_PREC_FP32_X6;
-  // bf16x6 3x3 weight gradients (k_wgrad3s, split at the operand read); DN_X6_WGRAD=0 keeps the
-  // fp32 k_wgrad3 (A/B: 26.7 vs 27.9 ms per step)
-  static const bool x6w_env = !getenv("DN_X6_WGRAD") || atoi(getenv("DN_X6_WGRAD")) != 0;
-  const bool x6w = x6 && x6w_env;
+  // bf16x6 3x3 weight gradients (k_wgrad3p / k_wgrad3q)
+  const bool x6w = x6;
   const int N = p.N, nf = p.nf, C = p.C;
   auto H = [&](int l) { return p.H >> l; };
   auto Wd = [&](int l) { return p.W >> l; };
@@ -824,9 +807,8 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     const int l = layer_level(i), nout = dgrad_nout(p, i);
     return x6_image_mode(N, H(l), Wd(l), p.P.L[i].cout, nout, x6_dgrad_zc(nout), true);
   };
-  // bf16x6 data gradients of the 96-channel deconvs (DN_X6_DECONV=0: the fp32 kernel, A/B)
-  static const bool x6_deconv = !getenv("DN_X6_DECONV") || atoi(getenv("DN_X6_DECONV")) != 0;
-  auto x6_dgrad_deconv = [&](int i) { return x6 && x6_deconv && p.packUXB[i] >= 0; };
+  // bf16x6 data gradients of the 96-channel deconvs
+  auto x6_dgrad_deconv = [&](int i) { return x6 && p.packUXB[i] >= 0; };
   auto deconv_dgrad = [&](const View& dy, int Nn, int h, int w, int cout, int i, int cin,
                           const View& mask, int epi, const View& dx, hipStream_t st) -> hipError_t {
     const OpTimer timer(st, "deconv_dgrad", 2.0 * Nn * h * w * cin * cout * 4, cout, cin, h, w, Nn);
@@ -839,10 +821,8 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     a.out = dx.p; a.out_stride = dx.stride; a.out_off = dx.off;
     return launch_deconv_dgrad_x6(a, ws + p.packUXB[i], st);
   };
-  // the head's data gradients in the bf16x6 arithmetic (k_head_bwd_x6; DN_X6_HEAD_BWD=0: the
-  // fp32-MFMA k_head_bwd)
-  static const bool hbx6_env = !getenv("DN_X6_HEAD_BWD") || atoi(getenv("DN_X6_HEAD_BWD")) != 0;
-  const bool head_bwd_x6 = x6 && hbx6_env && p.OC <= X6_HEAD_BWD_OCMAX;
+  // the head's data gradients in the bf16x6 arithmetic (k_head_bwd_x6)
+  const bool head_bwd_x6 = x6 && p.OC <= X6_HEAD_BWD_OCMAX;
   // flipped/transposed weight images for the data gradients, the head's images and the
   // weight gradients' zero padding: one launch
   {
@@ -1014,9 +994,8 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     dU = V(p.g_c[l], p.cs[l], 0);  // [u_{l+1} grad | skip grad]
   }
   // the head's and the decoder's reductions on the side stream now, behind their weight
-  // gradients, overlapping the encoder's data gradients (DN_RED_EARLY=0: all at the end)
-  static const bool red_early = !getenv("DN_RED_EARLY") || atoi(getenv("DN_RED_EARLY")) != 0;
-  if (side && red_early) {
+  // gradients, overlapping the encoder's data gradients
+  if (side) {
     DN_TIMED(s2, "reduce", 0, 0, 0, 0, 0, 0, red_flush(rb, s2));
     // dprm[tail_begin ..] (dec_conv5a .. nin_c) is final behind this flush on s2
     if (tail_ready) DN_TRY(hipEventRecord(tail_ready, s2));

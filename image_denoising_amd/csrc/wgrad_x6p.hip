@@ -25,9 +25,6 @@
 #include "conv_epi.h"
 #include "x6_core.h"
 
-#ifndef DN_WGP_FOLD
-#define DN_WGP_FOLD 1
-#endif
 
 namespace dn {
 
@@ -77,10 +74,9 @@ __device__ __forceinline__ int wp_idx(int r, int rw, int blk) {
   return r * rw + ((blk ^ ((r >> 3) & 1)) << 4);
 }
 
-// GL: the next stage's G operands are split into the other buffer at the end of the stage, with
-// X (a whole stage of load latency for both), instead of after the first kernel row (which then
-// issues the X loads into the same registers)
-template <int SWL, bool GL = false, int CO = 96>
+// The next stage's G and X operands are loaded at the start of the stage and split into the other
+// buffer at its end (a whole stage of load latency for both)
+template <int SWL, int CO = 96>
 __global__ __launch_bounds__(CO == 96 ? 256 : 192, 2) void k_wgrad3p(WgradArgs a0) {
   using C = Wp3Cfg<SWL, CO>;
   constexpr int MFW = C::MFW, SW = C::SW, SH = C::SH, XW = C::XW;
@@ -249,8 +245,10 @@ __global__ __launch_bounds__(CO == 96 ? 256 : 192, 2) void k_wgrad3p(WgradArgs a
     __bf16* nbuf = lds + (cb ^ 1) * C::BUF;
     pn = next(pn);
     const bool more = u + 1 < u_end;
-    if (more) load_g(pn);  // in flight during the first kernel row's MFMAs (GL: the whole stage)
-    if (GL && more) load_x(pn);
+    if (more) {  // in flight during the whole stage
+      load_g(pn);
+      load_x(pn);
+    }
     int aoff = abase;
     unsigned bmask = bmask0, bml = bm64[0], bmh = bm64[1];
     asm volatile("" : "+v"(aoff), "+v"(bmask));  // (addresses formed here, not held across stages)
@@ -265,54 +263,53 @@ __global__ __launch_bounds__(CO == 96 ? 256 : 192, 2) void k_wgrad3p(WgradArgs a
         av[pl][i] = tr_frag(p, p + 4 * C::GRW);
       }
     }
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      if (!GL && ky == 1 && more) {  // G of the next stage into the other buffer, then its X loads
-        store_g(nbuf);
-        load_x(pn);
+    // B fragments of tap t (three planes), read one tap ahead of their MFMAs: the reads of tap
+    // t + 1 are in flight during tap t's 18 MFMAs instead of being waited for at the head of
+    // every tap (96->96 @64 x 128^2 0.963 -> 0.934 ms, profiles/r5_wg_ab.log)
+    auto read_b = [&](int t, bf16x8 (&bv)[3]) {
+      const int ky = t / 3, kx = t - 3 * (t / 3), k = 2 * t, d = ky * XW + kx;
+      int oa, ob;
+      if (C::XRW == 64) {
+        const unsigned m = k < 16 ? bml : bmh;
+        oa = bbase64 + d * 64 + (int)(((m >> (2 * (k & 15))) & 3) << 4);
+        ob = bbase64 + (d + 4) * 64 + (int)(((m >> (2 * ((k + 1) & 15))) & 3) << 4);
+      } else {
+        oa = bbase + d * C::XRW + (int)((bmask >> k) & 1) * bsgn;
+        ob = bbase + (d + 4) * C::XRW + (int)((bmask >> (k + 1)) & 1) * bsgn;
       }
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int k = 2 * (3 * ky + kx);
-        const int d = ky * XW + kx;
-        int oa, ob;
-        if (C::XRW == 64) {
-          const unsigned m = k < 16 ? bml : bmh;
-          oa = bbase64 + d * 64 + (int)(((m >> (2 * (k & 15))) & 3) << 4);
-          ob = bbase64 + (d + 4) * 64 + (int)(((m >> (2 * ((k + 1) & 15))) & 3) << 4);
-        } else {
-          oa = bbase + d * C::XRW + (int)((bmask >> k) & 1) * bsgn;
-          ob = bbase + (d + 4) * C::XRW + (int)((bmask >> (k + 1)) & 1) * bsgn;
-        }
-        bf16x8 bv[3][1];
+      for (int pl = 0; pl < 3; ++pl) bv[pl] = tr_frag(buf + pl * C::PL + oa, buf + pl * C::PL + ob);
+    };
+    bf16x8 bvs[2][3];
+    read_b(0, bvs[0]);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) bv[pl][0] = tr_frag(buf + pl * C::PL + oa, buf + pl * C::PL + ob);
-        const int t = 3 * ky + kx;
-        // the six products of a fragment, one fragment at a time (a dependent 16x16x32 chain
-        // issues back-to-back, MI355X_MICROARCH.md): the five corrections chained from zero,
-        // the leading product a0 b0 last on top of them, so the 32-pixel block reaches the
-        // running sum through ONE round-to-nearest add (4 VALU per fragment instead of 8).  The
-        // block sum is still fresh per stage: the chain's accumulator is at most the block's
-        // own magnitude, as for a leading product summed from zero (DN_WGP_FOLD=0: x6_block's
-        // separate hi / lo sums and two adds, for A/B).
+    for (int t = 0; t < 9; ++t) {
+      if (t + 1 < 9) {
+        read_b(t + 1, bvs[(t + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const int sl = t & 1;
+      bf16x8 bv[3][1];
 #pragma unroll
-        for (int i = 0; i < MFW; ++i) {
-          const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-          f32x4 lo = mfma_bf16(av[0][i], bv[1][0], z);
-          lo = mfma_bf16(av[1][i], bv[0][0], lo);
-          lo = mfma_bf16(av[0][i], bv[2][0], lo);
-          lo = mfma_bf16(av[1][i], bv[1][0], lo);
-          lo = mfma_bf16(av[2][i], bv[0][0], lo);
-#if DN_WGP_FOLD
-          const f32x4 blk = mfma_bf16(av[0][i], bv[0][0], lo);
+      for (int pl = 0; pl < 3; ++pl) bv[pl][0] = bvs[sl][pl];
+      // the six products of a fragment, one fragment at a time (a dependent 16x16x32 chain
+      // issues back-to-back, MI355X_MICROARCH.md): the five corrections chained from zero,
+      // the leading product a0 b0 last on top of them, so the 32-pixel block reaches the
+      // running sum through ONE round-to-nearest add (4 VALU per fragment instead of 8).  The
+      // block sum is still fresh per stage: the chain's accumulator is at most the block's
+      // own magnitude, as for a leading product summed from zero.
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[t][i][0][r] = acc[t][i][0][r] + blk[r];
-#else
-          const f32x4 hi = mfma_bf16(av[0][i], bv[0][0], z);
-          x6_acc_add(acc[t][i][0], hi, lo);
-#endif
-          asm volatile("" : "+v"(acc[t][i][0]));
-        }
+      for (int i = 0; i < MFW; ++i) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        f32x4 lo = mfma_bf16(av[0][i], bv[1][0], z);
+        lo = mfma_bf16(av[1][i], bv[0][0], lo);
+        lo = mfma_bf16(av[0][i], bv[2][0], lo);
+        lo = mfma_bf16(av[1][i], bv[1][0], lo);
+        lo = mfma_bf16(av[2][i], bv[0][0], lo);
+        const f32x4 blk = mfma_bf16(av[0][i], bv[0][0], lo);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[t][i][0][r] = acc[t][i][0][r] + blk[r];
+        asm volatile("" : "+v"(acc[t][i][0]));
       }
     }
     if (do_bias) {
@@ -325,8 +322,10 @@ __global__ __launch_bounds__(CO == 96 ? 256 : 192, 2) void k_wgrad3p(WgradArgs a
         x6_acc_add(accb[i][0], hi, lo);
       }
     }
-    if (GL && more) store_g(nbuf);
-    if (more) store_x(nbuf);  // (waits for its loads itself)
+    if (more) {  // (waits for its loads itself)
+      store_g(nbuf);
+      store_x(nbuf);
+    }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own plane writes done
     __syncthreads();                     // next buffer complete; everyone done with this one
   }
@@ -355,6 +354,259 @@ __global__ __launch_bounds__(CO == 96 ? 256 : 192, 2) void k_wgrad3p(WgradArgs a
   }
 }
 
+// ------------------------------------------------------------------------------------
+// The encoder's 48 -> 48 weight gradients (k_wgrad3q; arch_unet.py:201-221, enc_conv1..5):
+// k_wgrad3p's plane scheme with FOUR waves.  The 3-wave form (one 16-channel input block per
+// wave) left two of a CU's four SIMDs with one wave and two with two (two 192-thread workgroups),
+// so the busier SIMDs set the pace with half the MFMA pipes idle (MFMA busy 0.30).  Here the
+// 27 B fragments of a stage (3 input-channel blocks j x 9 taps t, p = 9 j + t) are dealt to the
+// four waves 7 / 7 / 7 / 6 (p = 7 w + k), every wave multiplying each against all three output
+// fragments (acc[7][3]); the bias gradient goes to wave 3, which has one fragment fewer.
+//   K stage = 32 pixels (SH rows of SW), G [32 px][64] and X [XPIX][64] bf16 planes (48 channels
+//   used; 128-B rows, wp_flip64), two buffers, two workgroups per CU (78 KiB each).
+//   Split-pass items: 384 G quads + XPIX * 12 X quads dealt tid + 256 it; since 384 = 1.5 x 256,
+//   item 0 of every thread and item 1 of waves 0, 1 are G, the rest X: a wave-uniform type.
+//   B reads one fragment ahead of their MFMAs (as k_wgrad3p).
+// ------------------------------------------------------------------------------------
+template <int SWL>
+struct Wq3Cfg {
+  static constexpr int NTHR = 256, RW = 64, CIB = 48;
+  static constexpr int SW = 1 << SWL, SH = 32 >> SWL, XW = SW + 2, XPIX = (SH + 2) * XW;
+  static constexpr int GQ = 32 * 12, XQ = XPIX * 12, NQ = GQ + XQ;  // float4 items
+  static constexpr int NIT = (NQ + NTHR - 1) / NTHR;
+  static constexpr int GPL = 32 * RW, PL = GPL + XPIX * RW, BUF = 3 * PL;  // bf16
+  static constexpr int KMAX = 7;                                         // B fragments per wave
+  static_assert(GQ == NTHR + NTHR / 2, "item 1 is G exactly for waves 0 and 1");
+  static_assert(2 * BUF * 2 <= 81920, "two workgroups per CU");
+};
+
+template <int SWL>
+__global__ __launch_bounds__(256, 2) void k_wgrad3q(WgradArgs a) {
+  using C = Wq3Cfg<SWL>;
+  constexpr int SW = C::SW, SH = C::SH, XW = C::XW, NIT = C::NIT, KMAX = C::KMAX;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * C::BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lg = lane >> 4;
+  const int ci0 = blockIdx.y * C::CIB;
+  const int ux = (a.KW + SW - 1) / SW, uy = (a.KH + SH - 1) / SH;
+  const long U = (long)a.N * uy * ux;
+  const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
+  const bool do_bias = a.bias && blockIdx.y == 0 && wave == 3;
+  const int nk = wave == 3 ? 6 : 7;  // B fragments of this wave: p = 7 wave + k, k < nk
+
+  f32x4 acc[KMAX][3], accb[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) acc[k][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // ---- split-pass items (as k_wgrad3p): offset in the operand image relative to the stage
+  // origin; LDS index (low 16 bits) | halo-edge class (bits 16..)
+  auto is_g = [&](int it) { return it == 0 || (it == 1 && wave < 2); };  // wave-uniform
+  int ioff[NIT], ilde[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int q = tid + it * C::NTHR;
+    ioff[it] = 0; ilde[it] = 32 << 16;
+    if (q < C::GQ) {
+      const int px = q / 12, c = 4 * (q % 12);
+      ioff[it] = ((px >> SWL) * a.KW + (px & (SW - 1))) * a.g_stride + c;
+      ilde[it] = (wp_idx(px, 64, c >> 4) + (c & 15)) | ((c < a.Cout ? 0 : 32) << 16);
+    } else if (q < C::NQ) {
+      const int r = q - C::GQ, xp = r / 12, c = 4 * (r % 12);
+      const int yy = xp / XW, xx = xp - yy * XW;
+      ioff[it] = ((yy - 1) * a.KW + xx - 1) * a.x_stride + ci0 + c;
+      const int e = (yy == 0) | ((yy == SH + 1) << 1) | ((xx == 0) << 2) | ((xx == SW + 1) << 3) |
+                    ((ci0 + c < a.Cin ? 0 : 1) << 5);
+      ilde[it] = (C::GPL + wp_idx(xp, 64, c >> 4) + (c & 15)) | (e << 16);
+    }
+  }
+  const bool exact = a.KW % SW == 0 && a.KH % SH == 0;
+  f32x4 pv[NIT];  // the next stage's operands in flight
+  struct Pos { int n, iy, ix; };
+  auto pos_of = [&](long u) {
+    Pos p;
+    p.n = (int)(u / ((long)uy * ux));
+    const int rem = (int)(u - (long)p.n * uy * ux);
+    p.iy = rem / ux; p.ix = rem - p.iy * ux;
+    return p;
+  };
+  auto next = [&](Pos p) {
+    if (++p.ix == ux) { p.ix = 0; if (++p.iy == uy) { p.iy = 0; ++p.n; } }
+    return p;
+  };
+  auto load_all = [&](Pos p) {
+    const long img = (long)p.n * a.KH * a.KW;
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.g + img * a.g_stride + a.g_off), (short)0,
+        (int)((long)a.KH * a.KW * a.g_stride * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x + img * a.x_stride + a.x_off), (short)0,
+        (int)((long)a.KH * a.KW * a.x_stride * 4), 0x00020000);
+    const int py0 = p.iy * SH, px0 = p.ix * SW;
+    const int em = (py0 == 0) | ((py0 + SH >= a.KH) << 1) | ((px0 == 0) << 2) |
+                   ((px0 + SW >= a.KW) << 3) | (1 << 5);
+    const int gbase = (py0 * a.KW + px0) * a.g_stride, xbase = (py0 * a.KW + px0) * a.x_stride;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int q = tid + it * C::NTHR;
+      bool ok = !((ilde[it] >> 16) & em);
+      if (is_g(it)) {
+        if (!exact) {
+          const int pxl = q / 12;
+          ok = ok && py0 + (pxl >> SWL) < a.KH && px0 + (pxl & (SW - 1)) < a.KW;
+        }
+        pv[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               gr, ok ? (gbase + ioff[it]) * 4 : 0x7fffffff, 0, 0));
+      } else {
+        if (!exact && q < C::NQ) {
+          const int xp = (q - C::GQ) / 12, yy = xp / XW, xx = xp - yy * XW;
+          ok = ok && py0 - 1 + yy < a.KH && px0 - 1 + xx < a.KW;
+        }
+        pv[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               xr, ok ? (xbase + ioff[it]) * 4 : 0x7fffffff, 0, 0));
+      }
+    }
+  };
+  auto store_all = [&](__bf16* buf) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      if (tid + it * C::NTHR >= C::NQ) continue;
+      const int o = ilde[it] & 0xffff;
+      unsigned h0, m0, l0, h1, m1, l1;
+      split3x2(pv[it][0], pv[it][1], h0, m0, l0);
+      split3x2(pv[it][2], pv[it][3], h1, m1, l1);
+      typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2_t*>(buf + o) = u32x2_t{h0, h1};
+      *reinterpret_cast<u32x2_t*>(buf + o + C::PL) = u32x2_t{m0, m1};
+      *reinterpret_cast<u32x2_t*>(buf + o + 2 * C::PL) = u32x2_t{l0, l1};
+    }
+  };
+
+  // ---- MFMA operand addresses -----------------------------------------------------------
+  // A (G planes): lane 4q+p of group lg: row 8lg + 4t + q, columns 4p .. of block i ^ flip
+  const int abase = (8 * lg + (li >> 2)) * 64 + 4 * (li & 3);
+  const int aflip = wp_flip64(8 * lg + (li >> 2));  // (+4t leaves bits 1 and 3 alone)
+  // B (X planes): stage pixel 8lg + jj = (row pr0, column pc0 + jj); fragment (j, t): X row
+  // r0 + d (+4 for the second read), d = ky XW + kx, block j ^ flip(row); two bits per read
+  const int pr0 = (8 * lg) >> SWL, pc0 = (8 * lg) & (SW - 1);
+  const int r0 = pr0 * XW + pc0 + (li >> 2);
+  const int bbase = C::GPL + r0 * 64 + 4 * (li & 3);
+  unsigned bm0 = 0;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    const int p = 7 * wave + k, j = p / 9, t = p - 9 * j;
+    const int d = (t / 3) * XW + t % 3;
+    bm0 |= (unsigned)(((j ^ wp_flip64(r0 + d)) & 3) | (((j ^ wp_flip64(r0 + d + 4)) & 3) << 2)) << (4 * k);
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) ones[jj] = (__bf16)1.0f;
+
+  Pos pn = pos_of(u_beg);
+  if (u_beg < u_end) {
+    load_all(pn);
+    store_all(lds);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own plane writes done
+  __syncthreads();
+#pragma unroll 1
+  for (long u = u_beg; u < u_end; ++u) {
+    const int cb = (int)((u - u_beg) & 1);
+    const __bf16* buf = lds + cb * C::BUF;
+    __bf16* nbuf = lds + (cb ^ 1) * C::BUF;
+    pn = next(pn);
+    const bool more = u + 1 < u_end;
+    if (more) load_all(pn);  // in flight during the whole stage
+    int aoff = abase;
+    unsigned bm = bm0;
+    asm volatile("" : "+v"(aoff), "+v"(bm));
+    bf16x8 av[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int o = aoff + ((i ^ aflip) << 4);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const __bf16* pp = buf + pl * C::PL + o;
+        av[pl][i] = tr_frag(pp, pp + 4 * 64);
+      }
+    }
+    auto read_b = [&](int k, bf16x8 (&bv)[3]) {
+      const int p = 7 * wave + k, j = p / 9, t = p - 9 * j;  // (uniform)
+      const int d = (t / 3) * XW + t % 3;
+      const int oa = bbase + d * 64 + (int)(((bm >> (4 * k)) & 3) << 4);
+      const int ob = bbase + (d + 4) * 64 + (int)(((bm >> (4 * k + 2)) & 3) << 4);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) bv[pl] = tr_frag(buf + pl * C::PL + oa, buf + pl * C::PL + ob);
+    };
+    bf16x8 bvs[2][3];
+    read_b(0, bvs[0]);
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k + 1 < KMAX && k + 1 < nk) read_b(k + 1, bvs[(k + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (k < nk) {
+        const bf16x8(&bv)[3] = bvs[k & 1];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {  // k_wgrad3p's fold: five corrections, then a0 b0, one add
+          const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+          f32x4 lo = mfma_bf16(av[0][i], bv[1], z);
+          lo = mfma_bf16(av[1][i], bv[0], lo);
+          lo = mfma_bf16(av[0][i], bv[2], lo);
+          lo = mfma_bf16(av[1][i], bv[1], lo);
+          lo = mfma_bf16(av[2][i], bv[0], lo);
+          const f32x4 blk = mfma_bf16(av[0][i], bv[0], lo);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[k][i][r] = acc[k][i][r] + blk[r];
+          asm volatile("" : "+v"(acc[k][i]));
+        }
+      }
+    }
+    if (do_bias) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 hi = mfma_bf16(av[0][i], ones, z);
+        f32x4 lo = mfma_bf16(av[1][i], ones, z);
+        lo = mfma_bf16(av[2][i], ones, lo);
+        x6_acc_add(accb[i], hi, lo);
+      }
+    }
+    if (more) store_all(nbuf);  // (waits for its loads itself)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own plane writes done
+    __syncthreads();                     // next buffer complete; everyone done with this one
+  }
+
+  float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
+  const int cot = a.cout_total ? a.cout_total : a.Cout;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    if (k >= nk) continue;
+    const int p = 7 * wave + k, j = p / 9, t = p - 9 * j;
+    const int ci = ci0 + 16 * j + li;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = i * 16 + 4 * lg + r;
+        if (co < a.Cout && ci < a.Cin)
+          slab[((long)(a.co_base + co) * a.cin_total + a.ci_base + ci) * 9 + t] = acc[k][i][r];
+      }
+  }
+  if (do_bias && li == 0) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = i * 16 + 4 * lg + r;
+        if (co < a.Cout) slab[(long)cot * a.cin_total * 9 + a.co_base + co] = accb[i][r];
+      }
+  }
+}
+
 // 96 output channels (or 96-channel blocks, a.zc == 96), 32 input channels per workgroup,
 // 16-byte aligned NHWC views, images under 2 GiB per operand (32-bit buffer offsets)
 bool wgrad3p_ok(const WgradArgs& a) {
@@ -365,38 +617,34 @@ bool wgrad3p_ok(const WgradArgs& a) {
          (long)a.KH * a.KW * a.x_stride * 4 < 0x7fffffffL;
 }
 
-// DN_WGP_SWL: the widest stage row (log2 pixels, 3..5; default 4: 2 rows of 16 pixels, 72 X pixels
-// per stage instead of 102 for one row of 32) and DN_WGP_GL (default 1: the late G split); A/B on
-// one box (profiles/r4_wgp2_ab.log): 96->96 @64 x 128^2 1.04-1.06 (GL 0, SWL 5) -> 1.01-1.03 ms
+// Stage rows of at most 16 pixels (2 rows of 16: 72 X pixels per stage instead of 102 for one
+// row of 32) and the late G split measured best (profiles/r4_wgp2_ab.log).  The encoder's
+// 48 -> 48 layers take the 4-wave k_wgrad3q from 64^2 up; below that the 3-wave
+// k_wgrad3p<.., 48> measured faster (48->48 @64 x 32^2 0.050 vs 0.065 ms in-step): with 7
+// fragments per wave the short stages no longer hide the next stage's loads.
 hipError_t launch_wgrad3p(const WgradArgs& a, int splits, hipStream_t s, int nz) {
   if (!wgrad3p_ok(a)) return hipErrorInvalidValue;
-  static const int swl_max = getenv("DN_WGP_SWL") ? atoi(getenv("DN_WGP_SWL")) : 4;
-  static const bool gl = !getenv("DN_WGP_GL") || atoi(getenv("DN_WGP_GL")) != 0;
-  if (!a.zc && a.Cout == 48) {  // the encoder's 48 -> 48 layers: 3 waves, rows of <= 16 pixels
-    const dim3 grid(splits, (a.Cin + 47) / 48, nz), block(192);
-    if (a.KW >= 16 && swl_max >= 4) {
+  if (!a.zc && a.Cout == 48) {
+    const dim3 grid(splits, (a.Cin + 47) / 48, nz);
+    if (a.KW >= 64) {
+      prof_kernel("k_wgrad3q<4>");
+      hipLaunchKernelGGL(k_wgrad3q<4>, grid, dim3(256), 0, s, a);
+    } else if (a.KW >= 16) {
       prof_kernel("k_wgrad3p<4,gl,48>");
-      hipLaunchKernelGGL((k_wgrad3p<4, true, 48>), grid, block, 0, s, a);
+      hipLaunchKernelGGL((k_wgrad3p<4, 48>), grid, dim3(192), 0, s, a);
     } else {
       prof_kernel("k_wgrad3p<3,gl,48>");
-      hipLaunchKernelGGL((k_wgrad3p<3, true, 48>), grid, block, 0, s, a);
+      hipLaunchKernelGGL((k_wgrad3p<3, 48>), grid, dim3(192), 0, s, a);
     }
     return hipGetLastError();
   }
   const dim3 grid(splits, (a.Cin + 31) / 32, nz), block(256);
-  const int swl = a.KW >= 32 && swl_max >= 5 ? 5 : (a.KW >= 16 && swl_max >= 4 ? 4 : 3);
-  static const char* kn[2][3] = {{"k_wgrad3p<3>", "k_wgrad3p<4>", "k_wgrad3p<5>"},
-                                 {"k_wgrad3p<3,gl>", "k_wgrad3p<4,gl>", "k_wgrad3p<5,gl>"}};
-  prof_kernel(kn[gl][swl - 3]);
-  if (swl == 5) {
-    if (gl) hipLaunchKernelGGL((k_wgrad3p<5, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_wgrad3p<5>), grid, block, 0, s, a);
-  } else if (swl == 4) {
-    if (gl) hipLaunchKernelGGL((k_wgrad3p<4, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_wgrad3p<4>), grid, block, 0, s, a);
+  if (a.KW >= 16) {
+    prof_kernel("k_wgrad3p<4,gl>");
+    hipLaunchKernelGGL((k_wgrad3p<4>), grid, block, 0, s, a);
   } else {
-    if (gl) hipLaunchKernelGGL((k_wgrad3p<3, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_wgrad3p<3>), grid, block, 0, s, a);
+    prof_kernel("k_wgrad3p<3,gl>");
+    hipLaunchKernelGGL((k_wgrad3p<3>), grid, block, 0, s, a);
   }
   return hipGetLastError();
 }

@@ -139,43 +139,16 @@ __device__ __forceinline__ void x6_block(f32x4 (&acc)[MT][NT], const bf16x8 (&av
 // correct, so the matrix core's alignment bias on that chain is <= 2^-7 of the bias a chained
 // leading sum would carry -- below one fp32 rounding of the output over a K = 864 dot product --
 // while the block costs 4 VALU adds per fragment instead of 8 and no fresh lo chain.
-// DN_X6_CARRY=0 builds the per-block form (accl stays zero) for A/B runs.
-#ifndef DN_X6_CARRY
-#define DN_X6_CARRY 1
-#endif
-#ifndef DN_X6_ABL_CHAIN
-#define DN_X6_ABL_CHAIN 0
-#endif
-// fragment-group width of the carried form: one chain per fragment is enough (a single
-// 16x16x32 bf16 accumulation chain issues back-to-back, MI355X_MICROARCH.md), and the narrow
-// group keeps the hi temporaries and the B look-ahead small enough for the extra accl registers
-#ifndef DN_X6_QGC
-#define DN_X6_QGC 1
-#endif
-constexpr int x6_qgc(int mt, int nt) {
-  return DN_X6_CARRY ? (DN_X6_QGC > 0 ? DN_X6_QGC : x6_qg(mt, nt)) : x6_qg(mt, nt);
-}
+// fragment-group width of the carried form: one chain per fragment (a single 16x16x32 bf16
+// accumulation chain issues back-to-back, MI355X_MICROARCH.md); the narrow group keeps the hi
+// temporaries and the B look-ahead small enough for the extra accl registers
+constexpr int x6_qgc(int, int) { return 1; }
 template <int MT, int NT, int QG>
 __device__ __forceinline__ void x6_group_c(f32x4 (&acc)[MT][NT], f32x4 (&accl)[MT][NT],
                                            const bf16x8 (&av)[3][MT], const bf16x8 (&bv)[3][NT],
                                            int q0) {
-#if DN_X6_CARRY
   const f32x4 z = {0.f, 0.f, 0.f, 0.f};
   constexpr int PA[5] = {0, 1, 0, 1, 2}, PB[5] = {1, 0, 2, 1, 0};
-#if DN_X6_ABL_CHAIN  // diagnostic ablation only (biased sums): the leading product chained into acc
-  (void)z;
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int g = 0; g < QG; ++g) acc[m][q0 + g] = mfma_bf16(av[0][m], bv[0][q0 + g], acc[m][q0 + g]);
-#pragma unroll
-  for (int j = 0; j < 5; ++j)
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int g = 0; g < QG; ++g)
-        accl[m][q0 + g] = mfma_bf16(av[PA[j]][m], bv[PB[j]][q0 + g], accl[m][q0 + g]);
-#else
   f32x4 hi[MT][QG];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
@@ -194,11 +167,6 @@ __device__ __forceinline__ void x6_group_c(f32x4 (&acc)[MT][NT], f32x4 (&accl)[M
     for (int g = 0; g < QG; ++g)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[m][q0 + g][r] = acc[m][q0 + g][r] + hi[m][g][r];
-#endif
-#else
-  (void)accl;
-  x6_group<MT, NT, QG>(acc, av, bv, q0);
-#endif
 }
 
 template <int MT, int NT, int QG>
