@@ -619,14 +619,15 @@ bool wgrad3p_ok(const WgradArgs& a) {
 
 // Stage rows of at most 16 pixels (2 rows of 16: 72 X pixels per stage instead of 102 for one
 // row of 32) and the late G split measured best (profiles/r4_wgp2_ab.log).  The encoder's
-// 48 -> 48 layers take the 4-wave k_wgrad3q from 64^2 up; below that the 3-wave
-// k_wgrad3p<.., 48> measured faster (48->48 @64 x 32^2 0.050 vs 0.065 ms in-step): with 7
-// fragments per wave the short stages no longer hide the next stage's loads.
+// 48 -> 48 layers take the 4-wave k_wgrad3q at 128^2 (0.35-0.36 -> 0.31-0.33 ms); below that
+// the 3-wave k_wgrad3p<.., 48> measured faster (@64^2 0.120-0.127 vs 0.131-0.133 ms,
+// profiles/r5_wg_ab.log; @32^2 0.050 vs 0.065 ms in-step): with 7 fragments per wave the
+// shorter stages no longer hide the next stage's loads.
 hipError_t launch_wgrad3p(const WgradArgs& a, int splits, hipStream_t s, int nz) {
   if (!wgrad3p_ok(a)) return hipErrorInvalidValue;
   if (!a.zc && a.Cout == 48) {
     const dim3 grid(splits, (a.Cin + 47) / 48, nz);
-    if (a.KW >= 64) {
+    if (a.KW >= 128) {
       prof_kernel("k_wgrad3q<4>");
       hipLaunchKernelGGL(k_wgrad3q<4>, grid, dim3(256), 0, s, a);
     } else if (a.KW >= 16) {
