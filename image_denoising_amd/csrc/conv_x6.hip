@@ -2429,14 +2429,33 @@ __global__ __launch_bounds__(512, 1) void k_deconv_x6(FwdArgs a, const __bf16* w
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         a.out + ((long)n * 2 * a.OH + 2 * gy + pa) * out_row + a.out_off, (short)0,
         (int)(out_row * 4), 0x00020000);
-    const int off = gx < a.OW ? ((2 * gx + pb) * a.out_stride + 4 * lg) * 4 : 0x7fffffff;
+    // Whole 128-B lines per store: a lane holds 4 channels of fragments f and f + 1 of its own
+    // pixel, so one store per fragment wrote only 64 B of each pixel's 32-channel line, and the
+    // L2 filled the other half from HBM before the second store came (0.75 GB of extra fetch per
+    // 256^2 launch, profiles/r5a_pmc_step.json).  Adjacent lanes (pixels 2p, 2p + 1 of the
+    // wave-tile) swap one fragment's registers (DPP quad_perm [1,0,3,2]), and each store
+    // instruction writes the full line (channels 32k .. 32k + 31) of one pixel per lane pair:
+    // the even lane its fragment-f quad, the odd lane the even pixel's fragment-(f + 1) quad.
+    const bool ev = (li & 1) == 0;
+    const int gxa = gx - (li & 1);  // the pair's even pixel; gxa + 1 the odd one
+    const int offa = gxa < a.OW ? ((2 * gxa + pb) * a.out_stride + 4 * lg + (ev ? 0 : 16)) * 4 : 0x7fffffff;
+    const int offb = gxa + 1 < a.OW ? ((2 * gxa + 2 + pb) * a.out_stride + 4 * lg + (ev ? 0 : 16)) * 4
+                                     : 0x7fffffff;
 #pragma unroll
-    for (int f = 0; f < 6; ++f) {
-      const float4 bb = *reinterpret_cast<const float4*>(lbias + f * 16 + 4 * lg);
-      const float4 o = make_float4(out[f][0][0] + bb.x, out[f][0][1] + bb.y, out[f][0][2] + bb.z,
-                                   out[f][0][3] + bb.w);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rs, off + 64 * f, 0,
-                                             0);
+    for (int f = 0; f < 6; f += 2) {
+      const float4 b0 = *reinterpret_cast<const float4*>(lbias + f * 16 + 4 * lg);
+      const float4 b1 = *reinterpret_cast<const float4*>(lbias + f * 16 + 16 + 4 * lg);
+      const f32x4 o0 = {out[f][0][0] + b0.x, out[f][0][1] + b0.y, out[f][0][2] + b0.z, out[f][0][3] + b0.w};
+      const f32x4 o1 = {out[f + 1][0][0] + b1.x, out[f + 1][0][1] + b1.y, out[f + 1][0][2] + b1.z,
+                        out[f + 1][0][3] + b1.w};
+      f32x4 t;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        t[r] = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+                                             __builtin_bit_cast(int, ev ? o1[r] : o0[r]), 0xB1, 0xF, 0xF, false));
+      const f32x4 va = ev ? o0 : t, vb = ev ? t : o1;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, va), rs, offa + 64 * f, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, vb), rs, offb + 64 * f, 0, 0);
     }
   };
   // three input register sets: a wave-tile's input is requested two tiles before it is used

@@ -50,6 +50,8 @@ def main():
         # sequence): bench.py picks the dominant shape's launches out of the last step
         if len(f) == len(w):
             out[k]["per_launch_bytes"] = [round(a * 2048 + b * 1024) for a, b in zip(f, w)]
+            out[k]["per_launch_fetch"] = [round(a * 2048) for a in f]
+            out[k]["per_launch_write"] = [round(b * 1024) for b in w]
     doc = {"method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes with "
                      "--kernel-trace over `bench.py --steps 2 --warmup 1 --no-cpu-baseline` "
                      "(tools/gpu_run.sh pmc); per-launch means over every dispatch of the kernel "
