@@ -35,8 +35,13 @@
 
 namespace dn {
 
+// NO = 96 output channels: wave (nh, ph) = output channels 48nh .. +47 x all 4 M fragments;
+// NO = 48 (the encoder's 48 -> 48 convs): wave (mh, ph) = all 48 output channels x M fragments
+// 2mh, 2mh + 1 (tile rows 4mh .. 4mh + 3), the same V and the same stage sequence
+template <int NO = 96>
 struct WCfg {
-  static constexpr int WAVES = 4, MT = 4, NTW = 3, NP = 96, NPOS = 4, NJ = 8;
+  static constexpr int WAVES = 4, MT = NO == 96 ? 4 : 2, NTW = 3, NP = NO, NPOS = 4, NJ = 8;
+  static constexpr int HF = MT / 2;                    // M fragments a wave keeps after the exchange
   static constexpr int TW = 16, TH = 8, IH = TH + 2, IW = TW + 2, KC = 32;
   static constexpr int SPC = 12;                       // weight stages per full chunk (ky, p)
   static constexpr int VPL = IH * 4 * NJ * NPOS * 8;   // bf16 per plane of V (quads of 8)
@@ -45,10 +50,11 @@ struct WCfg {
   static constexpr int WSTP = x6_wst(NP);
   static constexpr int VITEMS = (IH * NJ * 8 + WAVES * 64 - 1) / (WAVES * 64);  // transform items
   static constexpr int PS = 16 * NTW + 4;
-  static constexpr int XCH = WAVES * 2 * NTW * 2 * 4 * 64;  // floats of the exchange area
+  static constexpr int XCH = WAVES * HF * NTW * 2 * 4 * 64;  // floats of the exchange area
   static constexpr int LEND = (XCH + WAVES * 16 * PS) * 4;  // exchange + epilogue staging (over V)
   static constexpr int LBYTES = VBYTES > LEND ? VBYTES : LEND;
   static_assert(2 * LBYTES <= 163840, "two workgroups per CU");
+  static_assert(NO == 96 || NO == 48, "96 or 48 output channels");
 };
 
 // 16-B quad index of V element (row, kq, j, p): p is XOR-swizzled by row & 1 and the bit-reversed
@@ -98,17 +104,18 @@ __device__ __forceinline__ void w6_for(F&& f) {
 // TAIL (x6_tail_mode of K) packs the last chunk's channels: 1 (<= 4 channels): one stage per
 // position, k = 4 ky + channel; 2 (<= 16 channels): two stages per position, k = 16 (ky - 2s) +
 // channel.  Full chunks: stage 4 ky + p, k = channel.
-template <int TAIL>
+template <int TAIL, int NO = 96>
 __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
-  using C = WCfg;
-  constexpr int MT = C::MT, NTW = C::NTW;
+  using C = WCfg<NO>;
+  constexpr int MT = C::MT, NTW = C::NTW, HF = C::HF;
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
   __bf16* lv = reinterpret_cast<__bf16*>(lds_raw);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lg = lane >> 4;
-  const int nh = wave & 1, ph = wave >> 1;
+  const int nh = NO == 96 ? wave & 1 : 0, ph = wave >> 1;
+  const int mb = NO == 96 ? 0 : 2 * (wave & 1);  // the wave's first M fragment
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
   int bxr, byr;
   xcd_tile(bxr, byr);
@@ -227,7 +234,7 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
     bf16x8 av[3][MT];
 #pragma unroll
     for (int f = 0; f < MT; ++f) {
-      const int row0 = 2 * f + (liv >> 3), j = liv & 7;
+      const int row0 = 2 * (mb + f) + (liv >> 3), j = liv & 7;
       if constexpr (MODE == 0) {
         const int o = w6_vq(row0 + ky0, lgv, j, p) * 8;
 #pragma unroll
@@ -320,23 +327,23 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
 
   // output transform: ph 0 holds m0, m1, ph 1 holds m2, m3.  Partial sums per tile:
   //   ph 0: (y0, y1) += (m0 + m1, m1);   ph 1: (y0, y1) += (m2, -m2 - m3)
-  // wave ph keeps M fragments 2ph, 2ph+1 (tile rows 4ph .. 4ph+3) and hands the other two's
-  // partials to its partner (same nh) through LDS
+  // wave ph keeps HF of its MT M fragments (96: 2ph, 2ph+1 = tile rows 4ph .. 4ph+3; 48: its
+  // fragment mb + ph) and hands the other HF's partials to its partner (wave ^ 2) through LDS
   __builtin_amdgcn_s_waitcnt(0xC07F);
   w6_barrier();  // every wave is done with V: it becomes the exchange area
-  f32x4 y[2][2][NTW];  // [f - 2ph][output parity][q]
+  f32x4 y[HF][2][NTW];  // [kept fragment][output parity][q]
   {
-    float* xo = reinterpret_cast<float*>(lds_raw) + (wave * 2 * NTW * 2) * 4 * 64;  // mine, out
-    const int pw = wave ^ 2;                                                        // partner
-    const float* xi = reinterpret_cast<const float*>(lds_raw) + (pw * 2 * NTW * 2) * 4 * 64;
+    float* xo = reinterpret_cast<float*>(lds_raw) + (wave * HF * NTW * 2) * 4 * 64;  // mine, out
+    const int pw = wave ^ 2;                                                         // partner
+    const float* xi = reinterpret_cast<const float*>(lds_raw) + (pw * HF * NTW * 2) * 4 * 64;
     // compile-time fragment indices per position half (a run-time index would put acc in memory)
     auto part = [&](auto phc) {
       constexpr int PH = decltype(phc)::value;
 #pragma unroll
-      for (int ff = 0; ff < 2; ++ff)
+      for (int ff = 0; ff < HF; ++ff)
 #pragma unroll
         for (int q = 0; q < NTW; ++q) {
-          constexpr int FO = 2 * (1 - PH), FK = 2 * PH;  // the partner's fragments, mine
+          constexpr int FO = HF * (1 - PH), FK = HF * PH;  // the partner's fragments, mine
           f32x4 o0, o1, k0, k1;
           if constexpr (PH == 0) {
             o0 = acc[0][FO + ff][q] + acc[1][FO + ff][q]; o1 = acc[1][FO + ff][q];
@@ -356,7 +363,7 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
     __builtin_amdgcn_s_waitcnt(0xC07F);
     w6_barrier();
 #pragma unroll
-    for (int ff = 0; ff < 2; ++ff)
+    for (int ff = 0; ff < HF; ++ff)
 #pragma unroll
       for (int q = 0; q < NTW; ++q) {
         // y0 = (m0 + m1) + m2, y1 = m1 + (-m2 - m3): ph 0's part first in both
@@ -366,15 +373,15 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
         else { y[ff][0][q] = i0 + y[ff][0][q]; y[ff][1][q] = i1 + y[ff][1][q]; }
       }
   }
-  // epilogue: this wave's 4 tile rows 4ph + r (fragment 2ph + r/2, half r%2), channels
+  // epilogue: this wave's 2 HF tile rows wrow + r (kept fragment r/2, half r%2), channels
   // 48nh .. +47; the fragment's lane (li, lg) holds tiles 4lg .. 4lg+3 of the fragment's 16,
   // i.e. row half lg >> 1, tiles 4 (lg & 1) + e -> pixels 2 (4 (lg & 1) + e) + parity
   float* st = reinterpret_cast<float*>(lds_raw) + C::XCH + wave * 16 * C::PS;
-  f32x4 outr[4][NTW];  // rows as the vec epilogue's acc: pixel 4lg' + r of row m
+  f32x4 outr[2 * HF][NTW];  // rows as the vec epilogue's acc: pixel 4lg' + r of row m
   // stage each row through LDS in the C/D map the epilogue expects: write the row's 16 pixels
   // x 48 channels, read back as acc-layout registers
 #pragma unroll
-  for (int r4 = 0; r4 < 4; ++r4) {
+  for (int r4 = 0; r4 < 2 * HF; ++r4) {
     const int ff = r4 >> 1, hf = r4 & 1;
     if ((lg >> 1) == hf) {
 #pragma unroll
@@ -397,7 +404,8 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   {
     const int cz = (a.zc ? (int)blockIdx.z * a.zc : 0) + nh * 16 * NTW;
     const int nout = a.NOUT - cz < 16 * NTW ? a.NOUT - cz : 16 * NTW;
-    if (nout > 0) fwd_epilogue_at<NTW, 4, C::PS>(a, outr, st, ty0, tx0, n, 4 * ph, cz, nout);
+    const int wrow = 2 * (mb + HF * ph);  // (even: a fused 2x2 pool sees whole windows)
+    if (nout > 0) fwd_epilogue_at<NTW, 2 * HF, C::PS>(a, outr, st, ty0, tx0, n, wrow, cz, nout);
   }
 }
 
@@ -761,29 +769,37 @@ hipError_t launch_fwd_w6s(const FwdArgs& a, const unsigned* list, const int* cnt
   return hipGetLastError();
 }
 
-int w6_stages_per_chunk() { return WCfg::SPC; }
+int w6_stages_per_chunk() { return WCfg<96>::SPC; }
 
-// k_c3w6 for a 96-output-channel forward / data gradient on a PK_W6 image (a.x6_tail & X6_W6)
+// k_c3w6 for a 96- or 48-output-channel forward / data gradient on a PK_W6 image (a.x6_tail &
+// X6_W6); a fused 2x2 max-pool (a.pool_out) through the float4 epilogue as the direct kernels
 hipError_t launch_fwd_w6(const FwdArgs& a, hipStream_t s) {
-  using C = WCfg;
+  using C = WCfg<96>;  // (tile geometry: both widths)
   const bool aux = a.epi == EPI_MASK || a.epi == EPI_BIAS_ADD;
   const int tail = a.x6_tail & 7;
   const int nz = a.zc ? (a.NOUT + a.zc - 1) / a.zc : 1;
-  if ((a.zc ? a.zc != 96 : a.NOUT != 96) || a.out_layout != OUT_NHWC || a.sel_rd ||
+  const int np = a.zc ? a.zc : a.NOUT;
+  if ((np != 96 && np != 48) || a.out_layout != OUT_NHWC || a.sel_rd ||
       ((a.out_stride | a.out_off | a.NOUT) & 3) || (aux && ((a.mask_stride | a.mask_off) & 3)) ||
       a.epi < EPI_BIAS || a.epi > EPI_BIAS_ADD || ((a.in_stride | a.in_off | a.K) & 3) ||
       (long)C::IH * a.IWt * a.in_stride * 4 >= 0x7fffffffL || tail != x6_tail_mode(a.K))
     return hipErrorInvalidValue;
+  if (a.pool_out && (a.epi != EPI_BIAS_ACT || ((a.pool_stride | a.pool_off) & 3) || ((a.OH | a.OW) & 1)))
+    return hipErrorInvalidValue;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
   const dim3 grid(tx * ty, a.N, nz), block(C::WAVES * 64);
-  static const char* kn[3] = {"k_c3w6<0>", "k_c3w6<1>", "k_c3w6<2>"};
-  prof_kernel(kn[tail]);
-  if (tail == 1)
-    hipLaunchKernelGGL(k_c3w6<1>, grid, block, 0, s, a);
-  else if (tail == 2)
-    hipLaunchKernelGGL(k_c3w6<2>, grid, block, 0, s, a);
-  else
-    hipLaunchKernelGGL(k_c3w6<0>, grid, block, 0, s, a);
+  static const char* kn[2][3] = {{"k_c3w6<0>", "k_c3w6<1>", "k_c3w6<2>"},
+                                 {"k_c3w6<0,48>", "k_c3w6<1,48>", "k_c3w6<2,48>"}};
+  prof_kernel(kn[np == 48][tail]);
+  if (np == 48) {
+    if (tail == 1) hipLaunchKernelGGL((k_c3w6<1, 48>), grid, block, 0, s, a);
+    else if (tail == 2) hipLaunchKernelGGL((k_c3w6<2, 48>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_c3w6<0, 48>), grid, block, 0, s, a);
+  } else {
+    if (tail == 1) hipLaunchKernelGGL(k_c3w6<1>, grid, block, 0, s, a);
+    else if (tail == 2) hipLaunchKernelGGL(k_c3w6<2>, grid, block, 0, s, a);
+    else hipLaunchKernelGGL(k_c3w6<0>, grid, block, 0, s, a);
+  }
   return hipGetLastError();
 }
 

@@ -1234,9 +1234,9 @@ __device__ __forceinline__ void pk_x6(const PackJob& j, long e) {
   }
   __bf16 h, m, l;
   split3(v, h, m, l);
-  // (block z's image starts at z x x6_pack_elems / nz: 12 stage slots per chunk for 96-wide
-  // blocks, which have room for the Winograd image too)
-  __bf16* st = static_cast<__bf16*>(j.out) + ((long)z * nch * (NP == 96 ? 12 : 9) + ct) * wst;
+  // (block z's image starts at z x x6_pack_elems / nz: 12 stage slots per chunk for 96- and
+  // 48-wide blocks, which have room for the Winograd image too)
+  __bf16* st = static_cast<__bf16*>(j.out) + ((long)z * nch * (NP == 96 || NP == 48 ? 12 : 9) + ct) * wst;
   const int o = nn * 32 + x6_swz(nn, kk >> 3) * 8 + (kk & 7);
   st[o] = h;
   st[NP * 32 + o] = m;
@@ -1468,13 +1468,13 @@ long x6_pack_elems(int K, int nout, int zc) {
   const int np = x6_np(nout, zc);
   if (np == 0 || (zc > 0 && zc != np)) return -1;
   const int nz = zc > 0 ? (nout + zc - 1) / zc : 1;
-  // 96-output blocks: room for the Winograd image (12 stages per chunk) as well
-  const int spc = np == 96 ? 12 : 9;
+  // 96- and 48-output blocks: room for the Winograd image (12 stages per chunk) as well
+  const int spc = np == 96 || np == 48 ? 12 : 9;
   return (long)nz * ((K + 31) / 32) * spc * x6_wst(np);
 }
 
-// DN_X6_W6=1/0: 96-output-channel large-grid launches on the Winograd kernel or not (default
-// DN_X6_W6_DEFAULT)
+// DN_X6_W6=1/0: 96- and 48-output-channel large-grid launches on the Winograd kernel or not
+// (default DN_X6_W6_DEFAULT)
 #ifndef DN_X6_W6_DEFAULT
 #define DN_X6_W6_DEFAULT 1
 #endif
@@ -1490,7 +1490,8 @@ int x6_image_mode(int N, int H, int W, int K, int nout, int zc, bool aligned) {
   const int nz = zc > 0 ? (nout + zc - 1) / zc : 1;
   // DN_W6_MIN_TILES: tuning probe for the smallest Winograd launch (default one full round)
   static const long min_t = getenv("DN_W6_MIN_TILES") ? atol(getenv("DN_W6_MIN_TILES")) : 512;
-  const bool w6 = w6_enabled() && x6_np(nout, zc) == 96 && (zc == 0 ? nout == 96 : zc == 96) &&
+  const int np = x6_np(nout, zc);
+  const bool w6 = w6_enabled() && (np == 96 || np == 48) && (zc == 0 ? nout == np : zc == np) &&
                   t8 * nz >= min_t;
   if (!w6 && !x6_pipelined(N, H, W, nout, zc)) return 0;
   return x6_tail_mode(K) | (w6 ? X6_W6 : 0);
@@ -1505,8 +1506,9 @@ bool pack_job_x6(const WView& wv, int K, int nout, int zc, void* out, int mode, 
   const long total = x6_pack_elems(K, nout, zc);
   const int tail = mode & 7;
   const bool w6 = (mode & X6_W6) != 0;
+  const int npw = x6_np(nout, zc);
   if (total < 0 || wv.taps != 9 || (tail && tail != x6_tail_mode(K)) ||
-      (w6 && (zc == 0 ? nout != 96 : zc != 96)))
+      (w6 && ((npw != 96 && npw != 48) || (zc == 0 ? nout != npw : zc != npw))))
     return false;
   WView v = wv;
   if (zc > 0) v.sZ = (long)zc * wv.sN;  // block z = output channels [z*zc, z*zc + zc)
@@ -1594,8 +1596,8 @@ bool x6_pipelined(int N, int H, int W, int nout, int zc) {
 hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s) {
   const int np = x6_np(a.NOUT, a.zc);
   if (np == 0 || (a.zc > 0 && a.zc != np)) return hipErrorInvalidValue;
-  // a fused pool: the float4 epilogue of a tiled kernel (k_c3w6 has none), even sides
-  if (a.pool_out && (a.epi != EPI_BIAS_ACT || a.out_layout != OUT_NHWC || (a.x6_tail & X6_W6) ||
+  // a fused pool: the float4 epilogue of a tiled kernel, even sides
+  if (a.pool_out && (a.epi != EPI_BIAS_ACT || a.out_layout != OUT_NHWC ||
                      ((a.out_stride | a.out_off | a.NOUT) & 3) || ((a.OH | a.OW) & 1)))
     return hipErrorInvalidValue;
   const int nz = a.zc > 0 ? (a.NOUT + a.zc - 1) / a.zc : 1;

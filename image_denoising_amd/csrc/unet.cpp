@@ -415,10 +415,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // bias / activation / storage)
   // the pipelined split-bf16 kernel takes a partial last K chunk (dec_conv1a's x channels,
   // the 48-channel encoder's second chunk) packed over fewer stages (x6_tail_mode)
-  // (x6_image_mode: | X6_W6 for the Winograd kernel on the 96-output layers.  In forward-only
-  // plans dec_conv1b stays on the direct kernel: the N2N no-grad pass evaluates it at the pair
-  // pixels only (k_c3x6s, direct arithmetic), bit-identical to the full no-grad forward only if
-  // that one's dec_conv1b is direct too -- test_unet_forward_n2n_pair_pixels_bit_identical)
+  // (x6_image_mode: | X6_W6 for the Winograd kernel on the 96- and 48-output layers from one
+  // round of 8 x 16 tiles)
   // the encoder's 2x2 max-pools fused into the x6 convs' epilogues (DN_POOL_FUSE=0: separate
   // k_pool_fwd launches, A/B)
   static const bool pool_fuse = !getenv("DN_POOL_FUSE") || atoi(getenv("DN_POOL_FUSE")) != 0;
@@ -472,7 +470,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
       a.x6_tail = x6_tail_f(i);  // a partial last K chunk packed over fewer stages
       a.wp = ws + p.packX[i]; a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
       a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = layout;
-      if (pool && pool_fuse && act && layout == OUT_NHWC && !(a.x6_tail & X6_W6)) {
+      if (pool && pool_fuse && act && layout == OUT_NHWC) {
         a.pool_out = pool->p; a.pool_stride = pool->stride; a.pool_off = pool->off;
         a.pool_only = pool_only;
         if (pooled) *pooled = true;
