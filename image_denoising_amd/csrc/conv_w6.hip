@@ -788,7 +788,7 @@ hipError_t launch_fwd_w6(const FwdArgs& a, hipStream_t s) {
     return hipErrorInvalidValue;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
   const dim3 grid(tx * ty, a.N, nz), block(C::WAVES * 64);
-  static const char* kn[2][3] = {{"k_c3w6<0>", "k_c3w6<1>", "k_c3w6<2>"},
+  static const char* kn[2][3] = {{"k_c3w6<0,96>", "k_c3w6<1,96>", "k_c3w6<2,96>"},
                                  {"k_c3w6<0,48>", "k_c3w6<1,48>", "k_c3w6<2,48>"}};
   prof_kernel(kn[np == 48][tail]);
   if (np == 48) {

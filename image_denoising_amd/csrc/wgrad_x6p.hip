@@ -364,19 +364,23 @@ __global__ __launch_bounds__(CO == 96 ? 256 : 192, 2) void k_wgrad3p(WgradArgs a
 // fragments (acc[7][3]); the bias gradient goes to wave 3, which has one fragment fewer.
 //   K stage = 32 pixels (SH rows of SW), G [32 px][64] and X [XPIX][64] bf16 planes (48 channels
 //   used; 128-B rows, wp_flip64), two buffers, two workgroups per CU (78 KiB each).
-//   Split-pass items: 384 G quads + XPIX * 12 X quads dealt tid + 256 it; since 384 = 1.5 x 256,
-//   item 0 of every thread and item 1 of waves 0, 1 are G, the rest X: a wave-uniform type.
+//   Split-pass items: 16 quad slots per pixel (4 blocks x 4 quads; block 3 is the row padding,
+//   its lanes neither load nor store), G's 512 slots = items 0 and 1 of every thread, then X's.
+//   A 16-lane group of a ds_write_b64 (banks mod 32 dwords) thus writes the four blocks of ONE
+//   pixel row, which the row swizzle keeps on four distinct 32-B bank sets: conflict-free
+//   writes (12 real quads per pixel dealt 16 lanes at a time put blocks of two pixels on the same
+//   banks: 25 % of the LDS-active cycles in conflicts, profiles/r5_pmc_sq_n2n.txt).
 //   B reads one fragment ahead of their MFMAs (as k_wgrad3p).
 // ------------------------------------------------------------------------------------
 template <int SWL>
 struct Wq3Cfg {
   static constexpr int NTHR = 256, RW = 64, CIB = 48;
   static constexpr int SW = 1 << SWL, SH = 32 >> SWL, XW = SW + 2, XPIX = (SH + 2) * XW;
-  static constexpr int GQ = 32 * 12, XQ = XPIX * 12, NQ = GQ + XQ;  // float4 items
+  static constexpr int GQ = 32 * 16, XQ = XPIX * 16, NQ = GQ + XQ;  // float4 slots
   static constexpr int NIT = (NQ + NTHR - 1) / NTHR;
   static constexpr int GPL = 32 * RW, PL = GPL + XPIX * RW, BUF = 3 * PL;  // bf16
   static constexpr int KMAX = 7;                                         // B fragments per wave
-  static_assert(GQ == NTHR + NTHR / 2, "item 1 is G exactly for waves 0 and 1");
+  static_assert(GQ == 2 * NTHR, "items 0 and 1 of every thread are G");
   static_assert(2 * BUF * 2 <= 81920, "two workgroups per CU");
 };
 
@@ -405,22 +409,24 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3q(WgradArgs a) {
 
   // ---- split-pass items (as k_wgrad3p): offset in the operand image relative to the stage
   // origin; LDS index (low 16 bits) | halo-edge class (bits 16..)
-  auto is_g = [&](int it) { return it == 0 || (it == 1 && wave < 2); };  // wave-uniform
+  auto is_g = [&](int it) { return it < 2; };
+  // (bit 21: no data -- loads zeros; bit 22: padding slot -- not stored either)
   int ioff[NIT], ilde[NIT];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int q = tid + it * C::NTHR;
-    ioff[it] = 0; ilde[it] = 32 << 16;
+    ioff[it] = 0; ilde[it] = (32 | 64) << 16;
     if (q < C::GQ) {
-      const int px = q / 12, c = 4 * (q % 12);
+      const int px = q >> 4, c = 4 * (q & 15);
       ioff[it] = ((px >> SWL) * a.KW + (px & (SW - 1))) * a.g_stride + c;
-      ilde[it] = (wp_idx(px, 64, c >> 4) + (c & 15)) | ((c < a.Cout ? 0 : 32) << 16);
+      ilde[it] = (wp_idx(px, 64, c >> 4) + (c & 15)) |
+                 ((c >= 48 ? 32 | 64 : (c < a.Cout ? 0 : 32)) << 16);
     } else if (q < C::NQ) {
-      const int r = q - C::GQ, xp = r / 12, c = 4 * (r % 12);
+      const int r = q - C::GQ, xp = r >> 4, c = 4 * (r & 15);
       const int yy = xp / XW, xx = xp - yy * XW;
       ioff[it] = ((yy - 1) * a.KW + xx - 1) * a.x_stride + ci0 + c;
       const int e = (yy == 0) | ((yy == SH + 1) << 1) | ((xx == 0) << 2) | ((xx == SW + 1) << 3) |
-                    ((ci0 + c < a.Cin ? 0 : 1) << 5);
+                    (c >= 48 ? 32 | 64 : ((ci0 + c < a.Cin ? 0 : 1) << 5));
       ilde[it] = (C::GPL + wp_idx(xp, 64, c >> 4) + (c & 15)) | (e << 16);
     }
   }
@@ -456,14 +462,14 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3q(WgradArgs a) {
       bool ok = !((ilde[it] >> 16) & em);
       if (is_g(it)) {
         if (!exact) {
-          const int pxl = q / 12;
+          const int pxl = q >> 4;
           ok = ok && py0 + (pxl >> SWL) < a.KH && px0 + (pxl & (SW - 1)) < a.KW;
         }
         pv[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                gr, ok ? (gbase + ioff[it]) * 4 : 0x7fffffff, 0, 0));
       } else {
         if (!exact && q < C::NQ) {
-          const int xp = (q - C::GQ) / 12, yy = xp / XW, xx = xp - yy * XW;
+          const int xp = (q - C::GQ) >> 4, yy = xp / XW, xx = xp - yy * XW;
           ok = ok && py0 - 1 + yy < a.KH && px0 - 1 + xx < a.KW;
         }
         pv[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -474,7 +480,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3q(WgradArgs a) {
   auto store_all = [&](__bf16* buf) {
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      if (tid + it * C::NTHR >= C::NQ) continue;
+      if (tid + it * C::NTHR >= C::NQ || ((ilde[it] >> 22) & 1)) continue;  // (padding slots)
       const int o = ilde[it] & 0xffff;
       unsigned h0, m0, l0, h1, m1, l1;
       split3x2(pv[it][0], pv[it][1], h0, m0, l0);
@@ -631,20 +637,20 @@ hipError_t launch_wgrad3p(const WgradArgs& a, int splits, hipStream_t s, int nz)
       prof_kernel("k_wgrad3q<4>");
       hipLaunchKernelGGL(k_wgrad3q<4>, grid, dim3(256), 0, s, a);
     } else if (a.KW >= 16) {
-      prof_kernel("k_wgrad3p<4,gl,48>");
+      prof_kernel("k_wgrad3p<4,48>");
       hipLaunchKernelGGL((k_wgrad3p<4, 48>), grid, dim3(192), 0, s, a);
     } else {
-      prof_kernel("k_wgrad3p<3,gl,48>");
+      prof_kernel("k_wgrad3p<3,48>");
       hipLaunchKernelGGL((k_wgrad3p<3, 48>), grid, dim3(192), 0, s, a);
     }
     return hipGetLastError();
   }
   const dim3 grid(splits, (a.Cin + 31) / 32, nz), block(256);
   if (a.KW >= 16) {
-    prof_kernel("k_wgrad3p<4,gl>");
+    prof_kernel("k_wgrad3p<4,96>");
     hipLaunchKernelGGL((k_wgrad3p<4>), grid, block, 0, s, a);
   } else {
-    prof_kernel("k_wgrad3p<3,gl>");
+    prof_kernel("k_wgrad3p<3,96>");
     hipLaunchKernelGGL((k_wgrad3p<3>), grid, block, 0, s, a);
   }
   return hipGetLastError();
