@@ -389,7 +389,7 @@ def main():
                     help="finetune only: bf16 = mixed-precision frozen base (BASELINE configs[4])")
     ap.add_argument("--conv-precision", choices=["fp32", "fp32_x6"], default="fp32_x6",
                     help="UNet 3x3 convs: fp32 operands split exactly into three bf16 pieces on "
-                         "the bf16 matrix cores (fp32_x6, default: fp32-accurate, DESIGN.md §11), "
+                         "the bf16 matrix cores (fp32_x6, default: fp32-accurate, DESIGN.md §12), "
                          "or fp32 operands on the fp32 matrix cores")
     ap.add_argument("--arch", choices=["UNet", "UNetImproved"], default="UNet",
                     help="network (train.py:305-313 / finetune.py --arch)")

@@ -235,7 +235,7 @@ class UNet(nn.Module):
         'fp32'    fp32 operands on the fp32 matrix cores (v_mfma_f32_16x16x4_f32);
         'fp32_x6' fp32 operands split exactly into three bf16 pieces, the six piece products
                   of order <= 2 on the bf16 matrix cores, fp32 accumulation -- the rounding
-                  error of an fp32 dot product (DESIGN.md §11) at 2.67x the matrix-core peak."""
+                  error of an fp32 dot product (DESIGN.md §12) at 2.67x the matrix-core peak."""
         if mode not in self._PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(self._PRECISIONS)}")
         self.precision = mode

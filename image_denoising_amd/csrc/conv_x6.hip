@@ -7,7 +7,7 @@
 // 2^-8(i+j); the six with i+j <= 2 are kept (a0b0, a0b1, a1b0, a0b2, a1b1, a2b0), the dropped
 // three are below 2^-23 |ab|, i.e. one fp32 rounding.  Each piece product is exact in the
 // MFMA's fp32 accumulator, so the result has the error of an fp32 dot product (measured
-// against fp64: the same rms error as the fp32 MFMA path, DESIGN.md §11).  Six
+// against fp64: the same rms error as the fp32 MFMA path, DESIGN.md §12).  Six
 // v_mfma_f32_16x16x32_bf16 (16 cycles each) replace eight v_mfma_f32_16x16x4_f32 (32 cycles)
 // per 16x16x32 block: a 2.67x higher matrix-core ceiling for the same fp32-accurate result.
 //

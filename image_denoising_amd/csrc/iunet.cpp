@@ -74,7 +74,7 @@ bool ggeom(int ksize, int K, int nout, GGeom& g) {
 // 32 reduction channels (on large grids a partial last chunk of <= 16 channels costs 5 of 9
 // stages, `tail`), so they take the convs that fill those tiles; the 24-channel level and
 // small-grid K = 48 stay on the fp32 kernels, where the padding would cost more than the
-// faster matrix cores give (measured per shape, DESIGN.md §9)
+// faster matrix cores give (measured per shape, DESIGN.md §10)
 bool x6_shape(int nout) { return nout == 32 || nout % 48 == 0; }
 bool x6_takes(int K, int nout, int tail) {
   // 32-wide tiles with K < 80 were staging-bound on round 2's 8-row kernels (no gain for 32x48,

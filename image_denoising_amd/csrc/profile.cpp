@@ -2,7 +2,7 @@
 // site of the U-Net executors and the step's elementwise entry points records a pair of HIP
 // events on the stream it launches on, with the op, its shape and its algorithmic FLOPs, and the
 // executors run single-stream so the event pairs bracket one kernel each.  bench.py reads the
-// records of one profiled step to report the step's own per-shape roofline (DESIGN.md §5).
+// records of one profiled step to report the step's own per-shape roofline (DESIGN.md §6).
 #include <cstdio>
 #include <cstring>
 #include <mutex>

@@ -198,11 +198,11 @@ def build_network(log_name: str, n_channel: int, n_feature: int):
     from .improved_unet import ImprovedUNet
 
     if "UNET" in log_name and "blindspot" in log_name:
-        raise SystemExit("the blind-spot UNet is out of scope on this path (DESIGN.md §8)")
+        raise SystemExit("the blind-spot UNet is out of scope on this path (DESIGN.md §9)")
     if "UNET" in log_name:
         return UNet(in_nc=n_channel, out_nc=n_channel, n_feature=n_feature)
     if "RESNET" in log_name:
-        raise SystemExit("RESNET is out of scope on this path (DESIGN.md §8)")
+        raise SystemExit("RESNET is out of scope on this path (DESIGN.md §9)")
     if "UNetImproved" in log_name:
         return ImprovedUNet(in_nc=n_channel, out_nc=n_channel, n_feature=n_feature)
     raise SystemExit(f"--log_name {log_name!r} names no network (evaluation.py:32-50)")

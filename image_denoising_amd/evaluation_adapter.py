@@ -43,7 +43,7 @@ def build_model(arch: str, n_channel: int, n_feature: int, hidden: int):
     from .finetune import build_base_model
 
     if arch == "RESNET":
-        raise SystemExit("RESNET is out of scope on this path (DESIGN.md §8)")
+        raise SystemExit("RESNET is out of scope on this path (DESIGN.md §9)")
     base = build_base_model(arch, n_channel, n_feature)
     return DenoiserWithAdapter(base, in_channels=n_channel, hidden_channels=hidden,
                                freeze_base=True, use_no_grad_for_base=True)

@@ -164,7 +164,7 @@ class ImprovedUNet(nn.Module):
     def set_precision(self, mode: str) -> "ImprovedUNet":
         """Arithmetic of the 3x3 convolutions' forward and data gradient: 'fp32' (fp32 matrix
         cores) or 'fp32_x6' (exact three-piece bf16 split, six products, fp32 accumulation;
-        DESIGN.md §11).  Weight gradients and the 1x1 / noise-estimator convs stay fp32."""
+        DESIGN.md §12).  Weight gradients and the 1x1 / noise-estimator convs stay fp32."""
         if mode not in self._PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(self._PRECISIONS)}")
         self.precision = mode
