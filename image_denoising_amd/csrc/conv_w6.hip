@@ -104,6 +104,12 @@ __device__ __forceinline__ void w6_for(F&& f) {
 // TAIL (x6_tail_mode of K) packs the last chunk's channels: 1 (<= 4 channels): one stage per
 // position, k = 4 ky + channel; 2 (<= 16 channels): two stages per position, k = 16 (ky - 2s) +
 // channel.  Full chunks: stage 4 ky + p, k = channel.
+// TAIL 3 (X6_T1: the last chunk has ONE live channel, dec_conv1a's image channel at C = 1): one
+// stage per position whose single MFMA per fragment pair holds all six split products of the
+// three kernel rows, k = 8 ky + slot, slot = (h,h) (h,m) (m,h) (h,l) (l,h) (m,m) of (v, u):
+// lane group ky reads its row's (h, m, l) of v as one 8-B slot, the packer lays u's pieces out
+// in slot order (pk_w6).  1 MFMA instead of 6, summed from zero and added to the running sum
+// as the other blocks' hi + lo.
 template <int TAIL, int NO = 96>
 __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   using C = WCfg<NO>;
@@ -177,6 +183,20 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
           v[2][c] = d[it][2][c] - d[it][1][c];
           v[3][c] = d[it][1][c] - d[it][3][c];
         }
+        typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+        if constexpr (TAIL == 3 && C4 == 1) {
+          // one live channel: the (h, m, l) of v_p as one 8-B slot of plane 0
+#pragma unroll
+          for (int p = 0; p < 4; p += 2) {
+            unsigned h, m, l;
+            split3x2(v[p][0], v[p + 1][0], h, m, l);
+            *reinterpret_cast<u32x2_t*>(lv + w6_vt(row, j, p) * 4) =
+                u32x2_t{(h & 0xffffu) | (m << 16), l & 0xffffu};
+            *reinterpret_cast<u32x2_t*>(lv + w6_vt(row, j, p + 1) * 4) =
+                u32x2_t{(h >> 16) | (m & 0xffff0000u), l >> 16};
+          }
+          continue;
+        }
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           unsigned h0, m0, l0, h1, m1, l1;
@@ -184,7 +204,6 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
           split3x2(v[p][2], v[p][3], h1, m1, l1);
           // bf16 index in a plane (tail mode 1: the 8-B slot layout w6_vt)
           const int o = C4 == 1 ? w6_vt(row, j, p) * 4 : w6_vq(row, c4 >> 1, j, p) * 8 + (c4 & 1) * 4;
-          typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
           *reinterpret_cast<u32x2_t*>(lv + o) = u32x2_t{h0, h1};
           *reinterpret_cast<u32x2_t*>(lv + C::VPL + o) = u32x2_t{m0, m1};
           *reinterpret_cast<u32x2_t*>(lv + 2 * C::VPL + o) = u32x2_t{l0, l1};
@@ -217,7 +236,7 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   // stage list of this wave for chunk c (image stage index); tail chunks per TAIL
   auto stage_of = [&](int c, int s, bool tailc) -> int {
     if (!tailc) return c * C::SPC + (s >> 1) * 4 + 2 * ph + (s & 1);  // s = 2 ky + pi
-    if (TAIL == 1) return c * C::SPC + 2 * ph + s;                     // s = pi
+    if (TAIL == 1 || TAIL == 3) return c * C::SPC + 2 * ph + s;       // s = pi
     return c * C::SPC + 2 * (2 * ph + (s >> 1)) + (s & 1);             // s = 2 pi + half
   };
 
@@ -225,10 +244,10 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   // fragment q: 2 x 2 M fragments x 6 products, its adds pinned, and the next stage's fragment q
   // requested into the registers it frees
   auto stage = [&](auto mode_tag, int s, int nxt, int liv, int lgv) {
-    constexpr int MODE = decltype(mode_tag)::value;  // 0 full, 1 / 2 tail
+    constexpr int MODE = decltype(mode_tag)::value;  // 0 full, 1 / 2 / 3 tail
     int pi, ky0;
     if (MODE == 0) { pi = s & 1; ky0 = s >> 1; }
-    else if (MODE == 1) { pi = s; ky0 = 0; }
+    else if (MODE == 1 || MODE == 3) { pi = s; ky0 = 0; }
     else { pi = s >> 1; ky0 = 2 * (s & 1); }
     const int p = 2 * ph + pi;
     bf16x8 av[3][MT];
@@ -239,6 +258,13 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
         const int o = w6_vq(row0 + ky0, lgv, j, p) * 8;
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) av[pl][f] = *reinterpret_cast<const bf16x8*>(lv + pl * C::VPL + o);
+      } else if constexpr (MODE == 3) {
+        // lane group ky: (h, m, l, 0) of kernel row ky -> A slots (h, h, m, h, l, m, 0, 0)
+        const int ky = lgv;
+        const bf16x4 q4 = *reinterpret_cast<const bf16x4*>(lv + w6_vt(row0 + (ky < 3 ? ky : 0), j, p) * 4);
+        const bf16x8 z8 = {};
+        const bf16x8 v8 = __builtin_shufflevector(q4, q4, 0, 0, 1, 0, 2, 1, 3, 3);
+        av[0][f] = ky > 2 ? z8 : v8;
       } else if constexpr (MODE == 1) {
         // lane group 0: channels 0..3 of ky 0 and 1; group 1: ky 2 and zeros; 2, 3: zeros
         const int ka = 2 * lgv, kb = ka + 1;
@@ -272,6 +298,11 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
       for (int q = 0; q < NTW; ++q) {
 #pragma unroll
         for (int mp = 0; mp < MT; ++mp) {  // one M fragment per MFMA group
+          if constexpr (MODE == 3) {
+            const f32x4 t = mfma_bf16(av[0][mp], w[0][q], f32x4{0.f, 0.f, 0.f, 0.f});
+            acc[PI][mp][q] = acc[PI][mp][q] + t;
+            continue;
+          }
           f32x4(&ah)[1][NTW] = *reinterpret_cast<f32x4(*)[1][NTW]>(&acc[PI][mp]);
           bf16x8 a2[3][1];
 #pragma unroll
@@ -314,11 +345,11 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
     int liv = li, lgv = lg, tidv = tid;
     asm volatile("" : "+v"(liv), "+v"(lgv), "+v"(tidv));
     if (c > 0) w6_barrier();
-    transform(std::integral_constant<int, TAIL == 1 ? 1 : 4>{}, c * C::KC, tidv);
+    transform(std::integral_constant<int, TAIL == 2 ? 4 : 1>{}, c * C::KC, tidv);
     __builtin_amdgcn_s_waitcnt(0xC07F);
     w6_barrier();
-    constexpr int NS = TAIL == 1 ? 2 : 4;
-    using MD = std::integral_constant<int, TAIL == 1 ? 1 : 2>;
+    constexpr int NS = TAIL == 2 ? 4 : 2;
+    using MD = std::integral_constant<int, TAIL>;
     w6_for<0, NS>([&](auto si) {
       constexpr int s = decltype(si)::value;
       stage(MD{}, s, s + 1 < NS ? stage_of(c, s + 1, true) : -1, liv, lgv);
@@ -788,15 +819,19 @@ hipError_t launch_fwd_w6(const FwdArgs& a, hipStream_t s) {
     return hipErrorInvalidValue;
   const int tx = (a.OW + C::TW - 1) / C::TW, ty = (a.OH + C::TH - 1) / C::TH;
   const dim3 grid(tx * ty, a.N, nz), block(C::WAVES * 64);
-  static const char* kn[2][3] = {{"k_c3w6<0,96>", "k_c3w6<1,96>", "k_c3w6<2,96>"},
-                                 {"k_c3w6<0,48>", "k_c3w6<1,48>", "k_c3w6<2,48>"}};
-  prof_kernel(kn[np == 48][tail]);
+  // X6_T1: a one-channel tail chunk in the six-slot layout (96 outputs only)
+  const bool t1 = (a.x6_tail & X6_T1) != 0;
+  if (t1 && (tail != 1 || np != 96)) return hipErrorInvalidValue;
+  static const char* kn[2][4] = {{"k_c3w6<0,96>", "k_c3w6<1,96>", "k_c3w6<2,96>", "k_c3w6<3,96>"},
+                                 {"k_c3w6<0,48>", "k_c3w6<1,48>", "k_c3w6<2,48>", ""}};
+  prof_kernel(kn[np == 48][t1 ? 3 : tail]);
   if (np == 48) {
     if (tail == 1) hipLaunchKernelGGL((k_c3w6<1, 48>), grid, block, 0, s, a);
     else if (tail == 2) hipLaunchKernelGGL((k_c3w6<2, 48>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_c3w6<0, 48>), grid, block, 0, s, a);
   } else {
-    if (tail == 1) hipLaunchKernelGGL(k_c3w6<1>, grid, block, 0, s, a);
+    if (t1) hipLaunchKernelGGL(k_c3w6<3>, grid, block, 0, s, a);
+    else if (tail == 1) hipLaunchKernelGGL(k_c3w6<1>, grid, block, 0, s, a);
     else if (tail == 2) hipLaunchKernelGGL(k_c3w6<2>, grid, block, 0, s, a);
     else hipLaunchKernelGGL(k_c3w6<0>, grid, block, 0, s, a);
   }

@@ -1247,7 +1247,8 @@ __device__ __forceinline__ void pk_x6(const PackJob& j, long e) {
 // Winograd F(2,3) image of k_c3w6 (conv_w6.hip): [chunk][stage][piece][n < 96][32 k] as pk_x6,
 // stage 4 ky + p holding u_p = G g of kernel row ky (g = the three kx taps of (k, n)):
 // u = (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2), each rounded once from fp64, then split.
-// Last chunk (tail): 1: stage p, k = 4 ky + channel; 2: stage 2p + h, k = 16 (ky - 2h) + channel.
+// Last chunk (tail): 1: stage p, k = 4 ky + channel; 2: stage 2p + h, k = 16 (ky - 2h) + channel;
+// 3 (X6_T1): stage p, k = 8 ky + slot, plane 0 = u's piece of each of the six products (k_c3w6).
 __device__ __forceinline__ void pk_w6(const PackJob& j, long e0) {
   const int NP = j.g0, nch = j.nch, wst = x6_wst(NP), pad = wst - 3 * NP * 32;
   const long per_z = (long)nch * 12 * NP * 32;  // one image per output-channel block z (zc)
@@ -1255,9 +1256,12 @@ __device__ __forceinline__ void pk_w6(const PackJob& j, long e0) {
   const long e = e0 - (long)z * per_z;
   const int kk = (int)(e % 32), nn = (int)((e / 32) % NP);
   const int cs = (int)(e / (32L * NP)), c = cs / 12, s = cs % 12;
-  int ky = s >> 2, p = s & 3, k = c * 32 + kk;
+  int ky = s >> 2, p = s & 3, k = c * 32 + kk, slot = -1;
   bool live = true;
-  if (j.tail == 1 && c == nch - 1) {
+  if (j.tail == 3 && c == nch - 1) {  // X6_T1: k = 8 ky + product slot, channel c * 32 only
+    p = s; ky = kk >> 3; slot = kk & 7; k = c * 32;
+    live = s < 4 && ky < 3 && slot < 6;
+  } else if (j.tail == 1 && c == nch - 1) {
     p = s; ky = kk >> 2; k = c * 32 + (kk & 3);
     live = s < 4 && kk < 12;
   } else if (j.tail == 2 && c == nch - 1) {
@@ -1278,6 +1282,10 @@ __device__ __forceinline__ void pk_w6(const PackJob& j, long e0) {
   }
   __bf16 h, m, l;
   split3(v, h, m, l);
+  if (slot >= 0) {  // u's piece of product slot (h,h) (h,m) (m,h) (h,l) (l,h) (m,m), plane 0 only
+    h = slot == 1 || slot == 5 ? m : (slot == 3 ? l : h);
+    m = l = (__bf16)0.f;
+  }
   __bf16* st = static_cast<__bf16*>(j.out) + ((long)z * nch * 12 + cs) * wst;
   const int o = nn * 32 + x6_swz(nn, kk >> 3) * 8 + (kk & 7);
   st[o] = h;
@@ -1518,6 +1526,10 @@ bool pack_job_x6(const WView& wv, int K, int nout, int zc, void* out, int mode, 
   j.K = K; j.NOUT = zc > 0 ? zc : nout; j.g0 = x6_np(nout, zc); j.nch = (K + 31) / 32;
   j.nz = zc > 0 ? (nout + zc - 1) / zc : 1; j.zc = zc; j.ntot = nout; j.tail = tail;
   if (w6) j.kind = PK_W6;
+  if (mode & X6_T1) {  // one live channel in the last chunk: k_c3w6's six-slot tail
+    if (!w6 || tail != 1 || npw != 96 || K % 32 != 1) return false;
+    j.tail = 3;
+  }
   return true;
 }
 

@@ -380,6 +380,9 @@ hipError_t launch_fwd_x6(const FwdArgs& a, hipStream_t s);
 // k_c3w6 (conv_w6.hip): the 1-D Winograd F(2,3) bf16x6 kernel for 96 output channels, on a PK_W6
 // image; FwdArgs::x6_tail carries X6_W6 | x6_tail_mode(K) for it (see x6_image_mode)
 constexpr int X6_W6 = 8;
+// | X6_T1 (with X6_W6 and tail mode 1): the last chunk holds ONE live channel (the rest zero
+// weights / zero pad channels), packed and consumed in k_c3w6's six-slot tail layout (TAIL 3)
+constexpr int X6_T1 = 16;
 hipError_t launch_fwd_w6(const FwdArgs& a, hipStream_t s);
 // the N2N pair-pixel dec_conv1b on the Winograd kernel (conv_w6.hip k_c3w6s): the cells of rd
 // listed per tile orientation (list: 2 N (OH/2)(OW/2) uint32, cnt: 2 N int), then the pass over

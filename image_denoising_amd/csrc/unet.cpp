@@ -425,7 +425,9 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   auto x6_tail_f = [&](int i) -> int {
     const Layer& L = p.P.L[i];
     const int l = layer_level(i);
-    return x6_image_mode(N, H(l), Wd(l), i == D1A ? p.c1kp : L.cin, L.cout, 0, true);
+    const int m = x6_image_mode(N, H(l), Wd(l), i == D1A ? p.c1kp : L.cin, L.cout, 0, true);
+    // dec_conv1a at C = 1 on the Winograd kernel: the image channel alone in the last chunk
+    return m | (i == D1A && (m & X6_W6) && (m & 7) == 1 && L.cin % 32 == 1 && L.cout == 96 ? X6_T1 : 0);
   };
   // bf16 base (forward-only plans): bf16 storage of the decoder's a-conv outputs, whose only
   // reader is the matching b-conv
