@@ -74,6 +74,19 @@ __device__ __forceinline__ int wp_idx(int r, int rw, int blk) {
   return r * rw + ((blk ^ ((r >> 3) & 1)) << 4);
 }
 
+// diagnostic ablations of k_wgrad3p (wrong results, timing only; tools/probes/r5_wgabl.sh,
+// profiles/r5_wgrad_ablation.log): NOS = no next-stage loads / splits / plane writes, NOLD = no
+// next-stage global loads (the stale registers are split and written), NOBAR = no barrier
+#ifndef DN_WG_ABL_NOS
+#define DN_WG_ABL_NOS 0
+#endif
+#ifndef DN_WG_ABL_NOLD
+#define DN_WG_ABL_NOLD 0
+#endif
+#ifndef DN_WG_ABL_NOBAR
+#define DN_WG_ABL_NOBAR 0
+#endif
+
 // The next stage's G and X operands are loaded at the start of the stage and split into the other
 // buffer at its end (a whole stage of load latency for both)
 template <int SWL, int CO = 96>
@@ -245,7 +258,7 @@ __global__ __launch_bounds__(CO == 96 ? 256 : 192, 2) void k_wgrad3p(WgradArgs a
     __bf16* nbuf = lds + (cb ^ 1) * C::BUF;
     pn = next(pn);
     const bool more = u + 1 < u_end;
-    if (more) {  // in flight during the whole stage
+    if (more && !DN_WG_ABL_NOS && !DN_WG_ABL_NOLD) {  // in flight during the whole stage
       load_g(pn);
       load_x(pn);
     }
@@ -322,12 +335,12 @@ __global__ __launch_bounds__(CO == 96 ? 256 : 192, 2) void k_wgrad3p(WgradArgs a
         x6_acc_add(accb[i][0], hi, lo);
       }
     }
-    if (more) {  // (waits for its loads itself)
+    if (more && !DN_WG_ABL_NOS) {  // (waits for its loads itself)
       store_g(nbuf);
       store_x(nbuf);
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own plane writes done
-    __syncthreads();                     // next buffer complete; everyone done with this one
+    if (!DN_WG_ABL_NOBAR) __syncthreads();  // next buffer complete; everyone done with this one
   }
 
   float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
