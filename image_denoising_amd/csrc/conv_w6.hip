@@ -463,7 +463,11 @@ struct SCfgW {
   static constexpr int VBYTES = 3 * VPL * 2;        // 48 KiB
   static constexpr int WSTP = x6_wst(NP);
   static constexpr int XCH = WAVES * 2 * NTW * 2 * 4 * 64;  // floats of the exchange area
-  static constexpr int LBYTES = VBYTES > XCH * 4 ? VBYTES : XCH * 4;
+  // output stage: [cell][pixel s][96 ch], cells 208 floats apart (the four cells a 4-byte write
+  // instruction covers land 16 banks apart)
+  static constexpr int OCS = 208, OBYTES = CELLS * OCS * 4;
+  static constexpr int LB0 = VBYTES > XCH * 4 ? VBYTES : XCH * 4;
+  static constexpr int LBYTES = LB0 > OBYTES ? LB0 : OBYTES;
   static_assert(2 * (LBYTES + CELLS * 4) <= 163840, "two workgroups per CU");
 };
 
@@ -749,8 +753,14 @@ __global__ __launch_bounds__(256, 2) void k_c3w6s(FwdArgs a, const unsigned* __r
       }
   }
   // epilogue: lane (li, lg) of fragment 2ph + ff holds cells 16(2ph + ff) + 4lg + e (e < 4),
-  // output channel 48nh + 16q + li; bias + LeakyReLU, then the two pixels of the cell to the pair
-  // image row ci, columns 2cj + s (s = 0 takes pair[rd][0]: y0 unless the entry's swap bit)
+  // output channel 48nh + 16q + li; bias + LeakyReLU into the output stage (pixel s = 0 takes
+  // pair[rd][0]: y0 unless the entry's swap bit), then every cell's two pixels (columns 2cj,
+  // 2cj + 1 of pair-image row ci: 768 contiguous bytes) leave as whole 128-B lines, float4 per
+  // lane (per-lane 4-byte stores had the two waves of a pixel write halves of one line at
+  // different times)
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  w6_barrier();  // every wave has read its partner's partial sums: the area becomes the stage
+  float* ost = reinterpret_cast<float*>(lds_raw);
 #pragma unroll
   for (int q = 0; q < NTW; ++q) {
     const int ch = 48 * nh + 16 * q + li;
@@ -759,16 +769,27 @@ __global__ __launch_bounds__(256, 2) void k_c3w6s(FwdArgs a, const unsigned* __r
     for (int ff = 0; ff < 2; ++ff)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const unsigned en = lent[16 * (2 * ph + ff) + 4 * lg + e];
-        if (en == 0xffffffffu) continue;
-        const int cj = en & 0x7fff, ci = (en >> 15) & 0x7fff, sw = en >> 31;
+        const int cell = 16 * (2 * ph + ff) + 4 * lg + e;
+        const int sw = (int)(lent[cell] >> 31);
         float v0 = y[ff][0][q][e] + b, v1 = y[ff][1][q][e] + b;
         v0 = v0 > 0.f ? v0 : v0 * 0.2f;
         v1 = v1 > 0.f ? v1 : v1 * 0.2f;
-        float* dst = a.out + (((long)n * (a.OH / 2) + ci) * a.OW + 2 * cj) * a.out_stride + a.out_off + ch;
-        dst[0] = sw ? v1 : v0;
-        dst[a.out_stride] = sw ? v0 : v1;
+        ost[cell * C::OCS + (sw ? 96 : 0) + ch] = v0;
+        ost[cell * C::OCS + (sw ? 0 : 96) + ch] = v1;
       }
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  w6_barrier();
+#pragma unroll
+  for (int i = 0; i < C::CELLS * 48 / 256; ++i) {
+    const int e = tid + 256 * i, cell = e / 48, w = e - 48 * cell;  // w: float4 of the two pixels
+    const unsigned en = lent[cell];
+    if (en == 0xffffffffu) continue;
+    const int cj = en & 0x7fff, ci = (en >> 15) & 0x7fff;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(ost + cell * C::OCS + 4 * w);
+    float* dst = a.out + (((long)n * (a.OH / 2) + ci) * a.OW + 2 * cj + (w >= 24)) * a.out_stride + a.out_off +
+                 4 * (w >= 24 ? w - 24 : w);
+    *reinterpret_cast<f32x4*>(dst) = v;
   }
 }
 
@@ -786,7 +807,8 @@ hipError_t launch_w6s_lists(const unsigned char* rd, int N, int OH, int OW, unsi
 hipError_t launch_fwd_w6s(const FwdArgs& a, const unsigned* list, const int* cnt, const void* wpv,
                           hipStream_t s) {
   if (a.NOUT != 96 || a.K % 32 || a.K <= 0 || a.zc || a.epi != EPI_BIAS_ACT || !a.bias ||
-      a.out_layout != OUT_NHWC || ((a.in_stride | a.in_off) & 3) || (a.OH | a.OW) & 1 ||
+      a.out_layout != OUT_NHWC || ((a.in_stride | a.in_off | a.out_stride | a.out_off) & 3) ||
+      a.out_stride < 96 || (a.OH | a.OW) & 1 ||
       a.IHt != a.OH || a.IWt != a.OW || (long)a.IHt * a.IWt * a.in_stride * 4 >= 0x7fffffffL ||
       (a.x6_tail & 7) != 0)
     return hipErrorInvalidValue;

@@ -17,6 +17,11 @@
 namespace dn {
 
 constexpr int E0_CO = 48;
+// k_enc0_fwd's output stage keeps 48 floats per pixel, channel quad q of pixel p at quad
+// q ^ ((p >> 2) & 3): a 16-lane float4 write then covers all 16 four-bank groups (unswizzled, pixels
+// p and p + 4 shared groups: 31 % of the launch's LDS-active cycles in conflicts,
+// profiles/r4_pmc_sq_n2n.txt)
+__device__ __forceinline__ int e0_quad(int p, int q) { return p * (E0_CO / 4) + (q ^ ((p >> 2) & 3)); }
 
 template <int C>
 __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, int N, int H,
@@ -63,7 +68,7 @@ __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, i
       }
       v.x = v.x > 0.f ? v.x : v.x * 0.2f; v.y = v.y > 0.f ? v.y : v.y * 0.2f;
       v.z = v.z > 0.f ? v.z : v.z * 0.2f; v.w = v.w > 0.f ? v.w : v.w * 0.2f;
-      *reinterpret_cast<float4*>(st + tid * E0_CO + 4 * cq) = v;
+      reinterpret_cast<float4*>(st)[e0_quad(tid, cq)] = v;
     }
     // the input's slice of the up1 concat buffer (centre tap = the pixel itself), and the
     // compact NCHW copy the weight gradients read (only when a backward follows)
@@ -86,7 +91,7 @@ __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, i
     typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
     u16x4* o2 = reinterpret_cast<u16x4*>(reinterpret_cast<unsigned short*>(out) + p0 * E0_CO);
     for (int e = tid; e < npx * (E0_CO / 4); e += 256) {
-      const float4 v = s4[e];
+      const float4 v = s4[e0_quad(e / (E0_CO / 4), e % (E0_CO / 4))];
       const __bf16 q[4] = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
       o2[e] = u16x4{__builtin_bit_cast(unsigned short, q[0]), __builtin_bit_cast(unsigned short, q[1]),
                     __builtin_bit_cast(unsigned short, q[2]), __builtin_bit_cast(unsigned short, q[3])};
@@ -94,7 +99,7 @@ __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, i
     return;
   }
   float4* o4 = reinterpret_cast<float4*>(out + p0 * E0_CO);
-  for (int e = tid; e < npx * (E0_CO / 4); e += 256) o4[e] = s4[e];
+  for (int e = tid; e < npx * (E0_CO / 4); e += 256) o4[e] = s4[e0_quad(e / (E0_CO / 4), e % (E0_CO / 4))];
 }
 
 // Weight gradient of a 3x3 conv with few input channels C and CO output channels:
@@ -104,8 +109,9 @@ __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, i
 // image rows [R*b/splits, R*(b+1)/splits) of the flattened N*H rows (possibly none: it then
 // writes zeros, so every slab row is defined) and walks them in 128-pixel segments: the
 // gradient segment [128][CO] is staged in LDS with float4 loads, the input rows y-1..y+1
-// (+halo) likewise; then NG = 256/CO pixel phases x CO output channels accumulate
-// W[co][ci][t] and b[co] from broadcast LDS reads (threads past NG*CO only load).
+// (+halo) likewise, from registers the previous segment's loads filled; then NG = 256/CO pixel
+// phases x CO output channels accumulate W[co][ci][t] and b[co] from broadcast LDS reads
+// (threads past NG*CO only load).
 // Slab row = W[co][cin_total][3][3] then b[co]; this kernel fills input channels
 // [ci_base, ci_base + C) (+ b if with_bias).
 constexpr int E0_SEG = 128;
@@ -126,34 +132,66 @@ __global__ __launch_bounds__(256) void k_wgrad_c3_thin(const float* __restrict__
   for (int j = 0; j <= KT; ++j) acc[j] = 0.f;
   const long R = (long)N * H, HW = (long)H * W;
   const int rb = (int)(R * blockIdx.x / gridDim.x), re = (int)(R * (blockIdx.x + 1) / gridDim.x);
-  for (int row = rb; row < re; ++row) {
+  // the block's segments k = (row rb + k / nseg, columns (k % nseg) * SEG ..); segment k + 1's
+  // gradient and input values are loaded into registers while segment k computes
+  const int nseg = (W + SEG - 1) / SEG;
+  const long nk = (long)(re - rb) * nseg;
+  constexpr int GI = (SEG * CO / 4 + 255) / 256, XI = (3 * C * (SEG + 2) + 255) / 256;
+  float4 pgv[GI];
+  float pxv[XI];
+  auto seg_w = [&](long k) { const int x0 = (int)(k % nseg) * SEG; return W - x0 < SEG ? W - x0 : SEG; };
+  auto load = [&](long k) {
+    const int row = rb + (int)(k / nseg), x0 = (int)(k % nseg) * SEG, seg = seg_w(k);
     const int n = row / H, y = row - n * H;
-    for (int x0 = 0; x0 < W; x0 += SEG) {
-      const int seg = W - x0 < SEG ? W - x0 : SEG;
-      __syncthreads();
-      const float4* g4 = reinterpret_cast<const float4*>(g + ((long)row * W + x0) * CO);
-      for (int e = tid; e < seg * (CO / 4); e += 256) reinterpret_cast<float4*>(gr)[e] = g4[e];
-      for (int e = tid; e < 3 * C * (seg + 2); e += 256) {
-        const int dy = e / (C * (seg + 2)), r = e - dy * (C * (seg + 2));
-        const int ci = r / (seg + 2), xx = r - ci * (seg + 2);
-        const int gy = y + dy - 1, gx = x0 + xx - 1;
-        xr[dy][ci][xx] = (gy >= 0 && gy < H && gx >= 0 && gx < W)
-                             ? x[((long)n * C + ci) * HW + (long)gy * W + gx]
-                             : 0.f;
-      }
-      __syncthreads();
-      if (grp < NG) {
-        for (int px = grp; px < seg; px += NG) {
-          const float gv = gr[px * CO + co];
+    const float4* g4 = reinterpret_cast<const float4*>(g + ((long)row * W + x0) * CO);
 #pragma unroll
-          for (int dy = 0; dy < 3; ++dy)
+    for (int i = 0; i < GI; ++i) {
+      const int e = tid + 256 * i;
+      pgv[i] = e < seg * (CO / 4) ? g4[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
-            for (int ci = 0; ci < C; ++ci)
+    for (int i = 0; i < XI; ++i) {
+      const int e = tid + 256 * i;
+      const int dy = e / (C * (seg + 2)), r = e - dy * (C * (seg + 2));
+      const int ci = r / (seg + 2), xx = r - ci * (seg + 2);
+      const int gy = y + dy - 1, gx = x0 + xx - 1;
+      pxv[i] = (e < 3 * C * (seg + 2) && gy >= 0 && gy < H && gx >= 0 && gx < W)
+                   ? x[((long)n * C + ci) * HW + (long)gy * W + gx]
+                   : 0.f;
+    }
+  };
+  auto store = [&](int seg) {
 #pragma unroll
-              for (int dx = 0; dx < 3; ++dx)
-                acc[ci * 9 + dy * 3 + dx] = fmaf(gv, xr[dy][ci][px + dx], acc[ci * 9 + dy * 3 + dx]);
-          acc[KT] += gv;
-        }
+    for (int i = 0; i < GI; ++i) {
+      const int e = tid + 256 * i;
+      if (e < seg * (CO / 4)) reinterpret_cast<float4*>(gr)[e] = pgv[i];
+    }
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int e = tid + 256 * i;
+      const int dy = e / (C * (seg + 2)), r = e - dy * (C * (seg + 2));
+      const int ci = r / (seg + 2), xx = r - ci * (seg + 2);
+      if (e < 3 * C * (seg + 2)) xr[dy][ci][xx] = pxv[i];
+    }
+  };
+  if (nk > 0) load(0);
+  for (long k = 0; k < nk; ++k) {
+    const int seg = seg_w(k);
+    __syncthreads();  // every thread is done with segment k - 1's stage
+    store(seg);
+    if (k + 1 < nk) load(k + 1);
+    __syncthreads();
+    if (grp < NG) {
+      for (int px = grp; px < seg; px += NG) {
+        const float gv = gr[px * CO + co];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int ci = 0; ci < C; ++ci)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+              acc[ci * 9 + dy * 3 + dx] = fmaf(gv, xr[dy][ci][px + dx], acc[ci * 9 + dy * 3 + dx]);
+        acc[KT] += gv;
       }
     }
   }
