@@ -562,11 +562,15 @@ def _device_activations(net, x, r):
 
 @pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("C,N,H,W", [(1, 2, 64, 64), (1, 1, 32, 32), (1, 3, 32, 96),
-                                     (3, 2, 64, 32), (1, 2, 128, 128)])
+                                     (3, 2, 64, 32), (1, 2, 128, 128), (1, 4, 128, 128),
+                                     (3, 4, 128, 128)])
 def test_unet_unit_gain_fwd_bwd_vs_fp64(C, N, H, W, prec):
     """Every level contributes O(1) (unit-gain weights).  Forward vs fp64 within 1e-4; all 50
     parameter gradients vs an fp64 backward that takes LeakyReLU slopes and pool routing from
-    the device's own fp32 activations (so only the rounding of the linear ops remains)."""
+    the device's own fp32 activations (so only the rounding of the linear ops remains).
+    (4 x 128^2: one full round of 8 x 16 tiles at the top level, so the Winograd kernels run
+    there -- dec_conv1a's one-channel tail as one MFMA per fragment pair at C = 1, the packed
+    four-channel tail at C = 3 -- as in the bench step.)"""
     from oracle.unet_ref import forward, layer_table
 
     net = _net(C, prec)
