@@ -1393,6 +1393,9 @@ int wgrad1_splits(int mode, int N, int KH, int KW) {
   const long units = (long)N * KH * ((KW + 31) / 32);
   long sp = 768 / z;
   if (sp > units / 2) sp = units / 2;
+  // UP2: whole groups of 8 (k_wgrad1p's XCD map of the four parity blocks; splits past the
+  // pixel count write zero rows)
+  if (z == 4) sp = sp < 8 ? 8 : sp / 8 * 8;
   return (int)(sp < 1 ? 1 : sp);
 }
 

@@ -691,6 +691,12 @@ struct Wp1Cfg {
   static_assert(2 * BUF * 2 <= 81920, "two workgroups per CU");
 };
 
+#ifndef DN_WG1_PD
+#define DN_WG1_PD 2
+#endif
+// stages of operands in flight (1 or 2): two stages took the deconv weight gradients 0.346-0.348 ->
+// 0.298-0.305 ms/step, the 1x1 ones unchanged (profiles/r5_wgrad1_pd_ab.log)
+constexpr int WG1_PD = DN_WG1_PD;
 template <bool UP2>
 __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
   using C = Wp1Cfg;
@@ -699,8 +705,15 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int li = lane & 15, lg = lane >> 4;
+  // UP2: one flat grid of 4 x splits blocks; block b = (split, parity) with parity (b >> 3) & 3,
+  // so the four parity blocks of a split are dispatched within 32 blocks of each other onto the
+  // same XCD (b % 8) and three of the four reads of its low-res input rows hit that XCD's L2
+  // (parity-major z launches read them at four different times: 1.27x the operand bytes)
+  const int nsp = UP2 ? (int)gridDim.x / 4 : (int)gridDim.x;
+  const int bsp = UP2 ? (int)((blockIdx.x & 7) | ((blockIdx.x >> 5) << 3)) : (int)blockIdx.x;
+  const int bz = UP2 ? (int)((blockIdx.x >> 3) & 3) : 0;
   const long U = (npx + C::PX - 1) / C::PX;
-  const long u_beg = U * blockIdx.x / gridDim.x, u_end = U * (blockIdx.x + 1) / gridDim.x;
+  const long u_beg = U * bsp / nsp, u_end = U * (bsp + 1) / nsp;
   const bool do_bias = wn == 0;
 
   f32x4 acc[3][3], accb[3][1];
@@ -721,9 +734,9 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
     ioff[it] = px * (it < NG ? a.g_stride : a.x_stride) + c;
     ilds[it] = (it < NG ? 0 : C::GPL) + wp_idx(px, C::C, c >> 4) + (c & 15);
   }
-  f32x4 pv[C::NIT];
-  const int pa = UP2 ? (int)(blockIdx.z >> 1) : 0, pb = UP2 ? (int)(blockIdx.z & 1) : 0;
-  auto load = [&](long u) {
+  f32x4 pv[C::NIT], pv2[WG1_PD == 2 ? C::NIT : 1];
+  const int pa = bz >> 1, pb = bz & 1;
+  auto load = [&](long u, f32x4* dst) {
     const long p0 = u * C::PX;
     const int np = npx - p0 < C::PX ? (int)(npx - p0) : C::PX;
     const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
@@ -737,11 +750,11 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
         const int xx = (int)(p - r * a.KW);
         const float* src = a.g + ((2 * r + pa) * 2 * a.KW + 2 * xx + pb) * a.g_stride + a.g_off +
                            (ioff[it] - ipx[it] * a.g_stride);
-        pv[it] = ipx[it] < np ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
+        dst[it] = ipx[it] < np ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
         continue;
       }
       const int off = ipx[it] < np ? ioff[it] * 4 : 0x7fffffff;
-      pv[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(it < NG ? gr : xr, off, 0, 0));
+      dst[it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(it < NG ? gr : xr, off, 0, 0));
     }
   };
   auto store = [&](__bf16* buf) {
@@ -765,9 +778,10 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
   for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
 
   if (u_beg < u_end) {
-    load(u_beg);
+    load(u_beg, pv);
     store(lds);
   }
+  if (WG1_PD == 2 && u_beg + 1 < u_end) load(u_beg + 1, pv);
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own plane writes done
   __syncthreads();
 #pragma unroll 1
@@ -775,7 +789,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
     const int cb = (int)((u - u_beg) & 1);
     const __bf16* buf = lds + cb * C::BUF;
     const bool more = u + 1 < u_end;
-    if (more) load(u + 1);  // in flight during this stage's MFMAs
+    if (u + WG1_PD < u_end) load(u + WG1_PD, WG1_PD == 2 ? pv2 : pv);  // in flight during the stage(s)
     int aoff = abase;
     asm volatile("" : "+v"(aoff));
     bf16x8 av[3][3], bv[3][3];
@@ -818,11 +832,15 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
       }
     }
     if (more) store(lds + (cb ^ 1) * C::BUF);  // (waits for its loads itself)
+    if (WG1_PD == 2) {
+#pragma unroll
+      for (int it = 0; it < C::NIT; ++it) pv[it] = pv2[it];
+    }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __syncthreads();  // next buffer complete; everyone done with this one
   }
   // slab row (UP2: parity z's block of gridDim.x rows, the deconv layout [ci][co])
-  float* slab = a.slab + ((long)blockIdx.z * gridDim.x + blockIdx.x) * a.slab_stride;
+  float* slab = a.slab + ((long)bz * nsp + bsp) * a.slab_stride;
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -854,10 +872,12 @@ hipError_t launch_wgrad1p(const WgradArgs& a, int splits, hipStream_t s, bool up
   if (!wgrad1p_ok(a) || splits < 1 || a.slab_stride < 96 * 96 + 96) return hipErrorInvalidValue;
   const long npx = (long)a.N * a.KH * a.KW;
   if (up2) {
-    prof_kernel("k_wgrad1p<up2>");
-    hipLaunchKernelGGL(k_wgrad1p<true>, dim3(splits, 1, 4), dim3(256), 0, s, a, npx);
+    // (the flat grid's block -> (split, parity) map needs whole groups of 32 blocks)
+    if (splits % 8) return hipErrorInvalidValue;
+    prof_kernel("k_wgrad1p<true>");
+    hipLaunchKernelGGL(k_wgrad1p<true>, dim3(4 * splits), dim3(256), 0, s, a, npx);
   } else {
-    prof_kernel("k_wgrad1p");
+    prof_kernel("k_wgrad1p<false>");
     hipLaunchKernelGGL(k_wgrad1p<false>, dim3(splits), dim3(256), 0, s, a, npx);
   }
   return hipGetLastError();
