@@ -4,7 +4,7 @@
 set -u; cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 LIBS=${LIBS:-"- base"}; OPS=${OPS:-"wgrad_up wgrad1"}
 : > gpurun_out/libab.log
-for r in 1 2; do
+for r in $(seq 1 ${ROUNDS:-2}); do
   for v in $LIBS; do
     if [ "$v" = "-" ]; then lib=image_denoising_amd/libdenoise_hip.so; else lib=image_denoising_amd/libdenoise_hip_$v.so; fi
     DN_LIB_PATH=$lib timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-eval > gpurun_out/libab_${v}_$r.log 2>&1 || exit $?
