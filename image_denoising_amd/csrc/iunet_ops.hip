@@ -41,12 +41,23 @@ __global__ __launch_bounds__(256) void k_chan_sums(const float* __restrict__ a, 
   if (l < PL) {
     const float* an = a + (long)n * P * as + ao + 4 * q;
     const float* bn = b ? b + (long)n * P * bs + bo + 4 * q : nullptr;
-    for (long p = p0 + l; p < p1; p += PL) {
-      const float4 x = *reinterpret_cast<const float4*>(an + p * as);
-      const float4 y = bn ? *reinterpret_cast<const float4*>(bn + p * bs) : x;
-      v[0] += x.x; v[1] += x.y; v[2] += x.z; v[3] += x.w;
-      v[4] += (double)x.x * y.x; v[5] += (double)x.y * y.y;
-      v[6] += (double)x.z * y.z; v[7] += (double)x.w * y.w;
+    // four pixels' loads in flight per thread, summed in the same order as one at a time
+    constexpr int UB = 4;
+    for (long p = p0 + l; p < p1; p += UB * PL) {
+      float4 x[UB], y[UB];
+#pragma unroll
+      for (int j = 0; j < UB; ++j) {
+        const long pj = p + (long)j * PL;
+        x[j] = pj < p1 ? *reinterpret_cast<const float4*>(an + pj * as) : make_float4(0.f, 0.f, 0.f, 0.f);
+        y[j] = bn && pj < p1 ? *reinterpret_cast<const float4*>(bn + pj * bs) : x[j];
+      }
+#pragma unroll
+      for (int j = 0; j < UB; ++j) {
+        if (p + (long)j * PL >= p1) break;
+        v[0] += x[j].x; v[1] += x[j].y; v[2] += x[j].z; v[3] += x[j].w;
+        v[4] += (double)x[j].x * y[j].x; v[5] += (double)x[j].y * y[j].y;
+        v[6] += (double)x[j].z * y[j].z; v[7] += (double)x[j].w * y[j].w;
+      }
     }
   }
 #pragma unroll
@@ -165,6 +176,9 @@ __global__ __launch_bounds__(64) void k_gn_dparams(const double* __restrict__ pa
 }
 
 // y = x*A + (x2 ? x2*B : 0) + Cc  (per (n, c) coefficients)  [+ LeakyReLU]  [+ res]
+// (IDX = unsigned when every index fits 32 bits: 64-bit division per element cost more than the
+// float4 it addresses)
+template <typename IDX>
 __global__ __launch_bounds__(256) void k_affine(const float* __restrict__ x, int xs, int xo,
                                                 const float* __restrict__ x2, int x2s, int x2o,
                                                 const float* __restrict__ A,
@@ -173,11 +187,11 @@ __global__ __launch_bounds__(256) void k_affine(const float* __restrict__ x, int
                                                 const float* __restrict__ res, int rs, int ro,
                                                 float* __restrict__ y, int ys, int yo, long P,
                                                 int C, long total4) {
-  const int C4 = C >> 2;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total4; e += (long)gridDim.x * 256) {
+  const IDX C4 = (IDX)(C >> 2), PP = (IDX)P;
+  for (IDX e = (IDX)blockIdx.x * 256 + threadIdx.x; e < (IDX)total4; e += (IDX)gridDim.x * 256) {
     const int q = (int)(e % C4);
-    const long pix = e / C4;  // n*P + p
-    const long n = pix / P;
+    const long pix = (long)(e / C4);  // n*P + p
+    const long n = (long)((IDX)pix / PP);
     const long ci = n * C + 4 * q;
     const float4 v = *reinterpret_cast<const float4*>(x + pix * xs + xo + 4 * q);
     const float4 a = *reinterpret_cast<const float4*>(A + ci);
@@ -472,10 +486,17 @@ hipError_t launch_affine(const View& x, const View* x2, const float* A, const fl
                          const float* Cc, int act, const View* res, const View& y, int N, long P,
                          int C, hipStream_t s) {
   const long total4 = (long)N * P * (C / 4);
-  hipLaunchKernelGGL(k_affine, dim3(nblocks(total4)), dim3(256), 0, s, x.p, x.stride, x.off,
-                     x2 ? x2->p : nullptr, x2 ? x2->stride : 0, x2 ? x2->off : 0, A, B, Cc, act,
-                     res ? res->p : nullptr, res ? res->stride : 0, res ? res->off : 0, y.p,
-                     y.stride, y.off, P, C, total4);
+  // (32-bit indices: total4 plus one grid stride below 2^32)
+  if (total4 + (long)nblocks(total4) * 256 < (1L << 32))
+    hipLaunchKernelGGL(k_affine<unsigned>, dim3(nblocks(total4)), dim3(256), 0, s, x.p, x.stride, x.off,
+                       x2 ? x2->p : nullptr, x2 ? x2->stride : 0, x2 ? x2->off : 0, A, B, Cc, act,
+                       res ? res->p : nullptr, res ? res->stride : 0, res ? res->off : 0, y.p,
+                       y.stride, y.off, P, C, total4);
+  else
+    hipLaunchKernelGGL(k_affine<unsigned long>, dim3(nblocks(total4)), dim3(256), 0, s, x.p, x.stride,
+                       x.off, x2 ? x2->p : nullptr, x2 ? x2->stride : 0, x2 ? x2->off : 0, A, B, Cc,
+                       act, res ? res->p : nullptr, res ? res->stride : 0, res ? res->off : 0, y.p,
+                       y.stride, y.off, P, C, total4);
   return hipGetLastError();
 }
 
