@@ -35,13 +35,22 @@
 
 namespace dn {
 
-// NO = 96 output channels: wave (nh, ph) = output channels 48nh .. +47 x all 4 M fragments;
-// NO = 48 (the encoder's 48 -> 48 convs): wave (mh, ph) = all 48 output channels x M fragments
-// 2mh, 2mh + 1 (tile rows 4mh .. 4mh + 3), the same V and the same stage sequence
-template <int NO = 96>
+// NO = 96 output channels: wave (nh, ph) = output channels 48nh .. +47 x all 4 M fragments x
+// positions 2ph, 2ph + 1.  NO = 48 (the encoder's 48 -> 48 convs, the 96 -> 144 data gradient's
+// 48-channel blocks): wave p = all 48 output channels x all 4 M fragments x position p (P1: each
+// weight fragment feeds four MFMA groups; the four positions' partial sums meet in LDS after the
+// last chunk; 48->48 @256^2 0.99-1.01 -> 0.96 ms, @128^2 data gradient 0.248 -> 0.240 ms,
+// profiles/r5_w48p1_ab.log).  The four-channel tail mode keeps the two-position form (wave (mh,
+// ph) = M fragments 2mh, 2mh + 1 x positions 2ph, 2ph + 1); DN_W6_48P1 = 0 selects it throughout.
+#ifndef DN_W6_48P1
+#define DN_W6_48P1 1
+#endif
+template <int NO = 96, bool P1_ = false>
 struct WCfg {
-  static constexpr int WAVES = 4, MT = NO == 96 ? 4 : 2, NTW = 3, NP = NO, NPOS = 4, NJ = 8;
-  static constexpr int HF = MT / 2;                    // M fragments a wave keeps after the exchange
+  static constexpr bool P1 = NO == 48 && P1_;
+  static constexpr int WAVES = 4, MT = NO == 96 || P1 ? 4 : 2, NTW = 3, NP = NO, NPOS = 4, NJ = 8;
+  static constexpr int NPW = P1 ? 1 : 2;               // positions per wave
+  static constexpr int HF = P1 ? 1 : MT / 2;           // M fragments a wave keeps after the exchange
   static constexpr int TW = 16, TH = 8, IH = TH + 2, IW = TW + 2, KC = 32;
   static constexpr int SPC = 12;                       // weight stages per full chunk (ky, p)
   static constexpr int VPL = IH * 4 * NJ * NPOS * 8;   // bf16 per plane of V (quads of 8)
@@ -50,7 +59,8 @@ struct WCfg {
   static constexpr int WSTP = x6_wst(NP);
   static constexpr int VITEMS = (IH * NJ * 8 + WAVES * 64 - 1) / (WAVES * 64);  // transform items
   static constexpr int PS = 16 * NTW + 4;
-  static constexpr int XCH = WAVES * HF * NTW * 2 * 4 * 64;  // floats of the exchange area
+  static constexpr int XCH = P1 ? WAVES * MT * NTW * 4 * 64       // floats of the exchange area
+                                : WAVES * HF * NTW * 2 * 4 * 64;
   static constexpr int LEND = (XCH + WAVES * 16 * PS) * 4;  // exchange + epilogue staging (over V)
   static constexpr int LBYTES = VBYTES > LEND ? VBYTES : LEND;
   static_assert(2 * LBYTES <= 163840, "two workgroups per CU");
@@ -112,16 +122,18 @@ __device__ __forceinline__ void w6_for(F&& f) {
 // as the other blocks' hi + lo.
 template <int TAIL, int NO = 96>
 __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
-  using C = WCfg<NO>;
-  constexpr int MT = C::MT, NTW = C::NTW, HF = C::HF;
+  using C = WCfg<NO, NO == 48 && DN_W6_48P1 && TAIL != 1>;
+  constexpr int MT = C::MT, NTW = C::NTW, HF = C::HF, NPW = C::NPW;
+  constexpr bool P1 = C::P1;
+  static_assert(!P1 || TAIL == 0 || TAIL == 2, "one position per wave: tail modes 0 and 2");
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[C::LBYTES];
   __bf16* lv = reinterpret_cast<__bf16*>(lds_raw);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lg = lane >> 4;
-  const int nh = NO == 96 ? wave & 1 : 0, ph = wave >> 1;
-  const int mb = NO == 96 ? 0 : 2 * (wave & 1);  // the wave's first M fragment
+  const int nh = NO == 96 ? wave & 1 : 0, ph = P1 ? 0 : wave >> 1;
+  const int mb = NO == 96 || P1 ? 0 : 2 * (wave & 1);  // the wave's first M fragment
   const int tiles_x = (a.OW + C::TW - 1) / C::TW;
   int bxr, byr;
   xcd_tile(bxr, byr);
@@ -130,10 +142,10 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   const float* inb = a.in + (long)n * a.IHt * a.IWt * a.in_stride + a.in_off;
   const int nch = (a.K + C::KC - 1) / C::KC;
 
-  // acc[pi][f][q]: position 2ph + pi, M fragment f, N fragment q
-  f32x4 acc[2][MT][NTW];
+  // acc[pi][f][q]: position 2ph + pi (P1: position wave), M fragment f, N fragment q
+  f32x4 acc[NPW][MT][NTW];
 #pragma unroll
-  for (int pi = 0; pi < 2; ++pi)
+  for (int pi = 0; pi < NPW; ++pi)
 #pragma unroll
     for (int f = 0; f < MT; ++f)
 #pragma unroll
@@ -235,6 +247,7 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
 
   // stage list of this wave for chunk c (image stage index); tail chunks per TAIL
   auto stage_of = [&](int c, int s, bool tailc) -> int {
+    if (P1) return tailc ? c * C::SPC + 2 * wave + s : c * C::SPC + 4 * s + wave;  // s = half / ky
     if (!tailc) return c * C::SPC + (s >> 1) * 4 + 2 * ph + (s & 1);  // s = 2 ky + pi
     if (TAIL == 1 || TAIL == 3) return c * C::SPC + 2 * ph + s;       // s = pi
     return c * C::SPC + 2 * (2 * ph + (s >> 1)) + (s & 1);             // s = 2 pi + half
@@ -246,10 +259,11 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   auto stage = [&](auto mode_tag, int s, int nxt, int liv, int lgv) {
     constexpr int MODE = decltype(mode_tag)::value;  // 0 full, 1 / 2 / 3 tail
     int pi, ky0;
-    if (MODE == 0) { pi = s & 1; ky0 = s >> 1; }
+    if (P1) { pi = 0; ky0 = MODE == 0 ? s : 2 * (s & 1); }
+    else if (MODE == 0) { pi = s & 1; ky0 = s >> 1; }
     else if (MODE == 1 || MODE == 3) { pi = s; ky0 = 0; }
     else { pi = s >> 1; ky0 = 2 * (s & 1); }
-    const int p = 2 * ph + pi;
+    const int p = P1 ? wave : 2 * ph + pi;
     bf16x8 av[3][MT];
 #pragma unroll
     for (int f = 0; f < MT; ++f) {
@@ -315,7 +329,8 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
         __builtin_amdgcn_sched_barrier(0);
       }
     };
-    if (pi == 0) run(std::integral_constant<int, 0>{});
+    if constexpr (P1) run(std::integral_constant<int, 0>{});
+    else if (pi == 0) run(std::integral_constant<int, 0>{});
     else run(std::integral_constant<int, 1>{});
   };
 
@@ -334,9 +349,10 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
     if (!DN_W6_ABL_NOT || c == 0) transform(std::integral_constant<int, 8>{}, c * C::KC, tidv);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own V stores done
     w6_barrier();
-    w6_for<0, 6>([&](auto si) {
+    constexpr int NSF = P1 ? 3 : 6;  // stages of a full chunk per wave
+    w6_for<0, NSF>([&](auto si) {
       constexpr int s = decltype(si)::value;
-      const int nxt = s + 1 < 6 ? stage_of(c, s + 1, false) : (more ? stage_of(c + 1, 0, next_tail) : -1);
+      const int nxt = s + 1 < NSF ? stage_of(c, s + 1, false) : (more ? stage_of(c + 1, 0, next_tail) : -1);
       stage(std::integral_constant<int, 0>{}, s, nxt, liv, lgv);
     });
   }
@@ -348,7 +364,7 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
     transform(std::integral_constant<int, TAIL == 2 ? 4 : 1>{}, c * C::KC, tidv);
     __builtin_amdgcn_s_waitcnt(0xC07F);
     w6_barrier();
-    constexpr int NS = TAIL == 2 ? 4 : 2;
+    constexpr int NS = TAIL == 2 ? (P1 ? 2 : 4) : 2;
     using MD = std::integral_constant<int, TAIL>;
     w6_for<0, NS>([&](auto si) {
       constexpr int s = decltype(si)::value;
@@ -356,13 +372,37 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
     });
   }
 
+  f32x4 y[HF][2][NTW];  // [kept fragment][output parity][q]
+  if constexpr (P1) {
+    // one position per wave: every wave's m_p of all four M fragments into LDS, then wave w
+    // forms M fragment w from the four: y0 = (m0 + m1) + m2, y1 = m1 + (-m2 - m3) (the order of
+    // the two-position form below)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    w6_barrier();  // every wave is done with V: it becomes the exchange area
+    float* xa = reinterpret_cast<float*>(lds_raw);
+#pragma unroll
+    for (int f = 0; f < MT; ++f)
+#pragma unroll
+      for (int q = 0; q < NTW; ++q)
+        *reinterpret_cast<f32x4*>(xa + (((wave * MT + f) * NTW + q) * 64 + lane) * 4) = acc[0][f][q];
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    w6_barrier();
+#pragma unroll
+    for (int q = 0; q < NTW; ++q) {
+      f32x4 m[4];
+#pragma unroll
+      for (int pp = 0; pp < 4; ++pp)
+        m[pp] = *reinterpret_cast<const f32x4*>(xa + (((pp * MT + wave) * NTW + q) * 64 + lane) * 4);
+      y[0][0][q] = (m[0] + m[1]) + m[2];
+      y[0][1][q] = m[1] + (-m[2] - m[3]);
+    }
+  } else {
   // output transform: ph 0 holds m0, m1, ph 1 holds m2, m3.  Partial sums per tile:
   //   ph 0: (y0, y1) += (m0 + m1, m1);   ph 1: (y0, y1) += (m2, -m2 - m3)
   // wave ph keeps HF of its MT M fragments (96: 2ph, 2ph+1 = tile rows 4ph .. 4ph+3; 48: its
   // fragment mb + ph) and hands the other HF's partials to its partner (wave ^ 2) through LDS
   __builtin_amdgcn_s_waitcnt(0xC07F);
   w6_barrier();  // every wave is done with V: it becomes the exchange area
-  f32x4 y[HF][2][NTW];  // [kept fragment][output parity][q]
   {
     float* xo = reinterpret_cast<float*>(lds_raw) + (wave * HF * NTW * 2) * 4 * 64;  // mine, out
     const int pw = wave ^ 2;                                                         // partner
@@ -404,6 +444,7 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
         else { y[ff][0][q] = i0 + y[ff][0][q]; y[ff][1][q] = i1 + y[ff][1][q]; }
       }
   }
+  }
   // epilogue: this wave's 2 HF tile rows wrow + r (kept fragment r/2, half r%2), channels
   // 48nh .. +47; the fragment's lane (li, lg) holds tiles 4lg .. 4lg+3 of the fragment's 16,
   // i.e. row half lg >> 1, tiles 4 (lg & 1) + e -> pixels 2 (4 (lg & 1) + e) + parity
@@ -435,7 +476,7 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   {
     const int cz = (a.zc ? (int)blockIdx.z * a.zc : 0) + nh * 16 * NTW;
     const int nout = a.NOUT - cz < 16 * NTW ? a.NOUT - cz : 16 * NTW;
-    const int wrow = 2 * (mb + HF * ph);  // (even: a fused 2x2 pool sees whole windows)
+    const int wrow = P1 ? 2 * wave : 2 * (mb + HF * ph);  // (even: a fused 2x2 pool sees whole windows)
     if (nout > 0) fwd_epilogue_at<NTW, 2 * HF, C::PS>(a, outr, st, ty0, tx0, n, wrow, cz, nout);
   }
 }
