@@ -157,6 +157,10 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(inb + ry0 * row_floats), (short)0, (int)((ry1 - ry0) * row_floats * 4),
       0x00020000);
+  // (TAIL 3: the tail channel's compact image rows, a.in_t1)
+  const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(TAIL == 3 ? a.in_t1 + ((long)n * a.IHt + ry0) * a.IWt : a.in), (short)0,
+      TAIL == 3 ? (int)((ry1 - ry0) * (long)a.IWt * 4) : 0, 0x00020000);
   // chunk k0's V: item (row, j, c4) = channels 4c4 .. 4c4+3 of Winograd tile j of input row row,
   // from the four input pixels 2j .. 2j+3 of the halo tile (loaded for all of a thread's items
   // first, so their latencies overlap)
@@ -178,6 +182,12 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
       for (int i = 0; i < 4; ++i) {
         const int gx = ix0 + 2 * j + i;
         const bool ok = rok && gx >= 0 && gx < a.IWt;
+        if constexpr (TAIL == 3 && C4 == 1) {  // the one live channel from the compact image
+          const int off = ok ? ((gy - ry0) * a.IWt + gx) * 4 : 0x7fffffff;
+          d[it][i] = f32x4{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(trs, off, 0, 0)),
+                           0.f, 0.f, 0.f};
+          continue;
+        }
         const int off = ok ? (((gy - ry0) * a.IWt + gx) * a.in_stride + k) * 4 : 0x7fffffff;
         d[it][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
       }
@@ -884,7 +894,8 @@ hipError_t launch_fwd_w6(const FwdArgs& a, hipStream_t s) {
   const dim3 grid(tx * ty, a.N, nz), block(C::WAVES * 64);
   // X6_T1: a one-channel tail chunk in the six-slot layout (96 outputs only)
   const bool t1 = (a.x6_tail & X6_T1) != 0;
-  if (t1 && (tail != 1 || np != 96)) return hipErrorInvalidValue;
+  if (t1 && (tail != 1 || np != 96 || !a.in_t1 || (long)a.IHt * a.IWt * 4 >= 0x7fffffffL))
+    return hipErrorInvalidValue;
   static const char* kn[2][4] = {{"k_c3w6<0,96>", "k_c3w6<1,96>", "k_c3w6<2,96>", "k_c3w6<3,96>"},
                                  {"k_c3w6<0,48>", "k_c3w6<1,48>", "k_c3w6<2,48>", ""}};
   prof_kernel(kn[np == 48][t1 ? 3 : tail]);

@@ -108,6 +108,9 @@ struct FwdArgs {
   // mixed-precision bf16 forward (conv_bf16.hip): the input / output activations are stored as
   // bf16 (RNE of the fp32 value; strides and offsets in elements) instead of fp32
   int in_bf16, out_bf16;
+  // X6_T1 (k_c3w6's one-channel tail): that channel read from this compact [N][IHt][IWt] image
+  // (the network input) instead of channel K - 4 of `in` -- its concat slice need not be written
+  const float* in_t1;
 };
 
 // Fused output head (arch_unet.py:186-190, 253-257): the dec_conv1b kernel keeps its

@@ -76,7 +76,9 @@ __global__ __launch_bounds__(256) void k_enc0_fwd(const float* __restrict__ x, i
 #pragma unroll
       for (int ci = 0; ci < C; ++ci) xcopy[(n * C + ci) * hw + r] = xin[4 * C + ci];
     float* d = cat + p * cat_stride + cat_off;
-    if (C == 1 && cat_zero_to - cat_off == 4 && ((cat_stride | cat_off) & 3) == 0) {
+    // (no concat buffer: the plan's dec_conv1a reads the input itself, X6_T1)
+    if (!cat) {
+    } else if (C == 1 && cat_zero_to - cat_off == 4 && ((cat_stride | cat_off) & 3) == 0) {
       *reinterpret_cast<float4*>(d) = make_float4(xin[4], 0.f, 0.f, 0.f);
     } else {
 #pragma unroll

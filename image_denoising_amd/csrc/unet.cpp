@@ -470,6 +470,7 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
       // channel as a reduction channel (its packed weights are zero) keeps K % 4 == 0
       if (i == D1A) a.K = p.c1kp;
       a.x6_tail = x6_tail_f(i);  // a partial last K chunk packed over fewer stages
+      if (a.x6_tail & X6_T1) a.in_t1 = x;  // the image channel straight from the network input
       a.wp = ws + p.packX[i]; a.bias = b; a.epi = act ? EPI_BIAS_ACT : EPI_BIAS;
       a.out = out.p; a.out_stride = out.stride; a.out_off = out.off; a.out_layout = layout;
       if (pool && pool_fuse && act && layout == OUT_NHWC) {
@@ -596,8 +597,10 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   // enc_conv0, fused with pool0 = x -> channels [2nf, 2nf+C) of the up1 concat buffer
   DN_TIMED(s, "enc0", 2.0 * N * p.H * p.W * C * nf * 9, C, nf, p.H, p.W, N,
            launch_enc0_fwd(x, N, C, p.H, p.W, prm + p.P.L[ENC0].woff, Bs(ENC0), ws + p.a0,
-                           ws + p.c1, p.c1s, 2 * nf, p.c1kp, p.with_bwd ? ws + p.xin : nullptr, s,
-                           enc0_bf16));
+                           // (dec_conv1a reading x itself, X6_T1: the concat slice is never read --
+                           // 16 scattered bytes per 512-B pixel cost the launch 0.19 ms/step)
+                           x6 && (x6_tail_f(D1A) & X6_T1) ? nullptr : ws + p.c1, p.c1s, 2 * nf,
+                           p.c1kp, p.with_bwd ? ws + p.xin : nullptr, s, enc0_bf16));
   {  // enc_conv1 + pool1 -> skip slice of c2
     const View pv = V(p.c[1], p.cs[1], 2 * nf);
     bool pooled = false;
