@@ -114,7 +114,8 @@ __device__ __forceinline__ void w6_for(F&& f) {
 // TAIL (x6_tail_mode of K) packs the last chunk's channels: 1 (<= 4 channels): one stage per
 // position, k = 4 ky + channel; 2 (<= 16 channels): two stages per position, k = 16 (ky - 2s) +
 // channel.  Full chunks: stage 4 ky + p, k = channel.
-// TAIL 3 (X6_T1: the last chunk has ONE live channel, dec_conv1a's image channel at C = 1): one
+// TAIL 3 (X6_T1: the last chunk has ONE live channel, dec_conv1a's image channel at C = 1, read
+// from the compact network input a.in_t1 rather than the concat buffer): one
 // stage per position whose single MFMA per fragment pair holds all six split products of the
 // three kernel rows, k = 8 ky + slot, slot = (h,h) (h,m) (m,h) (h,l) (l,h) (m,m) of (v, u):
 // lane group ky reads its row's (h, m, l) of v as one 8-B slot, the packer lays u's pieces out
