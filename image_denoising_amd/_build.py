@@ -29,8 +29,11 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
             *os.environ.get("DN_EXTRA_CXXFLAGS", "").split()]
 # the bf16x6 kernels keep their fp32 adds scalar: the SLP vectorizer would pair them into
 # v_pk_add_f32, which costs more issue cycles beside MFMAs than the two adds (x6_core.h)
+# conv_w6.hip: LLVM's max-memory-clause scheduling strategy, 19.10 -> 19.05 ms/step over six
+# same-box pairs (profiles/r5_w6_sched_ab.log); for every file it slowed the weight gradients
 FILE_FLAGS = {"conv_x6.hip": ["-fno-slp-vectorize"],
-              "conv_w6.hip": ["-fno-slp-vectorize"], "wgrad_x6p.hip": ["-fno-slp-vectorize"]}
+              "conv_w6.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
+              "wgrad_x6p.hip": ["-fno-slp-vectorize"]}
 
 
 def source_hash() -> str:
