@@ -113,7 +113,10 @@ __device__ __forceinline__ void w6_for(F&& f) {
 
 // TAIL (x6_tail_mode of K) packs the last chunk's channels: 1 (<= 4 channels): one stage per
 // position, k = 4 ky + channel; 2 (<= 16 channels): two stages per position, k = 16 (ky - 2s) +
-// channel.  Full chunks: stage 4 ky + p, k = channel.
+// channel for s = 0; s = 1 holds kernel row 2 alone, its six products in three MFMAs (stage mode
+// 4): k < 16 pairs v's (h, h, h) with u's (h, m, l), k >= 16 the same channels' (m, l, m) with
+// (h, h, m), so the three sums are hh + mh, hm + lh, hl + mm.  Full chunks: stage 4 ky + p,
+// k = channel.
 // TAIL 3 (X6_T1: the last chunk has ONE live channel, dec_conv1a's image channel at C = 1, read
 // from the compact network input a.in_t1 rather than the concat buffer): one
 // stage per position whose single MFMA per fragment pair holds all six split products of the
@@ -268,14 +271,14 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
   // fragment q: 2 x 2 M fragments x 6 products, its adds pinned, and the next stage's fragment q
   // requested into the registers it frees
   auto stage = [&](auto mode_tag, int s, int nxt, int liv, int lgv) {
-    constexpr int MODE = decltype(mode_tag)::value;  // 0 full, 1 / 2 / 3 tail
+    constexpr int MODE = decltype(mode_tag)::value;  // 0 full, 1 / 2 / 3 / 4 tail
     int pi, ky0;
     if (P1) { pi = 0; ky0 = MODE == 0 ? s : 2 * (s & 1); }
     else if (MODE == 0) { pi = s & 1; ky0 = s >> 1; }
     else if (MODE == 1 || MODE == 3) { pi = s; ky0 = 0; }
     else { pi = s >> 1; ky0 = 2 * (s & 1); }
     const int p = P1 ? wave : 2 * ph + pi;
-    bf16x8 av[3][MT];
+    bf16x8 av[3][MT];  // (mode 4: av[0] = A of the (h | m) halves, av[1] = A of (h | l))
 #pragma unroll
     for (int f = 0; f < MT; ++f) {
       const int row0 = 2 * (mb + f) + (liv >> 3), j = liv & 7;
@@ -283,6 +286,12 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
         const int o = w6_vq(row0 + ky0, lgv, j, p) * 8;
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) av[pl][f] = *reinterpret_cast<const bf16x8*>(lv + pl * C::VPL + o);
+      } else if constexpr (MODE == 4) {
+        // kernel row 2 of a tail-2 chunk: lane groups 0, 1 read channels 0..15 from plane h,
+        // groups 2, 3 the same channels from plane m (av[0]) and plane l (av[1])
+        const int o = w6_vq(row0 + 2, lgv & 1, j, p) * 8, up = lgv >> 1;
+        av[0][f] = *reinterpret_cast<const bf16x8*>(lv + up * C::VPL + o);
+        av[1][f] = *reinterpret_cast<const bf16x8*>(lv + 2 * up * C::VPL + o);
       } else if constexpr (MODE == 3) {
         // lane group ky: (h, m, l, 0) of kernel row ky -> A slots (h, h, m, h, l, m, 0, 0)
         const int ky = lgv;
@@ -326,6 +335,16 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
           if constexpr (MODE == 3) {
             const f32x4 t = mfma_bf16(av[0][mp], w[0][q], f32x4{0.f, 0.f, 0.f, 0.f});
             acc[PI][mp][q] = acc[PI][mp][q] + t;
+            continue;
+          }
+          if constexpr (MODE == 4) {  // (hl + mm) + (hm + lh) from zero, then hh + mh
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            f32x4 lo = mfma_bf16(av[0][mp], w[2][q], z);
+            lo = mfma_bf16(av[1][mp], w[1][q], lo);
+            const f32x4 hi = mfma_bf16(av[0][mp], w[0][q], z);
+            x6_acc_add(acc[PI][mp][q], hi, lo);
+            asm volatile("" : "+v"(acc[PI][mp][q]));
+            __builtin_amdgcn_sched_barrier(0);
             continue;
           }
           f32x4(&ah)[1][NTW] = *reinterpret_cast<f32x4(*)[1][NTW]>(&acc[PI][mp]);
@@ -379,7 +398,9 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
     using MD = std::integral_constant<int, TAIL>;
     w6_for<0, NS>([&](auto si) {
       constexpr int s = decltype(si)::value;
-      stage(MD{}, s, s + 1 < NS ? stage_of(c, s + 1, true) : -1, liv, lgv);
+      const int nxt = s + 1 < NS ? stage_of(c, s + 1, true) : -1;
+      if constexpr (TAIL == 2 && (s & 1)) stage(std::integral_constant<int, 4>{}, s, nxt, liv, lgv);
+      else stage(MD{}, s, nxt, liv, lgv);
     });
   }
 

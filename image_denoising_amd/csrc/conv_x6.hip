@@ -1247,7 +1247,9 @@ __device__ __forceinline__ void pk_x6(const PackJob& j, long e) {
 // Winograd F(2,3) image of k_c3w6 (conv_w6.hip): [chunk][stage][piece][n < 96][32 k] as pk_x6,
 // stage 4 ky + p holding u_p = G g of kernel row ky (g = the three kx taps of (k, n)):
 // u = (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2), each rounded once from fp64, then split.
-// Last chunk (tail): 1: stage p, k = 4 ky + channel; 2: stage 2p + h, k = 16 (ky - 2h) + channel;
+// Last chunk (tail): 1: stage p, k = 4 ky + channel; 2: stage 2p + h, k = 16 (ky - 2h) + channel
+// for h = 0, h = 1: kernel row 2, k = channel with planes (h, m, l) and k = 16 + channel with
+// planes (h, h, m) (k_c3w6's stage mode 4);
 // 3 (X6_T1): stage p, k = 8 ky + slot, plane 0 = u's piece of each of the six products (k_c3w6).
 __device__ __forceinline__ void pk_w6(const PackJob& j, long e0) {
   const int NP = j.g0, nch = j.nch, wst = x6_wst(NP), pad = wst - 3 * NP * 32;
@@ -1257,7 +1259,7 @@ __device__ __forceinline__ void pk_w6(const PackJob& j, long e0) {
   const int kk = (int)(e % 32), nn = (int)((e / 32) % NP);
   const int cs = (int)(e / (32L * NP)), c = cs / 12, s = cs % 12;
   int ky = s >> 2, p = s & 3, k = c * 32 + kk, slot = -1;
-  bool live = true;
+  bool live = true, dup = false;
   if (j.tail == 3 && c == nch - 1) {  // X6_T1: k = 8 ky + product slot, channel c * 32 only
     p = s; ky = kk >> 3; slot = kk & 7; k = c * 32;
     live = s < 4 && ky < 3 && slot < 6;
@@ -1267,6 +1269,7 @@ __device__ __forceinline__ void pk_w6(const PackJob& j, long e0) {
   } else if (j.tail == 2 && c == nch - 1) {
     p = s >> 1; ky = 2 * (s & 1) + (kk >> 4); k = c * 32 + (kk & 15);
     live = s < 8 && ky < 3;
+    if ((s & 1) && kk >= 16) { ky = 2; live = s < 8; dup = true; }
   }
   float v = 0.f;
   if (live && k < j.K && nn < j.NOUT && (j.zc == 0 || z * j.zc + nn < j.ntot)) {
@@ -1285,6 +1288,10 @@ __device__ __forceinline__ void pk_w6(const PackJob& j, long e0) {
   if (slot >= 0) {  // u's piece of product slot (h,h) (h,m) (m,h) (h,l) (l,h) (m,m), plane 0 only
     h = slot == 1 || slot == 5 ? m : (slot == 3 ? l : h);
     m = l = (__bf16)0.f;
+  }
+  if (dup) {  // tail 2, kernel row 2, upper half: planes (h, h, m)
+    l = m;
+    m = h;
   }
   __bf16* st = static_cast<__bf16*>(j.out) + ((long)z * nch * 12 + cs) * wst;
   const int o = nn * 32 + x6_swz(nn, kk >> 3) * 8 + (kk & 7);
