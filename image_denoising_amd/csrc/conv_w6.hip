@@ -112,7 +112,7 @@ __device__ __forceinline__ void w6_for(F&& f) {
 }
 
 // TAIL (x6_tail_mode of K) packs the last chunk's channels: 1 (<= 4 channels): one stage per
-// position, k = 4 ky + channel; 2 (<= 16 channels): two stages per position, k = 16 (ky - 2s) +
+// position, k = 4 ky + channel in each K half, the products paired as in mode 4 below; 2 (<= 16 channels): two stages per position, k = 16 (ky - 2s) +
 // channel for s = 0; s = 1 holds kernel row 2 alone, its six products in three MFMAs (stage mode
 // 4): k < 16 pairs v's (h, h, h) with u's (h, m, l), k >= 16 the same channels' (m, l, m) with
 // (h, h, m), so the three sums are hh + mh, hm + lh, hl + mm.  Full chunks: stage 4 ky + p,
@@ -300,18 +300,20 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
         const bf16x8 v8 = __builtin_shufflevector(q4, q4, 0, 0, 1, 0, 2, 1, 3, 3);
         av[0][f] = ky > 2 ? z8 : v8;
       } else if constexpr (MODE == 1) {
-        // lane group 0: channels 0..3 of ky 0 and 1; group 1: ky 2 and zeros; 2, 3: zeros
-        const int ka = 2 * lgv, kb = ka + 1;
-        const int oa = w6_vt(row0 + (ka < 3 ? ka : 0), j, p) * 4;
+        // lane groups 0 / 2: channels 0..3 of ky 0 and 1; 1 / 3: ky 2 and zeros; groups 0, 1
+        // from plane h, groups 2, 3 from plane m (av[0]) and plane l (av[1]) (the paired
+        // products of stage mode 4)
+        const int ka = 2 * (lgv & 1), kb = ka + 1, up = lgv >> 1;
+        const int oa = w6_vt(row0 + ka, j, p) * 4;
         const int ob = w6_vt(row0 + (kb < 3 ? kb : 0), j, p) * 4;
         const bf16x4 z4 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          bf16x4 va = *reinterpret_cast<const bf16x4*>(lv + pl * C::VPL + oa);
+        for (int i = 0; i < 2; ++i) {
+          const int pl = (1 + i) * up;
+          const bf16x4 va = *reinterpret_cast<const bf16x4*>(lv + pl * C::VPL + oa);
           bf16x4 vb = *reinterpret_cast<const bf16x4*>(lv + pl * C::VPL + ob);
-          if (ka > 2) va = z4;
           if (kb > 2) vb = z4;
-          av[pl][f] = __builtin_shufflevector(va, vb, 0, 1, 2, 3, 4, 5, 6, 7);
+          av[i][f] = __builtin_shufflevector(va, vb, 0, 1, 2, 3, 4, 5, 6, 7);
         }
       } else {
         // lane groups 0, 1: channels 0..15 of ky0 (quads 0, 1); 2, 3: those of ky0 + 1
@@ -337,7 +339,7 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
             acc[PI][mp][q] = acc[PI][mp][q] + t;
             continue;
           }
-          if constexpr (MODE == 4) {  // (hl + mm) + (hm + lh) from zero, then hh + mh
+          if constexpr (MODE == 4 || MODE == 1) {  // (hl + mm) + (hm + lh) from zero, then hh + mh
             const f32x4 z = {0.f, 0.f, 0.f, 0.f};
             f32x4 lo = mfma_bf16(av[0][mp], w[2][q], z);
             lo = mfma_bf16(av[1][mp], w[1][q], lo);

@@ -1247,7 +1247,8 @@ __device__ __forceinline__ void pk_x6(const PackJob& j, long e) {
 // Winograd F(2,3) image of k_c3w6 (conv_w6.hip): [chunk][stage][piece][n < 96][32 k] as pk_x6,
 // stage 4 ky + p holding u_p = G g of kernel row ky (g = the three kx taps of (k, n)):
 // u = (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2), each rounded once from fp64, then split.
-// Last chunk (tail): 1: stage p, k = 4 ky + channel; 2: stage 2p + h, k = 16 (ky - 2h) + channel
+// Last chunk (tail): 1: stage p, k = 4 ky + channel (k < 16; k = 16 + 4 ky + channel with planes
+// (h, h, m)); 2: stage 2p + h, k = 16 (ky - 2h) + channel
 // for h = 0, h = 1: kernel row 2, k = channel with planes (h, m, l) and k = 16 + channel with
 // planes (h, h, m) (k_c3w6's stage mode 4);
 // 3 (X6_T1): stage p, k = 8 ky + slot, plane 0 = u's piece of each of the six products (k_c3w6).
@@ -1263,9 +1264,10 @@ __device__ __forceinline__ void pk_w6(const PackJob& j, long e0) {
   if (j.tail == 3 && c == nch - 1) {  // X6_T1: k = 8 ky + product slot, channel c * 32 only
     p = s; ky = kk >> 3; slot = kk & 7; k = c * 32;
     live = s < 4 && ky < 3 && slot < 6;
-  } else if (j.tail == 1 && c == nch - 1) {
-    p = s; ky = kk >> 2; k = c * 32 + (kk & 3);
-    live = s < 4 && kk < 12;
+  } else if (j.tail == 1 && c == nch - 1) {  // both K halves k = 4 ky + channel, upper (h, h, m)
+    p = s; ky = (kk & 15) >> 2; k = c * 32 + (kk & 3);
+    live = s < 4 && (kk & 15) < 12;
+    dup = kk >= 16;
   } else if (j.tail == 2 && c == nch - 1) {
     p = s >> 1; ky = 2 * (s & 1) + (kk >> 4); k = c * 32 + (kk & 15);
     live = s < 8 && ky < 3;

@@ -7,7 +7,7 @@ LIBS=${LIBS:-"- base"}; OPS=${OPS:-"wgrad_up wgrad1"}
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in $LIBS; do
     if [ "$v" = "-" ]; then lib=image_denoising_amd/libdenoise_hip.so; else lib=image_denoising_amd/libdenoise_hip_$v.so; fi
-    DN_LIB_PATH=$lib timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-eval > gpurun_out/libab_${v}_$r.log 2>&1 || exit $?
+    DN_LIB_PATH=$lib timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-eval ${BARGS:-} > gpurun_out/libab_${v}_$r.log 2>&1 || exit $?
     python3 - gpurun_out/libab_${v}_$r.log "$v" "$r" "$OPS" >> gpurun_out/libab.log <<'PY'
 import json, sys
 s = open(sys.argv[1]).read(); i = s.find('{"metric"'); d = json.loads(s[i:s.find('\n', i)])
