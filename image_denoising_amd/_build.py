@@ -37,9 +37,14 @@ FILE_FLAGS = {"conv_x6.hip": ["-fno-slp-vectorize"],
 
 
 def source_hash() -> str:
-    """sha256 (first 16 hex digits) over the library's sources, headers and C-ABI header, in a
-    fixed order.  Compiled into dn_version() so a test can tie a loaded .so to the tree."""
+    """sha256 (first 16 hex digits) over the effective compile flags (CXXFLAGS including
+    DN_EXTRA_CXXFLAGS, and every per-file flag set) and the library's sources, headers and C-ABI
+    header, in a fixed order.  Compiled into dn_version() so a test can tie a loaded .so to the
+    tree; a flag-only change rebuilds every object (the stamp in build() differs)."""
     h = hashlib.sha256()
+    h.update(" ".join([HIPCC, *CXXFLAGS]).encode() + b"\0")
+    for f in sorted(FILE_FLAGS):
+        h.update(f.encode() + b":" + " ".join(FILE_FLAGS[f]).encode() + b"\0")
     paths = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     paths.append(os.path.join(ROOT, "include", "denoise_hip.h"))
     for p in paths:

@@ -598,7 +598,9 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
   DN_TIMED(s, "enc0", 2.0 * N * p.H * p.W * C * nf * 9, C, nf, p.H, p.W, N,
            launch_enc0_fwd(x, N, C, p.H, p.W, prm + p.P.L[ENC0].woff, Bs(ENC0), ws + p.a0,
                            // (dec_conv1a reading x itself, X6_T1: the concat slice is never read --
-                           // 16 scattered bytes per 512-B pixel cost the launch 0.19 ms/step)
+                           // 16 scattered bytes per 512-B pixel cost the launch 0.19 ms/step; c1's
+                           // channels [2nf, c1s) then hold stale data, which the debug-buffer
+                           // contract in denoise_hip.h states)
                            x6 && (x6_tail_f(D1A) & X6_T1) ? nullptr : ws + p.c1, p.c1s, 2 * nf,
                            p.c1kp, p.with_bwd ? ws + p.xin : nullptr, s, enc0_bf16));
   {  // enc_conv1 + pool1 -> skip slice of c2

@@ -694,8 +694,13 @@ struct Wp1Cfg {
 #ifndef DN_WG1_PD
 #define DN_WG1_PD 2
 #endif
-// stages of operands in flight (1 or 2): two stages took the deconv weight gradients 0.346-0.348 ->
-// 0.298-0.305 ms/step, the 1x1 ones unchanged (profiles/r5_wgrad1_pd_ab.log)
+// WG1_PD = 2: stage u + 2's loads are issued at the head of stage u into a second register set
+// (pv2), stage u + 1's operands (pv) are split into the other LDS buffer at the end of stage u,
+// then pv = pv2.  That copy waits for the u + 2 loads inside stage u, so load latency is still
+// hidden behind ONE stage only; what the form buys is that the split / plane writes of stage u + 1
+// no longer wait for their own loads (issued a whole stage earlier).  Measured: the deconv weight
+// gradients 0.346-0.348 -> 0.298-0.305 ms/step, the 1x1 ones unchanged
+// (profiles/r5_wgrad1_pd_ab.log).
 constexpr int WG1_PD = DN_WG1_PD;
 template <bool UP2>
 __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
@@ -789,7 +794,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
     const int cb = (int)((u - u_beg) & 1);
     const __bf16* buf = lds + cb * C::BUF;
     const bool more = u + 1 < u_end;
-    if (u + WG1_PD < u_end) load(u + WG1_PD, WG1_PD == 2 ? pv2 : pv);  // in flight during the stage(s)
+    if (u + WG1_PD < u_end) load(u + WG1_PD, WG1_PD == 2 ? pv2 : pv);  // in flight during this stage
     int aoff = abase;
     asm volatile("" : "+v"(aoff));
     bf16x8 av[3][3], bv[3][3];
@@ -832,7 +837,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
       }
     }
     if (more) store(lds + (cb ^ 1) * C::BUF);  // (waits for its loads itself)
-    if (WG1_PD == 2) {
+    if (WG1_PD == 2) {  // (waits for the u + 2 loads issued at this stage's head)
 #pragma unroll
       for (int it = 0; it < C::NIT; ++it) pv[it] = pv2[it];
     }

@@ -176,7 +176,11 @@ dn_status dn_unet_backward_split(const dn_unet_cfg* cfg, const float* params, co
 
 /* Debug/introspection: (offset_floats, channel_stride, level) of every NHWC buffer of the
    workspace plan, in the order c1 a0 a1 c2..c5 a2..a5 p5 a6 d{2..5}a d{2..5}b d1a d1b nin_a nin_b
-   [g_nb g_na g_d1b g_d1a g_c1 g_c2..g_c5 g_d{2..5}a g_d{2..5}b g_a2..g_a5 g_a6 g_p5 g_a0 g_a1]. */
+   [g_nb g_na g_d1b g_d1a g_c1 g_c2..g_c5 g_d{2..5}a g_d{2..5}b g_a2..g_a5 g_a6 g_p5 g_a0 g_a1].
+   c1 = [up1 (2*nf) | image (C) | pad] is reported with its full pixel stride, but only the up1
+   channels [0, 2*nf) are guaranteed to be written: when the bf16x6 Winograd dec_conv1a reads the
+   image channel from the network input itself (C = 1, unet.cpp X6_T1), enc_conv0 does not copy
+   the image into c1 and channels [2*nf, stride) hold stale workspace data. */
 dn_status dn_unet_debug_buffers(const dn_unet_cfg* cfg, int N, int H, int W, int with_backward,
                                 int64_t* desc, int max_entries, int* n_entries);
 
