@@ -537,7 +537,9 @@ struct WgCfg {
 };
 
 template <int MODE, int MF, int NW, int CIF>
-__global__ __launch_bounds__(NW * 64, MF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a0) {
+// (occupancy targets the register allocation reaches: k_wgrad<W_C1, 1, 1, 2> holds two input-
+// channel fragments per wave and gets 3 waves per SIMD, not 4)
+__global__ __launch_bounds__(NW * 64, MF >= 2 || CIF >= 2 ? 3 : 4) void k_wgrad(WgradArgs a0) {
   using C = WgCfg<MODE, MF, NW, CIF>;
   const WgradArgs a = wg_block(a0);
   __shared__ __attribute__((aligned(16))) float lds[C::LG + C::LX];
@@ -735,7 +737,9 @@ struct Wg3Cfg {
 };
 
 template <int CO_FR, int WM, int WN, int SWL = 5>
-__global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad3(WgradArgs a0) {
+// (k_wgrad3<2, 1, 2 or 4, *>, the 32-output ImprovedUNet blocks with 32 / 64 input channels per
+// workgroup: 2 waves per SIMD is what its registers allow)
+__global__ __launch_bounds__(64 * WM * WN, CO_FR == 2 && WN != 3 ? 2 : 3) void k_wgrad3(WgradArgs a0) {
   using C = Wg3Cfg<CO_FR, WM, WN>;
   const WgradArgs a = wg_block(a0);
   __shared__ __attribute__((aligned(16))) float lds[2 * C::LBUF];
@@ -969,13 +973,53 @@ __global__ __launch_bounds__(64 * WM * WN, 3) void k_wgrad1(WgradArgs a0, int up
 // 64 elements of one job, its four waves sum interleaved quarters of the rows (four loads in
 // flight per lane), then wave 0 adds the four partials.  blockIdx.x -> job by the jobs' first
 // workgroups (b0, increasing).
+constexpr int RED_VF = 12;  // 16-B rows a lane keeps in flight (vector jobs)
+// Vector jobs (j.vec, red_add): a lane owns FOUR consecutive elements, contiguous in every slab
+// row, and reads them with one 16-byte load per row -- the same per-element summation order as
+// the scalar form (bit-identical results) with a quarter of the load instructions and 4x the bytes
+// in flight (the scalar form waited on its loads: SQ_WAIT_ANY 0.86, profiles/r5zz_pmc_sq_n2n.txt).
 __global__ __launch_bounds__(256) void k_reduce_batch(RedBatch b) {
   __shared__ float part[4][64];
+  __shared__ f32x4 part4[4][64];
   int jj = 0;
   for (int q = 1; q < b.n; ++q)
     if ((int)blockIdx.x >= b.j[q].b0) jj = q;
   const RedJob& j = b.j[jj];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (j.vec) {
+    const long e = ((long)((int)blockIdx.x - j.b0) * 64 + lane) * 4;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    if (e < j.n) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(j.slab + (e / j.ig) * j.is1 + e % j.ig);
+      const long stride = j.stride / 4;
+      int i = wave;
+      for (; i + 4 * (RED_VF - 1) < j.splits; i += 4 * RED_VF) {  // RED_VF rows in flight
+        f32x4 v[RED_VF];
+#pragma unroll
+        for (int k = 0; k < RED_VF; ++k) v[k] = src[(long)(i + 4 * k) * stride];
+#pragma unroll
+        for (int k = 0; k < RED_VF; ++k)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[r] += v[k][r];
+      }
+      for (; i < j.splits; i += 4) {
+        const f32x4 v = src[(long)i * stride];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[r] += v[r];
+      }
+    }
+    part4[wave][lane] = s;
+    __syncthreads();
+    if (wave == 0 && e < j.n) {
+      const f32x4 p0 = part4[0][lane], p1 = part4[1][lane], p2 = part4[2][lane], p3 = part4[3][lane];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long er = e + r;
+        j.out[(er / j.og) * j.os1 + j.ooff + er % j.og] = ((p0[r] + p1[r]) + p2[r]) + p3[r];
+      }
+    }
+    return;
+  }
   const long e = (long)((int)blockIdx.x - j.b0) * 64 + lane;
   float s = 0.f;
   if (e < j.n) {
@@ -1469,7 +1513,11 @@ hipError_t red_add(RedBatch* b, const RedJob& j, hipStream_t s) {
   }
   r.j[r.n] = j;
   r.j[r.n].b0 = r.blocks;
-  r.blocks += (j.n + 63) / 64;
+  // four elements per lane where they are contiguous and 16-B aligned in every slab row
+  const int vec = j.is2 == 1 && j.ig % 4 == 0 && j.is1 % 4 == 0 && j.stride % 4 == 0 &&
+                  j.n % 4 == 0 && (reinterpret_cast<uintptr_t>(j.slab) & 15) == 0;
+  r.j[r.n].vec = vec;
+  r.blocks += vec ? (j.n + 255) / 256 : (j.n + 63) / 64;
   ++r.n;
   return b ? hipSuccess : red_flush(r, s);
 }

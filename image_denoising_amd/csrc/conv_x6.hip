@@ -2270,7 +2270,8 @@ __global__ __launch_bounds__(512, 1) void k_head_bwd_x6(HeadBwdArgs h, const __b
         t[q][2] = fmaf(w.z, dy[o], t[q][2]); t[q][3] = fmaf(w.w, dy[o], t[q][3]);
       }
     }
-    const __amdgpu_buffer_rsrc_t wnb = rsrc(h.g_nb, px0, npx_t);
+    // (h.g_nb null: k_head_wgrad_x6 recomputes g_nb from dy and nb, nothing stores it)
+    const __amdgpu_buffer_rsrc_t wnb = rsrc(h.g_nb ? h.g_nb : h.nb, px0, h.g_nb ? npx_t : 0);
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       mask(t[q], nb[q]);

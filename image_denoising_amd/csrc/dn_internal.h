@@ -154,6 +154,9 @@ struct WgradArgs {
   const float* zeros;                   // >= 16 zero bytes (LDS-DMA source for padding)
   int co_base, cout_total;              // this launch's first output channel / the layer's Cout
   int zc;                               // > 0: blockIdx.z = output-channel block of zc channels
+  // k_wgrad1p of nin_b with the gradient operand recomputed (head_gnb > 0 = nin_c's outputs):
+  // g = leaky'(nb) (Wc^T dy) per pixel, with g pointing at nb (k_head_bwd_x6's order and result)
+  int head_gnb; const float* hd_dy; int hd_dy_stride; const float* hd_wc;
 };
 
 // strided NHWC view: element (pixel, c) at p[pixel * stride + off + c]
@@ -223,6 +226,7 @@ struct RedJob {
   const float* slab;
   float* out;
   int stride, splits, n, ig, is1, is2, og, os1, ooff, b0;  // b0: first workgroup of the job
+  int vec;  // set by red_add: four contiguous 16-B aligned elements per lane (k_reduce_batch)
 };
 constexpr int kRedJobs = 40;
 struct RedBatch {

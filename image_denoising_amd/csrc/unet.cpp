@@ -370,8 +370,10 @@ hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const flo
 
 hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, int cout, int cin,
                  float* dwb, float* slab, int splits, hipStream_t s, bool x6, const float* zeros,
-                 RedBatch* rb) {
+                 RedBatch* rb, int head_gnb, const float* hd_dy, int hd_dy_stride,
+                 const float* hd_wc) {
   WgradArgs a{};
+  a.head_gnb = head_gnb; a.hd_dy = hd_dy; a.hd_dy_stride = hd_dy_stride; a.hd_wc = hd_wc;
   a.g = g.p; a.g_stride = g.stride; a.g_off = g.off;
   a.x = x.p; a.x_stride = x.stride; a.x_off = x.off;
   a.N = N; a.KH = KH; a.KW = KW; a.Cout = cout; a.Cin = cin;
@@ -828,6 +830,9 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   };
   // the head's data gradients in the bf16x6 arithmetic (k_head_bwd_x6)
   const bool head_bwd_x6 = x6 && p.OC <= X6_HEAD_BWD_OCMAX;
+  // g_nb (the nin_b output's gradient) recomputed by nin_b's weight gradient (k_wgrad1p<., GNB>)
+  // from nb and dy instead of being stored by k_head_bwd_x6 and read back (384 B per pixel less)
+  const bool head_gnb = head_bwd_x6;
   // flipped/transposed weight images for the data gradients, the head's images and the
   // weight gradients' zero padding: one launch
   {
@@ -911,7 +916,9 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     h.wc = prm + p.P.L[NINC].woff; h.oc = OC;
     h.dy = dyv.p; h.dy_stride = dyv.stride;
     h.nb = ws + p.nb; h.na = ws + p.na; h.d1b = ws + p.d1b;
-    h.g_nb = ws + p.g_nb; h.g_na = ws + p.g_na; h.g_d1b = ws + p.g_d1b;
+    // (head_gnb: nin_b's weight gradient recomputes g_nb, nothing reads a stored one)
+    h.g_nb = head_gnb ? nullptr : ws + p.g_nb;
+    h.g_na = ws + p.g_na; h.g_d1b = ws + p.g_d1b;
     h.npx = (long)N * H(0) * Wd(0);
     DN_TIMED(s, "head_bwd", 2.0 * h.npx * 96 * (2 * 96 + OC), OC, 96, H(0), Wd(0), N,
              head_bwd_x6 ? launch_head_bwd_x6(h, ws + p.packHB, s) : launch_head_bwd(h, s));
@@ -925,8 +932,10 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     DN_TRY(wgrad(W_C1, dyv, V(p.nb, 96), N, H(0), Wd(0), OC, 96, G(NINC), SL(NINC),
                  p.splits[NINC], s2, false, Z, &rb));
   DN_TRY(fork());
-  DN_TRY(wgrad(W_C1, V(p.g_nb, 96), V(p.na, 96), N, H(0), Wd(0), 96, 96, G(NINB), SL(NINB),
-               p.splits[NINB], s2, x6, Z, &rb));
+  // (head_gnb: the gradient operand g_nb recomputed from nb and dy inside k_wgrad1p)
+  DN_TRY(wgrad(W_C1, head_gnb ? V(p.nb, 96) : V(p.g_nb, 96), V(p.na, 96), N, H(0), Wd(0), 96, 96,
+               G(NINB), SL(NINB), p.splits[NINB], s2, x6, Z, &rb,
+               head_gnb ? OC : 0, dyv.p, dyv.stride, prm + p.P.L[NINC].woff));
   DN_TRY(fork());
   DN_TRY(wgrad(W_C1, V(p.g_na, 96), V(p.d1b, 96), N, H(0), Wd(0), 96, 96, G(NINA), SL(NINA),
                p.splits[NINA], s2, x6, Z, &rb));

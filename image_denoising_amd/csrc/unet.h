@@ -119,6 +119,7 @@ hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const flo
 // serve as the DMA padding; rb: the reduction is queued, not launched
 hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, int cout, int cin,
                  float* dwb, float* slab, int splits, hipStream_t s, bool x6 = false,
-                 const float* zeros = nullptr, RedBatch* rb = nullptr);
+                 const float* zeros = nullptr, RedBatch* rb = nullptr, int head_gnb = 0,
+                 const float* hd_dy = nullptr, int hd_dy_stride = 0, const float* hd_wc = nullptr);
 
 }  // namespace dn

@@ -702,7 +702,10 @@ struct Wp1Cfg {
 // gradients 0.346-0.348 -> 0.298-0.305 ms/step, the 1x1 ones unchanged
 // (profiles/r5_wgrad1_pd_ab.log).
 constexpr int WG1_PD = DN_WG1_PD;
-template <bool UP2>
+// GNB > 0 (nin_b's weight gradient, GNB = nin_c's outputs): the gradient operand is recomputed
+// from the nin_b activation (a.g) and dL/dy as g = leaky'(nb) (Wc^T dy) -- k_head_bwd_x6's
+// fmaf order, the same values -- so the data-gradient pass does not store g_nb (384 B per pixel).
+template <bool UP2, int GNB = 0>
 __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
   using C = Wp1Cfg;
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * C::BUF];
@@ -740,10 +743,30 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
     ilds[it] = (it < NG ? 0 : C::GPL) + wp_idx(px, C::C, c >> 4) + (c & 15);
   }
   f32x4 pv[C::NIT], pv2[WG1_PD == 2 ? C::NIT : 1];
+  constexpr int GO = GNB > 0 ? GNB : 1;
+  float dv[NG][GO], dv2[WG1_PD == 2 ? NG : 1][GO];  // (GNB) dy of the G items' pixels
+  f32x4 wcr[NG][GO];                                   // (GNB) Wc[o][c .. c + 3] of the G items
+  if constexpr (GNB > 0) {
+#pragma unroll
+    for (int it = 0; it < NG; ++it)
+#pragma unroll
+      for (int o = 0; o < GNB; ++o)
+        wcr[it][o] = *reinterpret_cast<const f32x4*>(a.hd_wc + o * 96 + (ioff[it] - ipx[it] * a.g_stride));
+  }
   const int pa = bz >> 1, pb = bz & 1;
-  auto load = [&](long u, f32x4* dst) {
+  auto load = [&](long u, f32x4* dst, float (*ddst)[GO]) {
     const long p0 = u * C::PX;
     const int np = npx - p0 < C::PX ? (int)(npx - p0) : C::PX;
+    if constexpr (GNB > 0) {
+      const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(a.hd_dy + p0 * a.hd_dy_stride), (short)0, np * a.hd_dy_stride * 4, 0x00020000);
+#pragma unroll
+      for (int it = 0; it < NG; ++it)
+#pragma unroll
+        for (int o = 0; o < GNB; ++o)
+          ddst[it][o] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                      dr, (ipx[it] * a.hd_dy_stride + o) * 4, 0, 0));
+    }
     const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a.g + p0 * a.g_stride + a.g_off), (short)0, np * a.g_stride * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
@@ -766,9 +789,21 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
 #pragma unroll
     for (int it = 0; it < C::NIT; ++it) {
       const int o = ilds[it];
+      f32x4 v = pv[it];
+      if constexpr (GNB > 0) {
+        if (it < NG) {  // g_nb = leaky'(nb) (Wc^T dy)
+          f32x4 t = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int oo = 0; oo < GNB; ++oo)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t[e] = fmaf(wcr[it][oo][e], dv[it][oo], t[e]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = pv[it][e] > 0.f ? t[e] : t[e] * 0.2f;
+        }
+      }
       unsigned h0, m0, l0, h1, m1, l1;
-      split3x2(pv[it][0], pv[it][1], h0, m0, l0);
-      split3x2(pv[it][2], pv[it][3], h1, m1, l1);
+      split3x2(v[0], v[1], h0, m0, l0);
+      split3x2(v[2], v[3], h1, m1, l1);
       typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
       *reinterpret_cast<u32x2_t*>(buf + o) = u32x2_t{h0, h1};
       *reinterpret_cast<u32x2_t*>(buf + o + C::PL) = u32x2_t{m0, m1};
@@ -783,10 +818,10 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
   for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
 
   if (u_beg < u_end) {
-    load(u_beg, pv);
+    load(u_beg, pv, dv);
     store(lds);
   }
-  if (WG1_PD == 2 && u_beg + 1 < u_end) load(u_beg + 1, pv);
+  if (WG1_PD == 2 && u_beg + 1 < u_end) load(u_beg + 1, pv, dv);
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own plane writes done
   __syncthreads();
 #pragma unroll 1
@@ -794,7 +829,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
     const int cb = (int)((u - u_beg) & 1);
     const __bf16* buf = lds + cb * C::BUF;
     const bool more = u + 1 < u_end;
-    if (u + WG1_PD < u_end) load(u + WG1_PD, WG1_PD == 2 ? pv2 : pv);  // in flight during this stage
+    if (u + WG1_PD < u_end) load(u + WG1_PD, WG1_PD == 2 ? pv2 : pv, WG1_PD == 2 ? dv2 : dv);  // in flight during this stage
     int aoff = abase;
     asm volatile("" : "+v"(aoff));
     bf16x8 av[3][3], bv[3][3];
@@ -840,6 +875,12 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
     if (WG1_PD == 2) {  // (waits for the u + 2 loads issued at this stage's head)
 #pragma unroll
       for (int it = 0; it < C::NIT; ++it) pv[it] = pv2[it];
+      if constexpr (GNB > 0) {
+#pragma unroll
+        for (int it = 0; it < NG; ++it)
+#pragma unroll
+          for (int o = 0; o < GNB; ++o) dv[it][o] = dv2[it][o];
+      }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __syncthreads();  // next buffer complete; everyone done with this one
@@ -881,11 +922,21 @@ hipError_t launch_wgrad1p(const WgradArgs& a, int splits, hipStream_t s, bool up
     if (splits % 8) return hipErrorInvalidValue;
     prof_kernel("k_wgrad1p<true>");
     hipLaunchKernelGGL(k_wgrad1p<true>, dim3(4 * splits), dim3(256), 0, s, a, npx);
+  } else if (a.head_gnb > 0) {
+    if (a.head_gnb > 4 || !a.hd_dy || !a.hd_wc || a.g_stride != 96 || a.g_off) return hipErrorInvalidValue;
+    prof_kernel("k_wgrad1p<false,gnb>");
+#define DN_GNB(K) hipLaunchKernelGGL((k_wgrad1p<false, K>), dim3(splits), dim3(256), 0, s, a, npx)
+    if (a.head_gnb == 1) DN_GNB(1);
+    else if (a.head_gnb == 2) DN_GNB(2);
+    else if (a.head_gnb == 3) DN_GNB(3);
+    else DN_GNB(4);
+#undef DN_GNB
   } else {
     prof_kernel("k_wgrad1p<false>");
     hipLaunchKernelGGL(k_wgrad1p<false>, dim3(splits), dim3(256), 0, s, a, npx);
   }
   return hipGetLastError();
 }
+
 
 }  // namespace dn
