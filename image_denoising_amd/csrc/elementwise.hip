@@ -145,6 +145,57 @@ __global__ __launch_bounds__(256) void k_subsample(const float* __restrict__ img
   }
 }
 
+// Four cells per thread (cells 4b .. 4b + 3 of one sub-image row share Philox block b: one
+// Philox evaluation instead of four), float4 / uchar4 stores; the same values as k_subsample.
+// Needs w % 4 == 0 and cell_base % 4 == 0 (launch_subsample checks).
+__global__ __launch_bounds__(256) void k_subsample4(const float* __restrict__ img, int N, int C,
+                                                    int H, int W, const uint8_t* __restrict__ rd_in,
+                                                    uint64_t seed, uint64_t offset,
+                                                    uint64_t cell_base, float* __restrict__ sub1,
+                                                    float* __restrict__ sub2,
+                                                    uint8_t* __restrict__ rd_out) {
+  const int h = H >> 1, w = W >> 1;
+  const long quads = (long)N * h * w / 4;
+  for (long qd = (long)blockIdx.x * 256 + threadIdx.x; qd < quads; qd += (long)gridDim.x * 256) {
+    const long cell = 4 * qd;
+    int rd[4];
+    if (rd_in) {
+      const uchar4 r4 = reinterpret_cast<const uchar4*>(rd_in)[qd];
+      rd[0] = r4.x & 7; rd[1] = r4.y & 7; rd[2] = r4.z & 7; rd[3] = r4.w & 7;
+    } else {
+      const uint64_t blk = (cell_base + (uint64_t)cell) >> 2;
+      const U32x4 o = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), (uint32_t)offset,
+                                    (uint32_t)(offset >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) rd[k] = (int)(o.v[k] & 7u);
+    }
+    if (rd_out) reinterpret_cast<uchar4*>(rd_out)[qd] =
+        make_uchar4((uint8_t)rd[0], (uint8_t)rd[1], (uint8_t)rd[2], (uint8_t)rd[3]);
+    const int j = (int)(cell % w);
+    const long t = cell / w;
+    const int i = (int)(t % h);
+    const int n = (int)(t / h);
+    for (int c = 0; c < C; ++c) {
+      const float* p = img + ((long)n * C + c) * H * W + (long)(2 * i) * W + 2 * j;
+      const float4 r0a = *reinterpret_cast<const float4*>(p), r0b = *reinterpret_cast<const float4*>(p + 4);
+      const float4 r1a = *reinterpret_cast<const float4*>(p + W), r1b = *reinterpret_cast<const float4*>(p + W + 4);
+      const float cellv[4][4] = {{r0a.x, r0a.y, r1a.x, r1a.y}, {r0a.z, r0a.w, r1a.z, r1a.w},
+                                 {r0b.x, r0b.y, r1b.x, r1b.y}, {r0b.z, r0b.w, r1b.z, r1b.w}};
+      float4 o1, o2;
+      float* a1 = &o1.x;
+      float* a2 = &o2.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a1[k] = cellv[k][kPairA[rd[k]]];
+        a2[k] = cellv[k][kPairB[rd[k]]];
+      }
+      const long o = (((long)n * C + c) * h + i) * w + j;
+      *reinterpret_cast<float4*>(sub1 + o) = o1;
+      *reinterpret_cast<float4*>(sub2 + o) = o2;
+    }
+  }
+}
+
 // generate_mask_pair output format: mask[4*cell + k] (train.py:163-171)
 __global__ __launch_bounds__(256) void k_masks(const uint8_t* __restrict__ rd, int64_t ncells,
                                                uint8_t* __restrict__ m1, uint8_t* __restrict__ m2) {
@@ -196,6 +247,39 @@ __global__ __launch_bounds__(256) void k_noise(const float* __restrict__ clean, 
     const float z = philox_normal(seed, offset, elem_base + (uint64_t)e);
     const float s = std_img ? std_img[e / per_image] : std_;
     noisy[e] = clean[e] + s * z;
+  }
+}
+
+// Four elements per thread (elements 4b .. 4b + 3 are Philox block b's two Box-Muller pairs):
+// one Philox evaluation and two logs / square roots instead of four, float4 loads and stores;
+// the same values as k_noise (philox_normal's operations, sinf / cosf separately).  Needs
+// per_image % 4 == 0, elem_base % 4 == 0 and 16-B aligned buffers (launch_noise checks).
+__global__ __launch_bounds__(256) void k_noise4(const float* __restrict__ clean, int N,
+                                                int64_t per_image, float std_,
+                                                const float* __restrict__ std_img, uint64_t seed,
+                                                uint64_t offset, uint64_t elem_base,
+                                                float* __restrict__ noisy) {
+  const long quads = (long)N * per_image / 4;
+  for (long qd = (long)blockIdx.x * 256 + threadIdx.x; qd < quads; qd += (long)gridDim.x * 256) {
+    const long e = 4 * qd;
+    const uint64_t blk = (elem_base + (uint64_t)e) >> 2;
+    const U32x4 o = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), (uint32_t)offset,
+                                  (uint32_t)(offset >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+    float z[4];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const uint32_t a = o.v[2 * p], b = o.v[2 * p + 1];
+      const float u1 = ((float)(a >> 8) + 1.0f) * (1.0f / 16777216.0f);
+      const float u2 = (float)(b >> 8) * (1.0f / 16777216.0f);
+      const float r = sqrtf(-2.0f * logf(u1));
+      const float th = 6.283185307179586f * u2;
+      z[2 * p] = r * cosf(th);
+      z[2 * p + 1] = r * sinf(th);
+    }
+    const float sd = std_img ? std_img[e / per_image] : std_;
+    const float4 c4 = reinterpret_cast<const float4*>(clean)[qd];
+    reinterpret_cast<float4*>(noisy)[qd] =
+        make_float4(c4.x + sd * z[0], c4.y + sd * z[1], c4.z + sd * z[2], c4.w + sd * z[3]);
   }
 }
 
@@ -444,8 +528,16 @@ hipError_t launch_subsample(const float* img, int N, int C, int H, int W, const 
                             uint64_t seed, uint64_t offset, uint64_t cell_base, float* sub1,
                             float* sub2, uint8_t* rd_out, hipStream_t s) {
   const long cells = (long)N * (H / 2) * (W / 2);
-  hipLaunchKernelGGL(k_subsample, dim3(grid_for(cells, 256, 65536)), dim3(256), 0, s, img, N, C,
-                     H, W, rd_in, seed, offset, cell_base, sub1, sub2, rd_out);
+  const bool v4 = (W / 2) % 4 == 0 && cell_base % 4 == 0 && W % 4 == 0 &&
+                  ((reinterpret_cast<uintptr_t>(img) | reinterpret_cast<uintptr_t>(sub1) |
+                    reinterpret_cast<uintptr_t>(sub2) | reinterpret_cast<uintptr_t>(rd_in) |
+                    reinterpret_cast<uintptr_t>(rd_out)) & 15) == 0;
+  if (v4)
+    hipLaunchKernelGGL(k_subsample4, dim3(grid_for(cells / 4, 256, 65536)), dim3(256), 0, s, img,
+                       N, C, H, W, rd_in, seed, offset, cell_base, sub1, sub2, rd_out);
+  else
+    hipLaunchKernelGGL(k_subsample, dim3(grid_for(cells, 256, 65536)), dim3(256), 0, s, img, N, C,
+                       H, W, rd_in, seed, offset, cell_base, sub1, sub2, rd_out);
   return hipGetLastError();
 }
 
@@ -468,8 +560,13 @@ hipError_t launch_noise(const float* clean, int N, int64_t per_image, float std_
                         const float* std_per_image, uint64_t seed, uint64_t offset,
                         uint64_t elem_base, float* noisy, hipStream_t s) {
   const long total = (long)N * per_image;
-  hipLaunchKernelGGL(k_noise, dim3(grid_for(total, 256, 65536)), dim3(256), 0, s, clean, N,
-                     per_image, std_, std_per_image, seed, offset, elem_base, noisy);
+  if (per_image % 4 == 0 && elem_base % 4 == 0 &&
+      ((reinterpret_cast<uintptr_t>(clean) | reinterpret_cast<uintptr_t>(noisy)) & 15) == 0)
+    hipLaunchKernelGGL(k_noise4, dim3(grid_for(total / 4, 256, 65536)), dim3(256), 0, s, clean, N,
+                       per_image, std_, std_per_image, seed, offset, elem_base, noisy);
+  else
+    hipLaunchKernelGGL(k_noise, dim3(grid_for(total, 256, 65536)), dim3(256), 0, s, clean, N,
+                       per_image, std_, std_per_image, seed, offset, elem_base, noisy);
   return hipGetLastError();
 }
 

@@ -1047,6 +1047,10 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                              ws + p.g_a1, s));
     }
   }
+  // the encoder's deep-level reductions (up5, enc_conv6 .. enc_conv2) on the side stream now,
+  // beside enc_conv1's data gradient, so the serial tail of the step (after the last data
+  // gradient) only reduces enc_conv1's and enc_conv0's slabs
+  if (side) DN_TIMED(s2, "reduce", 0, 0, 0, 0, 0, 0, red_flush(rb, s2));
   // enc_conv1 (input a0), enc_conv0 (input x = c1 slice; no data gradient needed)
   DN_TRY(fork());
   DN_TRY(wgrad(W_C3, V(p.g_a1, nf), V(p.a0, nf), N, H(0), Wd(0), nf, nf, G(ENC1), SL(ENC1),
