@@ -755,6 +755,10 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
 struct SideStream {
   hipStream_t st = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  // the slab reductions' own stream (round 6): a flush there overlaps both the data-gradient
+  // chain and the remaining weight gradients instead of delaying the latter on `st`
+  hipStream_t rst = nullptr;
+  hipEvent_t rfork = nullptr, rjoin = nullptr;
 };
 
 // One side stream (and its fork / join events) per host thread and device: keyed on the
@@ -771,7 +775,10 @@ struct SideStreams {
       // (HIP releases a stream / event with work still pending once that work completes)
       (void)hipEventDestroy(ss.fork);
       (void)hipEventDestroy(ss.join);
+      (void)hipEventDestroy(ss.rfork);
+      (void)hipEventDestroy(ss.rjoin);
       (void)hipStreamDestroy(ss.st);
+      (void)hipStreamDestroy(ss.rst);
     }
   }
 };
@@ -788,7 +795,10 @@ static SideStream* side_stream(hipStream_t s) {
     if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
     if (hipStreamCreateWithFlags(&ss.st, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&ss.rst, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ss.rfork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ss.rjoin, hipEventDisableTiming) != hipSuccess)
       ss = SideStream{};
     if (cur != dev) (void)hipSetDevice(cur);
     if (!ss.st) return nullptr;
@@ -874,6 +884,15 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     if (!side) return hipSuccess;
     hipError_t e = hipEventRecord(side->fork, s);
     return e != hipSuccess ? e : hipStreamWaitEvent(side->st, side->fork, 0);
+  };
+  // the queued slab reductions on the reduction stream, behind the weight gradients queued on
+  // the side stream so far (one stream: on s, in order)
+  auto flush_side = [&]() -> hipError_t {
+    if (!side) return red_flush(rb, s);
+    hipError_t e = hipEventRecord(side->rfork, s2);
+    if (e == hipSuccess) e = hipStreamWaitEvent(side->rst, side->rfork, 0);
+    if (e == hipSuccess) e = red_flush(rb, side->rst);
+    return e;
   };
   auto SL = [&](int i) { return ws + p.slab[i]; };
   // 3x3 data gradients: the fp32 kernel or the bf16x6 one
@@ -1010,9 +1029,9 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   // the head's and the decoder's reductions on the side stream now, behind their weight
   // gradients, overlapping the encoder's data gradients
   if (side) {
-    DN_TIMED(s2, "reduce", 0, 0, 0, 0, 0, 0, red_flush(rb, s2));
-    // dprm[tail_begin ..] (dec_conv5a .. nin_c) is final behind this flush on s2
-    if (tail_ready) DN_TRY(hipEventRecord(tail_ready, s2));
+    DN_TIMED(side->rst, "reduce", 0, 0, 0, 0, 0, 0, flush_side());
+    // dprm[tail_begin ..] (dec_conv5a .. nin_c) is final behind this flush
+    if (tail_ready) DN_TRY(hipEventRecord(tail_ready, side->rst));
     tail_ready = nullptr;
   }
   // up5: x = a6 (level 5), dU = g_c5[0:nf]
@@ -1050,20 +1069,25 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
   // the encoder's deep-level reductions (up5, enc_conv6 .. enc_conv2) on the side stream now,
   // beside enc_conv1's data gradient, so the serial tail of the step (after the last data
   // gradient) only reduces enc_conv1's and enc_conv0's slabs
-  if (side) DN_TIMED(s2, "reduce", 0, 0, 0, 0, 0, 0, red_flush(rb, s2));
-  // enc_conv1 (input a0), enc_conv0 (input x = c1 slice; no data gradient needed)
-  DN_TRY(fork());
-  DN_TRY(wgrad(W_C3, V(p.g_a1, nf), V(p.a0, nf), N, H(0), Wd(0), nf, nf, G(ENC1), SL(ENC1),
-               p.splits[ENC1], s2, x6w, Z, &rb));
+  if (side) DN_TIMED(side->rst, "reduce", 0, 0, 0, 0, 0, 0, flush_side());
+  // enc_conv1 (input a0), enc_conv0 (input x = c1 slice; no data gradient needed).  Two
+  // streams: enc_conv1's weight gradient on the main stream behind its data gradient and
+  // enc_conv0's beside it on the side stream, which is still working through the encoder's
+  // weight gradients (both streams end together instead of the side stream alone for ~0.5 ms,
+  // profiles/r6_step_timeline.txt)
   DN_TRY(conv_dgrad(V(p.g_a1, nf), N, H(0), Wd(0), nf, Wt(ENC1), nf, 3, EPI_MASK, V(p.a0, nf),
                     V(p.g_a0, nf), s));
   DN_TRY(fork());
   DN_TIMED(s2, "wgrad3_thin", 2.0 * N * H(0) * Wd(0) * nf * C * 9, C, nf, H(0), Wd(0), N,
            launch_enc0_wgrad(ws + p.g_a0, nf, ws + p.xin, N, C, H(0), Wd(0), SL(ENC0) + 64,
                              p.splits[ENC0], G(ENC0), s2, &rb));
-  if (side) {  // join the weight-gradient branch before the reduction reads the slabs
+  DN_TRY(wgrad(W_C3, V(p.g_a1, nf), V(p.a0, nf), N, H(0), Wd(0), nf, nf, G(ENC1), SL(ENC1),
+               p.splits[ENC1], s, x6w, Z, &rb));
+  if (side) {  // join the weight-gradient and reduction branches before the last reduction
     DN_TRY(hipEventRecord(side->join, s2));
     DN_TRY(hipStreamWaitEvent(s, side->join, 0));
+    DN_TRY(hipEventRecord(side->rjoin, side->rst));
+    DN_TRY(hipStreamWaitEvent(s, side->rjoin, 0));
   }
   DN_TIMED(s, "reduce", 0, 0, 0, 0, 0, 0, red_flush(rb, s));
   if (tail_ready) DN_TRY(hipEventRecord(tail_ready, s));  // one stream: everything is final here
