@@ -87,6 +87,22 @@ __device__ __forceinline__ int w6_vt(int row, int j, int p) {
   return (row * 8 + j) * 4 + (p ^ (row & 3));
 }
 
+// transform item e -> (channel quad c4, Winograd tile j, input row).  C4 = 4 (the 16-channel
+// tail chunk): a 16-lane group of the 8-B V writes covers two rows x two tiles x four quads
+// (c4 = e & 3, j = 2 (e >> 4 & 3) + (e >> 2 & 1), row = 2 (e >> 6) + (e >> 3 & 1)), so the row
+// bit of w6_vq's swizzle separates what the tile pairs j, j + 2 of one row put on the same banks
+// (the one-row order c4 + 4 j was 2-way); otherwise c4 fastest, then j, then row.
+template <int C4>
+__device__ __forceinline__ void w6_item(int e, int& c4, int& j, int& row) {
+  if constexpr (C4 == 4) {
+    c4 = e & 3;
+    j = 2 * ((e >> 4) & 3) + ((e >> 2) & 1);
+    row = 2 * (e >> 6) + ((e >> 3) & 1);
+  } else {
+    c4 = e % C4; j = (e / C4) & 7; row = e / (8 * C4);
+  }
+}
+
 __device__ __forceinline__ void w6_barrier() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   __builtin_amdgcn_s_barrier();
@@ -179,7 +195,8 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
 #pragma unroll
     for (int it = ig; it < ig + W6_TG && it < VIT; ++it) {
       const int e = tid + it * C::WAVES * 64;
-      const int c4 = e % C4, j = (e / C4) & 7, row = e / (8 * C4);
+      int c4, j, row;
+      w6_item<C4>(e, c4, j, row);
       const int gy = iy0 + row, k = k0 + 4 * c4;
       const bool rok = e < NIT && gy >= 0 && gy < a.IHt && k < a.K;
 #pragma unroll
@@ -200,7 +217,8 @@ __global__ __launch_bounds__(256, 2) void k_c3w6(FwdArgs a) {
     for (int it = ig; it < ig + W6_TG && it < VIT; ++it) {
       const int e = tid + it * C::WAVES * 64;
       if (e < NIT) {
-        const int c4 = e % C4, j = (e / C4) & 7, row = e / (8 * C4);
+        int c4, j, row;
+        w6_item<C4>(e, c4, j, row);
         f32x4 v[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
