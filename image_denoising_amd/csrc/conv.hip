@@ -1476,6 +1476,11 @@ hipError_t launch_wgrad1(int mode, const WgradArgs& a0, float* dwb, hipStream_t 
     e = hipGetLastError();
   }
   if (e != hipSuccess) return e;
+  if (!up2 && a.hd_slab_c) {  // nin_c's weight gradient formed by the same launch (k_wgrad1p GNB)
+    const long rc = (long)a.head_gnb * 96 + a.head_gnb;
+    e = launch_reduce(a.hd_slab_c, rc, sp, rc, a.hd_dwc, s, rb);
+    if (e != hipSuccess) return e;
+  }
   if (!up2) return launch_reduce(a.slab, row, sp, row, dwb, s, rb);
   // W[ci][co][a][b] in output order: element e = 4 (ci*Cout + co) + ab lives in parity ab's
   // block of sp rows

@@ -157,6 +157,9 @@ struct WgradArgs {
   // k_wgrad1p of nin_b with the gradient operand recomputed (head_gnb > 0 = nin_c's outputs):
   // g = leaky'(nb) (Wc^T dy) per pixel, with g pointing at nb (k_head_bwd_x6's order and result)
   int head_gnb; const float* hd_dy; int hd_dy_stride; const float* hd_wc;
+  // (head_gnb) nin_c's weight gradient from the same nb / dy reads: one slab row per workgroup,
+  // [oc][96] then the bias [oc] (k_wgrad_thin's layout), or null
+  float* hd_slab_c; float* hd_dwc;  // (and its reduction's destination: nin_c's [W | b])
 };
 
 // strided NHWC view: element (pixel, c) at p[pixel * stride + off + c]
@@ -323,6 +326,7 @@ bool wgrad1p_ok(const WgradArgs& a);  // 96 -> 96 1x1 on k_wgrad1p (bf16x6)
 hipError_t launch_wgrad1p(const WgradArgs& a, int splits, hipStream_t s, bool up2 = false);
 bool wgrad1_ok(int mode, const WgradArgs& a);
 long wgrad_slab_floats(int mode, int N, int KH, int KW, int cin, int cout);
+int wgrad1_splits(int mode, int N, int KH, int KW);  // k_wgrad1 / k_wgrad1p split count
 hipError_t launch_wgrad1(int mode, const WgradArgs& a, float* dwb, hipStream_t s,
                          RedBatch* rb = nullptr, bool x6 = false);
 hipError_t launch_reduce_scatter(const float* slab, long slab_stride, int splits, long n,

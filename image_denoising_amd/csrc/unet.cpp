@@ -236,6 +236,11 @@ bool build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, Plan& p, st
       long need = (i == ENC0 || i == D1A || (i == NINC && p.OC <= 4))
                       ? (long)sp * (L.wcount + L.cout)
                       : wgrad_slab_floats(mode, N, KH, KW, L.cin, L.cout);
+      // (nin_c: also the rows nin_b's k_wgrad1p<., GNB> writes its weight gradient into)
+      if (i == NINC && p.OC <= 4) {
+        const long s1 = wgrad1_splits(W_C1, N, KH, KW);
+        if (s1 * (L.wcount + L.cout) > need) need = s1 * (L.wcount + L.cout);
+      }
       if (i == D1A) need += (long)enc0_wgrad_splits(N, KH, KW) * 96 * p.C * 9;  // input slice
       p.slab[i] = alloc_f(64 + need);
       p.slab_floats += 64 + need;
@@ -371,9 +376,10 @@ hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const flo
 hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, int cout, int cin,
                  float* dwb, float* slab, int splits, hipStream_t s, bool x6, const float* zeros,
                  RedBatch* rb, int head_gnb, const float* hd_dy, int hd_dy_stride,
-                 const float* hd_wc) {
+                 const float* hd_wc, float* hd_slab_c, float* hd_dwc) {
   WgradArgs a{};
   a.head_gnb = head_gnb; a.hd_dy = hd_dy; a.hd_dy_stride = hd_dy_stride; a.hd_wc = hd_wc;
+  a.hd_slab_c = hd_slab_c; a.hd_dwc = hd_dwc;
   a.g = g.p; a.g_stride = g.stride; a.g_off = g.off;
   a.x = x.p; a.x_stride = x.stride; a.x_off = x.off;
   a.N = N; a.KH = KH; a.KW = KW; a.Cout = cout; a.Cin = cin;
@@ -942,19 +948,24 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
     DN_TIMED(s, "head_bwd", 2.0 * h.npx * 96 * (2 * 96 + OC), OC, 96, H(0), Wd(0), N,
              head_bwd_x6 ? launch_head_bwd_x6(h, ws + p.packHB, s) : launch_head_bwd(h, s));
   }
+  const bool fold_c = head_gnb && OC == 1;  // nin_c's weight gradient inside nin_b's (k_wgrad1p)
+  if (!fold_c) {
+    DN_TRY(fork());
+    if (OC <= 4)
+      DN_TIMED(s2, "wgrad1", 2.0 * N * H(0) * Wd(0) * 96 * OC, 96, OC, H(0), Wd(0), N,
+               launch_wgrad_thin(dyv.p, dyv.stride, OC, ws + p.nb, (long)N * H(0) * Wd(0),
+                               SL(NINC) + 64, p.splits[NINC], G(NINC), s2, &rb));
+    else
+      DN_TRY(wgrad(W_C1, dyv, V(p.nb, 96), N, H(0), Wd(0), OC, 96, G(NINC), SL(NINC),
+                   p.splits[NINC], s2, false, Z, &rb));
+  }
   DN_TRY(fork());
-  if (OC <= 4)
-    DN_TIMED(s2, "wgrad1", 2.0 * N * H(0) * Wd(0) * 96 * OC, 96, OC, H(0), Wd(0), N,
-             launch_wgrad_thin(dyv.p, dyv.stride, OC, ws + p.nb, (long)N * H(0) * Wd(0),
-                             SL(NINC) + 64, p.splits[NINC], G(NINC), s2, &rb));
-  else
-    DN_TRY(wgrad(W_C1, dyv, V(p.nb, 96), N, H(0), Wd(0), OC, 96, G(NINC), SL(NINC),
-                 p.splits[NINC], s2, false, Z, &rb));
-  DN_TRY(fork());
-  // (head_gnb: the gradient operand g_nb recomputed from nb and dy inside k_wgrad1p)
+  // (head_gnb: the gradient operand g_nb recomputed from nb and dy inside k_wgrad1p, which also
+  // forms nin_c's weight gradient from those reads into nin_c's slab)
   DN_TRY(wgrad(W_C1, head_gnb ? V(p.nb, 96) : V(p.g_nb, 96), V(p.na, 96), N, H(0), Wd(0), 96, 96,
                G(NINB), SL(NINB), p.splits[NINB], s2, x6, Z, &rb,
-               head_gnb ? OC : 0, dyv.p, dyv.stride, prm + p.P.L[NINC].woff));
+               head_gnb ? OC : 0, dyv.p, dyv.stride, prm + p.P.L[NINC].woff,
+               fold_c ? SL(NINC) + 64 : nullptr, G(NINC)));
   DN_TRY(fork());
   DN_TRY(wgrad(W_C1, V(p.g_na, 96), V(p.d1b, 96), N, H(0), Wd(0), 96, 96, G(NINA), SL(NINA),
                p.splits[NINA], s2, x6, Z, &rb));

@@ -120,6 +120,7 @@ hipError_t deconv_dgrad(const View& dy, int N, int h, int w, int cout, const flo
 hipError_t wgrad(int mode, const View& g, const View& x, int N, int KH, int KW, int cout, int cin,
                  float* dwb, float* slab, int splits, hipStream_t s, bool x6 = false,
                  const float* zeros = nullptr, RedBatch* rb = nullptr, int head_gnb = 0,
-                 const float* hd_dy = nullptr, int hd_dy_stride = 0, const float* hd_wc = nullptr);
+                 const float* hd_dy = nullptr, int hd_dy_stride = 0, const float* hd_wc = nullptr,
+                 float* hd_slab_c = nullptr, float* hd_dwc = nullptr);
 
 }  // namespace dn

@@ -705,6 +705,10 @@ constexpr int WG1_PD = DN_WG1_PD;
 // GNB > 0 (nin_b's weight gradient, GNB = nin_c's outputs): the gradient operand is recomputed
 // from the nin_b activation (a.g) and dL/dy as g = leaky'(nb) (Wc^T dy) -- k_head_bwd_x6's
 // fmaf order, the same values -- so the data-gradient pass does not store g_nb (384 B per pixel).
+// With a.hd_slab_c it also forms nin_c's weight gradient dWc[o][c] = sum dy[o] nb[c] and
+// dbc[o] = sum dy[o] from the same registers (per-thread sums of its three channel quads, then
+// a fixed-order sum over the workgroup's threads): the separate k_wgrad_thin pass and its
+// 388 B per pixel of reads go away.
 template <bool UP2, int GNB = 0>
 __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
   using C = Wp1Cfg;
@@ -746,6 +750,17 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
   constexpr int GO = GNB > 0 ? GNB : 1;
   float dv[NG][GO], dv2[WG1_PD == 2 ? NG : 1][GO];  // (GNB) dy of the G items' pixels
   f32x4 wcr[NG][GO];                                   // (GNB) Wc[o][c .. c + 3] of the G items
+  // (the nin_c fold for one nin_c output only -- the N2N head of C = 1: more outputs' partial
+  // sums do not fit beside the operands, and k_wgrad_thin keeps them)
+  constexpr bool FOLDC = GNB == 1;
+  f32x4 gwc[NG][GO];                                   // (FOLDC) dWc partial sums of the G items
+  float gbc[GO];                                       // (FOLDC) dbc partial sums (quad 0 items)
+#pragma unroll
+  for (int o = 0; o < GO; ++o) {
+    gbc[o] = 0.f;
+#pragma unroll
+    for (int it = 0; it < NG; ++it) gwc[it][o] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   if constexpr (GNB > 0) {
 #pragma unroll
     for (int it = 0; it < NG; ++it)
@@ -794,9 +809,14 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
         if (it < NG) {  // g_nb = leaky'(nb) (Wc^T dy)
           f32x4 t = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int oo = 0; oo < GNB; ++oo)
+          for (int oo = 0; oo < GNB; ++oo) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) t[e] = fmaf(wcr[it][oo][e], dv[it][oo], t[e]);
+            for (int e = 0; e < 4; ++e) {
+              t[e] = fmaf(wcr[it][oo][e], dv[it][oo], t[e]);
+              if (FOLDC) gwc[it][oo][e] = fmaf(dv[it][oo], pv[it][e], gwc[it][oo][e]);  // dWc
+            }
+            if (FOLDC && ioff[it] - ipx[it] * a.g_stride == 0) gbc[oo] += dv[it][oo];  // dbc
+          }
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = pv[it][e] > 0.f ? t[e] : t[e] * 0.2f;
         }
@@ -902,6 +922,38 @@ __global__ __launch_bounds__(256, 2) void k_wgrad1p(WgradArgs a, long npx) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) slab[C::C * C::C + (3 * wm + i) * 16 + 4 * lg + r] = accb[i][0][r];
   }
+  if constexpr (FOLDC) {
+    if (a.hd_slab_c) {
+      // item it of thread t holds channel quad (t + 16 it) % 24 (q = t + 256 it, 256 = 10 x 24 +
+      // 16); every thread's partials into LDS (the stage buffers are free after the loop's last
+      // barrier), then output (o, c) sums the (it, t) whose quad is c / 4, it-major, t ascending
+      float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+      for (int it = 0; it < NG; ++it)
+#pragma unroll
+        for (int o = 0; o < GNB; ++o)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) red[((it * C::NTHR + tid) * GNB + o) * 4 + e] = gwc[it][o][e];
+      float* redb = red + NG * C::NTHR * GNB * 4;
+#pragma unroll
+      for (int o = 0; o < GNB; ++o) redb[tid * GNB + o] = gbc[o];
+      __syncthreads();
+      float* slc = a.hd_slab_c + (long)blockIdx.x * (GNB * 96 + GNB);
+      for (int oc = tid; oc < GNB * 96 + GNB; oc += C::NTHR) {
+        float sum = 0.f;
+        if (oc < GNB * 96) {
+          const int o = oc / 96, c = oc % 96, k = c >> 2, e = c & 3;
+          for (int it = 0; it < NG; ++it)  // the threads t = k - 16 it (mod 24), ascending
+            for (int t = (k + 48 - 16 * it) % 24; t < C::NTHR; t += 24)
+              sum += red[((it * C::NTHR + t) * GNB + o) * 4 + e];
+        } else {
+          const int o = oc - GNB * 96;
+          for (int t = 0; t < C::NTHR; ++t) sum += redb[t * GNB + o];
+        }
+        slc[oc] = sum;
+      }
+    }
+  }
 }
 
 // 96 -> 96 1x1, NHWC views with 16-byte aligned pixels (g / x stride and offset % 4 == 0)
@@ -923,7 +975,9 @@ hipError_t launch_wgrad1p(const WgradArgs& a, int splits, hipStream_t s, bool up
     prof_kernel("k_wgrad1p<true>");
     hipLaunchKernelGGL(k_wgrad1p<true>, dim3(4 * splits), dim3(256), 0, s, a, npx);
   } else if (a.head_gnb > 0) {
-    if (a.head_gnb > 4 || !a.hd_dy || !a.hd_wc || a.g_stride != 96 || a.g_off) return hipErrorInvalidValue;
+    if (a.head_gnb > 4 || !a.hd_dy || !a.hd_wc || a.g_stride != 96 || a.g_off ||
+        (a.hd_slab_c && a.head_gnb != 1))  // (the nin_c fold: one output only)
+      return hipErrorInvalidValue;
     prof_kernel("k_wgrad1p<false,gnb>");
 #define DN_GNB(K) hipLaunchKernelGGL((k_wgrad1p<false, K>), dim3(splits), dim3(256), 0, s, a, npx)
     if (a.head_gnb == 1) DN_GNB(1);
