@@ -602,6 +602,13 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     }
   }
   if (pack == PACK_ONLY) return DN_OK;
+  // the pair pass's cell lists first: they depend on the pair choices only, and built here they
+  // run beside the other stream's work instead of alone right before the pair pass (~20 us of a
+  // step in which nothing else ran, profiles/r6_step_timeline.txt)
+  if (w6_sel)
+    DN_TIMED(s, "sel_lists", 0, 0, 0, 0, 0, 0,
+             launch_w6s_lists(sel_rd, N, H(0), Wd(0), reinterpret_cast<unsigned*>(ws + p.w6s_list),
+                              reinterpret_cast<int*>(ws + p.w6s_cnt), s));
   // enc_conv0, fused with pool0 = x -> channels [2nf, 2nf+C) of the up1 concat buffer
   DN_TIMED(s, "enc0", 2.0 * N * p.H * p.W * C * nf * 9, C, nf, p.H, p.W, N,
            launch_enc0_fwd(x, N, C, p.H, p.W, prm + p.P.L[ENC0].woff, Bs(ENC0), ws + p.a0,
@@ -691,7 +698,6 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
     if (w6_sel) {  // the cells listed per tile orientation, then the Winograd pass over them
       unsigned* list = reinterpret_cast<unsigned*>(ws + p.w6s_list);
       int* cnt = reinterpret_cast<int*>(ws + p.w6s_cnt);
-      DN_TIMED(s, "sel_lists", 0, 0, 0, 0, 0, 0, launch_w6s_lists(sel_rd, N, H(0), Wd(0), list, cnt, s));
       DN_TIMED(s, "fwd3sel", 2.0 * N * (H(0) / 2) * Wd(0) * 96 * 96 * 9, 96, 96, H(0) / 2, Wd(0), N,
                launch_fwd_w6s(a, list, cnt, ws + p.packXV, s));
     } else {
