@@ -1401,7 +1401,7 @@ hipError_t pack_flush(PackBatch& b, hipStream_t s) {
   if (b.n == 0) return hipSuccess;
   long blocks = 1;
   for (int i = 0; i < b.n; ++i) blocks = std::max(blocks, (pack_job_elems(b.j[i]) + 255) / 256);
-  hipLaunchKernelGGL(k_pack_batch, dim3((unsigned)std::min(blocks, 128L), (unsigned)b.n), dim3(256),
+  hipLaunchKernelGGL(k_pack_batch, dim3((unsigned)std::min(blocks, 1024L), (unsigned)b.n), dim3(256),
                      0, s, b);
   b.n = 0;
   return hipGetLastError();

@@ -361,7 +361,8 @@ bool iunet_build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, IPlan
       b.dz2 = alloc(l, ch);
       b.dg1 = alloc(l, ch);
       b.dz1 = alloc(l, ch);
-      b.dzj = alloc(l, GROWTH);
+      for (int j = 0; j < 4; ++j) b.dzj[j] = alloc(l, GROWTH);
+      b.dzf = alloc(l, ch);
     };
     for (int i = 0; i < 4; ++i) gblock(p.dl[i], i, 48 << i);
     gblock(p.bb, 4, 384);
@@ -373,9 +374,11 @@ bool iunet_build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, IPlan
     }
     p.dxb = alloc(4, 384);
     p.dzfin = alloc(0, 4);
-    p.dps = alloc(1, 4 * 24);   // largest unshuffled PixelShuffle gradient: up3 at H/2, 96 ch
+    for (int k = 0; k < 4; ++k)  // unshuffled PixelShuffle gradient of up block k (4 x out ch)
+      p.dps[k] = alloc(4 - k, 4 * P.up[k].out);
     p.dpool = alloc(1, 48);     // largest pooled-input gradient: level 1 (48 ch at H/2)
-    p.dza = alloc(0, 48);       // level-conv pre-activation gradient (level 0 is the largest)
+    for (int i = 0; i < 4; ++i)  // level-conv pre-activation gradients
+      p.dza[i] = alloc(i, 48 << i);
     p.dsg = alloc(0, 4);
     p.dh = alloc(0, 48);
     p.ca = allocf((long)N * 384);
@@ -497,6 +500,9 @@ struct Ctx {
   float* ws;
   hipStream_t s;
   int prec;
+  // backward: the weight gradients' stream (s when running on one stream) and its fork event
+  hipStream_t s2 = nullptr;
+  hipEvent_t fork = nullptr;
   View V(long o, int stride, int off = 0) const { return View{ws + o, stride, off}; }
   const float* Wt(const IConv& c) const { return prm + c.w; }
   const float* Bs(const IConv& c) const { return c.b >= 0 ? prm + c.b : nullptr; }
@@ -632,7 +638,13 @@ namespace {
 // dW (+ db) of a conv from g = dL/d(conv output) and its input x; written into dprm
 dn_status wgrad_g(const Ctx& c, float* dprm, int mode, const IConv& L, const View& g, const View& x,
                   int h, int w) {
-  OpScope prof(c.s, "wgrad", L.cout, L.cin, L.k, h, w, c.p.N, 1.0);
+  // on the side stream, behind the main stream's work so far (g is its latest output)
+  const hipStream_t s2 = c.s2 ? c.s2 : c.s;
+  if (s2 != c.s) {
+    IU_TRY(hipEventRecord(c.fork, c.s));
+    IU_TRY(hipStreamWaitEvent(s2, c.fork, 0));
+  }
+  OpScope prof(s2, "wgrad", L.cout, L.cin, L.k, h, w, c.p.N, 1.0);
   const int taps = mode == W_C3 ? 9 : 1;
   const bool bias = L.b >= 0;
   if (bias && L.b != L.w + (long)L.cout * L.cin * taps) {
@@ -652,15 +664,15 @@ dn_status wgrad_g(const Ctx& c, float* dprm, int mode, const IConv& L, const Vie
   a.zeros = slab; a.slab = slab + 64; a.slab_stride = n;
   a.wlayout = 0; a.cin_total = L.cin; a.ci_base = 0; a.bias = bias ? 1 : 0;
   int sp = gwgrad_splits(mode, c.p.N, h, w, L.cin, L.cout);
-  IU_TRY(hipMemsetAsync(slab, 0, 64 * sizeof(float), c.s));
+  IU_TRY(hipMemsetAsync(slab, 0, 64 * sizeof(float), s2));
   // fp32_x6: the 3x3 weight gradients on the bf16x6 kernel too
   if (c.prec == DN_PREC_FP32_X6 && mode == W_C3 && gwgrad_x6_ok(a)) {
     sp = gwgrad_x6_splits(a, sp);
-    IU_TRY(launch_gwgrad_x6(a, sp, c.s));
+    IU_TRY(launch_gwgrad_x6(a, sp, s2));
   } else {
-    IU_TRY(launch_gwgrad(mode, a, sp, c.s));
+    IU_TRY(launch_gwgrad(mode, a, sp, s2));
   }
-  IU_TRY(launch_reduce(slab + 64, n, sp, n, dprm + L.w, c.s));
+  IU_TRY(launch_reduce(slab + 64, n, sp, n, dprm + L.w, s2));
   return DN_OK;
 }
 
@@ -723,10 +735,10 @@ dn_status rdb_bwd(const Ctx& c, float* dprm, const IRdb& R, const IBlockBufs& b,
   IU_TRY(launch_vadd(c.V(b.dF, FS), dr, npx, C, c.s));  // out = x + lff(...)
   for (int j = 3; j >= 0; --j) {
     const int o = C + GROWTH * j;
-    IU_TRY(launch_vmask(c.V(b.dzj, GROWTH), c.V(b.dF, FS, o), c.V(b.F, FS, o), npx, GROWTH, c.s));
-    if (dn_status st = wgrad_g(c, dprm, W_C3, R.conv[j], c.V(b.dzj, GROWTH), c.V(b.F, FS), h, w))
-      return st;
-    if (dn_status st = dgrad_g(c, R.conv[j], c.V(b.dzj, GROWTH), h, w, o, EPI_ACCUM, kNone,
+    const View dzj = c.V(b.dzj[j], GROWTH);
+    IU_TRY(launch_vmask(dzj, c.V(b.dF, FS, o), c.V(b.F, FS, o), npx, GROWTH, c.s));
+    if (dn_status st = wgrad_g(c, dprm, W_C3, R.conv[j], dzj, c.V(b.F, FS), h, w)) return st;
+    if (dn_status st = dgrad_g(c, R.conv[j], dzj, h, w, o, EPI_ACCUM, kNone,
                                c.V(b.dF, FS)))
       return st;
   }
@@ -739,7 +751,21 @@ dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, floa
                          hipStream_t s, int prec) {
   const StreamDeviceGuard device_guard(s);
   if (prec != DN_PREC_FP32 && prec != DN_PREC_FP32_X6) return DN_ERR_ARG;
-  const Ctx c{p, prm, ws, s, prec};
+  // The weight gradients (and their slab reductions) run on a side stream beside the
+  // data-gradient chain (DN_BWD_STREAMS=0 or per-op profiling: one stream).  Each is forked after
+  // the launch that produced its output gradient; every buffer one reads (the forward's
+  // activations, dz2 / dz1 / dr / dzf of a block, dzj[j], dps[k], dza[i], dzfin, dsg, dh once
+  // written) is not rewritten later in the pass, and only they use the slab.  Joined at the end.
+  static const bool two_env = !getenv("DN_BWD_STREAMS") || atoi(getenv("DN_BWD_STREAMS")) != 0;
+  SideStream* side = two_env && !prof_on() && !g_prof.on ? side_stream(s) : nullptr;
+  Ctx c{p, prm, ws, s, prec};
+  if (side) { c.s2 = side->st; c.fork = side->fork; }
+  const hipStream_t s2 = side ? side->st : s;
+  auto fork = [&]() -> hipError_t {
+    if (!side) return hipSuccess;
+    hipError_t e = hipEventRecord(side->fork, s);
+    return e != hipSuccess ? e : hipStreamWaitEvent(s2, side->fork, 0);
+  };
   const IParams& P = p.P;
   const int N = p.N, H = p.H, W = p.W, C = P.C, OC = P.OC;
   const long HW = (long)H * W;
@@ -759,15 +785,15 @@ dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, floa
     const IBlockBufs& b = p.ul[k];
     if (dn_status st = res_bwd(c, dprm, u.res, b, dcur, h, w)) return st;
     if (dn_status st = rdb_bwd(c, dprm, u.rdb, b, h, w)) return st;
-    // f = leaky(fuse(cc)): dz = dF[:, :out] * leaky'(f)  (into dzj-sized scratch: out <= 192)
-    const View dzf = c.V(b.dz1, out);
+    // f = leaky(fuse(cc)): dz = dF[:, :out] * leaky'(f)
+    const View dzf = c.V(b.dzf, out);
     IU_TRY(launch_vmask(dzf, c.V(b.dF, FS), c.V(b.F, FS), (long)N * h * w, out, s));
     if (dn_status st = wgrad_g(c, dprm, W_C3, u.fuse, dzf, c.V(p.cc[k], 3 * out), h, w)) return st;
     if (dn_status st = dgrad_g(c, u.fuse, dzf, h, w, 3 * out, EPI_PLAIN, kNone,
                                c.V(p.dcc[k], 3 * out)))
       return st;
     // PixelShuffle backward, then conv_ps (input: bottle output or the previous up block)
-    float* gps = ws + p.dps;
+    float* gps = ws + p.dps[k];
     IU_TRY(launch_unshuffle(c.V(p.dcc[k], 3 * out), N, h / 2, w / 2, out, gps, s));
     const View xin = k == 0 ? c.V(p.xb, 384) : c.V(p.xu[k - 1], u.in);
     if (dn_status st = wgrad_g(c, dprm, W_C3, u.ps, View{gps, 4 * out, 0}, xin, h / 2, w / 2))
@@ -793,7 +819,7 @@ dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, floa
     IU_TRY(launch_vpool_bwd_acc(skip, N, h, w, nf, dpooled, dskip, s));
     if (dn_status st = res_bwd(c, dprm, L.res, b, dskip, h, w)) return st;
     if (dn_status st = rdb_bwd(c, dprm, L.rdb, b, h, w)) return st;
-    const View dza = c.V(p.dza, nf);
+    const View dza = c.V(p.dza[i], nf);
     IU_TRY(launch_vmask(dza, c.V(b.dF, FS), c.V(b.F, FS), (long)N * h * w, nf, s));
     if (i > 0) {
       const View xi = c.V(p.pool[i], L.conv.cin);
@@ -808,11 +834,12 @@ dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, floa
       float* slab = ws + p.slab;
       const long n = 48L * (C + 1) * 9 + 48;
       const int st = enc0_wgrad_splits(N, H, W);
-      IU_TRY(launch_wgrad_c3_thin(ws + p.dza, 48, ws + p.xin, N, C, H, W, slab, n, C + 1, 0, 1, st,
-                                  s));
-      IU_TRY(launch_wgrad_c3_thin(ws + p.dza, 48, ws + p.sig, N, 1, H, W, slab, n, C + 1, C, 0, st,
-                                  s));
-      IU_TRY(launch_reduce(slab, n, st, n, dprm + L.conv.w, s));
+      IU_TRY(fork());
+      IU_TRY(launch_wgrad_c3_thin(ws + p.dza[0], 48, ws + p.xin, N, C, H, W, slab, n, C + 1, 0, 1, st,
+                                  s2));
+      IU_TRY(launch_wgrad_c3_thin(ws + p.dza[0], 48, ws + p.sig, N, 1, H, W, slab, n, C + 1, C, 0, st,
+                                  s2));
+      IU_TRY(launch_reduce(slab, n, st, n, dprm + L.conv.w, s2));
       // d sigma (channel C of x0) through the sigmoid: flipped weight column ci = C
       WView fv{};
       fv.w = prm + L.conv.w; fv.off = (long)C * 9; fv.sN = 9; fv.sK = (long)(C + 1) * 9;
@@ -830,8 +857,13 @@ dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, floa
     float* slab = ws + p.slab;
     const long n = 48L * C * 9 + 48;
     const int st = enc0_wgrad_splits(N, H, W);
-    IU_TRY(launch_wgrad_c3_thin(ws + p.dh, 48, ws + p.xin, N, C, H, W, slab, n, C, 0, 1, st, s));
-    IU_TRY(launch_reduce(slab, n, st, n, dprm + P.ne0.w, s));
+    IU_TRY(fork());
+    IU_TRY(launch_wgrad_c3_thin(ws + p.dh, 48, ws + p.xin, N, C, H, W, slab, n, C, 0, 1, st, s2));
+    IU_TRY(launch_reduce(slab, n, st, n, dprm + P.ne0.w, s2));
+  }
+  if (side) {  // the caller's stream continues after every weight gradient
+    IU_TRY(hipEventRecord(side->join, s2));
+    IU_TRY(hipStreamWaitEvent(s, side->join, 0));
   }
   g_prof.flush("iunet backward");
   return DN_OK;

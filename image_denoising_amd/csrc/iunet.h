@@ -33,7 +33,9 @@ struct IBlockBufs {
   long z1 = 0, a1 = 0, z2 = 0;  // ResBlock conv1 out, leaky(GN1), conv2 out
   long st1 = 0, st2 = 0;        // GN stats (mean, rstd) per (n, group)
   // gradients
-  long dF = 0, dr = 0, dz2 = 0, dg1 = 0, dz1 = 0, dzj = 0;
+  // (dzj per growth conv, dzf = the up block's fuse-conv gradient: the weight gradients read
+  // them on the side stream while the data-gradient chain goes on)
+  long dF = 0, dr = 0, dz2 = 0, dg1 = 0, dz1 = 0, dzj[4] = {0, 0, 0, 0}, dzf = 0;
 };
 
 struct IPlan {
@@ -52,8 +54,8 @@ struct IPlan {
   long gpart = 0;                     // GN partial sums (doubles)
   long pack = 0, pack_floats = 0;     // packed weight scratch (one layer at a time)
   // gradients
-  long dzfin = 0, dcc[4] = {0, 0, 0, 0}, dps = 0, dxu[3] = {0, 0, 0}, dxb = 0, dpool = 0;
-  long dza = 0, dsg = 0, dh = 0, ca = 0, cb = 0, ccf = 0;
+  long dzfin = 0, dcc[4] = {0, 0, 0, 0}, dps[4] = {0, 0, 0, 0}, dxu[3] = {0, 0, 0}, dxb = 0, dpool = 0;
+  long dza[4] = {0, 0, 0, 0}, dsg = 0, dh = 0, ca = 0, cb = 0, ccf = 0;
   long slab = 0, slab_floats = 0;
   long total_floats = 0;
 };

@@ -763,16 +763,8 @@ dn_status unet_forward(const Plan& p, const float* prm, const float* x, float* y
 // (the accumulations into a concat gradient's skip slice touch channels no weight gradient
 // reads) and write their own slabs, so they overlap the data-gradient chain; each is forked
 // from the main stream after the kernel that produced its gradient, and the branch is joined
-// before the batched reduction.
-struct SideStream {
-  hipStream_t st = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  // the slab reductions' own stream (round 6): a flush there overlaps both the data-gradient
-  // chain and the remaining weight gradients instead of delaying the latter on `st`
-  hipStream_t rst = nullptr;
-  hipEvent_t rfork = nullptr, rjoin = nullptr;
-};
-
+// before the batched reduction.  (struct SideStream: unet.h)
+//
 // One side stream (and its fork / join events) per host thread and device: keyed on the
 // device of the caller's stream (not hipGetDevice(), which a caller need not have set to it) and
 // created under a guard for that device; thread-local, so two host threads running backwards on
@@ -795,7 +787,7 @@ struct SideStreams {
   }
 };
 
-static SideStream* side_stream(hipStream_t s) {
+SideStream* side_stream(hipStream_t s) {
   thread_local SideStreams owner;
   std::map<int, SideStream>& per_device = owner.per_device;
   hipDevice_t dev = 0;

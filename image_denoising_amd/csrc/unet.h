@@ -89,6 +89,19 @@ dn_status unet_backward(const Plan& p, const float* prm, const float* dy, float*
                         float* ws, hipStream_t s, int prec = DN_PREC_FP32,
                         hipEvent_t tail_ready = nullptr);
 // first float of the parameter range the backward finishes early (dec_conv5a .. nin_c)
+// The backward's side streams (unet.cpp): weight gradients on `st`, slab reductions on `rst`,
+// with their fork / join events; one set per host thread and device (nullptr when creating them
+// failed: run on one stream).  Shared by the UNet and ImprovedUNet executors.
+struct SideStream {
+  hipStream_t st = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  // the slab reductions' own stream (round 6): a flush there overlaps both the data-gradient
+  // chain and the remaining weight gradients instead of delaying the latter on `st`
+  hipStream_t rst = nullptr;
+  hipEvent_t rfork = nullptr, rjoin = nullptr;
+};
+SideStream* side_stream(hipStream_t s);
+
 long tail_begin(const Plan& p);
 // zc of the bf16x6 data gradient of a 3x3 layer producing nout channels (0: one block)
 int x6_dgrad_zc(int nout);

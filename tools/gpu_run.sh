@@ -5,7 +5,8 @@
 # STEP: tests[:FILES]   pytest -m gpu (all, or comma-separated files)  -> gpurun_out/pytest_gpu.log
 #       bench           default bench line, CPU baseline included      -> gpurun_out/bench.log
 #       quick[:ARGS]    bench line without the CPU baseline ('+'-separated bench args) -> gpurun_out/quick.log
-#       stats:TAG       rocprofv3 --kernel-trace --stats over a 3-step bench -> gpurun_out/prof/TAG
+#       stats:TAG[:ARGS] rocprofv3 --kernel-trace --stats over a 3-step bench ('+'-separated bench
+#                       args) -> gpurun_out/prof/TAG, plus the step timeline
 #       pmc:TAG[:ARGS]  FETCH_SIZE / WRITE_SIZE passes over a 2-step bench -> profiles/TAG_pmc_step.json
 #       stamps:TAG:K+N+H  k_c3x6p stage timeline from a DN_X6_STAMPS build (tools/x6_stamps.py)
 #       sq:NAME:CTRS    one SQ counter pass (<= 8 SQ counters, '+'-separated) over a 2-step bench
@@ -48,11 +49,14 @@ for step in "$@"; do
     quick)
       timeout -k 10 240 python -u bench.py --no-cpu-baseline ${arg//+/ } > gpurun_out/quick.log 2>&1 || fail "$step" $?
       grep '^{' gpurun_out/quick.log | cut -c1-400 ;;
-    stats)
-      rm -rf gpurun_out/prof/$arg; mkdir -p gpurun_out/prof
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/$arg -o run \
-        -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof/$arg.log 2>&1 || fail "$step" $?
-      summ_stats gpurun_out/prof/$arg ;;
+    stats)  # stats:TAG[:bench args, '+'-separated]
+      tag=${arg%%:*}; bargs=${arg#*:}; [ "$bargs" = "$arg" ] && bargs=""; bargs=${bargs//+/ }
+      rm -rf gpurun_out/prof/$tag; mkdir -p gpurun_out/prof
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/$tag -o run \
+        -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline $bargs > gpurun_out/prof/$tag.log 2>&1 || fail "$step" $?
+      summ_stats gpurun_out/prof/$tag
+      f=$(find gpurun_out/prof/$tag -name '*kernel_trace.csv' | head -1)
+      [ -n "$f" ] && python3 tools/step_timeline.py "$f" ;;
     pmc)  # pmc:TAG[:bench args, '+'-separated]
       tag=${arg%%:*}; bargs=${arg#*:}; [ "$bargs" = "$arg" ] && bargs=""; bargs=${bargs//+/ }
       rm -rf gpurun_out/pmc_step_$tag; mkdir -p gpurun_out/pmc_step_$tag
