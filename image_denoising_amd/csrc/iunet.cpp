@@ -39,6 +39,12 @@ namespace {
     }                                                                     \
   } while (0)
 
+// a launch of a pass body, skipped in its dry run (Ctx::dry)
+#define IU_RUN(c, x)                 \
+  do {                               \
+    if (!(c).dry) IU_TRY(x);         \
+  } while (0)
+
 constexpr int GROWTH = 32;  // RDB growth (arch_unet.py:437)
 constexpr float GN_EPS = 1e-5f;
 
@@ -103,22 +109,22 @@ long gpack_floats(int ksize, int K, int nout) {
 }
 
 // forward image of conv weight [cout][cin][k][k] (reduction K = cin, outputs = cout)
-hipError_t gpack_fwd(const float* w, int ksize, int cin, int cout, float* out, hipStream_t s) {
+bool gjob_fwd(const float* w, int ksize, int cin, int cout, float* out, PackJob& j) {
   GGeom g;
-  if (!ggeom(ksize, cin, cout, g)) return hipErrorInvalidValue;
+  if (!ggeom(ksize, cin, cout, g)) return false;
   WView wv = conv_fwd_view(w, cin, ksize);
   wv.sZ = (long)g.np * wv.sN;
-  return launch_pack(g.gather, wv, cin, g.np, g.nz, out, s, g.np, cout);
+  return pack_job(g.gather, wv, cin, g.np, g.nz, out, g.np, cout, j);
 }
 
 // data-gradient image: reduction over the layer's cout, outputs = its first nout input channels
-hipError_t gpack_dgrad(const float* w, int ksize, int cin_total, int cout, int nout, float* out,
-                       hipStream_t s) {
+bool gjob_dgrad(const float* w, int ksize, int cin_total, int cout, int nout, float* out,
+                PackJob& j) {
   GGeom g;
-  if (!ggeom(ksize, cout, nout, g)) return hipErrorInvalidValue;
+  if (!ggeom(ksize, cout, nout, g)) return false;
   WView wv = conv_dgrad_view(w, cin_total, ksize);
   wv.sZ = (long)g.np * wv.sN;
-  return launch_pack(g.gather, wv, cout, g.np, g.nz, out, s, g.np, nout);
+  return pack_job(g.gather, wv, cout, g.np, g.nz, out, g.np, nout, j);
 }
 
 hipError_t grun(int ksize, const View& in, int N, int H, int W, int K, const float* wp, int nout,
@@ -323,37 +329,43 @@ bool iunet_build_plan(const dn_unet_cfg& c, int N, int H, int W, bool bwd, IPlan
   p.sc = allocf((long)N * 384);
   p.sh = allocf((long)N * 384);
   p.gpart = allocf(2L * 2 * std::max(2048L, (long)N) * 384);  // N*S splits x 384 ch x 2 doubles
-  // packed-weight scratch: max over every conv (forward and data-gradient images)
-  long pk = 0;
-  long x6max = 0;
-  auto pf = [&](int k, int K, int nout) {
-    pk = std::max(pk, gpack_floats(k, K, nout));
+  // packed-weight arena: one slot per conv of a pass (forward images; the backward's
+  // data-gradient images reuse the region), each sized for the fp32 or the split-bf16 image,
+  // whichever the launch takes.  A pass packs every slot in a few batched launches first.
+  long fsum = 0, bsum = 0;
+  auto slot = [](int k, int K, int nout) {
+    long f = gpack_floats(k, K, nout);
     if (k == 3)  // every shape x6_takes may route (-1 where the x6 kernels have no tile)
-      x6max = std::max(x6max, (x6_pack_elems(K, nout, x6_zc(nout)) + 1) / 2);
+      f = std::max(f, (x6_pack_elems(K, nout, x6_zc(nout)) + 1) / 2);
+    return (std::max(f, 0L) + 63) / 64 * 64;
   };
+  auto pf = [&](int k, int K, int nout) { fsum += slot(k, K, nout); };
+  auto pb = [&](int k, int K, int nout) { bsum += slot(k, K, nout); };
   for (int i = 0; i < 4; ++i) {
     const ILevel& L = P.down[i];
     pf(3, L.conv.cin, L.conv.cout);
-    if (i > 0) pf(3, L.conv.cout, L.conv.cin);
+    if (i > 0) pb(3, L.conv.cout, L.conv.cin);
   }
   auto rdbp = [&](const IRdb& r) {
-    for (int j = 0; j < 4; ++j) { pf(3, r.conv[j].cin, GROWTH); pf(3, GROWTH, r.conv[j].cin); }
-    pf(1, r.lff.cin, r.C); pf(1, r.C, r.lff.cin);
+    for (int j = 0; j < 4; ++j) { pf(3, r.conv[j].cin, GROWTH); pb(3, GROWTH, r.conv[j].cin); }
+    pf(1, r.lff.cin, r.C); pb(1, r.C, r.lff.cin);
   };
-  auto resp = [&](const IRes& r) { pf(3, r.C, r.C); };
+  auto resp = [&](const IRes& r) {
+    for (int t = 0; t < 2; ++t) { pf(3, r.C, r.C); pb(3, r.C, r.C); }
+  };
   for (int i = 0; i < 4; ++i) { rdbp(P.down[i].rdb); resp(P.down[i].res); }
   rdbp(P.brdb); resp(P.bres);
   for (int k = 0; k < 4; ++k) {
     const IUp& u = P.up[k];
-    pf(3, u.ps.cin, u.ps.cout); pf(3, u.ps.cout, u.ps.cin);
-    pf(3, u.fuse.cin, u.fuse.cout); pf(3, u.fuse.cout, u.fuse.cin);
+    pf(3, u.ps.cin, u.ps.cout); pb(3, u.ps.cout, u.ps.cin);
+    pf(3, u.fuse.cin, u.fuse.cout); pb(3, u.fuse.cout, u.fuse.cin);
     rdbp(u.rdb); resp(u.res);
   }
-  pf(3, 1, 48);         // ne2 data gradient
-  pf(3, P.OC, 24);      // final data gradient (x_up3 part)
-  pk = std::max(pk, x6max);  // the split-bf16 images of the same 3x3 convs
-  p.pack = allocf(pk);
-  p.pack_floats = pk;
+  pb(3, 1, 48);         // ne2 data gradient
+  pb(3, P.OC, 24);      // final data gradient (x_up3 part)
+  const long arena = bwd ? std::max(fsum, bsum) : fsum;
+  p.pack = allocf(arena);
+  p.pack_floats = arena;
   if (bwd) {
     auto gblock = [&](IBlockBufs& b, int l, int ch) {
       b.dF = alloc(l, ch + 4 * GROWTH);
@@ -503,7 +515,17 @@ struct Ctx {
   // backward: the weight gradients' stream (s when running on one stream) and its fork event
   hipStream_t s2 = nullptr;
   hipEvent_t fork = nullptr;
+  // A pass runs twice: dry (every conv queues its weight image into the next arena slot, nothing
+  // else launches), then the batched packs, then for real (each conv takes the same slot).
+  bool dry = false;
+  PackBatch* pb = nullptr;
+  long* next = nullptr;
   View V(long o, int stride, int off = 0) const { return View{ws + o, stride, off}; }
+  float* slot(long floats) const {  // the next conv's arena slot (nullptr: arena overrun)
+    const long o = *next;
+    *next += (floats + 63) / 64 * 64;
+    return *next <= p.pack_floats ? ws + p.pack + o : nullptr;
+  }
   const float* Wt(const IConv& c) const { return prm + c.w; }
   const float* Bs(const IConv& c) const { return c.b >= 0 ? prm + c.b : nullptr; }
 };
@@ -512,22 +534,37 @@ const View kNone{nullptr, 0, 0};
 
 dn_status conv_fwd(const Ctx& c, const IConv& L, const View& in, int h, int w, int epi,
                    const View& out, int layout = OUT_NHWC, const View& aux = kNone) {
-  OpScope prof(c.s, "fwd", L.cout, L.cin, L.k, h, w, c.p.N, 1.0);
-  float* pk = c.ws + c.p.pack;
   const int tail = x6_tail_for(in, c.p.N, h, w, L.cin, L.cout, w6_views(out, layout, aux, L.cout));
-  if (c.prec == DN_PREC_FP32_X6 && L.k == 3 && x6_takes(L.cin, L.cout, tail)) {
-    IU_TRY(launch_pack_x6(conv_fwd_view(c.Wt(L), L.cin, 3), L.cin, L.cout, x6_zc(L.cout), pk,
-                          c.s, tail));
-    IU_TRY(x6run(in, c.p.N, h, w, L.cin, pk, L.cout, c.Bs(L), epi, out, layout, aux, tail, c.s));
+  const bool x6 = c.prec == DN_PREC_FP32_X6 && L.k == 3 && x6_takes(L.cin, L.cout, tail);
+  float* pk = c.slot(x6 ? (x6_pack_elems(L.cin, L.cout, x6_zc(L.cout)) + 1) / 2
+                        : gpack_floats(L.k, L.cin, L.cout));
+  if (!pk) {
+    set_error("ImprovedUNet: packed-weight arena overrun (forward)");
+    return DN_ERR_ARG;
+  }
+  if (c.dry) {
+    PackJob j;
+    const bool ok = x6 ? pack_job_x6(conv_fwd_view(c.Wt(L), L.cin, 3), L.cin, L.cout,
+                                     x6_zc(L.cout), pk, tail, j)
+                       : gjob_fwd(c.Wt(L), L.k, L.cin, L.cout, pk, j);
+    if (!ok) {
+      set_error("ImprovedUNet: no weight image for a forward conv");
+      return DN_ERR_ARG;
+    }
+    IU_TRY(pack_add(*c.pb, j, c.s));
     return DN_OK;
   }
-  IU_TRY(gpack_fwd(c.Wt(L), L.k, L.cin, L.cout, pk, c.s));
-  IU_TRY(grun(L.k, in, c.p.N, h, w, L.cin, pk, L.cout, c.Bs(L), epi, out, layout, aux, c.s));
+  OpScope prof(c.s, "fwd", L.cout, L.cin, L.k, h, w, c.p.N, 1.0);
+  if (x6)
+    IU_TRY(x6run(in, c.p.N, h, w, L.cin, pk, L.cout, c.Bs(L), epi, out, layout, aux, tail, c.s));
+  else
+    IU_TRY(grun(L.k, in, c.p.N, h, w, L.cin, pk, L.cout, c.Bs(L), epi, out, layout, aux, c.s));
   return DN_OK;
 }
 
 dn_status gn_fwd(const Ctx& c, const IGN& g, const View& z, int h, int w, float* stats, int act,
                  const View* res, const View& out) {
+  if (c.dry) return DN_OK;
   OpScope prof(c.s, "gn", g.C, 1, 1, h, w, c.p.N, 0.0);
   const int N = c.p.N;
   const long P = (long)h * w;
@@ -567,29 +604,28 @@ WView thin_view(const float* w, int cin) {  // weight [o][cin][3][3] as W(o, k, 
   return v;
 }
 
-}  // namespace
-
-dn_status iunet_forward(const IPlan& p, const float* prm, const float* x, float* y, float* ws,
-                        hipStream_t s, int prec) {
-  const StreamDeviceGuard device_guard(s);
-  if (prec != DN_PREC_FP32 && prec != DN_PREC_FP32_X6) return DN_ERR_ARG;
-  const Ctx c{p, prm, ws, s, prec};
+// the forward's launches (Ctx::dry: only the convs' weight images are queued)
+dn_status forward_body(const Ctx& c, const float* x, float* y) {
+  const IPlan& p = c.p;
+  const float* prm = c.prm;
+  float* ws = c.ws;
+  const hipStream_t s = c.s;
   const IParams& P = p.P;
   const int N = p.N, H = p.H, W = p.W, C = P.C;
   // noise estimator: h = leaky(ne0(x)) (also writes x into x0[:, :C], zeros x0[:, C:4])
-  IU_TRY(launch_enc0_fwd(x, N, C, H, W, prm + P.ne0.w, prm + P.ne0.b, ws + p.h, ws + p.x0, 4, 0, 4,
-                         nullptr, s));
-  IU_TRY(launch_conv3_thin(c.V(p.h, 48), N, H, W, 48, thin_view(prm + P.ne2.w, 48), prm + P.ne2.b,
-                           TE_SIGMOID, kNone, c.V(p.x0, 4, C), 0, 1, s));
+  IU_RUN(c, launch_enc0_fwd(x, N, C, H, W, prm + P.ne0.w, prm + P.ne0.b, ws + p.h, ws + p.x0, 4,
+                            0, 4, nullptr, s));
+  IU_RUN(c, launch_conv3_thin(c.V(p.h, 48), N, H, W, 48, thin_view(prm + P.ne2.w, 48),
+                              prm + P.ne2.b, TE_SIGMOID, kNone, c.V(p.x0, 4, C), 0, 1, s));
   if (p.with_bwd) {
-    IU_TRY(hipMemcpyAsync(ws + p.xin, x, sizeof(float) * (size_t)N * C * H * W,
-                          hipMemcpyDeviceToDevice, s));
-    IU_TRY(launch_conv3_thin(c.V(p.h, 48), N, H, W, 48, thin_view(prm + P.ne2.w, 48),
-                             prm + P.ne2.b, TE_SIGMOID, kNone, View{ws + p.sig, 0, 0}, 1, 1, s));
+    IU_RUN(c, hipMemcpyAsync(ws + p.xin, x, sizeof(float) * (size_t)N * C * H * W,
+                             hipMemcpyDeviceToDevice, s));
+    IU_RUN(c, launch_conv3_thin(c.V(p.h, 48), N, H, W, 48, thin_view(prm + P.ne2.w, 48),
+                                prm + P.ne2.b, TE_SIGMOID, kNone, View{ws + p.sig, 0, 0}, 1, 1, s));
   }
-  IU_TRY(launch_nchw_to_slice(x, N, C, H, W, ws + p.cf, 28, 24, 28, s));  // final concat input
-  // encoder
-  View xi = c.V(p.x0, 4);
+  IU_RUN(c, launch_nchw_to_slice(x, N, C, H, W, ws + p.cf, 28, 24, 28, s));  // final concat input
+                                 // encoder
+                                 View xi = c.V(p.x0, 4);
   for (int i = 0; i < 4; ++i) {
     const ILevel& L = P.down[i];
     const int h = H >> i, w = W >> i, nf = L.conv.cout, FS = nf + 4 * GROWTH;
@@ -600,7 +636,7 @@ dn_status iunet_forward(const IPlan& p, const float* prm, const float* x, float*
     const View skip = c.V(p.cc[k], 3 * out, out);
     if (dn_status st = res_fwd(c, L.res, b, h, w, skip)) return st;
     const View dst = i < 3 ? c.V(p.pool[i + 1], nf) : c.V(p.bb.F, 384 + 4 * GROWTH);
-    IU_TRY(launch_vpool_fwd(skip, N, h, w, nf, dst, s));
+    IU_RUN(c, launch_vpool_fwd(skip, N, h, w, nf, dst, s));
     xi = dst;
   }
   // bottleneck
@@ -621,11 +657,30 @@ dn_status iunet_forward(const IPlan& p, const float* prm, const float* x, float*
     if (dn_status st = res_fwd(c, u.res, b, h, w, o)) return st;
     xk = o;
   }
-  IU_TRY(launch_conv3_thin(c.V(p.cf, 28), N, H, W, 24 + C, thin_view(prm + P.fin.w, 24 + C),
-                           prm + P.fin.b, TE_SIGMOID, kNone, View{y, 0, 0}, 1, P.OC, s));
+  IU_RUN(c, launch_conv3_thin(c.V(p.cf, 28), N, H, W, 24 + C, thin_view(prm + P.fin.w, 24 + C),
+                              prm + P.fin.b, TE_SIGMOID, kNone, View{y, 0, 0}, 1, P.OC, s));
   if (p.with_bwd)
-    IU_TRY(hipMemcpyAsync(ws + p.yout, y, sizeof(float) * (size_t)N * P.OC * H * W,
-                          hipMemcpyDeviceToDevice, s));
+    IU_RUN(c, hipMemcpyAsync(ws + p.yout, y, sizeof(float) * (size_t)N * P.OC * H * W,
+                             hipMemcpyDeviceToDevice, s));
+  return DN_OK;
+}
+
+}  // namespace
+
+// Every pass: a dry run queues the weight image of each conv into its arena slot, the queued
+// packs launch (24 images per launch), then the pass runs on them.
+dn_status iunet_forward(const IPlan& p, const float* prm, const float* x, float* y, float* ws,
+                        hipStream_t s, int prec) {
+  const StreamDeviceGuard device_guard(s);
+  if (prec != DN_PREC_FP32 && prec != DN_PREC_FP32_X6) return DN_ERR_ARG;
+  PackBatch pb;
+  long next = 0;
+  Ctx c{p, prm, ws, s, prec};
+  c.pb = &pb; c.next = &next; c.dry = true;
+  if (dn_status st = forward_body(c, x, y)) return st;
+  IU_TRY(pack_flush(pb, s));
+  next = 0; c.dry = false;
+  if (dn_status st = forward_body(c, x, y)) return st;
   g_prof.flush("iunet forward");
   return DN_OK;
 }
@@ -638,6 +693,7 @@ namespace {
 // dW (+ db) of a conv from g = dL/d(conv output) and its input x; written into dprm
 dn_status wgrad_g(const Ctx& c, float* dprm, int mode, const IConv& L, const View& g, const View& x,
                   int h, int w) {
+  if (c.dry) return DN_OK;
   // on the side stream, behind the main stream's work so far (g is its latest output)
   const hipStream_t s2 = c.s2 ? c.s2 : c.s;
   if (s2 != c.s) {
@@ -679,22 +735,37 @@ dn_status wgrad_g(const Ctx& c, float* dprm, int mode, const IConv& L, const Vie
 // dx (first nout input channels) = conv^T(g) with epilogue epi (aux = mask / residual)
 dn_status dgrad_g(const Ctx& c, const IConv& L, const View& g, int h, int w, int nout, int epi,
                   const View& aux, const View& dx) {
-  OpScope prof(c.s, "dgrad", nout, L.cout, L.k, h, w, c.p.N, 1.0);
-  float* pk = c.ws + c.p.pack;
   const int tail = x6_tail_for(g, c.p.N, h, w, L.cout, nout, w6_views(dx, OUT_NHWC, aux, nout));
-  if (c.prec == DN_PREC_FP32_X6 && L.k == 3 && x6_takes(L.cout, nout, tail)) {
-    IU_TRY(launch_pack_x6(conv_dgrad_view(c.Wt(L), L.cin, 3), L.cout, nout, x6_zc(nout), pk,
-                          c.s, tail));
-    IU_TRY(x6run(g, c.p.N, h, w, L.cout, pk, nout, nullptr, epi, dx, OUT_NHWC, aux, tail, c.s));
+  const bool x6 = c.prec == DN_PREC_FP32_X6 && L.k == 3 && x6_takes(L.cout, nout, tail);
+  float* pk = c.slot(x6 ? (x6_pack_elems(L.cout, nout, x6_zc(nout)) + 1) / 2
+                        : gpack_floats(L.k, L.cout, nout));
+  if (!pk) {
+    set_error("ImprovedUNet: packed-weight arena overrun (backward)");
+    return DN_ERR_ARG;
+  }
+  if (c.dry) {
+    PackJob j;
+    const bool ok = x6 ? pack_job_x6(conv_dgrad_view(c.Wt(L), L.cin, 3), L.cout, nout,
+                                     x6_zc(nout), pk, tail, j)
+                       : gjob_dgrad(c.Wt(L), L.k, L.cin, L.cout, nout, pk, j);
+    if (!ok) {
+      set_error("ImprovedUNet: no weight image for a data gradient");
+      return DN_ERR_ARG;
+    }
+    IU_TRY(pack_add(*c.pb, j, c.s));
     return DN_OK;
   }
-  IU_TRY(gpack_dgrad(c.Wt(L), L.k, L.cin, L.cout, nout, pk, c.s));
-  IU_TRY(grun(L.k, g, c.p.N, h, w, L.cout, pk, nout, nullptr, epi, dx, OUT_NHWC, aux, c.s));
+  OpScope prof(c.s, "dgrad", nout, L.cout, L.k, h, w, c.p.N, 1.0);
+  if (x6)
+    IU_TRY(x6run(g, c.p.N, h, w, L.cout, pk, nout, nullptr, epi, dx, OUT_NHWC, aux, tail, c.s));
+  else
+    IU_TRY(grun(L.k, g, c.p.N, h, w, L.cout, pk, nout, nullptr, epi, dx, OUT_NHWC, aux, c.s));
   return DN_OK;
 }
 
 dn_status gn_bwd(const Ctx& c, float* dprm, const IGN& g, const View& dy, const View& z, int h,
                  int w, const float* stats, const View& dz) {
+  if (c.dry) return DN_OK;
   OpScope prof(c.s, "gnbwd", g.C, 1, 1, h, w, c.p.N, 0.0);
   const int N = c.p.N;
   const long P = (long)h * w;
@@ -732,11 +803,11 @@ dn_status rdb_bwd(const Ctx& c, float* dprm, const IRdb& R, const IBlockBufs& b,
   const View dr = c.V(b.dr, C);
   if (dn_status st = wgrad_g(c, dprm, W_C1, R.lff, dr, c.V(b.F, FS), h, w)) return st;
   if (dn_status st = dgrad_g(c, R.lff, dr, h, w, FS, EPI_PLAIN, kNone, c.V(b.dF, FS))) return st;
-  IU_TRY(launch_vadd(c.V(b.dF, FS), dr, npx, C, c.s));  // out = x + lff(...)
-  for (int j = 3; j >= 0; --j) {
-    const int o = C + GROWTH * j;
+  IU_RUN(c, launch_vadd(c.V(b.dF, FS), dr, npx, C, c.s));  // out = x + lff(...)
+                        for (int j = 3; j >= 0; --j) {
+                        const int o = C + GROWTH * j;
     const View dzj = c.V(b.dzj[j], GROWTH);
-    IU_TRY(launch_vmask(dzj, c.V(b.dF, FS, o), c.V(b.F, FS, o), npx, GROWTH, c.s));
+    IU_RUN(c, launch_vmask(dzj, c.V(b.dF, FS, o), c.V(b.F, FS, o), npx, GROWTH, c.s));
     if (dn_status st = wgrad_g(c, dprm, W_C3, R.conv[j], dzj, c.V(b.F, FS), h, w)) return st;
     if (dn_status st = dgrad_g(c, R.conv[j], dzj, h, w, o, EPI_ACCUM, kNone,
                                c.V(b.dF, FS)))
@@ -745,21 +816,12 @@ dn_status rdb_bwd(const Ctx& c, float* dprm, const IRdb& R, const IBlockBufs& b,
   return DN_OK;
 }
 
-}  // namespace
-
-dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, float* dprm, float* ws,
-                         hipStream_t s, int prec) {
-  const StreamDeviceGuard device_guard(s);
-  if (prec != DN_PREC_FP32 && prec != DN_PREC_FP32_X6) return DN_ERR_ARG;
-  // The weight gradients (and their slab reductions) run on a side stream beside the
-  // data-gradient chain (DN_BWD_STREAMS=0 or per-op profiling: one stream).  Each is forked after
-  // the launch that produced its output gradient; every buffer one reads (the forward's
-  // activations, dz2 / dz1 / dr / dzf of a block, dzj[j], dps[k], dza[i], dzfin, dsg, dh once
-  // written) is not rewritten later in the pass, and only they use the slab.  Joined at the end.
-  static const bool two_env = !getenv("DN_BWD_STREAMS") || atoi(getenv("DN_BWD_STREAMS")) != 0;
-  SideStream* side = two_env && !prof_on() && !g_prof.on ? side_stream(s) : nullptr;
-  Ctx c{p, prm, ws, s, prec};
-  if (side) { c.s2 = side->st; c.fork = side->fork; }
+// the backward's launches (Ctx::dry: only the data gradients' weight images are queued)
+dn_status backward_body(const Ctx& c, const float* dy, float* dprm, SideStream* side) {
+  const IPlan& p = c.p;
+  const float* prm = c.prm;
+  float* ws = c.ws;
+  const hipStream_t s = c.s;
   const hipStream_t s2 = side ? side->st : s;
   auto fork = [&]() -> hipError_t {
     if (!side) return hipSuccess;
@@ -770,11 +832,11 @@ dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, floa
   const int N = p.N, H = p.H, W = p.W, C = P.C, OC = P.OC;
   const long HW = (long)H * W;
   // final: dz = dy * y(1-y)  (stride-4 NHWC), then its weight / data gradients
-  IU_TRY(launch_dsigmoid_nchw(ws + p.yout, dy, N, OC, HW, ws + p.dzfin, 4, s));
+  IU_RUN(c, launch_dsigmoid_nchw(ws + p.yout, dy, N, OC, HW, ws + p.dzfin, 4, s));
   if (dn_status st = wgrad_g(c, dprm, W_C3, P.fin, c.V(p.dzfin, 4), c.V(p.cf, 28), H, W)) return st;
   // gradient of x_up3 = the first 24 channels of the final concat (the input slice needs
   // none); dh (48 channels) is free until the noise estimator's backward
-  IU_TRY(hipMemsetAsync(ws + p.dsg, 0, sizeof(float) * 4 * (size_t)N * HW, s));
+  IU_RUN(c, hipMemsetAsync(ws + p.dsg, 0, sizeof(float) * 4 * (size_t)N * HW, s));
   const View dfin = c.V(p.dh, 24);
   if (dn_status st = dgrad_g(c, P.fin, c.V(p.dzfin, 4), H, W, 24, EPI_PLAIN, kNone, dfin)) return st;
   // decoder, last block first
@@ -787,14 +849,14 @@ dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, floa
     if (dn_status st = rdb_bwd(c, dprm, u.rdb, b, h, w)) return st;
     // f = leaky(fuse(cc)): dz = dF[:, :out] * leaky'(f)
     const View dzf = c.V(b.dzf, out);
-    IU_TRY(launch_vmask(dzf, c.V(b.dF, FS), c.V(b.F, FS), (long)N * h * w, out, s));
+    IU_RUN(c, launch_vmask(dzf, c.V(b.dF, FS), c.V(b.F, FS), (long)N * h * w, out, s));
     if (dn_status st = wgrad_g(c, dprm, W_C3, u.fuse, dzf, c.V(p.cc[k], 3 * out), h, w)) return st;
     if (dn_status st = dgrad_g(c, u.fuse, dzf, h, w, 3 * out, EPI_PLAIN, kNone,
                                c.V(p.dcc[k], 3 * out)))
       return st;
     // PixelShuffle backward, then conv_ps (input: bottle output or the previous up block)
     float* gps = ws + p.dps[k];
-    IU_TRY(launch_unshuffle(c.V(p.dcc[k], 3 * out), N, h / 2, w / 2, out, gps, s));
+    IU_RUN(c, launch_unshuffle(c.V(p.dcc[k], 3 * out), N, h / 2, w / 2, out, gps, s));
     const View xin = k == 0 ? c.V(p.xb, 384) : c.V(p.xu[k - 1], u.in);
     if (dn_status st = wgrad_g(c, dprm, W_C3, u.ps, View{gps, 4 * out, 0}, xin, h / 2, w / 2))
       return st;
@@ -816,11 +878,11 @@ dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, floa
     const int k = 3 - i, out = P.up[k].out;
     const View skip = c.V(p.cc[k], 3 * out, out), dskip = c.V(p.dcc[k], 3 * out, out);
     // d s_i = (skip gradient from the fuse conv) + maxpool backward of d x_{i+1}
-    IU_TRY(launch_vpool_bwd_acc(skip, N, h, w, nf, dpooled, dskip, s));
+    IU_RUN(c, launch_vpool_bwd_acc(skip, N, h, w, nf, dpooled, dskip, s));
     if (dn_status st = res_bwd(c, dprm, L.res, b, dskip, h, w)) return st;
     if (dn_status st = rdb_bwd(c, dprm, L.rdb, b, h, w)) return st;
     const View dza = c.V(p.dza[i], nf);
-    IU_TRY(launch_vmask(dza, c.V(b.dF, FS), c.V(b.F, FS), (long)N * h * w, nf, s));
+    IU_RUN(c, launch_vmask(dza, c.V(b.dF, FS), c.V(b.F, FS), (long)N * h * w, nf, s));
     if (i > 0) {
       const View xi = c.V(p.pool[i], L.conv.cin);
       if (dn_status st = wgrad_g(c, dprm, W_C3, L.conv, dza, xi, h, w)) return st;
@@ -834,18 +896,18 @@ dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, floa
       float* slab = ws + p.slab;
       const long n = 48L * (C + 1) * 9 + 48;
       const int st = enc0_wgrad_splits(N, H, W);
-      IU_TRY(fork());
-      IU_TRY(launch_wgrad_c3_thin(ws + p.dza[0], 48, ws + p.xin, N, C, H, W, slab, n, C + 1, 0, 1, st,
-                                  s2));
-      IU_TRY(launch_wgrad_c3_thin(ws + p.dza[0], 48, ws + p.sig, N, 1, H, W, slab, n, C + 1, C, 0, st,
-                                  s2));
-      IU_TRY(launch_reduce(slab, n, st, n, dprm + L.conv.w, s2));
+      IU_RUN(c, fork());
+      IU_RUN(c, launch_wgrad_c3_thin(ws + p.dza[0], 48, ws + p.xin, N, C, H, W, slab, n, C + 1, 0,
+                                     1, st, s2));
+      IU_RUN(c, launch_wgrad_c3_thin(ws + p.dza[0], 48, ws + p.sig, N, 1, H, W, slab, n, C + 1, C,
+                                     0, st, s2));
+      IU_RUN(c, launch_reduce(slab, n, st, n, dprm + L.conv.w, s2));
       // d sigma (channel C of x0) through the sigmoid: flipped weight column ci = C
       WView fv{};
       fv.w = prm + L.conv.w; fv.off = (long)C * 9; fv.sN = 9; fv.sK = (long)(C + 1) * 9;
       fv.sT = 1; fv.taps = 9; fv.flip = 1;
-      IU_TRY(launch_conv3_thin(dza, N, H, W, 48, fv, nullptr, TE_DSIG, c.V(p.x0, 4, C),
-                               c.V(p.dsg, 4), 0, 1, s));
+      IU_RUN(c, launch_conv3_thin(dza, N, H, W, 48, fv, nullptr, TE_DSIG, c.V(p.x0, 4, C),
+                                  c.V(p.dsg, 4), 0, 1, s));
     }
   }
   // noise estimator: ne2 (48 -> 1) and ne0 (C -> 48)
@@ -857,14 +919,40 @@ dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, floa
     float* slab = ws + p.slab;
     const long n = 48L * C * 9 + 48;
     const int st = enc0_wgrad_splits(N, H, W);
-    IU_TRY(fork());
-    IU_TRY(launch_wgrad_c3_thin(ws + p.dh, 48, ws + p.xin, N, C, H, W, slab, n, C, 0, 1, st, s2));
-    IU_TRY(launch_reduce(slab, n, st, n, dprm + P.ne0.w, s2));
+    IU_RUN(c, fork());
+    IU_RUN(c, launch_wgrad_c3_thin(ws + p.dh, 48, ws + p.xin, N, C, H, W, slab, n, C, 0, 1, st,
+                                   s2));
+    IU_RUN(c, launch_reduce(slab, n, st, n, dprm + P.ne0.w, s2));
   }
   if (side) {  // the caller's stream continues after every weight gradient
-    IU_TRY(hipEventRecord(side->join, s2));
-    IU_TRY(hipStreamWaitEvent(s, side->join, 0));
+    IU_RUN(c, hipEventRecord(side->join, s2));
+    IU_RUN(c, hipStreamWaitEvent(s, side->join, 0));
   }
+  return DN_OK;
+}
+
+}  // namespace
+
+dn_status iunet_backward(const IPlan& p, const float* prm, const float* dy, float* dprm, float* ws,
+                         hipStream_t s, int prec) {
+  const StreamDeviceGuard device_guard(s);
+  if (prec != DN_PREC_FP32 && prec != DN_PREC_FP32_X6) return DN_ERR_ARG;
+  // The weight gradients (and their slab reductions) run on a side stream beside the
+  // data-gradient chain (DN_BWD_STREAMS=0 or per-op profiling: one stream).  Each is forked after
+  // the launch that produced its output gradient; every buffer one reads (the forward's
+  // activations, dz2 / dz1 / dr / dzf of a block, dzj[j], dps[k], dza[i], dzfin, dsg, dh once
+  // written) is not rewritten later in the pass, and only they use the slab.  Joined at the end.
+  static const bool two_env = !getenv("DN_BWD_STREAMS") || atoi(getenv("DN_BWD_STREAMS")) != 0;
+  SideStream* side = two_env && !prof_on() && !g_prof.on ? side_stream(s) : nullptr;
+  PackBatch pb;
+  long next = 0;
+  Ctx c{p, prm, ws, s, prec};
+  if (side) { c.s2 = side->st; c.fork = side->fork; }
+  c.pb = &pb; c.next = &next; c.dry = true;
+  if (dn_status st = backward_body(c, dy, dprm, side)) return st;
+  IU_TRY(pack_flush(pb, s));
+  next = 0; c.dry = false;
+  if (dn_status st = backward_body(c, dy, dprm, side)) return st;
   g_prof.flush("iunet backward");
   return DN_OK;
 }

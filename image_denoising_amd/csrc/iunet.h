@@ -52,7 +52,7 @@ struct IPlan {
   long cf = 0;                        // final concat [x_up3 (24) | x (C) | 0]  stride 28
   long sc = 0, sh = 0;                // GN scale / shift scratch [N * 384]
   long gpart = 0;                     // GN partial sums (doubles)
-  long pack = 0, pack_floats = 0;     // packed weight scratch (one layer at a time)
+  long pack = 0, pack_floats = 0;     // packed-weight arena (one slot per conv of a pass)
   // gradients
   long dzfin = 0, dcc[4] = {0, 0, 0, 0}, dps[4] = {0, 0, 0, 0}, dxu[3] = {0, 0, 0}, dxb = 0, dpool = 0;
   long dza[4] = {0, 0, 0, 0}, dsg = 0, dh = 0, ca = 0, cb = 0, ccf = 0;
