@@ -37,6 +37,7 @@ SIGNATURES = {
     "dn_version": (c_char_p, []),
     "dn_abi_version": (c_int, []),
     "dn_profile_ops": (c_int, [c_int]),
+    "dn_prepare_streams": (c_int, [c_void_p]),
     "dn_profile_ops_read": (c_int, [c_void_p, c_int, POINTER(c_int)]),
     "dn_last_error": (c_int, [c_char_p, c_size_t]),
     "dn_unet_param_count": (c_int, [POINTER(DnCfg), POINTER(c_size_t)]),

@@ -49,6 +49,26 @@ int dn_last_error(char* buf, size_t len) {
   return (int)s.size();
 }
 
+dn_status dn_prepare_streams(void* stream) {
+  DN_GUARD_BEGIN
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  const StreamDeviceGuard device_guard(s);
+  SideStream* ss = side_stream(s);
+  if (!ss) return fail(DN_ERR_HIP, "creating the backward's side streams failed");
+  // one marker on each (its first submission binds it to a hardware queue), ordered after the
+  // caller's stream and joined back into it
+  if (hipEventRecord(ss->fork, s) != hipSuccess ||
+      hipStreamWaitEvent(ss->st, ss->fork, 0) != hipSuccess ||
+      hipStreamWaitEvent(ss->rst, ss->fork, 0) != hipSuccess ||
+      hipEventRecord(ss->join, ss->st) != hipSuccess ||
+      hipEventRecord(ss->rjoin, ss->rst) != hipSuccess ||
+      hipStreamWaitEvent(s, ss->join, 0) != hipSuccess ||
+      hipStreamWaitEvent(s, ss->rjoin, 0) != hipSuccess)
+    return fail(DN_ERR_HIP, "marker on the backward's side streams failed");
+  return DN_OK;
+  DN_GUARD_END
+}
+
 dn_status dn_unet_param_count(const dn_unet_cfg* cfg, size_t* count) {
   DN_GUARD_BEGIN
   if (!cfg || !count) return fail(DN_ERR_ARG, "null argument");

@@ -24,6 +24,44 @@ import torch
 import torch.distributed as dist
 
 
+# The step's own streams, one of each kind per device: "side" (the N2N no-grad pass beside the
+# gradient pass) and "comm" (the early gradient bucket's all-reduce).  HIP binds a stream to one
+# of GPU_MAX_HW_QUEUES (default 4) hardware queues at its first submission and shares queues
+# after that; streams sharing a queue run one after the other.  In a one-rank RCCL run the no-grad
+# pass shared the main stream's queue (RCCL's streams had taken the free ones first): 19.34-19.45
+# against 18.97 ms/step for the plain bench; with prepare_streams() (the step's streams touched
+# before the process group exists) 19.08-19.18 against 18.92-19.01 (profiles/r6_dp1_streams.log).
+# Raising GPU_MAX_HW_QUEUES instead made every launch slower (8: +0.8, 16: +1.3 ms/step under
+# torchrun, profiles/r6_hwq.log).
+_STEP_STREAMS: dict = {}
+
+
+def step_stream(kind: str, device) -> torch.cuda.Stream:
+    """the cached stream `kind` ("side" / "comm") of `device`"""
+    key = (kind, torch.device(device))
+    st = _STEP_STREAMS.get(key)
+    if st is None:
+        st = _STEP_STREAMS[key] = torch.cuda.Stream(device=device)
+    return st
+
+
+def prepare_streams(device) -> None:
+    """First submissions on the streams whose work runs concurrently in the step -- the no-grad
+    pass's, then the library's weight-gradient and reduction streams -- so that with the main
+    stream they hold the four hardware queues before RCCL creates its streams.  The comm stream
+    comes last: it (like RCCL's streams) only carries work enqueued after the whole backward, so
+    sharing a queue costs it nothing but overlap, while a shared queue between two of the compute
+    streams serialises them."""
+    from . import _lib
+
+    device = torch.device(device)
+    with torch.cuda.stream(step_stream("side", device)):
+        torch.zeros(1, device=device)
+    _lib.call("dn_prepare_streams", torch.cuda.current_stream(device).cuda_stream)
+    with torch.cuda.stream(step_stream("comm", device)):
+        torch.zeros(1, device=device)
+
+
 def is_initialized() -> bool:
     return dist.is_available() and dist.is_initialized()
 
@@ -70,6 +108,7 @@ def init_from_env(backend: str = "nccl", force: bool = False) -> tuple[int, int,
     if want and not dist.is_initialized():
         if backend == "nccl":
             torch.cuda.set_device(local)
+            prepare_streams(torch.device("cuda", local))
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)

@@ -59,18 +59,12 @@ class N2NTrainer:
                          and hasattr(net, "_run_backward_split") and hasattr(net, "tail_begin"))
         self._tail_begin = net.tail_begin() if self.distributed and self._overlap else 0
 
-    _side = {}
-    _comm = {}
-
-    @classmethod
-    def _comm_stream(cls, device):
+    @staticmethod
+    def _comm_stream(device):
         """the stream the early gradient bucket's all-reduce is enqueued on"""
         if torch.device(device).type != "cuda":
             return None
-        st = cls._comm.get(device)
-        if st is None:
-            st = cls._comm[device] = torch.cuda.Stream(device=device)
-        return st
+        return dp.step_stream("comm", device)
 
     def _backward(self, dout, ws, N, h, w, ev):
         if ev is None:
@@ -78,14 +72,11 @@ class N2NTrainer:
         else:
             self.net._run_backward_split(dout, self.grad, ws, N, h, w, ev)
 
-    @classmethod
-    def _side_stream(cls, device):
+    @staticmethod
+    def _side_stream(device):
         if os.environ.get("DN_STEP_STREAMS", "1") == "0" or torch.device(device).type != "cuda":
             return None
-        st = cls._side.get(device)
-        if st is None:
-            st = cls._side[device] = torch.cuda.Stream(device=device)
-        return st
+        return dp.step_stream("side", device)
 
     def lambda_for(self, epoch: int) -> float:
         # training_script.md:148 Lambda = epoch / n_epoch * ratio

@@ -100,6 +100,17 @@ dn_status dn_profile_ops(int enable);
    recorded (may exceed cap) and drops them. */
 dn_status dn_profile_ops_read(dn_op_record* out, int cap, int* count);
 
+/* ---- streams ---------------------------------------------------------------------- */
+/* Creates the backward's side streams for the device of `stream` (the weight-gradient and
+   reduction streams every U-Net / ImprovedUNet backward on this host thread uses) and submits a
+   marker on each, so they take their hardware queues now.  HIP binds a stream to one of
+   GPU_MAX_HW_QUEUES (default 4) hardware queues at its first submission and shares queues beyond
+   that; a data-parallel caller runs this (and touches its own step streams) before
+   torch.distributed / RCCL create their streams, so the step's concurrent streams keep queues of
+   their own (image_denoising_amd.dist.prepare_streams).  Optional: the backward creates them
+   on first use otherwise.  No reference counterpart (the reference runs one stream). */
+dn_status dn_prepare_streams(void* stream);
+
 /* ---- U-Net forward / backward: arch_unet.py:194-260 (UNet.forward) + autograd ---- */
 /* bytes of workspace for a batch N x H x W (H, W multiples of 32).  with_backward=1 sizes the
    saved activations, gradient buffers and weight-gradient slabs needed by dn_unet_backward.
