@@ -152,6 +152,36 @@ def test_grads_per_tensor_vs_oracle(shape, seed, prec):
     assert torch.equal(grad, grad2)
 
 
+@pytest.mark.parametrize("prec", PRECS)
+def test_backward_side_stream_equals_one_stream(prec):
+    """iunet_backward runs the weight gradients on a side stream beside the data-gradient chain;
+    with dn_profile_ops on, every launch runs on the caller's stream.  At a size where the two
+    streams overlap, both orders give bit-identical gradients (no buffer a weight gradient reads
+    is rewritten while it runs), and the batched weight packs of the two passes change nothing."""
+    from image_denoising_amd import _lib
+
+    N, C, H, W = 8, 1, 128, 128
+    net = _net(C, prec).to(DEV)
+    gen = torch.Generator().manual_seed(21)
+    x = torch.rand((N, C, H, W), generator=gen).to(DEV)
+    dy = torch.randn((N, C, H, W), generator=gen).to(DEV)
+    ws = net._workspace(N, H, W, with_backward=True, fresh=True)
+    y = torch.empty_like(x)
+    grads = []
+    try:
+        for one_stream in (False, True, False):
+            _lib.profile_ops(one_stream)
+            net._run_forward(x, y, ws)
+            g = torch.empty_like(net.flat_params)
+            net._run_backward(dy, g, ws, N, H, W)
+            torch.cuda.synchronize()
+            grads.append(g)
+    finally:
+        _lib.profile_ops(False)
+    assert torch.isfinite(grads[0]).all()
+    assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2])
+
+
 def test_module_autograd_and_no_grad_paths():
     net = _net(1).to(DEV)
     x = torch.rand(2, 1, 32, 32, device=DEV)
