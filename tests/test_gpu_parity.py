@@ -701,6 +701,28 @@ def test_n2n_step_deterministic(prec):
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
+def test_n2n_step_streams_equal_one_stream():
+    """the bench step's concurrency (weight gradients and slab reductions on the library's side
+    streams) against every library launch on the caller's stream (dn_profile_ops on), at a size
+    where the streams overlap (16 x 256^2): the gradient and the updated weights bit-identical"""
+    from image_denoising_amd import N2NTrainer, _lib
+
+    clean = torch.rand(16, 1, 256, 256, generator=torch.Generator().manual_seed(5)).to(DEV)
+    res = []
+    try:
+        for one_stream in (False, True):
+            _lib.profile_ops(one_stream)
+            net = _net(1, "fp32_x6")
+            tr = N2NTrainer(net, seed=3)
+            tr.train_step(clean, epoch=1)
+            torch.cuda.synchronize()
+            res.append((net.flat_params.detach().clone(), tr.grad.clone()))
+    finally:
+        _lib.profile_ops(False)
+    assert torch.isfinite(res[0][1]).all()
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][0], res[1][0])
+
+
 @pytest.mark.parametrize("style", ["gauss25", "poisson30", "poisson5_50", "gauss5_50"])
 def test_n2n_step_noise_styles(style):
     """N2NTrainer(noise_style=...) synthesises the step's noisy batch with the chosen train.py
