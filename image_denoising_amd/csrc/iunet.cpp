@@ -78,8 +78,8 @@ bool ggeom(int ksize, int K, int nout, GGeom& g) {
 
 // split-bf16 (DN_PREC_FP32_X6) 3x3 convs: the kernels tile 32, 48 or 96 output channels and
 // 32 reduction channels (on large grids a partial last chunk of <= 16 channels costs 5 of 9
-// stages, `tail`), so they take the convs that fill those tiles; the 24-channel level and
-// small-grid K = 48 stay on the fp32 kernels, where the padding would cost more than the
+// stages, `tail`), so they take the convs that fill those tiles; small-grid K = 48 and the
+// level conv (K = 4) stay on the fp32 kernels, where the padding would cost more than the
 // faster matrix cores give (measured per shape)
 bool x6_shape(int nout) { return nout == 32 || nout % 48 == 0; }
 bool x6_takes(int K, int nout, int tail) {
@@ -97,6 +97,9 @@ bool x6_takes(int K, int nout, int tail) {
   // the x6 ceiling
   if (K == 32 && nout >= 80 && nout % 8 == 0) return true;
   if (nout == 24 && K >= 72 && K % 4 == 0) return true;
+  // round 6: the top level's 24 -> 24 (ResBlock) and 24 -> 32 (first growth conv) too, one
+  // zero-padded chunk: fwd3 -0.25 ms/step against the fp32 kernel (profiles/r6_iunet_x624_ab.log)
+  if (K == 24 && (nout == 24 || nout == 32)) return true;
   return x6_shape(nout) && (K % 32 == 0 || K >= 128 || tail) && (K > 32 || nout % 96 == 0);
 }
 // output-channel blocks of the wide layers: 96, or 48 where 96 would pad (144 = 3 x 48)
