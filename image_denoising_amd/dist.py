@@ -38,7 +38,10 @@ _STEP_STREAMS: dict = {}
 
 def step_stream(kind: str, device) -> torch.cuda.Stream:
     """the cached stream `kind` ("side" / "comm") of `device`"""
-    key = (kind, torch.device(device))
+    device = torch.device(device)
+    if device.type == "cuda" and device.index is None:  # "cuda" and "cuda:<current>" share one
+        device = torch.device("cuda", torch.cuda.current_device())
+    key = (kind, device)
     st = _STEP_STREAMS.get(key)
     if st is None:
         st = _STEP_STREAMS[key] = torch.cuda.Stream(device=device)
